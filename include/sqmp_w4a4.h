@@ -1,0 +1,154 @@
+/*
+ * sqmp_w4a4.h -- C ABI of the MI355X-native W4A4 mixed-precision linear operator.
+ *
+ * Drop-in boundary for the hot path of adithyab100/smoothquant-mixedprecision:
+ *   W4A4Linear.from_float  (/root/reference/smoothquant/fake_quant.py:324-371)
+ *   W4A4Linear.forward     (/root/reference/smoothquant/fake_quant.py:279-322)
+ * The reference is pure Python (no FFI); these entry points replace the ATen calls that
+ * its forward and from_float make, and are bound from Python with ctypes by
+ * smoothquant-mixedprecision_amd/smoothquant/_lib.py.
+ *
+ * Conventions
+ *   - Plain C: device pointers, sizes, and a hipStream_t passed as `void*` (NULL = the
+ *     default stream).  Nothing is allocated; the caller owns every buffer, including the
+ *     workspace (size from the *_workspace_bytes queries).  No host synchronisation, so
+ *     every launch function may be captured into a hipGraph.
+ *   - Return value: SQMP_OK (0) or a negative status.  The Python layer maps
+ *     SQMP_EINVAL/SQMP_EUNSUPPORTED to ValueError (the reference's error type for bad
+ *     modes, fake_quant.py:256, :287, :361) and SQMP_EHIP/SQMP_EWORKSPACE to RuntimeError.
+ *   - dtype codes: model dtype D of x, W, bias, y (fp32 / fp16 / bf16).  All scale and
+ *     dequantized values are exact D values (rounded at the same points as the reference).
+ *
+ * Packed weight layout (produced by sqmp_pack_weight, consumed by the GEMMs)
+ *   Kp        packed K length: weight groups in weight-sorted column order, zero padded
+ *             (multiple of 128).  Position p < K holds original column perm[p].
+ *   codes     uint8 [N][Kp/2] for 4-bit weights: byte b of row n holds positions 2b (low
+ *             nibble) and 2b+1 (high nibble), nibble = code + 8 (code in [-7, 7]).
+ *             int8 [N][Kp] for 8-bit weights.  Salient columns and padding hold code 0.
+ *   wscale    D [N][ngw]: per-(row, group) scale; group of position p is p / Gw.
+ *   wsal      D [N][S_pad]: the salient weight columns, exact (fake_quant.py:363-365),
+ *             in salient_indices order, zero padded to S_pad (multiple of 64).
+ *   perm      int32 [Kp]: original column at packed position p, -1 for padding.
+ *   amap      int32 [Kp]: perm with salient columns replaced by -1 (GEMM A-operand map).
+ *   amap_fq   int32 [K]:  k, or -2 for salient k (in-place output-quant map).
+ *   nonsal    int32 [K-S]: non-salient columns, ascending (the x[:, mask] order).
+ */
+#ifndef SQMP_W4A4_H
+#define SQMP_W4A4_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SQMP_OK 0
+#define SQMP_EINVAL (-1)
+#define SQMP_EUNSUPPORTED (-2)
+#define SQMP_EHIP (-3)
+#define SQMP_EWORKSPACE (-4)
+
+enum sqmp_dtype { SQMP_F32 = 0, SQMP_F16 = 1, SQMP_BF16 = 2 };
+
+/* act_quant (fake_quant.py:246-256); PER_GROUP is the sorted variant the reference
+ * binds (:104-154); PER_GROUP_UNSORTED is the unwired :77-101 variant. */
+enum sqmp_act_mode {
+  SQMP_ACT_PER_TOKEN = 0,
+  SQMP_ACT_PER_TENSOR = 1,
+  SQMP_ACT_PER_GROUP = 2,
+  SQMP_ACT_PER_GROUP_UNSORTED = 3
+};
+
+/* weight_quant (fake_quant.py:348-361); PER_GROUP = sorted (:156-207). */
+enum sqmp_weight_mode {
+  SQMP_W_PER_CHANNEL = 0,
+  SQMP_W_PER_TENSOR = 1,
+  SQMP_W_PER_GROUP = 2,
+  SQMP_W_PER_GROUP_UNSORTED = 3,
+  SQMP_W_NONE = 4  /* no weight quantization: `codes` holds dense D [N][Kp] (a directly
+                      constructed W4A4Linear, fake_quant.py:227-235); GEMM n_bits = 0 */
+};
+
+/* Output of sqmp_quant_act. */
+enum sqmp_act_out {
+  SQMP_OUT_FP = 0,      /* out: D [M][Kp + S_pad]: x_hat at packed positions, exact
+                           salient x in the tail (operand of sqmp_gemm_fq) */
+  SQMP_OUT_I8 = 1,      /* out: int8 codes [M][Kp]; out_scale: fp32 [M] (the D scale);
+                           out_xs: D [M][S_pad] exact salient x (operand of sqmp_gemm_i8) */
+  SQMP_OUT_INPLACE = 2  /* fake-quantize `x` in place through amap_fq (output quant,
+                           fake_quant.py:308-316) */
+};
+
+/* Library identity. */
+const char* sqmp_version(void);
+const char* sqmp_status_string(int status);
+
+/* Host-only geometry of a packed weight (no GPU work).
+ * Replaces the implicit shapes of fake_quant.py:156-207 / :347-365. */
+int sqmp_weight_geometry(int K, int S, int wmode, int group_size, int* Kp, int* Gw,
+                         int* ngw, int* S_pad);
+
+size_t sqmp_pack_workspace_bytes(int N, int K);
+size_t sqmp_act_workspace_bytes(int M, int K);
+
+/* Offline weight quantization + packing: W4A4Linear.from_float (fake_quant.py:324-371)
+ * with quantize_weight_per_{channel,tensor}_absmax (:9-26), quantize_weight_per_group_
+ * absmax[_sort] (:29-53, :156-207) and the salient-column restore (:347, :363-365).
+ * `salient` (device int32 [S]) may be NULL when S == 0. */
+int sqmp_pack_weight(const void* w, int dtype, int N, int K, int wmode, int n_bits,
+                     int group_size, const int32_t* salient, int S, void* codes,
+                     void* wscale, void* wsal, int32_t* perm, int32_t* amap,
+                     int32_t* amap_fq, int32_t* nonsal, void* workspace, size_t ws_bytes,
+                     void* stream);
+
+/* The reference's dequantized `weight` buffer W_hat [N][K] in D (fake_quant.py:357-365). */
+int sqmp_dequant_weight(const void* codes, const void* wscale, const void* wsal,
+                        const int32_t* amap, const int32_t* salient, int dtype, int N,
+                        int K, int S, int n_bits, int Kp, int Gw, int ngw, int S_pad,
+                        void* w_hat, void* stream);
+
+/* W_hat in PACKED order, D [N][Kp] (salient and padding positions 0): the dense B operand
+ * (GEMM n_bits = 0) for group sizes finer than one 16-byte chunk of D (e.g. 4). */
+int sqmp_dequant_weight_packed(const void* codes, const void* wscale, int dtype, int N,
+                               int Kp, int Gw, int ngw, int n_bits, void* out, void* stream);
+
+/* Index maps for the identity column order (activation-only quantizers: the reference's
+ * quantize_activation_* primitives called directly, fake_quant.py:56-154). */
+int sqmp_build_maps(int K, const int32_t* salient, int S, int32_t* perm, int32_t* amap,
+                    int32_t* amap_fq, int32_t* nonsal, int Kp, void* stream);
+
+/* Runtime activation quantization: the pre-GEMM half of W4A4Linear.forward
+ * (fake_quant.py:291-304) with the bound act quantizer (:56-75, :77-101, :104-154).
+ * x: D [M][K] contiguous.  `amap` is the packed map (SQMP_OUT_FP / _I8, length Kp) or
+ * amap_fq (SQMP_OUT_INPLACE, length K).  `nonsal` lists the K-S columns the batch
+ * statistics run over. */
+int sqmp_quant_act(void* x, int dtype, int M, int K, int amode, int n_bits,
+                   int group_size, const int32_t* amap, int Kp, const int32_t* nonsal,
+                   const int32_t* salient, int S, int S_pad, int out_kind, void* out,
+                   void* out_scale, void* out_xs, void* workspace, size_t ws_bytes,
+                   void* stream);
+
+/* Faithful GEMM: y[M][N] = D( A[M][Kp+S_pad] . B^T + bias ), B decoded in-kernel from
+ * the int4/int8 codes as D(code * wscale) (bit-exact W_hat) for p < Kp and taken from
+ * wsal for the salient tail; D-MFMA with fp32 accumulation (fake_quant.py:306).
+ * n_bits = 4 / 8: codes are packed codes (group size a multiple of 8 elements, 4 for
+ * fp32); n_bits = 0: `codes` is a dense D [N][Kp] operand (SQMP_W_NONE or the output of
+ * sqmp_dequant_weight_packed), wscale unused. */
+int sqmp_gemm_fq(const void* a, const void* codes, const void* wscale, const void* wsal,
+                 const void* bias, void* y, int dtype, int M, int N, int Kp, int S_pad,
+                 int Gw, int ngw, int n_bits, void* stream);
+
+/* Integer GEMM (per_token / per_tensor activations): int8 act codes x int4 weight codes
+ * on the i8 MFMA, per-weight-group fp32 fold, per-row act scale, salient tail on the D
+ * MFMA, bias, one rounding to D.  Needs Gw % 64 == 0 and dtype fp16/bf16. */
+int sqmp_gemm_i8(const int8_t* a8, const float* ascale, const void* xs,
+                 const void* codes, const void* wscale, const void* wsal,
+                 const void* bias, void* y, int dtype, int M, int N, int Kp, int S_pad,
+                 int Gw, int ngw, int n_bits, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SQMP_W4A4_H */

@@ -1,0 +1,319 @@
+// Runtime activation quantization: the pre-GEMM half of W4A4Linear.forward
+// (/root/reference/smoothquant/fake_quant.py:291-304) and the output quantizer (:308-316).
+//
+// Reference semantics restated (x is [M][K] in D, S = salient columns, A = x[:, ~S]):
+//   per_token  (:56-64)   s[m]    = D(D(clamp(max_k |A[m,k]|, 1e-5)) / q_max)
+//   per_tensor (:67-75)   s       = same over the whole of A
+//   per_group  (:104-154) columns of A sorted ascending (stable) by their batch absmax
+//                         max_m |A[m,k]|; groups of G consecutive sorted columns;
+//                         s[m,g] per row and group.  (:77-101 unsorted variant: groups
+//                         of G consecutive non-salient columns.)
+//   x_hat = D(rne(D(x / s)) * s); salient columns pass through exactly (:297-301).
+//
+// Pipeline (per_group): colmax over M (1 kernel) -> stable rank of the K' non-salient
+// columns (1 kernel) -> this row kernel.  per_tensor: colmax -> row kernel.
+// per_token: row kernel only.
+//
+// Row kernel: persistent workgroups (grid-stride over rows).  Each workgroup builds its
+// LDS tables once (column -> group, output position -> (group, column)), then per row:
+// stage the row in LDS, per-(row, group) absmax with LDS atomics, scales, and writes the
+// output row in OUTPUT order with 16-B coalesced stores (gathering from the LDS row).
+#include "sqmp_internal.h"
+
+namespace sqmp {
+
+__device__ inline int fdiv_floor_a(int r, int G, float invG) {
+  int q = (int)((float)r * invG);
+  if ((q + 1) * G <= r) ++q;
+  if (q * G > r) --q;
+  return q;
+}
+
+constexpr uint32_t G_ZERO = 0xFFFFu;  // output position holds 0 (salient / padding)
+constexpr uint32_t G_PASS = 0xFFFEu;  // output position passes the input through
+
+enum { MODE_TOKEN = 0, MODE_TENSOR = 1, MODE_GROUP = 2 };
+
+template <class DT, int MODE, int OUT>
+__global__ __launch_bounds__(256) void quant_act_kernel(
+    typename DT::T* __restrict__ x, int M, int K, int q_max, int G, int nga,
+    const int32_t* __restrict__ amap, int P, const int32_t* __restrict__ nonsal, int Kn,
+    const int32_t* __restrict__ sal, int S, int S_pad,
+    const int32_t* __restrict__ rank_by_col, const uint32_t* __restrict__ cmax,
+    void* __restrict__ out, float* __restrict__ out_scale,
+    typename DT::T* __restrict__ out_xs) {
+  typedef typename DT::T T;
+  constexpr int VEC = 16 / sizeof(T);  // D elements per 16-B store
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_q[];
+  // LDS carve (all offsets 16-B aligned)
+  const int rowb = (int)round_up_dev(K * (int)sizeof(T), 16);
+  T* row = (T*)smem_q;                                        // K
+  uint32_t* ent = (uint32_t*)(smem_q + rowb);                 // P: (group << 16) | column
+  uint16_t* grp = (uint16_t*)(ent + P);                       // K: group of column
+  const int grpb = (int)round_up_dev(K * 2, 16);
+  uint32_t* gmax = (uint32_t*)((unsigned char*)grp + grpb);   // nga
+  float* sc = (float*)(gmax + nga);                           // nga
+  float* red = sc + nga;                                      // 16
+  const int tid = threadIdx.x;
+  const float invG = 1.0f / (float)G;
+
+  // ---- tables (once per workgroup)
+  for (int k = tid; k < K; k += 256) grp[k] = (uint16_t)G_ZERO;
+  __syncthreads();
+  for (int i = tid; i < Kn; i += 256) {
+    const int k = nonsal[i];
+    int g = 0;
+    if (MODE == MODE_GROUP) g = fdiv_floor_a(rank_by_col ? rank_by_col[k] : i, G, invG);
+    grp[k] = (uint16_t)g;
+  }
+  __syncthreads();
+  for (int p = tid; p < P; p += 256) {
+    const int k = amap[p];
+    uint32_t e;
+    if (k >= 0) e = ((uint32_t)grp[k] << 16) | (uint32_t)k;
+    else if (k == -2) e = (G_PASS << 16) | (uint32_t)p;
+    else e = G_ZERO << 16;
+    ent[p] = e;
+  }
+  float s_all = 0.f;
+  if (MODE == MODE_TENSOR) {
+    float m = 0.f;
+    for (int i = tid; i < Kn; i += 256) m = fmaxf(m, __uint_as_float(cmax[nonsal[i]]));
+    m = block_max(m, red);
+    s_all = group_scale<DT>(m, q_max);
+  }
+  __syncthreads();
+
+  const bool xvec = ((K * (int)sizeof(T)) % 16 == 0) && (((uintptr_t)x) % 16 == 0);
+  for (int m = blockIdx.x; m < M; m += gridDim.x) {
+    T* xr = x + (size_t)m * K;
+    // ---- stage the row
+    if (xvec) {
+      for (int c = tid; c < K / VEC; c += 256) ((u32x4*)row)[c] = ((const u32x4*)xr)[c];
+    } else {
+      for (int k = tid; k < K; k += 256) row[k] = xr[k];
+    }
+    if (MODE == MODE_GROUP)
+      for (int g = tid; g < nga; g += 256) gmax[g] = 0u;
+    __syncthreads();
+    // ---- statistics
+    float s_row = s_all;
+    if (MODE == MODE_TOKEN) {
+      float mx = 0.f;
+      for (int k = tid; k < K; k += 256)
+        if (grp[k] != G_ZERO) mx = fmaxf(mx, fabsf(DT::to_f(row[k])));
+      mx = block_max(mx, red);
+      s_row = group_scale<DT>(mx, q_max);
+    } else if (MODE == MODE_GROUP) {
+      for (int k = tid; k < K; k += 256) {
+        const uint32_t g = grp[k];
+        if (g != G_ZERO) {
+          const float v = fabsf(DT::to_f(row[k]));
+          if (v > 0.f) atomicMax(&gmax[g], __float_as_uint(v));
+        }
+      }
+      __syncthreads();
+      for (int g = tid; g < nga; g += 256) sc[g] = group_scale<DT>(__uint_as_float(gmax[g]), q_max);
+      __syncthreads();
+    }
+    // ---- outputs, in output order
+    if (OUT == SQMP_OUT_I8) {
+      int8_t* o = (int8_t*)out + (size_t)m * P;
+      for (int c = tid; c < P / 16; c += 256) {
+        uint32_t wv[4];
+#pragma unroll
+        for (int w4 = 0; w4 < 4; ++w4) {
+          uint32_t word = 0;
+#pragma unroll
+          for (int e4 = 0; e4 < 4; ++e4) {
+            const uint32_t e = ent[c * 16 + w4 * 4 + e4];
+            int code = 0;
+            if ((e >> 16) != G_ZERO) code = (int)quant_code<DT>(DT::to_f(row[e & 0xFFFFu]), s_row);
+            word |= ((uint32_t)code & 0xFFu) << (8 * e4);
+          }
+          wv[w4] = word;
+        }
+        ((u32x4*)o)[c] = u32x4{wv[0], wv[1], wv[2], wv[3]};
+      }
+      if (tid == 0) out_scale[m] = s_row;
+      T* xs = out_xs + (size_t)m * S_pad;
+      for (int j = tid; j < S_pad; j += 256) xs[j] = j < S ? row[sal[j]] : DT::from_f(0.f);
+    } else if (OUT == SQMP_OUT_FP) {
+      const int W = P + S_pad;
+      T* o = (T*)out + (size_t)m * W;
+      for (int c = tid; c < W / VEC; c += 256) {
+        T v[VEC];
+#pragma unroll
+        for (int e8 = 0; e8 < VEC; ++e8) {
+          const int p = c * VEC + e8;
+          float r = 0.f;
+          if (p < P) {
+            const uint32_t e = ent[p];
+            const uint32_t g = e >> 16;
+            if (g != G_ZERO) {
+              const float s = MODE == MODE_GROUP ? sc[g] : s_row;
+              const float t = DT::to_f(row[e & 0xFFFFu]);
+              r = __builtin_rintf(rd<DT>(t / s)) * s;  // x_hat, rounded to D below
+            }
+          } else if (p - P < S) {
+            r = DT::to_f(row[sal[p - P]]);
+          }
+          v[e8] = DT::from_f(r);
+        }
+        ((u32x4*)o)[c] = *(const u32x4*)v;
+      }
+    } else {  // SQMP_OUT_INPLACE: P == K, write back through amap_fq
+      if (xvec) {
+        for (int c = tid; c < K / VEC; c += 256) {
+          T v[VEC];
+#pragma unroll
+          for (int e8 = 0; e8 < VEC; ++e8) {
+            const int p = c * VEC + e8;
+            const uint32_t e = ent[p];
+            const uint32_t g = e >> 16;
+            if (g == G_PASS || g == G_ZERO) {
+              v[e8] = row[p];
+            } else {
+              const float s = MODE == MODE_GROUP ? sc[g] : s_row;
+              const float t = DT::to_f(row[e & 0xFFFFu]);
+              v[e8] = DT::from_f(__builtin_rintf(rd<DT>(t / s)) * s);
+            }
+          }
+          ((u32x4*)xr)[c] = *(const u32x4*)v;
+        }
+      } else {
+        for (int p = tid; p < K; p += 256) {
+          const uint32_t e = ent[p];
+          const uint32_t g = e >> 16;
+          if (g == G_PASS || g == G_ZERO) continue;
+          const float s = MODE == MODE_GROUP ? sc[g] : s_row;
+          const float t = DT::to_f(row[e & 0xFFFFu]);
+          xr[p] = DT::from_f(__builtin_rintf(rd<DT>(t / s)) * s);
+        }
+      }
+    }
+    __syncthreads();  // row / gmax reuse
+  }
+}
+
+static size_t quant_lds_bytes(int K, int P, int nga, int esize) {
+  return (size_t)round_up((long)K * esize, 16) + 4 * (size_t)P + (size_t)round_up(2L * K, 16) +
+         8 * (size_t)nga + 64;
+}
+
+template <class DT, int MODE, int OUT>
+static int quant_launch(void* x, int M, int K, int q_max, int G, int nga, const int32_t* amap,
+                        int P, const int32_t* nonsal, int Kn, const int32_t* sal, int S,
+                        int S_pad, const int32_t* rank, const uint32_t* cmax, void* out,
+                        void* out_scale, void* out_xs, hipStream_t s) {
+  typedef typename DT::T T;
+  const size_t lds = quant_lds_bytes(K, P, nga, sizeof(T));
+  if (lds > 160 * 1024) return SQMP_EUNSUPPORTED;
+  SQMP_HIP_CHECK(hipFuncSetAttribute((const void*)quant_act_kernel<DT, MODE, OUT>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  int per_cu = (int)((160 * 1024) / lds);
+  per_cu = per_cu < 1 ? 1 : (per_cu > 8 ? 8 : per_cu);
+  int grid = 256 * per_cu;
+  if (grid > M) grid = M;
+  quant_act_kernel<DT, MODE, OUT><<<dim3(grid), dim3(256), lds, s>>>(
+      (T*)x, M, K, q_max, G, nga, amap, P, nonsal, Kn, sal, S, S_pad, rank, cmax, out,
+      (float*)out_scale, (T*)out_xs);
+  SQMP_LAUNCH_CHECK();
+  return SQMP_OK;
+}
+
+template <class DT>
+static int quant_dispatch(void* x, int M, int K, int amode, int q_max, int G, int nga,
+                          const int32_t* amap, int P, const int32_t* nonsal, int Kn,
+                          const int32_t* sal, int S, int S_pad, const int32_t* rank,
+                          const uint32_t* cmax, int out_kind, void* out, void* out_scale,
+                          void* out_xs, hipStream_t s) {
+#define SQMP_Q(MODE, OUTK)                                                                  \
+  quant_launch<DT, MODE, OUTK>(x, M, K, q_max, G, nga, amap, P, nonsal, Kn, sal, S, S_pad, \
+                               rank, cmax, out, out_scale, out_xs, s)
+  const int mode = amode == SQMP_ACT_PER_TOKEN    ? MODE_TOKEN
+                   : amode == SQMP_ACT_PER_TENSOR ? MODE_TENSOR
+                                                  : MODE_GROUP;
+  if (out_kind == SQMP_OUT_FP) {
+    if (mode == MODE_TOKEN) return SQMP_Q(MODE_TOKEN, SQMP_OUT_FP);
+    if (mode == MODE_TENSOR) return SQMP_Q(MODE_TENSOR, SQMP_OUT_FP);
+    return SQMP_Q(MODE_GROUP, SQMP_OUT_FP);
+  }
+  if (out_kind == SQMP_OUT_I8) {
+    if (mode == MODE_TOKEN) return SQMP_Q(MODE_TOKEN, SQMP_OUT_I8);
+    if (mode == MODE_TENSOR) return SQMP_Q(MODE_TENSOR, SQMP_OUT_I8);
+    return SQMP_EUNSUPPORTED;  // per-group act scales do not factor out of an int GEMM
+  }
+  if (mode == MODE_TOKEN) return SQMP_Q(MODE_TOKEN, SQMP_OUT_INPLACE);
+  if (mode == MODE_TENSOR) return SQMP_Q(MODE_TENSOR, SQMP_OUT_INPLACE);
+  return SQMP_Q(MODE_GROUP, SQMP_OUT_INPLACE);
+#undef SQMP_Q
+}
+
+}  // namespace sqmp
+
+using namespace sqmp;
+
+extern "C" size_t sqmp_act_workspace_bytes(int M, int K) {
+  (void)M;
+  return 2 * sizeof(uint32_t) * (size_t)round_up(K > 0 ? K : 1, 64);
+}
+
+extern "C" int sqmp_quant_act(void* x, int dtype, int M, int K, int amode, int n_bits,
+                              int group_size, const int32_t* amap, int Kp,
+                              const int32_t* nonsal, const int32_t* salient, int S, int S_pad,
+                              int out_kind, void* out, void* out_scale, void* out_xs,
+                              void* workspace, size_t ws_bytes, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype < SQMP_F32 || dtype > SQMP_BF16 || M < 0 || K <= 0 || K > 65000) return SQMP_EINVAL;
+  if (amode < SQMP_ACT_PER_TOKEN || amode > SQMP_ACT_PER_GROUP_UNSORTED) return SQMP_EINVAL;
+  if (n_bits < 2 || n_bits > 8) return SQMP_EUNSUPPORTED;
+  if (S < 0 || S > K || !x || !amap || (K - S > 0 && !nonsal)) return SQMP_EINVAL;
+  if (out_kind == SQMP_OUT_INPLACE) {
+    if (Kp != K) return SQMP_EINVAL;
+  } else if (out_kind == SQMP_OUT_FP || out_kind == SQMP_OUT_I8) {
+    if (Kp < K || Kp % 128 != 0 || S_pad < S || S_pad % 64 != 0 || !out) return SQMP_EINVAL;
+    if (S > 0 && !salient) return SQMP_EINVAL;
+    if (out_kind == SQMP_OUT_I8 && (!out_scale || (S_pad > 0 && !out_xs))) return SQMP_EINVAL;
+    if (out_kind == SQMP_OUT_I8 && n_bits > 8) return SQMP_EUNSUPPORTED;
+  } else {
+    return SQMP_EINVAL;
+  }
+  const bool group = amode == SQMP_ACT_PER_GROUP || amode == SQMP_ACT_PER_GROUP_UNSORTED;
+  if (group && (group_size <= 0 || group_size > 65000)) return SQMP_EINVAL;
+  if (M == 0) return SQMP_OK;
+  if (ws_bytes < sqmp_act_workspace_bytes(M, K) || !workspace) return SQMP_EWORKSPACE;
+  uint32_t* cmax = (uint32_t*)workspace;
+  int32_t* rank = (int32_t*)((char*)workspace + sizeof(uint32_t) * round_up(K, 64));
+  const int Kn = K - S;
+  if (Kn == 0) {
+    // every channel salient: the reference skips quantization entirely (:299)
+    if (out_kind == SQMP_OUT_INPLACE) return SQMP_OK;
+  }
+  int st;
+  if (amode == SQMP_ACT_PER_TENSOR || amode == SQMP_ACT_PER_GROUP) {
+    st = launch_colmax(x, dtype, M, K, cmax, s);
+    if (st) return st;
+  }
+  if (amode == SQMP_ACT_PER_GROUP) {
+    st = launch_rank(cmax, nonsal, Kn, K, rank, s);
+    if (st) return st;
+  }
+  const int q_max = (1 << (n_bits - 1)) - 1;
+  const int nga = group ? (Kn > 0 ? cdiv(Kn, group_size) : 1) : 1;
+  const int32_t* rk = amode == SQMP_ACT_PER_GROUP ? rank : nullptr;
+  switch (dtype) {
+    case SQMP_F32:
+      return quant_dispatch<F32>(x, M, K, amode, q_max, group_size, nga, amap, Kp, nonsal,
+                                 Kn, salient, S, S_pad, rk, cmax, out_kind, out, out_scale,
+                                 out_xs, s);
+    case SQMP_F16:
+      return quant_dispatch<F16>(x, M, K, amode, q_max, group_size, nga, amap, Kp, nonsal,
+                                 Kn, salient, S, S_pad, rk, cmax, out_kind, out, out_scale,
+                                 out_xs, s);
+    default:
+      return quant_dispatch<BF16>(x, M, K, amode, q_max, group_size, nga, amap, Kp, nonsal,
+                                  Kn, salient, S, S_pad, rk, cmax, out_kind, out, out_scale,
+                                  out_xs, s);
+  }
+}

@@ -1,0 +1,97 @@
+// Shared device helpers for the W4A4 mixed-precision linear on MI355X (gfx950 / CDNA4).
+//
+// Numerics contract (mirrors /root/reference/smoothquant/fake_quant.py):
+//   * D is the model dtype (fp32 / fp16 / bf16).  Every elementwise quantizer op is
+//     computed in fp32 and rounded to D (PyTorch's opmath rule), round() is
+//     round-half-to-even, scales are `D(D(clamp(absmax, 1e-5)) / q_max)`.
+//   * Column sorts are stable ascending (ties -> lower column index first).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/sqmp_w4a4.h"
+
+namespace sqmp {
+
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// ---------------------------------------------------------------- dtype traits
+struct F32 {
+  typedef float T;
+  static constexpr int id = SQMP_F32;
+  __device__ static inline float to_f(T v) { return v; }
+  __device__ static inline T from_f(float v) { return v; }
+};
+struct F16 {
+  typedef _Float16 T;
+  static constexpr int id = SQMP_F16;
+  __device__ static inline float to_f(T v) { return (float)v; }
+  __device__ static inline T from_f(float v) { return (T)v; }  // RNE (v_cvt_f16_f32)
+};
+struct BF16 {
+  typedef __bf16 T;
+  static constexpr int id = SQMP_BF16;
+  __device__ static inline float to_f(T v) { return (float)v; }
+  __device__ static inline T from_f(float v) { return (T)v; }  // RNE (v_cvt_pk_bf16_f32)
+};
+
+// Round an fp32 value to D and widen it back (the "rounded to D" step).
+template <class DT>
+__device__ inline float rd(float v) {
+  return DT::to_f(DT::from_f(v));
+}
+
+// clamp(min=1e-5) then div by q_max, both rounded to D (fake_quant.py:14, 62, 139, 190).
+template <class DT>
+__device__ inline float group_scale(float absmax_d, int q_max) {
+  const float lo = rd<DT>(1e-5f);
+  float c = absmax_d < lo ? lo : absmax_d;
+  return rd<DT>(c / (float)q_max);
+}
+
+// code = round_half_even(D(t / s)) (fake_quant.py:15, 63, 142, 193).
+template <class DT>
+__device__ inline float quant_code(float t, float s) {
+  return __builtin_rintf(rd<DT>(t / s));
+}
+
+// ---------------------------------------------------------------- small utils
+__device__ inline float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+__device__ inline float block_max(float v, float* red /* >= 16 floats of LDS */) {
+  v = wave_max(v);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int nw = (blockDim.x + 63) >> 6;
+  __syncthreads();
+  if (lane == 0) red[wid] = v;
+  __syncthreads();
+  float r = 0.f;
+  for (int i = 0; i < nw; ++i) r = fmaxf(r, red[i]);
+  return r;
+}
+
+__host__ __device__ inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
+__host__ __device__ inline long round_up(long a, long b) { return (a + b - 1) / b * b; }
+__device__ inline long round_up_dev(long a, long b) { return (a + b - 1) / b * b; }
+
+}  // namespace sqmp
+
+#define SQMP_HIP_CHECK(expr)                        \
+  do {                                              \
+    hipError_t _e = (expr);                         \
+    if (_e != hipSuccess) return SQMP_EHIP;         \
+  } while (0)
+
+#define SQMP_LAUNCH_CHECK()                         \
+  do {                                              \
+    hipError_t _e = hipGetLastError();              \
+    if (_e != hipSuccess) return SQMP_EHIP;         \
+  } while (0)

@@ -1,0 +1,182 @@
+// Column statistics shared by the weight packer and the activation quantizer:
+//   * column absmax over all rows   (fake_quant.py:113 `t.abs().max(dim=0)`, :164 for W)
+//   * stable ascending column rank  (fake_quant.py:116 / :167 `torch.argsort(col_max)`,
+//                                    pinned to stable=True; ties -> lower index first)
+//   * index maps of the packed K axis (salient split of fake_quant.py:291-301, :347-365)
+#include "sqmp_internal.h"
+
+namespace sqmp {
+
+// ------------------------------------------------------------------ column absmax
+// Block = 4 waves; a lane owns VEC consecutive columns (one 16-B load per row), the four
+// waves split the block's row chunk, partial maxima meet in LDS, then one global
+// atomicMax per column per block.
+template <class DT, int VEC>
+__global__ __launch_bounds__(256) void colmax_kernel(const typename DT::T* __restrict__ x,
+                                                     int R, int C, int rows_per_block,
+                                                     uint32_t* __restrict__ cmax) {
+  typedef typename DT::T T;
+  __shared__ float red[4][64 * VEC];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int c0 = (blockIdx.x * 64 + lane) * VEC;
+  const int r0 = blockIdx.y * rows_per_block;
+  const int r1 = min(R, r0 + rows_per_block);
+  float m[VEC];
+#pragma unroll
+  for (int i = 0; i < VEC; ++i) m[i] = 0.f;
+  if (c0 + VEC <= C && VEC > 1) {
+    for (int r = r0 + wid; r < r1; r += 4) {
+      const u32x4 raw = *(const u32x4*)(x + (size_t)r * C + c0);
+      const T* v = (const T*)&raw;
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) m[i] = fmaxf(m[i], fabsf(DT::to_f(v[i])));
+    }
+  } else if (c0 < C) {
+    for (int r = r0 + wid; r < r1; r += 4)
+#pragma unroll
+      for (int i = 0; i < VEC; ++i)
+        if (c0 + i < C) m[i] = fmaxf(m[i], fabsf(DT::to_f(x[(size_t)r * C + c0 + i])));
+  }
+#pragma unroll
+  for (int i = 0; i < VEC; ++i) red[wid][lane * VEC + i] = m[i];
+  __syncthreads();
+  for (int t = threadIdx.x; t < 64 * VEC; t += 256) {
+    const float v = fmaxf(fmaxf(red[0][t], red[1][t]), fmaxf(red[2][t], red[3][t]));
+    const int c = blockIdx.x * 64 * VEC + t;
+    if (c < C && v > 0.f) atomicMax(&cmax[c], __float_as_uint(v));
+  }
+}
+
+template <class DT>
+static void colmax_launch(const void* x, int R, int C, uint32_t* cmax, hipStream_t s) {
+  typedef typename DT::T T;
+  constexpr int VEC = 16 / sizeof(T);
+  const bool vec_ok = ((C * sizeof(T)) % 16 == 0) && (((uintptr_t)x) % 16 == 0);
+  int rows_per_block = 128;
+  const int cblocks_v = cdiv(C, 64 * VEC);
+  // keep >= ~1024 blocks in flight when R is large, fewer row passes when R is small
+  while (rows_per_block > 16 && (long)cblocks_v * cdiv(R, rows_per_block) < 1024)
+    rows_per_block >>= 1;
+  dim3 block(256);
+  if (vec_ok) {
+    dim3 grid(cblocks_v, cdiv(R, rows_per_block));
+    colmax_kernel<DT, VEC><<<grid, block, 0, s>>>((const T*)x, R, C, rows_per_block, cmax);
+  } else {
+    dim3 grid(cdiv(C, 64), cdiv(R, rows_per_block));
+    colmax_kernel<DT, 1><<<grid, block, 0, s>>>((const T*)x, R, C, rows_per_block, cmax);
+  }
+}
+
+int launch_colmax(const void* x, int dtype, int R, int C, uint32_t* cmax, hipStream_t s) {
+  SQMP_HIP_CHECK(hipMemsetAsync(cmax, 0, sizeof(uint32_t) * (size_t)C, s));
+  if (R <= 0 || C <= 0) return SQMP_OK;
+  switch (dtype) {
+    case SQMP_F32: colmax_launch<F32>(x, R, C, cmax, s); break;
+    case SQMP_F16: colmax_launch<F16>(x, R, C, cmax, s); break;
+    case SQMP_BF16: colmax_launch<BF16>(x, R, C, cmax, s); break;
+    default: return SQMP_EINVAL;
+  }
+  SQMP_LAUNCH_CHECK();
+  return SQMP_OK;
+}
+
+// ------------------------------------------------------------------ stable rank
+// 2-D grid of (256 owners) x (1024 competitors); each owner counts competitors with a
+// smaller composite key (value bits << 32 | list index) and adds its partial count.
+// O(L^2) compares, fully parallel, deterministic and stable by construction.
+constexpr int RANK_TILE = 1024;
+
+__global__ __launch_bounds__(256) void rank_kernel(const uint32_t* __restrict__ cmax,
+                                                   const int32_t* __restrict__ cols, int L,
+                                                   int32_t* __restrict__ rank_by_col) {
+  __shared__ uint64_t keys[RANK_TILE];
+  const int j0 = blockIdx.y * RANK_TILE;
+  const int jn = min(RANK_TILE, L - j0);
+  for (int t = threadIdx.x; t < RANK_TILE; t += 256) {
+    const int j = j0 + t;
+    uint64_t k = ~0ull;  // sentinel: never smaller than a real key
+    if (t < jn) {
+      const int c = cols ? cols[j] : j;
+      k = ((uint64_t)cmax[c] << 32) | (uint32_t)j;
+    }
+    keys[t] = k;
+  }
+  __syncthreads();
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= L) return;
+  const int ci = cols ? cols[i] : i;
+  const uint64_t mine = ((uint64_t)cmax[ci] << 32) | (uint32_t)i;
+  int cnt = 0;
+#pragma unroll 8
+  for (int t = 0; t < RANK_TILE; ++t) cnt += keys[t] < mine ? 1 : 0;
+  if (cnt) atomicAdd(&rank_by_col[ci], cnt);
+}
+
+int launch_rank(const uint32_t* cmax, const int32_t* cols, int L, int C,
+                int32_t* rank_by_col, hipStream_t s) {
+  // rank_by_col is indexed by column: clear the whole column range the list can touch.
+  SQMP_HIP_CHECK(hipMemsetAsync(rank_by_col, 0, sizeof(int32_t) * (size_t)C, s));
+  if (L <= 0) return SQMP_OK;
+  dim3 grid(cdiv(L, 256), cdiv(L, RANK_TILE));
+  rank_kernel<<<grid, dim3(256), 0, s>>>(cmax, cols, L, rank_by_col);
+  SQMP_LAUNCH_CHECK();
+  return SQMP_OK;
+}
+
+// ------------------------------------------------------------------ index maps
+// One workgroup.  flag[k] marks salient columns; the non-salient list is an ordered
+// compaction (block-wide exclusive scan over per-thread chunk counts).
+__global__ __launch_bounds__(1024) void build_maps_kernel(
+    int K, int Kp, const int32_t* __restrict__ rank_by_col, const int32_t* __restrict__ sal,
+    int S, int32_t* __restrict__ perm, int32_t* __restrict__ amap,
+    int32_t* __restrict__ amap_fq, int32_t* __restrict__ nonsal) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_maps[];
+  int* scan = (int*)smem_maps;                      // 1024 ints
+  unsigned char* flag = smem_maps + 1024 * sizeof(int);  // K bytes
+  const int t = threadIdx.x;
+  for (int k = t; k < K; k += 1024) flag[k] = 0;
+  __syncthreads();
+  for (int j = t; j < S; j += 1024) flag[sal[j]] = 1;
+  __syncthreads();
+  for (int k = t; k < K; k += 1024) {
+    const int p = rank_by_col ? rank_by_col[k] : k;
+    perm[p] = k;
+    amap[p] = flag[k] ? -1 : k;
+    amap_fq[k] = flag[k] ? -2 : k;
+  }
+  for (int p = K + t; p < Kp; p += 1024) {
+    perm[p] = -1;
+    amap[p] = -1;
+  }
+  // ordered compaction of the non-salient columns
+  const int chunk = (K + 1023) / 1024;
+  const int kb = t * chunk, ke = min(K, kb + chunk);
+  int cnt = 0;
+  for (int k = kb; k < ke; ++k) cnt += flag[k] ? 0 : 1;
+  scan[t] = cnt;
+  __syncthreads();
+  for (int off = 1; off < 1024; off <<= 1) {
+    const int v = t >= off ? scan[t - off] : 0;
+    __syncthreads();
+    scan[t] += v;
+    __syncthreads();
+  }
+  int pos = scan[t] - cnt;
+  for (int k = kb; k < ke; ++k)
+    if (!flag[k]) nonsal[pos++] = k;
+}
+
+int launch_build_maps(int K, int Kp, const int32_t* rank_by_col, const int32_t* salient,
+                      int S, int32_t* perm, int32_t* amap, int32_t* amap_fq,
+                      int32_t* nonsal, hipStream_t s) {
+  const size_t lds = 1024 * sizeof(int) + (size_t)round_up(K, 16);
+  if (lds > 160 * 1024) return SQMP_EUNSUPPORTED;
+  SQMP_HIP_CHECK(hipFuncSetAttribute((const void*)build_maps_kernel,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  build_maps_kernel<<<dim3(1), dim3(1024), lds, s>>>(K, Kp, rank_by_col, salient, S, perm,
+                                                      amap, amap_fq, nonsal);
+  SQMP_LAUNCH_CHECK();
+  return SQMP_OK;
+}
+
+}  // namespace sqmp

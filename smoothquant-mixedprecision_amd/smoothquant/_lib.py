@@ -1,0 +1,87 @@
+"""ctypes binding of libsqmp_w4a4.so (the C ABI declared in include/sqmp_w4a4.h).
+
+The library is built in-tree by `smoothquant-mixedprecision_amd/build_ext.py` (or
+`__graft_entry__.build()`).  There is deliberately no fallback: if the library cannot be
+loaded, every quantized op raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libsqmp_w4a4.so")
+
+SQMP_OK, SQMP_EINVAL, SQMP_EUNSUPPORTED, SQMP_EHIP, SQMP_EWORKSPACE = 0, -1, -2, -3, -4
+
+F32, F16, BF16 = 0, 1, 2
+ACT_PER_TOKEN, ACT_PER_TENSOR, ACT_PER_GROUP, ACT_PER_GROUP_UNSORTED = 0, 1, 2, 3
+W_PER_CHANNEL, W_PER_TENSOR, W_PER_GROUP, W_PER_GROUP_UNSORTED, W_NONE = 0, 1, 2, 3, 4
+OUT_FP, OUT_I8, OUT_INPLACE = 0, 1, 2
+
+_vp, _i, _sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t
+_ip = ctypes.POINTER(ctypes.c_int)
+
+# name -> (restype, argtypes); the authoritative list of exported symbols
+SIGNATURES = {
+    "sqmp_version": (ctypes.c_char_p, []),
+    "sqmp_status_string": (ctypes.c_char_p, [_i]),
+    "sqmp_weight_geometry": (_i, [_i, _i, _i, _i, _ip, _ip, _ip, _ip]),
+    "sqmp_pack_workspace_bytes": (_sz, [_i, _i]),
+    "sqmp_act_workspace_bytes": (_sz, [_i, _i]),
+    "sqmp_pack_weight": (_i, [_vp, _i, _i, _i, _i, _i, _i, _vp, _i, _vp, _vp, _vp, _vp, _vp,
+                              _vp, _vp, _vp, _sz, _vp]),
+    "sqmp_dequant_weight": (_i, [_vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _i,
+                                 _vp, _vp]),
+    "sqmp_dequant_weight_packed": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _i, _vp, _vp]),
+    "sqmp_build_maps": (_i, [_i, _vp, _i, _vp, _vp, _vp, _vp, _i, _vp]),
+    "sqmp_quant_act": (_i, [_vp, _i, _i, _i, _i, _i, _i, _vp, _i, _vp, _vp, _i, _i, _i, _vp,
+                            _vp, _vp, _vp, _sz, _vp]),
+    "sqmp_gemm_fq": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _vp]),
+    "sqmp_gemm_i8": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i,
+                          _i, _vp]),
+}
+
+_lock = threading.Lock()
+_lib = None
+
+
+class SqmpError(RuntimeError):
+    """A HIP runtime failure inside libsqmp_w4a4."""
+
+
+def load():
+    """Load (once) and return the ctypes library; raise RuntimeError if it is missing."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                f"libsqmp_w4a4.so not found at {LIB_PATH}: build it with "
+                "`python smoothquant-mixedprecision_amd/build_ext.py` (hipcc, gfx950). "
+                "The W4A4 operator has no CPU fallback.")
+        lib = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+        return lib
+
+
+def check(status: int, what: str):
+    """Map a C status to the reference's exception types (ValueError for bad arguments /
+    unsupported modes, RuntimeError for device failures)."""
+    if status == SQMP_OK:
+        return
+    msg = load().sqmp_status_string(status).decode()
+    if status in (SQMP_EINVAL, SQMP_EUNSUPPORTED):
+        raise ValueError(f"{what}: {msg} (status {status})")
+    raise SqmpError(f"{what}: {msg} (status {status})")
+
+
+def version() -> str:
+    return load().sqmp_version().decode()

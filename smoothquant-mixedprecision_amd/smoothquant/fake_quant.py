@@ -1,0 +1,433 @@
+"""Drop-in `smoothquant.fake_quant` for MI355X: W4A4Linear + the model-surgery entry points.
+
+Same import path, names, constructor/forward signatures, attributes and error types as
+/root/reference/smoothquant/fake_quant.py, but the operator is real: weights are packed
+once to int4 (or int8) codes + per-group scales + an exact salient slice, and forward
+runs the HIP kernels of libsqmp_w4a4 (activation quantization + MFMA GEMM with the
+salient FP side-GEMM in the same workgroup).  There is no CPU path: a W4A4Linear whose
+tensors are not on a ROCm device raises.
+
+Reference map (file:line in fake_quant.py):
+  quantizer primitives       9-207   -> quantize_* below (GPU, same in-place semantics)
+  W4A4Linear.__init__      210-270   -> W4A4Linear.__init__
+  W4A4Linear.forward       279-322   -> W4A4Linear.forward
+  W4A4Linear.from_float    324-371   -> W4A4Linear.from_float
+  quantize_opt/llama_like/mixtral/falcon/model  377-799 -> same names
+"""
+from __future__ import annotations
+
+from functools import partial
+from typing import Optional
+
+import torch
+from torch import nn
+
+from . import ops
+from .ops import PackedWeight
+
+_ACT = ("per_token", "per_tensor", "per_group")
+_WEIGHT = ("per_channel", "per_tensor", "per_group")
+
+
+# ----------------------------------------------------------------------------------------
+# quantizer primitives (fake_quant.py:9-207) -- GPU implementations, reference semantics
+# ----------------------------------------------------------------------------------------
+def _fq_act(t: torch.Tensor, mode: str, n_bits: int, group_size: int = 128) -> torch.Tensor:
+    t2 = t.view(-1, t.shape[-1])
+    C = t2.shape[1]
+    _, _, amap_fq, nonsal = ops.build_maps(C, None, t2.device)
+    return ops.fake_quant_inplace(t2, mode, n_bits, group_size, amap_fq, nonsal, 0)
+
+
+@torch.no_grad()
+def quantize_activation_per_token_absmax(t, n_bits):
+    """fake_quant.py:56-64: in place on `t`, returns the 2-D view."""
+    return _fq_act(t, "per_token", n_bits)
+
+
+@torch.no_grad()
+def quantize_activation_per_tensor_absmax(t, n_bits):
+    """fake_quant.py:67-75: in place on `t`, returns the 2-D view."""
+    return _fq_act(t, "per_tensor", n_bits)
+
+
+@torch.no_grad()
+def quantize_activation_per_group_absmax(t, n_bits, group_size=128):
+    """fake_quant.py:77-101 (unsorted groups): returns a new tensor of t's shape."""
+    out = t.contiguous().clone()
+    _fq_act(out, "per_group_unsorted", n_bits, group_size)
+    return out.view(t.shape)
+
+
+@torch.no_grad()
+def quantize_activation_per_group_absmax_sort(t, n_bits, group_size=128):
+    """fake_quant.py:104-154 (sorted groups): returns a new tensor of t's shape."""
+    out = t.contiguous().clone()
+    _fq_act(out, "per_group", n_bits, group_size)
+    return out.view(t.shape)
+
+
+def _fq_weight(w: torch.Tensor, mode: str, n_bits: int, group_size: int) -> torch.Tensor:
+    return ops.dequant_weight(ops.pack_weight(w, mode, n_bits, group_size, None))
+
+
+@torch.no_grad()
+def quantize_weight_per_channel_absmax(w, n_bits):
+    """fake_quant.py:9-16: in place on `w`, returns `w`."""
+    w.copy_(_fq_weight(w, "per_channel", n_bits, 128))
+    return w
+
+
+@torch.no_grad()
+def quantize_weight_per_tensor_absmax(w, n_bits):
+    """fake_quant.py:19-26: in place on `w`, returns `w`."""
+    w.copy_(_fq_weight(w, "per_tensor", n_bits, 128))
+    return w
+
+
+@torch.no_grad()
+def quantize_weight_per_group_absmax(w, n_bits, group_size=128):
+    """fake_quant.py:29-53 (unsorted groups): returns a new tensor."""
+    return _fq_weight(w, "per_group_unsorted", n_bits, group_size)
+
+
+@torch.no_grad()
+def quantize_weight_per_group_absmax_sort(w, n_bits, group_size=128):
+    """fake_quant.py:156-207 (sorted groups): returns a new tensor."""
+    return _fq_weight(w, "per_group", n_bits, group_size)
+
+
+_ACT_FNS = {"per_token": quantize_activation_per_token_absmax,
+            "per_tensor": quantize_activation_per_tensor_absmax,
+            "per_group": quantize_activation_per_group_absmax_sort}
+
+_PACKED_BUFFERS = ("w_codes", "w_scale", "w_salient", "w_perm", "w_amap", "w_amap_fq",
+                   "w_nonsal", "salient_i32", "w_dense", "out_amap_fq", "out_nonsal")
+
+
+# ----------------------------------------------------------------------------------------
+# W4A4Linear (fake_quant.py:209-374)
+# ----------------------------------------------------------------------------------------
+class W4A4Linear(nn.Module):
+    """Mixed-precision W4A4 linear: salient input channels in D, the rest int4/int8.
+
+    Forward kernels (chosen per layer, see `kernel`):
+      "i8"  per_token / per_tensor activations: int8 act codes x int4 weight codes on the
+            i8 MFMA with per-group fp32 folds (exact scale factorisation).
+      "fq"  every act mode: dequantized activations x in-kernel-decoded weights on the D
+            MFMA (bit-exact operands; the reference's numerics up to accumulation order).
+    """
+
+    def __init__(self, in_features, out_features, bias=True, act_quant="per_token",
+                 quantize_output=False, importance=None, salient_prop=0, quant_bits=4,
+                 group_size=128):
+        super().__init__()
+        self.in_features = in_features
+        self.out_features = out_features
+        self.group_size = group_size
+        self.quant_bits = quant_bits
+        if act_quant not in _ACT:
+            raise ValueError(f"Invalid act_quant: {act_quant}")     # fake_quant.py:256
+        self.act_quant_name = act_quant
+        self.act_quant = partial(_ACT_FNS[act_quant], n_bits=quant_bits,
+                                 **({"group_size": group_size} if act_quant == "per_group" else {}))
+        if quantize_output:
+            self.output_quant_name = self.act_quant_name
+            self.output_quant = self.act_quant
+        else:
+            self.output_quant_name = "None"
+            self.output_quant = lambda x: x
+        self.salient_indices = None
+        if importance is not None and salient_prop > 0:             # :265-270
+            sorted_idx = torch.argsort(importance, descending=True, stable=True)
+            num_salient = max(1, int(salient_prop * len(sorted_idx)))
+            self.salient_indices = sorted_idx[:num_salient]
+        self.weight_quant_name = "None"
+        self.kernel = "auto"
+        self._meta = None
+        for name in _PACKED_BUFFERS:
+            self.register_buffer(name, None)
+        if bias:
+            self.register_buffer("bias", torch.zeros((1, out_features), dtype=torch.float16))
+        else:
+            self.register_buffer("bias", None)
+        # The reference starts from an unquantized random fp16 weight (:227-235); a directly
+        # constructed module draws it on the GPU and packs it as a dense operand on first use.
+        self._random_init = True
+
+    # ------------------------------------------------------------------ packing
+    def _install(self, pw: PackedWeight, weight_quant: str):
+        self.w_codes = pw.codes
+        self.w_scale = pw.wscale
+        self.w_salient = pw.wsal
+        self.w_perm = pw.perm
+        self.w_amap = pw.amap
+        self.w_amap_fq = pw.amap_fq
+        self.w_nonsal = pw.nonsal
+        self.salient_i32 = pw.salient
+        self.w_dense = pw.dense
+        self._meta = dict(N=pw.N, K=pw.K, S=pw.S, S_pad=pw.S_pad, Kp=pw.Kp, Gw=pw.Gw,
+                          ngw=pw.ngw, n_bits=pw.n_bits, wmode=pw.wmode, dtype=pw.dtype)
+        self.weight_quant_name = weight_quant
+        self._random_init = False
+        if self.output_quant_name != "None" and self.salient_indices is None:
+            _, _, self.out_amap_fq, self.out_nonsal = ops.build_maps(pw.N, None, pw.codes.device)
+
+    def _pack_from(self, w: torch.Tensor, weight_quant: str):
+        dev = w.device
+        wg = w.detach()
+        if dev.type != "cuda":
+            if not torch.cuda.is_available():
+                raise RuntimeError("W4A4Linear packing needs a ROCm GPU (no CPU implementation)")
+            wg = wg.to("cuda")
+        sal = self.salient_indices
+        pw = ops.pack_weight(wg, weight_quant if weight_quant in _WEIGHT else "none",
+                             self.quant_bits, self.group_size, sal)
+        self._install(pw, weight_quant)
+        if dev.type != "cuda":
+            self.to(dev)
+
+    def packed(self) -> PackedWeight:
+        if self._meta is None:
+            if not self._random_init:
+                raise RuntimeError("W4A4Linear has no packed weight")
+            if not torch.cuda.is_available():
+                raise RuntimeError("W4A4Linear needs a ROCm GPU (no CPU implementation)")
+            w = torch.randn(self.out_features, self.in_features, dtype=torch.float16,
+                            device="cuda")
+            self._pack_from(w, "None")
+        m = self._meta
+        return PackedWeight(self.w_codes, self.w_scale, self.w_salient, self.w_perm, self.w_amap,
+                            self.w_amap_fq, self.w_nonsal, self.salient_i32, m["N"], m["K"],
+                            m["S"], m["S_pad"], m["Kp"], m["Gw"], m["ngw"], m["n_bits"],
+                            m["wmode"], m["dtype"], self.w_dense)
+
+    # the reference's `weight` buffer (dequantized W_hat, fake_quant.py:357-365)
+    @property
+    def weight(self) -> torch.Tensor:
+        return ops.dequant_weight(self.packed())
+
+    @weight.setter
+    def weight(self, value: torch.Tensor):
+        # assigning a weight (reference: `new_module.weight = ...`) stores it unquantized,
+        # exactly what the reference's F.linear would then consume
+        self._pack_from(value.data if isinstance(value, nn.Parameter) else value, "None")
+
+    def __setattr__(self, name, value):
+        if name == "weight":
+            object.__setattr__(self, name, value)
+            return
+        super().__setattr__(name, value)
+
+    def _apply(self, fn, recurse=True):
+        # A dtype cast (model.half(), .to(torch.bfloat16)) turns the reference's dequantized
+        # W_hat buffer into cast(W_hat).  Mirror that: dequantize, cast, keep it as a dense
+        # operand (casting per-group scales instead would change the values).
+        if self._meta is not None and self.w_scale is not None:
+            probe = fn(torch.empty(0, dtype=self._meta["dtype"], device=self.w_scale.device))
+            if probe.dtype != self._meta["dtype"]:
+                w_new = fn(self.weight)
+                out = super()._apply(fn, recurse)
+                name = self.weight_quant_name
+                self._pack_from(w_new, "None")
+                self.weight_quant_name = name
+                return out
+        return super()._apply(fn, recurse)
+
+    def to(self, *args, **kwargs):
+        super().to(*args, **kwargs)
+        return self
+
+    # ------------------------------------------------------------------ forward
+    @torch.no_grad()
+    def forward(self, x):
+        x_shape = x.shape
+        if len(x_shape) == 3:
+            x2 = x.reshape(-1, x_shape[-1])
+        elif len(x_shape) == 2:
+            x2 = x
+        else:
+            raise ValueError(f"Unsupported input shape: {x_shape}")          # :287
+        if x.device.type != "cuda":
+            raise RuntimeError("W4A4Linear.forward runs on a ROCm GPU only (HIP kernels); "
+                               f"got a tensor on {x.device}")
+        pw = self.packed()
+        if x2.dtype != pw.dtype:
+            raise RuntimeError(f"expected input dtype {pw.dtype}, got {x2.dtype}")
+        mutate_input = (self.salient_indices is None and self.act_quant_name != "per_group"
+                        and x2.data_ptr() == x.data_ptr() and x2.is_contiguous())
+        xc = x2.contiguous()
+        bias = None if self.bias is None else self.bias.reshape(-1)
+        if bias is not None and bias.dtype != pw.dtype:
+            raise RuntimeError(f"bias dtype {bias.dtype} does not match {pw.dtype}")
+        bits = self.quant_bits
+        use_i8 = (self.kernel == "i8" or
+                  (self.kernel == "auto" and ops.i8_eligible(pw, self.act_quant_name, bits)))
+        if use_i8:
+            a8, sa, xs = ops.quant_act_i8(xc, pw, self.act_quant_name, bits)
+        else:
+            a = ops.quant_act_fp(xc, pw, self.act_quant_name, bits, self.group_size)
+        if mutate_input:
+            # the reference quantizes the caller's activation in place here (:304 -> :56-75)
+            ops.fake_quant_inplace(xc, self.act_quant_name, bits, self.group_size, pw.amap_fq,
+                                   pw.nonsal, 0)
+        y = ops.gemm_i8(a8, sa, xs, pw, bias) if use_i8 else ops.gemm_fq(a, pw, bias)
+        if self.output_quant_name != "None":                                 # :308-316
+            if self.salient_indices is not None:
+                if pw.N != pw.K:
+                    raise IndexError(
+                        f"The shape of the mask [{pw.K}] at index 0 does not match the shape "
+                        f"of the indexed tensor [{y.shape[0]}, {pw.N}] at index 1")
+                if pw.K - pw.S > 0:
+                    ops.fake_quant_inplace(y, self.output_quant_name, bits, self.group_size,
+                                           pw.amap_fq, pw.nonsal, pw.S)
+            else:
+                ops.fake_quant_inplace(y, self.output_quant_name, bits, self.group_size,
+                                       self.out_amap_fq, self.out_nonsal, 0)
+        if len(x_shape) == 3:
+            return y.view(x_shape[0], x_shape[1], -1)
+        return y
+
+    # ------------------------------------------------------------------ from_float
+    @staticmethod
+    def from_float(module, weight_quant="per_channel", act_quant="per_token",
+                   quantize_output=False, importance=None, salient_prop=0, quant_bits=4,
+                   group_size=128):
+        assert isinstance(module, torch.nn.Linear)                           # :335
+        new_module = W4A4Linear(module.in_features, module.out_features,
+                                module.bias is not None, act_quant=act_quant,
+                                quantize_output=quantize_output, importance=importance,
+                                salient_prop=salient_prop, quant_bits=quant_bits,
+                                group_size=group_size)
+        if weight_quant not in _WEIGHT:
+            raise ValueError(f"Invalid weight_quant: {weight_quant}")         # :361
+        new_module._pack_from(module.weight.data, weight_quant)
+        if module.bias is not None:
+            new_module.bias = module.bias                                     # :369-370
+        return new_module
+
+    def __repr__(self):
+        return (f"W4A4Linear({self.in_features}, {self.out_features}, bias={self.bias is not None}, "
+                f"weight_quant={self.weight_quant_name}, act_quant={self.act_quant_name}, "
+                f"output_quant={self.output_quant_name}, salient_indices={self.salient_indices})")
+
+
+# ----------------------------------------------------------------------------------------
+# model surgery (fake_quant.py:377-799)
+# ----------------------------------------------------------------------------------------
+def _importance(input_feat, key, guarded):
+    if guarded:
+        return sum(input_feat[key]).float() if input_feat else None
+    return sum(input_feat[key]).float()
+
+
+def _swap(parent, attr, key, input_feat, guarded, quantize_output=False, **kw):
+    imp = _importance(input_feat, key, guarded)
+    setattr(parent, attr, W4A4Linear.from_float(getattr(parent, attr), importance=imp,
+                                                quantize_output=quantize_output, **kw))
+
+
+def quantize_opt(model, weight_quant="per_tensor", act_quant="per_tensor",
+                 quantize_bmm_input=True, input_feat=None, salient_prop=0, quant_bits=4,
+                 group_size=128):
+    """fake_quant.py:377-461 (no guard on input_feat: a missing key raises KeyError)."""
+    from transformers.models.opt.modeling_opt import OPTAttention, OPTDecoderLayer
+    kw = dict(weight_quant=weight_quant, act_quant=act_quant, salient_prop=salient_prop,
+              quant_bits=quant_bits, group_size=group_size)
+    for name, m in list(model.model.named_modules()):
+        pre = "model." + name + "."
+        if isinstance(m, OPTDecoderLayer):
+            _swap(m, "fc1", pre + "fc1", input_feat, False, **kw)
+            _swap(m, "fc2", pre + "fc2", input_feat, False, **kw)
+        elif isinstance(m, OPTAttention):
+            for proj in ("q_proj", "k_proj", "v_proj"):
+                _swap(m, proj, pre + proj, input_feat, False, quantize_output=quantize_bmm_input, **kw)
+            _swap(m, "out_proj", pre + "out_proj", input_feat, False, **kw)
+    return model
+
+
+def quantize_llama_like(model, weight_quant="per_channel", act_quant="per_token",
+                        quantize_bmm_input=False, input_feat=None, salient_prop=0, quant_bits=4,
+                        group_size=128):
+    """fake_quant.py:464-561 (Llama and Mistral)."""
+    from transformers.models.llama.modeling_llama import LlamaAttention, LlamaMLP
+    from transformers.models.mistral.modeling_mistral import MistralAttention, MistralMLP
+    kw = dict(weight_quant=weight_quant, act_quant=act_quant, salient_prop=salient_prop,
+              quant_bits=quant_bits, group_size=group_size)
+    for name, m in list(model.model.named_modules()):
+        pre = "model." + name + "."
+        if isinstance(m, (LlamaMLP, MistralMLP)):
+            for proj in ("gate_proj", "up_proj", "down_proj"):
+                _swap(m, proj, pre + proj, input_feat, True, **kw)
+        elif isinstance(m, (LlamaAttention, MistralAttention)):
+            for proj in ("q_proj", "k_proj", "v_proj"):
+                _swap(m, proj, pre + proj, input_feat, True, quantize_output=quantize_bmm_input, **kw)
+            _swap(m, "o_proj", pre + "o_proj", input_feat, True, **kw)
+    return model
+
+
+def quantize_mixtral(model, weight_quant="per_channel", act_quant="per_token",
+                     quantize_bmm_input=False, input_feat=None, salient_prop=0, quant_bits=4,
+                     group_size=128):
+    """fake_quant.py:564-668.  Experts are swapped where they are nn.Linear modules
+    (w1/w2/w3); transformers >= 5 fuses them into 3-D parameters, which stay unquantized."""
+    from transformers.models.mixtral import modeling_mixtral as mm
+    kw = dict(weight_quant=weight_quant, act_quant=act_quant, salient_prop=salient_prop,
+              quant_bits=quant_bits, group_size=group_size)
+    expert_cls = getattr(mm, "MixtralBLockSparseTop2MLP", None) or getattr(mm, "MixtralBlockSparseTop2MLP", None)
+    for name, m in list(model.model.named_modules()):
+        pre = "model." + name + "."
+        if expert_cls is not None and isinstance(m, expert_cls):
+            for proj in ("w1", "w2", "w3"):
+                _swap(m, proj, pre + proj, input_feat, True, **kw)
+        elif isinstance(m, mm.MixtralAttention):
+            for proj in ("q_proj", "k_proj", "v_proj"):
+                _swap(m, proj, pre + proj, input_feat, True, quantize_output=quantize_bmm_input, **kw)
+            _swap(m, "o_proj", pre + "o_proj", input_feat, True, **kw)
+        elif isinstance(m, mm.MixtralSparseMoeBlock) and isinstance(getattr(m, "gate", None), nn.Linear):
+            _swap(m, "gate", pre + "gate", input_feat, True, **kw)
+    return model
+
+
+def quantize_falcon(model, weight_quant="per_channel", act_quant="per_token",
+                    quantize_bmm_input=True, input_feat=None, salient_prop=0, quant_bits=4,
+                    group_size=128):
+    """fake_quant.py:671-731 (iterates model.named_modules(), keys 'model.' + name)."""
+    from transformers.models.falcon.modeling_falcon import FalconAttention, FalconMLP
+    kw = dict(weight_quant=weight_quant, act_quant=act_quant, salient_prop=salient_prop,
+              quant_bits=quant_bits, group_size=group_size)
+    for name, m in list(model.named_modules()):
+        pre = "model." + name + "."
+        if isinstance(m, FalconMLP):
+            _swap(m, "dense_h_to_4h", pre + "dense_h_to_4h", input_feat, True, **kw)
+            _swap(m, "dense_4h_to_h", pre + "dense_4h_to_h", input_feat, True, **kw)
+        elif isinstance(m, FalconAttention):
+            _swap(m, "query_key_value", pre + "query_key_value", input_feat, True,
+                  quantize_output=quantize_bmm_input, **kw)
+            _swap(m, "dense", pre + "dense", input_feat, True, **kw)
+    return model
+
+
+def quantize_model(model, weight_quant="per_channel", act_quant="per_token",
+                   quantize_bmm_input=False, input_feat=None, salient_prop=None, quant_bits=4,
+                   group_size=128, min_prop=0, max_prop=0):
+    """fake_quant.py:734-799: dispatch on the HF model class."""
+    if input_feat is None:
+        input_feat = {}
+    from transformers.models.falcon.modeling_falcon import FalconPreTrainedModel
+    from transformers.models.llama.modeling_llama import LlamaPreTrainedModel
+    from transformers.models.mistral.modeling_mistral import MistralPreTrainedModel
+    from transformers.models.mixtral.modeling_mixtral import MixtralPreTrainedModel
+    from transformers.models.opt.modeling_opt import OPTPreTrainedModel
+    kw = dict(weight_quant=weight_quant, act_quant=act_quant,
+              quantize_bmm_input=quantize_bmm_input, input_feat=input_feat,
+              salient_prop=salient_prop, quant_bits=quant_bits, group_size=group_size)
+    if isinstance(model, OPTPreTrainedModel):
+        return quantize_opt(model, **kw)
+    if isinstance(model, (LlamaPreTrainedModel, MistralPreTrainedModel)):
+        return quantize_llama_like(model, **kw)
+    if isinstance(model, MixtralPreTrainedModel):
+        return quantize_mixtral(model, **kw)
+    if isinstance(model, FalconPreTrainedModel):
+        return quantize_falcon(model, **kw)
+    raise ValueError(f"Unsupported model type: {type(model)}")

@@ -1,0 +1,234 @@
+"""Torch-facing wrappers over the HIP C ABI (PyTorch supplies device memory and streams).
+
+Every function here launches libsqmp_w4a4 kernels on the caller's current stream and
+raises if a tensor is not on a ROCm device: the W4A4 operator has no CPU path.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass, field
+from typing import Optional
+
+import torch
+
+from . import _lib
+from ._lib import check, load
+
+DTYPE_CODE = {torch.float32: _lib.F32, torch.float16: _lib.F16, torch.bfloat16: _lib.BF16}
+ACT_MODES = {"per_token": _lib.ACT_PER_TOKEN, "per_tensor": _lib.ACT_PER_TENSOR,
+             "per_group": _lib.ACT_PER_GROUP, "per_group_unsorted": _lib.ACT_PER_GROUP_UNSORTED}
+WEIGHT_MODES = {"per_channel": _lib.W_PER_CHANNEL, "per_tensor": _lib.W_PER_TENSOR,
+                "per_group": _lib.W_PER_GROUP, "per_group_unsorted": _lib.W_PER_GROUP_UNSORTED,
+                "none": _lib.W_NONE}
+
+
+def _p(t: Optional[torch.Tensor]):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def _stream(t: torch.Tensor):
+    return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+def _require_gpu(t: torch.Tensor, what: str):
+    if t.device.type != "cuda":
+        raise RuntimeError(
+            f"{what}: tensors must live on a ROCm GPU (got {t.device}); the W4A4 operator is "
+            "implemented only as HIP kernels for gfx950")
+
+
+def _dtype_code(dt: torch.dtype) -> int:
+    if dt not in DTYPE_CODE:
+        raise ValueError(f"unsupported dtype {dt}; expected float32, float16 or bfloat16")
+    return DTYPE_CODE[dt]
+
+
+def geometry(K: int, S: int, wmode: int, group_size: int):
+    """(Kp, Gw, ngw, S_pad) of a packed weight (host only)."""
+    out = [ctypes.c_int() for _ in range(4)]
+    check(load().sqmp_weight_geometry(K, S, wmode, group_size, *[ctypes.byref(o) for o in out]),
+          "weight geometry")
+    return tuple(o.value for o in out)
+
+
+@dataclass
+class PackedWeight:
+    """Device buffers of one packed W4A4 weight (layout: include/sqmp_w4a4.h)."""
+    codes: torch.Tensor          # uint8 [N, Kp/2] (4-bit), int8-as-uint8 [N, Kp] (8-bit), D [N, Kp] (none)
+    wscale: torch.Tensor         # D [N, ngw]
+    wsal: torch.Tensor           # D [N, S_pad]
+    perm: torch.Tensor           # int32 [Kp]
+    amap: torch.Tensor           # int32 [Kp]
+    amap_fq: torch.Tensor        # int32 [K]
+    nonsal: torch.Tensor         # int32 [max(K-S,1)]
+    salient: Optional[torch.Tensor]  # int32 [S] or None
+    N: int
+    K: int
+    S: int
+    S_pad: int
+    Kp: int
+    Gw: int
+    ngw: int
+    n_bits: int                  # 4 / 8, or 0 for a dense D operand
+    wmode: int
+    dtype: torch.dtype
+    dense: Optional[torch.Tensor] = field(default=None)  # packed-order D operand for fine groups
+
+    @property
+    def gemm_operand(self):
+        """(B operand, n_bits) for sqmp_gemm_fq."""
+        if self.dense is not None:
+            return self.dense, 0
+        return self.codes, self.n_bits
+
+
+def build_maps(K: int, salient: Optional[torch.Tensor], device, Kp: Optional[int] = None):
+    """Identity-order index maps (perm, amap, amap_fq, nonsal) for K columns."""
+    S = 0 if salient is None else int(salient.numel())
+    Kp = K if Kp is None else Kp
+    i32 = dict(dtype=torch.int32, device=device)
+    perm = torch.empty(Kp, **i32)
+    amap = torch.empty(Kp, **i32)
+    amap_fq = torch.empty(K, **i32)
+    nonsal = torch.empty(max(K - S, 1), **i32)
+    ref = amap_fq
+    check(load().sqmp_build_maps(K, _p(salient), S, _p(perm), _p(amap), _p(amap_fq), _p(nonsal),
+                                 Kp, _stream(ref)), "build maps")
+    return perm, amap, amap_fq, nonsal
+
+
+def pack_weight(w: torch.Tensor, weight_quant: str, n_bits: int, group_size: int,
+                salient: Optional[torch.Tensor]) -> PackedWeight:
+    """Quantize + pack W [N, K] (fake_quant.py:324-371 without the module bookkeeping)."""
+    _require_gpu(w, "pack_weight")
+    if weight_quant not in WEIGHT_MODES:
+        raise ValueError(f"Invalid weight_quant: {weight_quant}")
+    wmode = WEIGHT_MODES[weight_quant]
+    w = w.contiguous()
+    N, K = w.shape
+    dt = _dtype_code(w.dtype)
+    sal = None
+    if salient is not None and salient.numel() > 0:
+        sal = salient.to(device=w.device, dtype=torch.int32).contiguous()
+    S = 0 if sal is None else sal.numel()
+    Kp, Gw, ngw, S_pad = geometry(K, S, wmode, group_size)
+    if wmode == _lib.W_NONE:
+        n_bits_eff = 0
+        codes = torch.empty((N, Kp), dtype=w.dtype, device=w.device)
+    else:
+        if n_bits not in (4, 8):
+            raise ValueError(f"quant_bits={n_bits}: packed weights support 4 or 8 bits")
+        n_bits_eff = n_bits
+        codes = torch.empty((N, Kp * n_bits // 8), dtype=torch.uint8, device=w.device)
+    wscale = torch.empty((N, ngw), dtype=w.dtype, device=w.device)
+    wsal = torch.empty((N, max(S_pad, 0)), dtype=w.dtype, device=w.device)
+    i32 = dict(dtype=torch.int32, device=w.device)
+    perm, amap = torch.empty(Kp, **i32), torch.empty(Kp, **i32)
+    amap_fq, nonsal = torch.empty(K, **i32), torch.empty(max(K - S, 1), **i32)
+    lib = load()
+    ws_bytes = lib.sqmp_pack_workspace_bytes(N, K)
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=w.device)
+    check(lib.sqmp_pack_weight(_p(w), dt, N, K, wmode, n_bits, group_size, _p(sal), S,
+                               _p(codes), _p(wscale), _p(wsal) if S_pad else None, _p(perm),
+                               _p(amap), _p(amap_fq), _p(nonsal), _p(ws), ws_bytes, _stream(w)),
+          "pack_weight")
+    pw = PackedWeight(codes, wscale, wsal, perm, amap, amap_fq, nonsal, sal, N, K, S, S_pad, Kp,
+                      Gw, ngw, n_bits_eff, wmode, w.dtype)
+    epc = 4 if w.dtype == torch.float32 else 8
+    if n_bits_eff and Gw % epc != 0:
+        # groups finer than one 16-B chunk: keep a dense packed-order operand for the GEMM
+        pw.dense = dequant_weight_packed(pw)
+    return pw
+
+
+def dequant_weight_packed(pw: PackedWeight) -> torch.Tensor:
+    out = torch.empty((pw.N, pw.Kp), dtype=pw.dtype, device=pw.codes.device)
+    check(load().sqmp_dequant_weight_packed(_p(pw.codes), _p(pw.wscale), _dtype_code(pw.dtype),
+                                            pw.N, pw.Kp, pw.Gw, pw.ngw, pw.n_bits, _p(out),
+                                            _stream(out)), "dequant_weight_packed")
+    return out
+
+
+def dequant_weight(pw: PackedWeight) -> torch.Tensor:
+    """The reference's `weight` buffer: W_hat [N, K] in D (salient columns exact)."""
+    _require_gpu(pw.codes, "dequant_weight")
+    w_hat = torch.zeros((pw.N, pw.K), dtype=pw.dtype, device=pw.codes.device)
+    check(load().sqmp_dequant_weight(_p(pw.codes), _p(pw.wscale), _p(pw.wsal) if pw.S_pad else None,
+                                     _p(pw.amap), _p(pw.salient), _dtype_code(pw.dtype), pw.N,
+                                     pw.K, pw.S, pw.n_bits, pw.Kp, pw.Gw, pw.ngw, pw.S_pad,
+                                     _p(w_hat), _stream(w_hat)), "dequant_weight")
+    return w_hat
+
+
+def _act_workspace(M: int, K: int, device):
+    n = load().sqmp_act_workspace_bytes(M, K)
+    return torch.empty(n, dtype=torch.uint8, device=device), n
+
+
+def quant_act_fp(x2: torch.Tensor, pw: PackedWeight, act_quant: str, n_bits: int,
+                 group_size: int) -> torch.Tensor:
+    """x [M, K] -> A [M, Kp + S_pad] in D: x_hat in packed order + exact salient tail."""
+    _require_gpu(x2, "quant_act")
+    M, K = x2.shape
+    a = torch.empty((M, pw.Kp + pw.S_pad), dtype=x2.dtype, device=x2.device)
+    ws, nb = _act_workspace(M, K, x2.device)
+    check(load().sqmp_quant_act(_p(x2), _dtype_code(x2.dtype), M, K, ACT_MODES[act_quant], n_bits,
+                                group_size, _p(pw.amap), pw.Kp, _p(pw.nonsal), _p(pw.salient), pw.S,
+                                pw.S_pad, _lib.OUT_FP, _p(a), None, None, _p(ws), nb,
+                                _stream(x2)), "quant_act")
+    return a
+
+
+def quant_act_i8(x2: torch.Tensor, pw: PackedWeight, act_quant: str, n_bits: int):
+    """x [M, K] -> (int8 codes [M, Kp], fp32 scales [M], exact salient x [M, S_pad])."""
+    _require_gpu(x2, "quant_act")
+    M, K = x2.shape
+    a8 = torch.empty((M, pw.Kp), dtype=torch.int8, device=x2.device)
+    sa = torch.empty((M,), dtype=torch.float32, device=x2.device)
+    xs = torch.empty((M, pw.S_pad), dtype=x2.dtype, device=x2.device)
+    ws, nb = _act_workspace(M, K, x2.device)
+    check(load().sqmp_quant_act(_p(x2), _dtype_code(x2.dtype), M, K, ACT_MODES[act_quant], n_bits,
+                                0, _p(pw.amap), pw.Kp, _p(pw.nonsal), _p(pw.salient), pw.S,
+                                pw.S_pad, _lib.OUT_I8, _p(a8), _p(sa), _p(xs) if pw.S_pad else None,
+                                _p(ws), nb, _stream(x2)), "quant_act")
+    return a8, sa, xs
+
+
+def fake_quant_inplace(t2: torch.Tensor, act_quant: str, n_bits: int, group_size: int,
+                       amap_fq: torch.Tensor, nonsal: torch.Tensor, S: int):
+    """Fake-quantize t [M, C] in place; columns marked -2 in amap_fq pass through."""
+    _require_gpu(t2, "fake_quant")
+    M, C = t2.shape
+    ws, nb = _act_workspace(M, C, t2.device)
+    check(load().sqmp_quant_act(_p(t2), _dtype_code(t2.dtype), M, C, ACT_MODES[act_quant], n_bits,
+                                group_size, _p(amap_fq), C, _p(nonsal), None, S, 0,
+                                _lib.OUT_INPLACE, None, None, None, _p(ws), nb, _stream(t2)),
+          "fake_quant")
+    return t2
+
+
+def gemm_fq(a: torch.Tensor, pw: PackedWeight, bias: Optional[torch.Tensor]) -> torch.Tensor:
+    M = a.shape[0]
+    y = torch.empty((M, pw.N), dtype=pw.dtype, device=a.device)
+    b_op, nb = pw.gemm_operand
+    check(load().sqmp_gemm_fq(_p(a), _p(b_op), _p(pw.wscale), _p(pw.wsal) if pw.S_pad else None,
+                              _p(bias), _p(y), _dtype_code(pw.dtype), M, pw.N, pw.Kp, pw.S_pad,
+                              pw.Gw, pw.ngw, nb, _stream(a)), "gemm_fq")
+    return y
+
+
+def gemm_i8(a8: torch.Tensor, sa: torch.Tensor, xs: torch.Tensor, pw: PackedWeight,
+            bias: Optional[torch.Tensor]) -> torch.Tensor:
+    M = a8.shape[0]
+    y = torch.empty((M, pw.N), dtype=pw.dtype, device=a8.device)
+    check(load().sqmp_gemm_i8(_p(a8), _p(sa), _p(xs) if pw.S_pad else None, _p(pw.codes),
+                              _p(pw.wscale), _p(pw.wsal) if pw.S_pad else None, _p(bias), _p(y),
+                              _dtype_code(pw.dtype), M, pw.N, pw.Kp, pw.S_pad, pw.Gw, pw.ngw,
+                              pw.n_bits, _stream(a8)), "gemm_i8")
+    return y
+
+
+def i8_eligible(pw: PackedWeight, act_quant: str, act_bits: int) -> bool:
+    """Whether the integer MFMA path computes this layer (exact-scale factorisation)."""
+    return (act_quant in ("per_token", "per_tensor") and pw.dtype != torch.float32
+            and pw.n_bits in (4, 8) and pw.dense is None and pw.Gw % 64 == 0 and act_bits <= 8)
