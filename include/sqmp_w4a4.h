@@ -22,12 +22,15 @@
  * Packed weight layout (produced by sqmp_pack_weight, consumed by the GEMMs)
  *   Kp        packed K length: weight groups in weight-sorted column order, zero padded
  *             (multiple of 128).  Position p < K holds original column perm[p].
- *   codes     uint8 [N][Kp/2] for 4-bit weights: byte b of row n holds positions 2b (low
- *             nibble) and 2b+1 (high nibble), nibble = code + 8 (code in [-7, 7]).
- *             int8 [N][Kp] for 8-bit weights.  Salient columns and padding hold code 0.
- *   wscale    D [N][ngw]: per-(row, group) scale; group of position p is p / Gw.
+ *   codes     4-bit weights: "bpack", uint8 [N][Kp/2].  Per row, per 128-position block,
+ *             16 dwords; dword (q*4 + s) holds the 8 codes of positions 32s + 8q + e
+ *             (e = 0..7): even e in nibble e/2, odd e in nibble 4 + e/2; nibble =
+ *             code + 8 (code in [-7, 7]).  One dwordx4 per MFMA lane group q is exactly
+ *             its four 16x16x32 B fragments (s = 0..3).
+ *             8-bit weights: int8 [N][Kp] row-major.  Salient columns and padding hold 0.
+ *   wscale    D [ngw][N]: per-(group, row) scale; group of position p is p / Gw.
  *   wsal      D [N][S_pad]: the salient weight columns, exact (fake_quant.py:363-365),
- *             in salient_indices order, zero padded to S_pad (multiple of 64).
+ *             in salient_indices order, zero padded to S_pad (multiple of 128).
  *   perm      int32 [Kp]: original column at packed position p, -1 for padding.
  *   amap      int32 [Kp]: perm with salient columns replaced by -1 (GEMM A-operand map).
  *   amap_fq   int32 [K]:  k, or -2 for salient k (in-place output-quant map).
@@ -74,7 +77,8 @@ enum sqmp_weight_mode {
 enum sqmp_act_out {
   SQMP_OUT_FP = 0,      /* out: D [M][Kp + S_pad]: x_hat at packed positions, exact
                            salient x in the tail (operand of sqmp_gemm_fq) */
-  SQMP_OUT_I8 = 1,      /* out: int8 codes [M][Kp]; out_scale: fp32 [M] (the D scale);
+  SQMP_OUT_I8 = 1,      /* out: int8 codes [M][roundup(Kp,256)] in the i8 GEMM's K order
+                           (sqmp_actquant.hip); out_scale: fp32 [M] (the D scale);
                            out_xs: D [M][S_pad] exact salient x (operand of sqmp_gemm_i8) */
   SQMP_OUT_INPLACE = 2  /* fake-quantize `x` in place through amap_fq (output quant,
                            fake_quant.py:308-316) */
@@ -129,7 +133,11 @@ int sqmp_quant_act(void* x, int dtype, int M, int K, int amode, int n_bits,
                    void* out_scale, void* out_xs, void* workspace, size_t ws_bytes,
                    void* stream);
 
-/* Faithful GEMM: y[M][N] = D( A[M][Kp+S_pad] . B^T + bias ), B decoded in-kernel from
+/* GEMM operand allocation rule: the activation operands (a / a8 / xs) are read in whole
+ * 128-row tiles by LDS-DMA, so their allocations must hold roundup(M, 128) rows (rows
+ * >= M may hold anything; they never reach y).  a8 rows are roundup(Kp, 256) bytes.
+ *
+ * Faithful GEMM: y[M][N] = D( A[M][Kp+S_pad] . B^T + bias ), B decoded in-kernel from
  * the int4/int8 codes as D(code * wscale) (bit-exact W_hat) for p < Kp and taken from
  * wsal for the salient tail; D-MFMA with fp32 accumulation (fake_quant.py:306).
  * n_bits = 4 / 8: codes are packed codes (group size a multiple of 8 elements, 4 for

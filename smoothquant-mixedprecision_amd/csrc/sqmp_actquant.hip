@@ -118,17 +118,29 @@ __global__ __launch_bounds__(256) void quant_act_kernel(
     }
     // ---- outputs, in output order
     if (OUT == SQMP_OUT_I8) {
-      int8_t* o = (int8_t*)out + (size_t)m * P;
-      for (int c = tid; c < P / 16; c += 256) {
+      // int8 codes in the K order of the i8 GEMM's fragments (sqmp_gemm.hip unpack_i8):
+      // byte p' of a row -> block p'>>7, sub-step half t=(p'>>6)&1, lane group q=(p'>>4)&3,
+      // idx=p'&15 -> packed position blk*128 + 32*(2t + idx/8) + 8q + E[idx&7],
+      // E = (0,4,1,5,2,6,3,7).  Rows are padded to a multiple of 256 codes.
+      const int P8 = (int)round_up_dev(P, 256);
+      int8_t* o = (int8_t*)out + (size_t)m * P8;
+      for (int c = tid; c < P8 / 16; c += 256) {
+        const int base = (c >> 3) * 128 + 8 * (c & 3);
+        const int t2 = ((c >> 2) & 1) * 2;
         uint32_t wv[4];
 #pragma unroll
         for (int w4 = 0; w4 < 4; ++w4) {
           uint32_t word = 0;
 #pragma unroll
           for (int e4 = 0; e4 < 4; ++e4) {
-            const uint32_t e = ent[c * 16 + w4 * 4 + e4];
+            const int idx = w4 * 4 + e4;
+            const int ee = ((idx & 1) << 2) | ((idx & 7) >> 1);
+            const int p = base + 32 * (t2 + (idx >> 3)) + ee;
             int code = 0;
-            if ((e >> 16) != G_ZERO) code = (int)quant_code<DT>(DT::to_f(row[e & 0xFFFFu]), s_row);
+            if (p < P) {
+              const uint32_t e = ent[p];
+              if ((e >> 16) != G_ZERO) code = (int)quant_code<DT>(DT::to_f(row[e & 0xFFFFu]), s_row);
+            }
             word |= ((uint32_t)code & 0xFFu) << (8 * e4);
           }
           wv[w4] = word;

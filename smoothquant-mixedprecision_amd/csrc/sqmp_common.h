@@ -9,7 +9,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include "../../include/sqmp_w4a4.h"
+#include "sqmp_w4a4.h"  // include/ (build_ext.py passes -I include)
 
 namespace sqmp {
 
@@ -79,6 +79,30 @@ __device__ inline float block_max(float v, float* red /* >= 16 floats of LDS */)
 }
 
 __host__ __device__ inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
+
+// ---------------------------------------------------------------- packed int4 layout
+// "bpack": per weight row, per 128-position block, 64 bytes = 16 dwords.  Dword
+// (q * 4 + s) holds the 8 codes of positions 32*s + 8*q + e (e = 0..7): lane group q of
+// an MFMA fragment loads its 16 bytes with one dwordx4 and dword s is exactly the B
+// fragment of f16 sub-step s.  Inside a dword, even e sit in the low half-word
+// (nibble e/2), odd e in the high half-word (nibble 4 + e/2), so
+// ((w >> 4i) & 0x000F000F) holds the pair (e=2i, e=2i+1) in two 16-bit lanes.
+// Nibble = code + 8 (offset binary, code in [-7, 7]).
+__host__ __device__ inline int bpack_dword(int p) {
+  const int kin = p & 127;
+  return (p >> 7) * 16 + ((kin >> 3) & 3) * 4 + (kin >> 5);
+}
+__host__ __device__ inline int bpack_shift(int p) {
+  const int e = p & 7;
+  return (e & 1) ? 16 + 4 * (e >> 1) : 4 * (e >> 1);
+}
+// packed position of element e of dword d
+__host__ __device__ inline int bpack_pos(int d, int e) {
+  return (d >> 4) * 128 + (d & 3) * 32 + ((d >> 2) & 3) * 8 + e;
+}
+__host__ __device__ inline int bpack_elem_of_shift(int sh) {  // inverse of bpack_shift
+  return sh >= 16 ? 2 * ((sh - 16) >> 2) + 1 : 2 * (sh >> 2);
+}
 __host__ __device__ inline long round_up(long a, long b) { return (a + b - 1) / b * b; }
 __device__ inline long round_up_dev(long a, long b) { return (a + b - 1) / b * b; }
 

@@ -20,7 +20,7 @@ __device__ inline int fdiv_floor(int r, int G, float invG) {
 
 template <class DT, int WBITS>
 __global__ __launch_bounds__(256) void pack_rows_kernel(
-    const typename DT::T* __restrict__ w, int K, int Kp, int Gw, int ngw, int q_max,
+    const typename DT::T* __restrict__ w, int N, int K, int Kp, int Gw, int ngw, int q_max,
     int per_tensor, const int32_t* __restrict__ perm, const int32_t* __restrict__ amap,
     const uint32_t* __restrict__ cmax, const int32_t* __restrict__ sal, int S, int S_pad,
     uint32_t* __restrict__ codes, typename DT::T* __restrict__ wscale,
@@ -64,7 +64,7 @@ __global__ __launch_bounds__(256) void pack_rows_kernel(
   for (int g = tid; g < ngw; g += 256) {
     const float s = WBITS == 0 ? 1.f : group_scale<DT>(__uint_as_float(gmax[per_tensor ? 0 : g]), q_max);
     sc[g] = s;
-    wscale[(size_t)n * ngw + g] = DT::from_f(s);
+    wscale[(size_t)g * N + n] = DT::from_f(s);  // [ngw][N]
   }
   __syncthreads();
   const float invG = 1.0f / (float)Gw;
@@ -76,16 +76,16 @@ __global__ __launch_bounds__(256) void pack_rows_kernel(
       dense[p] = DT::from_f(k >= 0 ? row[k] : 0.f);
     }
   } else if (WBITS == 4) {
-    const int nw = Kp / 8;  // 8 nibbles per 32-bit word
+    const int nw = Kp / 8;  // 8 nibbles per 32-bit word, bpack order (sqmp_common.h)
     for (int wi = tid; wi < nw; wi += 256) {
       uint32_t word = 0;
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        const int p = wi * 8 + e;
+        const int p = bpack_pos(wi, e);
         const int k = amap[p];
         int c = 0;
         if (k >= 0) c = (int)quant_code<DT>(row[k], sc[fdiv_floor(p, Gw, invG)]);
-        word |= (uint32_t)(c + 8) << (4 * e);
+        word |= (uint32_t)(c + 8) << bpack_shift(p);
       }
       codes[(size_t)n * nw + wi] = word;
     }
@@ -119,7 +119,7 @@ static int pack_rows_launch(const void* w, int N, int K, int Kp, int Gw, int ngw
   SQMP_HIP_CHECK(hipFuncSetAttribute((const void*)pack_rows_kernel<DT, WBITS>,
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   pack_rows_kernel<DT, WBITS><<<dim3(N), dim3(256), lds, s>>>(
-      (const T*)w, K, Kp, Gw, ngw, q_max, per_tensor, perm, amap, cmax, sal, S, S_pad,
+      (const T*)w, N, K, Kp, Gw, ngw, q_max, per_tensor, perm, amap, cmax, sal, S, S_pad,
       (uint32_t*)codes, (T*)wscale, (T*)wsal);
   SQMP_LAUNCH_CHECK();
   return SQMP_OK;
@@ -143,12 +143,12 @@ __global__ __launch_bounds__(256) void dequant_kernel(
     }
     int c;
     if (WBITS == 4) {
-      const uint8_t b = codes[(size_t)n * (Kp / 2) + p / 2];
-      c = (int)((p & 1) ? (b >> 4) : (b & 15)) - 8;
+      const uint32_t wd = ((const uint32_t*)codes)[(size_t)n * (Kp / 8) + bpack_dword(p)];
+      c = (int)((wd >> bpack_shift(p)) & 0xFu) - 8;
     } else {
       c = (int)(int8_t)codes[(size_t)n * Kp + p];
     }
-    const float s = DT::to_f(wscale[(size_t)n * ngw + p / Gw]);
+    const float s = DT::to_f(wscale[(size_t)(p / Gw) * N + n]);
     w_hat[(size_t)n * K + k] = DT::from_f((float)c * s);  // fake_quant.py:193 mul_ in D
   }
   const long tsal = (long)N * S;
@@ -169,13 +169,13 @@ __global__ __launch_bounds__(256) void dequant_packed_kernel(
     const int n = (int)(idx / Kp), p = (int)(idx % Kp);
     int c;
     if (WBITS == 4) {
-      const uint8_t b = codes[(size_t)n * (Kp / 2) + p / 2];
-      c = (int)((p & 1) ? (b >> 4) : (b & 15)) - 8;
+      const uint32_t wd = ((const uint32_t*)codes)[(size_t)n * (Kp / 8) + bpack_dword(p)];
+      c = (int)((wd >> bpack_shift(p)) & 0xFu) - 8;
     } else {
       c = (int)(int8_t)codes[(size_t)n * Kp + p];
     }
     const int g = min(p / Gw, ngw - 1);
-    out[idx] = DT::from_f((float)c * DT::to_f(wscale[(size_t)n * ngw + g]));
+    out[idx] = DT::from_f((float)c * DT::to_f(wscale[(size_t)g * N + n]));
   }
 }
 
@@ -230,7 +230,7 @@ extern "C" int sqmp_weight_geometry(int K, int S, int wmode, int group_size, int
   if (Kp) *Kp = kp;
   if (Gw) *Gw = gw;
   if (ngw) *ngw = ng;
-  if (S_pad) *S_pad = (int)round_up(S, 64);
+  if (S_pad) *S_pad = (int)round_up(S, 128);
   return SQMP_OK;
 }
 

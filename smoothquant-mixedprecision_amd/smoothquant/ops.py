@@ -54,8 +54,8 @@ def geometry(K: int, S: int, wmode: int, group_size: int):
 @dataclass
 class PackedWeight:
     """Device buffers of one packed W4A4 weight (layout: include/sqmp_w4a4.h)."""
-    codes: torch.Tensor          # uint8 [N, Kp/2] (4-bit), int8-as-uint8 [N, Kp] (8-bit), D [N, Kp] (none)
-    wscale: torch.Tensor         # D [N, ngw]
+    codes: torch.Tensor          # uint8 [N, Kp/2] bpack (4-bit), int8-as-uint8 [N, Kp] (8-bit), D [N, Kp] (none)
+    wscale: torch.Tensor         # D [ngw, N]
     wsal: torch.Tensor           # D [N, S_pad]
     perm: torch.Tensor           # int32 [Kp]
     amap: torch.Tensor           # int32 [Kp]
@@ -120,7 +120,7 @@ def pack_weight(w: torch.Tensor, weight_quant: str, n_bits: int, group_size: int
             raise ValueError(f"quant_bits={n_bits}: packed weights support 4 or 8 bits")
         n_bits_eff = n_bits
         codes = torch.empty((N, Kp * n_bits // 8), dtype=torch.uint8, device=w.device)
-    wscale = torch.empty((N, ngw), dtype=w.dtype, device=w.device)
+    wscale = torch.empty((ngw, N), dtype=w.dtype, device=w.device)  # [ngw][N]
     wsal = torch.empty((N, max(S_pad, 0)), dtype=w.dtype, device=w.device)
     i32 = dict(dtype=torch.int32, device=w.device)
     perm, amap = torch.empty(Kp, **i32), torch.empty(Kp, **i32)
@@ -160,6 +160,11 @@ def dequant_weight(pw: PackedWeight) -> torch.Tensor:
     return w_hat
 
 
+def _pad_rows(M: int) -> int:
+    """Activation operands are allocated with rows padded to the GEMM's 128-row tile."""
+    return max(128, (M + 127) // 128 * 128)
+
+
 def _act_workspace(M: int, K: int, device):
     n = load().sqmp_act_workspace_bytes(M, K)
     return torch.empty(n, dtype=torch.uint8, device=device), n
@@ -167,10 +172,13 @@ def _act_workspace(M: int, K: int, device):
 
 def quant_act_fp(x2: torch.Tensor, pw: PackedWeight, act_quant: str, n_bits: int,
                  group_size: int) -> torch.Tensor:
-    """x [M, K] -> A [M, Kp + S_pad] in D: x_hat in packed order + exact salient tail."""
+    """x [M, K] -> A [M, Kp + S_pad] in D: x_hat in packed order + exact salient tail.
+
+    The returned tensor is an M-row view of an allocation padded to a multiple of 128 rows
+    (the GEMM stages whole 128-row tiles by LDS-DMA; rows >= M are never stored)."""
     _require_gpu(x2, "quant_act")
     M, K = x2.shape
-    a = torch.empty((M, pw.Kp + pw.S_pad), dtype=x2.dtype, device=x2.device)
+    a = torch.empty((_pad_rows(M), pw.Kp + pw.S_pad), dtype=x2.dtype, device=x2.device)[:M]
     ws, nb = _act_workspace(M, K, x2.device)
     check(load().sqmp_quant_act(_p(x2), _dtype_code(x2.dtype), M, K, ACT_MODES[act_quant], n_bits,
                                 group_size, _p(pw.amap), pw.Kp, _p(pw.nonsal), _p(pw.salient), pw.S,
@@ -180,12 +188,14 @@ def quant_act_fp(x2: torch.Tensor, pw: PackedWeight, act_quant: str, n_bits: int
 
 
 def quant_act_i8(x2: torch.Tensor, pw: PackedWeight, act_quant: str, n_bits: int):
-    """x [M, K] -> (int8 codes [M, Kp], fp32 scales [M], exact salient x [M, S_pad])."""
+    """x [M, K] -> (int8 codes [M, roundup(Kp, 256)] in the i8 GEMM's K order, fp32
+    scales [M], exact salient x [M, S_pad])."""
     _require_gpu(x2, "quant_act")
     M, K = x2.shape
-    a8 = torch.empty((M, pw.Kp), dtype=torch.int8, device=x2.device)
+    Mp = _pad_rows(M)
+    a8 = torch.empty((Mp, (pw.Kp + 255) // 256 * 256), dtype=torch.int8, device=x2.device)[:M]
     sa = torch.empty((M,), dtype=torch.float32, device=x2.device)
-    xs = torch.empty((M, pw.S_pad), dtype=x2.dtype, device=x2.device)
+    xs = torch.empty((Mp, pw.S_pad), dtype=x2.dtype, device=x2.device)[:M]
     ws, nb = _act_workspace(M, K, x2.device)
     check(load().sqmp_quant_act(_p(x2), _dtype_code(x2.dtype), M, K, ACT_MODES[act_quant], n_bits,
                                 0, _p(pw.amap), pw.Kp, _p(pw.nonsal), _p(pw.salient), pw.S,
@@ -231,4 +241,4 @@ def gemm_i8(a8: torch.Tensor, sa: torch.Tensor, xs: torch.Tensor, pw: PackedWeig
 def i8_eligible(pw: PackedWeight, act_quant: str, act_bits: int) -> bool:
     """Whether the integer MFMA path computes this layer (exact-scale factorisation)."""
     return (act_quant in ("per_token", "per_tensor") and pw.dtype != torch.float32
-            and pw.n_bits in (4, 8) and pw.dense is None and pw.Gw % 64 == 0 and act_bits <= 8)
+            and pw.n_bits == 4 and pw.dense is None and pw.Gw % 64 == 0 and act_bits <= 8)

@@ -1,0 +1,33 @@
+"""Run only the W4A4 GEMM (and optionally the prepass) of BASELINE config 2 -- a target
+for rocprofv3 counter passes.  python tools/gemm_only.py [fq|i8] [iters] [prepass]"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "smoothquant-mixedprecision_amd")]
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+from smoothquant import ops  # noqa: E402
+
+kind = sys.argv[1] if len(sys.argv) > 1 else "fq"
+iters = int(sys.argv[2]) if len(sys.argv) > 2 else 10
+prepass = len(sys.argv) > 3 and sys.argv[3] == "prepass"
+dev = torch.device("cuda")
+act = "per_group" if kind == "fq" else "per_token"
+q, x, lin = bench.make_layer(dev, act, seed=1)
+pw = q.packed()
+if kind == "fq":
+    a = ops.quant_act_fp(x, pw, act, 4, bench.G)
+    for _ in range(iters):
+        if prepass:
+            ops.quant_act_fp(x, pw, act, 4, bench.G)
+        ops.gemm_fq(a, pw, lin.bias)
+else:
+    a8, sa, xs = ops.quant_act_i8(x, pw, act, 4)
+    for _ in range(iters):
+        if prepass:
+            ops.quant_act_i8(x, pw, act, 4)
+        ops.gemm_i8(a8, sa, xs, pw, lin.bias)
+torch.cuda.synchronize()
+print("done", kind, iters)
