@@ -22,13 +22,15 @@
  * Packed weight layout (produced by sqmp_pack_weight, consumed by the GEMMs)
  *   Kp        packed K length: weight groups in weight-sorted column order, zero padded
  *             (multiple of 128).  Position p < K holds original column perm[p].
- *   codes     4-bit weights: "bpack", uint8 [N][Kp/2].  Per row, per 128-position block,
- *             16 dwords; dword (q*4 + s) holds the 8 codes of positions 32s + 8q + e
+ *   Np        = roundup(N, 256): codes are allocated with Np rows (rows >= N are never
+ *             stored to y) and wscale rows have stride Np.
+ *   codes     4-bit weights: "bpack", uint8 [Np][Kp/2].  Per row, per 64-position block,
+ *             8 dwords; dword (q*2 + s) holds the 8 codes of positions 32s + 8q + e
  *             (e = 0..7): even e in nibble e/2, odd e in nibble 4 + e/2; nibble =
- *             code + 8 (code in [-7, 7]).  One dwordx4 per MFMA lane group q is exactly
- *             its four 16x16x32 B fragments (s = 0..3).
+ *             code + 8 (code in [-7, 7]).  One 8-byte read per MFMA lane group q is
+ *             exactly its two 16x16x32 B fragments (s = 0, 1), or its 16x16x64 i8 one.
  *             8-bit weights: int8 [N][Kp] row-major.  Salient columns and padding hold 0.
- *   wscale    D [ngw][N]: per-(group, row) scale; group of position p is p / Gw.
+ *   wscale    D [ngw][Np]: per-(group, row) scale; group of position p is p / Gw.
  *   wsal      D [N][S_pad]: the salient weight columns, exact (fake_quant.py:363-365),
  *             in salient_indices order, zero padded to S_pad (multiple of 128).
  *   perm      int32 [Kp]: original column at packed position p, -1 for padding.
@@ -134,7 +136,7 @@ int sqmp_quant_act(void* x, int dtype, int M, int K, int amode, int n_bits,
                    void* stream);
 
 /* GEMM operand allocation rule: the activation operands (a / a8 / xs) are read in whole
- * 128-row tiles by LDS-DMA, so their allocations must hold roundup(M, 128) rows (rows
+ * 256-row tiles by LDS-DMA, so their allocations must hold roundup(M, 256) rows (rows
  * >= M may hold anything; they never reach y).  a8 rows are roundup(Kp, 256) bytes.
  *
  * Faithful GEMM: y[M][N] = D( A[M][Kp+S_pad] . B^T + bias ), B decoded in-kernel from

@@ -118,15 +118,15 @@ __global__ __launch_bounds__(256) void quant_act_kernel(
     }
     // ---- outputs, in output order
     if (OUT == SQMP_OUT_I8) {
-      // int8 codes in the K order of the i8 GEMM's fragments (sqmp_gemm.hip unpack_i8):
-      // byte p' of a row -> block p'>>7, sub-step half t=(p'>>6)&1, lane group q=(p'>>4)&3,
-      // idx=p'&15 -> packed position blk*128 + 32*(2t + idx/8) + 8q + E[idx&7],
-      // E = (0,4,1,5,2,6,3,7).  Rows are padded to a multiple of 256 codes.
+      // int8 codes in the K order of the i8 GEMM's fragments (sqmp_mfma.h unpack_i8):
+      // byte p' of a row -> 64-code block p'>>6, lane group q=(p'>>4)&3, idx=p'&15 ->
+      // packed position blk*64 + 32*(idx/8) + 8q + E[idx&7], E = (0,4,1,5,2,6,3,7).
+      // Rows are padded to a multiple of 256 codes.
       const int P8 = (int)round_up_dev(P, 256);
       int8_t* o = (int8_t*)out + (size_t)m * P8;
       for (int c = tid; c < P8 / 16; c += 256) {
-        const int base = (c >> 3) * 128 + 8 * (c & 3);
-        const int t2 = ((c >> 2) & 1) * 2;
+        const int base = (c >> 2) * 64 + 8 * (c & 3);
+        const int t2 = 0;
         uint32_t wv[4];
 #pragma unroll
         for (int w4 = 0; w4 < 4; ++w4) {

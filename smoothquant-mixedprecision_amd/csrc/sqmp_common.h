@@ -81,24 +81,29 @@ __device__ inline float block_max(float v, float* red /* >= 16 floats of LDS */)
 __host__ __device__ inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
 
 // ---------------------------------------------------------------- packed int4 layout
-// "bpack": per weight row, per 128-position block, 64 bytes = 16 dwords.  Dword
-// (q * 4 + s) holds the 8 codes of positions 32*s + 8*q + e (e = 0..7): lane group q of
-// an MFMA fragment loads its 16 bytes with one dwordx4 and dword s is exactly the B
-// fragment of f16 sub-step s.  Inside a dword, even e sit in the low half-word
-// (nibble e/2), odd e in the high half-word (nibble 4 + e/2), so
-// ((w >> 4i) & 0x000F000F) holds the pair (e=2i, e=2i+1) in two 16-bit lanes.
-// Nibble = code + 8 (offset binary, code in [-7, 7]).
+// "bpack": per weight row, per 64-position block, 32 bytes = 8 dwords.  Dword (q * 2 + s)
+// holds the 8 codes of positions 32*s + 8*q + e (e = 0..7): lane group q of an MFMA
+// fragment reads its 8 bytes with one ds_read_b64; dword s is exactly its B fragment of
+// f16 sub-step s, and the pair (s = 0, 1) unpacks to its i8 16x16x64 fragment.  Inside a
+// dword, even e sit in the low half-word (nibble e/2), odd e in the high half-word
+// (nibble 4 + e/2), so ((w >> 4i) & 0x000F000F) holds the pair (e=2i, e=2i+1) in two
+// 16-bit lanes.  Nibble = code + 8 (offset binary, code in [-7, 7]).
 __host__ __device__ inline int bpack_dword(int p) {
-  const int kin = p & 127;
-  return (p >> 7) * 16 + ((kin >> 3) & 3) * 4 + (kin >> 5);
+  const int kin = p & 63;
+  return (p >> 6) * 8 + ((kin >> 3) & 3) * 2 + (kin >> 5);
 }
 __host__ __device__ inline int bpack_shift(int p) {
   const int e = p & 7;
   return (e & 1) ? 16 + 4 * (e >> 1) : 4 * (e >> 1);
 }
+// Weight rows are allocated padded to Np = roundup(N, 256) (one fast-GEMM N tile): the
+// codes buffer holds Np rows and wscale rows have stride Np, so whole tiles are staged by
+// LDS-DMA without per-lane clamps.  Rows >= N never reach y.
+__host__ __device__ inline int pad_n(int N) { return (N + 255) / 256 * 256; }
+
 // packed position of element e of dword d
 __host__ __device__ inline int bpack_pos(int d, int e) {
-  return (d >> 4) * 128 + (d & 3) * 32 + ((d >> 2) & 3) * 8 + e;
+  return (d >> 3) * 64 + (d & 1) * 32 + ((d >> 1) & 3) * 8 + e;
 }
 __host__ __device__ inline int bpack_elem_of_shift(int sh) {  // inverse of bpack_shift
   return sh >= 16 ? 2 * ((sh - 16) >> 2) + 1 : 2 * (sh >> 2);

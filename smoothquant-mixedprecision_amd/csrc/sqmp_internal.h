@@ -20,4 +20,13 @@ int launch_build_maps(int K, int Kp, const int32_t* rank_by_col, const int32_t* 
                       int S, int32_t* perm, int32_t* amap, int32_t* amap_fq,
                       int32_t* nonsal, hipStream_t s);
 
+// Fast GEMMs (sqmp_gemm_fast.hip); SQMP_EUNSUPPORTED when the shape has no fast kernel.
+int launch_gemm_fq_fast(int dtype, const void* a, const void* codes, const void* wscale,
+                        const void* wsal, const void* bias, void* y, int M, int N, int Kp,
+                        int S_pad, int Gw, int ngw, int n_bits, hipStream_t s);
+int launch_gemm_i8_fast(int dtype, const int8_t* a8, const float* ascale, const void* xs,
+                        const void* codes, const void* wscale, const void* wsal,
+                        const void* bias, void* y, int M, int N, int Kp, int S_pad, int Gw,
+                        int ngw, hipStream_t s);
+
 }  // namespace sqmp

@@ -1,0 +1,96 @@
+// MFMA wrappers, in-register weight decoders and LDS-DMA helpers shared by the GEMMs.
+#pragma once
+#include "sqmp_internal.h"
+
+namespace sqmp {
+
+typedef __attribute__((address_space(3))) void* lds_void_ptr;
+
+// XCD-aware bijective block remap + grouped ordering along M (tiles that share a weight
+// column block run together on one XCD).
+__device__ inline void tile_coords(int tiles_m, int tiles_n, int group_m, int& tm, int& tn) {
+  const int nwg = tiles_m * tiles_n;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  const int per_group = group_m * tiles_n;
+  const int gid = wg / per_group;
+  const int first_m = gid * group_m;
+  const int gsz = min(tiles_m - first_m, group_m);
+  const int in_g = wg - gid * per_group;
+  tm = first_m + in_g % gsz;
+  tn = in_g / gsz;
+}
+
+template <class DT> struct Mfma;
+template <> struct Mfma<F16> {
+  __device__ static inline void run(f32x4& acc, const u32x4& a, const u32x4& b) {
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(*(const f16x8*)&a, *(const f16x8*)&b, acc, 0, 0, 0);
+  }
+};
+template <> struct Mfma<BF16> {
+  __device__ static inline void run(f32x4& acc, const u32x4& a, const u32x4& b) {
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*(const bf16x8*)&a, *(const bf16x8*)&b, acc, 0, 0, 0);
+  }
+};
+template <> struct Mfma<F32> {
+  // 16x16x4 f32: lane group q supplies k = q; element e of the 16-B chunk is a separate
+  // k-slice, so four MFMAs consume the chunk (A and B use the same k assignment).
+  __device__ static inline void run(f32x4& acc, const u32x4& a, const u32x4& b) {
+    const float* af = (const float*)&a;
+    const float* bf = (const float*)&b;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(af[e], bf[e], acc, 0, 0, 0);
+  }
+};
+
+// One bpack dword (8 codes) + the raw 16-bit D scale -> the 8 D values D(code * s) of
+// one B fragment (exactly the reference's W_hat, fake_quant.py:193).
+template <class DT> struct Dec8;
+template <> struct Dec8<F16> {
+  typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+  // (0x6400 | nibble) is the half 1024 + nibble; minus 1032 gives the code exactly; the
+  // packed half multiply rounds code * s once (RNE).
+  __device__ static inline u32x4 run(uint32_t w, uint32_t sbits) {
+    const uint32_t s2b = sbits | (sbits << 16);
+    const h2 s2 = *(const h2*)&s2b;
+    const h2 off = {(_Float16)1032.0f, (_Float16)1032.0f};
+    uint32_t o[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint32_t bits = ((w >> (4 * i)) & 0x000F000Fu) | 0x64006400u;
+      h2 h = *(const h2*)&bits;
+      h = (h - off) * s2;
+      o[i] = *(const uint32_t*)&h;
+    }
+    return u32x4{o[0], o[1], o[2], o[3]};
+  }
+};
+template <> struct Dec8<BF16> {
+  // code * s is exact in fp32 (3-bit code x 8-bit bf16 mantissa); one RNE cast to bf16.
+  __device__ static inline u32x4 run(uint32_t w, uint32_t sbits) {
+    const float s = __uint_as_float(sbits << 16);
+    uint32_t o[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float lo = (float)((int)((w >> (4 * i)) & 0xFu) - 8) * s;
+      const float hi = (float)((int)((w >> (16 + 4 * i)) & 0xFu) - 8) * s;
+      const __bf16 bl = (__bf16)lo, bh = (__bf16)hi;
+      o[i] = (uint32_t)(*(const uint16_t*)&bl) | ((uint32_t)(*(const uint16_t*)&bh) << 16);
+    }
+    return u32x4{o[0], o[1], o[2], o[3]};
+  }
+};
+
+// int4 bpack dword -> two int8 dwords, byte order (e0,e4,e1,e5) and (e2,e6,e3,e7); the
+// i8 activation operand is written in the matching K order (sqmp_actquant.hip).
+__device__ inline void unpack_i8(uint32_t w, uint32_t& lo, uint32_t& hi) {
+  lo = ((w & 0x0F0F0F0Fu) + 0x78787878u) ^ 0x80808080u;
+  hi = (((w >> 4) & 0x0F0F0F0Fu) + 0x78787878u) ^ 0x80808080u;
+}
+
+__device__ inline void glds16(const void* src, unsigned char* lds_dst) {
+  __builtin_amdgcn_global_load_lds(src, (lds_void_ptr)lds_dst, 16, 0, 0);
+}
+
+}  // namespace sqmp

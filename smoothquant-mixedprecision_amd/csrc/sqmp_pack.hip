@@ -64,7 +64,7 @@ __global__ __launch_bounds__(256) void pack_rows_kernel(
   for (int g = tid; g < ngw; g += 256) {
     const float s = WBITS == 0 ? 1.f : group_scale<DT>(__uint_as_float(gmax[per_tensor ? 0 : g]), q_max);
     sc[g] = s;
-    wscale[(size_t)g * N + n] = DT::from_f(s);  // [ngw][N]
+    wscale[(size_t)g * pad_n(N) + n] = DT::from_f(s);  // [ngw][Np]
   }
   __syncthreads();
   const float invG = 1.0f / (float)Gw;
@@ -148,7 +148,7 @@ __global__ __launch_bounds__(256) void dequant_kernel(
     } else {
       c = (int)(int8_t)codes[(size_t)n * Kp + p];
     }
-    const float s = DT::to_f(wscale[(size_t)(p / Gw) * N + n]);
+    const float s = DT::to_f(wscale[(size_t)(p / Gw) * pad_n(N) + n]);
     w_hat[(size_t)n * K + k] = DT::from_f((float)c * s);  // fake_quant.py:193 mul_ in D
   }
   const long tsal = (long)N * S;
@@ -175,7 +175,7 @@ __global__ __launch_bounds__(256) void dequant_packed_kernel(
       c = (int)(int8_t)codes[(size_t)n * Kp + p];
     }
     const int g = min(p / Gw, ngw - 1);
-    out[idx] = DT::from_f((float)c * DT::to_f(wscale[(size_t)g * N + n]));
+    out[idx] = DT::from_f((float)c * DT::to_f(wscale[(size_t)g * pad_n(N) + n]));
   }
 }
 

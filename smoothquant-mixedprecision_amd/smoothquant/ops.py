@@ -43,6 +43,11 @@ def _dtype_code(dt: torch.dtype) -> int:
     return DTYPE_CODE[dt]
 
 
+def pad_n(N: int) -> int:
+    """Np = roundup(N, 256): rows of the packed codes and stride of the scale rows."""
+    return (N + 255) // 256 * 256
+
+
 def geometry(K: int, S: int, wmode: int, group_size: int):
     """(Kp, Gw, ngw, S_pad) of a packed weight (host only)."""
     out = [ctypes.c_int() for _ in range(4)]
@@ -54,8 +59,8 @@ def geometry(K: int, S: int, wmode: int, group_size: int):
 @dataclass
 class PackedWeight:
     """Device buffers of one packed W4A4 weight (layout: include/sqmp_w4a4.h)."""
-    codes: torch.Tensor          # uint8 [N, Kp/2] bpack (4-bit), int8-as-uint8 [N, Kp] (8-bit), D [N, Kp] (none)
-    wscale: torch.Tensor         # D [ngw, N]
+    codes: torch.Tensor          # uint8 [Np, Kp/2] bpack (4-bit), int8-as-uint8 [Np, Kp] (8-bit), D [Np, Kp] (none)
+    wscale: torch.Tensor         # D [ngw, Np]
     wsal: torch.Tensor           # D [N, S_pad]
     perm: torch.Tensor           # int32 [Kp]
     amap: torch.Tensor           # int32 [Kp]
@@ -112,15 +117,16 @@ def pack_weight(w: torch.Tensor, weight_quant: str, n_bits: int, group_size: int
         sal = salient.to(device=w.device, dtype=torch.int32).contiguous()
     S = 0 if sal is None else sal.numel()
     Kp, Gw, ngw, S_pad = geometry(K, S, wmode, group_size)
+    Np = pad_n(N)  # weight rows padded to one fast-GEMM N tile (include/sqmp_w4a4.h)
     if wmode == _lib.W_NONE:
         n_bits_eff = 0
-        codes = torch.empty((N, Kp), dtype=w.dtype, device=w.device)
+        codes = torch.zeros((Np, Kp), dtype=w.dtype, device=w.device)
     else:
         if n_bits not in (4, 8):
             raise ValueError(f"quant_bits={n_bits}: packed weights support 4 or 8 bits")
         n_bits_eff = n_bits
-        codes = torch.empty((N, Kp * n_bits // 8), dtype=torch.uint8, device=w.device)
-    wscale = torch.empty((ngw, N), dtype=w.dtype, device=w.device)  # [ngw][N]
+        codes = torch.zeros((Np, Kp * n_bits // 8), dtype=torch.uint8, device=w.device)
+    wscale = torch.zeros((ngw, Np), dtype=w.dtype, device=w.device)  # [ngw][Np]
     wsal = torch.empty((N, max(S_pad, 0)), dtype=w.dtype, device=w.device)
     i32 = dict(dtype=torch.int32, device=w.device)
     perm, amap = torch.empty(Kp, **i32), torch.empty(Kp, **i32)
@@ -161,8 +167,8 @@ def dequant_weight(pw: PackedWeight) -> torch.Tensor:
 
 
 def _pad_rows(M: int) -> int:
-    """Activation operands are allocated with rows padded to the GEMM's 128-row tile."""
-    return max(128, (M + 127) // 128 * 128)
+    """Activation operands are allocated with rows padded to the GEMM's 256-row tile."""
+    return max(256, (M + 255) // 256 * 256)
 
 
 def _act_workspace(M: int, K: int, device):
