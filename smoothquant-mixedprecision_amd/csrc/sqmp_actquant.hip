@@ -119,14 +119,14 @@ __global__ __launch_bounds__(256) void quant_act_kernel(
     // ---- outputs, in output order
     if (OUT == SQMP_OUT_I8) {
       // int8 codes in the K order of the i8 GEMM's fragments (sqmp_mfma.h unpack_i8):
-      // byte p' of a row -> 64-code block p'>>6, lane group q=(p'>>4)&3, idx=p'&15 ->
-      // packed position blk*64 + 32*(idx/8) + 8q + E[idx&7], E = (0,4,1,5,2,6,3,7).
+      // 16-byte chunk c of a row -> 64-code block c>>2, chunk cb=c&3 within it, byte idx ->
+      // packed position blk*64 + 16*(2*(cb>>1) + (idx>>3)) + 8*(cb&1) + E[idx&7],
+      // E = (0,4,1,5,2,6,3,7): the codes of bpack dwords (cb&1)*4 + 2*(cb>>1) + {0,1}.
       // Rows are padded to a multiple of 256 codes.
       const int P8 = (int)round_up_dev(P, 256);
       int8_t* o = (int8_t*)out + (size_t)m * P8;
       for (int c = tid; c < P8 / 16; c += 256) {
-        const int base = (c >> 2) * 64 + 8 * (c & 3);
-        const int t2 = 0;
+        const int base = (c >> 2) * 64 + 32 * ((c & 3) >> 1) + 8 * (c & 1);
         uint32_t wv[4];
 #pragma unroll
         for (int w4 = 0; w4 < 4; ++w4) {
@@ -135,7 +135,7 @@ __global__ __launch_bounds__(256) void quant_act_kernel(
           for (int e4 = 0; e4 < 4; ++e4) {
             const int idx = w4 * 4 + e4;
             const int ee = ((idx & 1) << 2) | ((idx & 7) >> 1);
-            const int p = base + 32 * (t2 + (idx >> 3)) + ee;
+            const int p = base + 16 * (idx >> 3) + ee;
             int code = 0;
             if (p < P) {
               const uint32_t e = ent[p];

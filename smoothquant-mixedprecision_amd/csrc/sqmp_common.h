@@ -81,16 +81,16 @@ __device__ inline float block_max(float v, float* red /* >= 16 floats of LDS */)
 __host__ __device__ inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
 
 // ---------------------------------------------------------------- packed int4 layout
-// "bpack": per weight row, per 64-position block, 32 bytes = 8 dwords.  Dword (q * 2 + s)
-// holds the 8 codes of positions 32*s + 8*q + e (e = 0..7): lane group q of an MFMA
-// fragment reads its 8 bytes with one ds_read_b64; dword s is exactly its B fragment of
-// f16 sub-step s, and the pair (s = 0, 1) unpacks to its i8 16x16x64 fragment.  Inside a
-// dword, even e sit in the low half-word (nibble e/2), odd e in the high half-word
-// (nibble 4 + e/2), so ((w >> 4i) & 0x000F000F) holds the pair (e=2i, e=2i+1) in two
-// 16-bit lanes.  Nibble = code + 8 (offset binary, code in [-7, 7]).
+// "bpack": per weight row, per 64-position block, 32 bytes = 8 dwords.  Dword (h * 4 + u)
+// holds the 8 codes of positions 16*u + 8*h + e (e = 0..7): the two 16-byte halves of a
+// block are exactly what lane half h of a 32x32x16 MFMA B operand needs for the block's
+// four K sub-steps u (one ds_read_b128).  Inside a dword, even e sit in the low half-word
+// (nibble e/2), odd e in the high half-word (nibble 4 + e/2), so (w & 0x000F000F) and
+// (w & 0x00F000F0) hold the pairs (e=0,1) and (e=2,3) in two 16-bit lanes without a
+// shift.  Nibble = code + 8 (offset binary, code in [-7, 7]).
 __host__ __device__ inline int bpack_dword(int p) {
   const int kin = p & 63;
-  return (p >> 6) * 8 + ((kin >> 3) & 3) * 2 + (kin >> 5);
+  return (p >> 6) * 8 + ((kin >> 3) & 1) * 4 + (kin >> 4);
 }
 __host__ __device__ inline int bpack_shift(int p) {
   const int e = p & 7;
@@ -103,7 +103,7 @@ __host__ __device__ inline int pad_n(int N) { return (N + 255) / 256 * 256; }
 
 // packed position of element e of dword d
 __host__ __device__ inline int bpack_pos(int d, int e) {
-  return (d >> 3) * 64 + (d & 1) * 32 + ((d >> 1) & 3) * 8 + e;
+  return (d >> 3) * 64 + (d & 3) * 16 + ((d >> 2) & 1) * 8 + e;
 }
 __host__ __device__ inline int bpack_elem_of_shift(int sh) {  // inverse of bpack_shift
   return sh >= 16 ? 2 * ((sh - 16) >> 2) + 1 : 2 * (sh >> 2);

@@ -1,25 +1,26 @@
 // Fast W4A4 GEMMs for gfx950 (fp16 / bf16): the F.linear of fake_quant.py:306.
 //
-// gemm_fq4 -- the faithful mixed-precision GEMM
+// gemm_fq5 -- the faithful mixed-precision GEMM
 //   y[M][N] = D( A[M][Kp + S_pad] . B^T + bias ):  A = dequantized activations x_hat in
 //   packed K order + the exact salient columns (bit-exact with the reference's q_x);
 //   B = int4 codes decoded in registers to D(code * scale) (bit-exact with the
-//   reference's W_hat), then the exact salient weight slice; MFMA 16x16x32 in D, fp32
-//   accumulation, one rounding to D.
+//   reference's W_hat), then the exact salient weight slice; v_mfma_f32_32x32x16 in D,
+//   fp32 accumulation, one rounding to D.
 //
-//   Tile 256 (M) x 256 (N) per 512-thread workgroup: 8 waves as 2 (M) x 4 (N), each
-//   128 x 64 = 8 x 4 MFMA tiles (128 fp32 accumulators per lane), two waves per SIMD so
-//   one wave's MFMAs cover the other's LDS reads and decode.  Every main-loop global byte
-//   moves by LDS-DMA (global_load_lds_dwordx4) into a 3-slot LDS ring, two 64-element
-//   K-stages ahead of the MFMAs:
+//   Tile 256 (M) x 256 (N) per 512-thread workgroup: 8 waves as WMW (M) x 8/WMW (N), two
+//   waves per SIMD, 128 fp32 accumulators per lane.  The 32x32x16 MFMA holds the SIMD's
+//   vector issue for 8 of its 32 cycles (16x16x32: 8 of 16), which leaves the issue
+//   slots the int4 decode needs.  Every main-loop global byte moves by LDS-DMA
+//   (global_load_lds_dwordx4) into a 3-slot LDS ring, two 64-element K-stages ahead:
 //     A  256 rows x 128 B, 16-B chunks XOR-swizzled by (row >> 1) & 7
-//     B  256 weight rows x one 32-B bpack block; each lane reads its 8 bytes (its two B
-//        fragments) with ds_read_b64, 8-B pieces swizzled by (row >> 2) & 2
-//     S  the block's group scales, 1 KiB per wave (its 64 columns).
-//   Waits are hand-counted (`s_waitcnt vmcnt(N)` keeps the next stage in flight) and the
-//   workgroup syncs once per stage with a raw s_barrier; no ordinary global load runs in
-//   the main loop, so the compiler never drains the ring.  The salient tail streams its
-//   exact B fragments through registers.
+//     B  256 weight rows x one 32-B bpack block; lane half h reads its 16-B half (its four
+//        sub-step fragments) with one ds_read_b128, halves swizzled by (row >> 3) & 1
+//     S  the block's group scales, 1 KiB per wave (its columns).
+//   Waits are hand-counted (`s_waitcnt vmcnt(N)` keeps the next stage in flight), the
+//   workgroup syncs once per stage with a raw s_barrier, and the LDS reads carry
+//   restrict-scoped alias info, so the compiler adds no drain of the ring.  Dense stages
+//   (the exact salient slice; every stage for dense weights) are 32 columns wide: A and
+//   B both 256 rows x 64 B in the slot, chunks swizzled by (row >> 2) & 3.
 //   The MFMA takes the weight fragment in its A slot, so each lane holds 4 consecutive
 //   output columns of one row: 8-byte stores in the epilogue.
 //
@@ -38,175 +39,234 @@ __device__ inline void raw_barrier() {
 }
 
 // ----------------------------------------------------------------- LDS ring geometry
-constexpr int F4_A = 32768;                      // 256 rows x 128 B
-constexpr int F4_B = 8192;                       // 256 rows x 32 B
-constexpr int F4_S = 8192;                       // 8 waves x 1 KiB
-constexpr int F4_SLOT = F4_A + F4_B + F4_S;      // 49152
-constexpr int F4_NSLOT = 3;                      // 147456 B of 160 KiB
-constexpr int F4_VM_CODES = 4 + 1 + 1;           // DMA ops per wave per codes stage
-constexpr int F4_VM_DENSE = 4;                   // ... per dense (A-only) stage
-
-// A stage image: row r, 16-B chunk c at r*128 + ((c ^ ((r >> 1) & 7)) << 4)
-__device__ inline const u32x4* a4_frag(const unsigned char* st, int row, int chunk) {
-  return (const u32x4*)(st + row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4));
-}
+constexpr int F5_A = 32768;                      // 256 rows x 128 B
+constexpr int F5_B = 8192;                       // 256 rows x 32 B
+constexpr int F5_S = 8192;                       // 8 waves x 1 KiB
+constexpr int F5_SLOT = F5_A + F5_B + F5_S;      // 49152
+constexpr int F5_NSLOT = 3;                      // 147456 B of 160 KiB
+constexpr int F5_VM_CODES = 4 + 1 + 1;           // DMA ops per wave per codes stage
+constexpr int F5_VM_DENSE = 2 + 2;              // ... per 32-column dense stage
+constexpr int F5_DB = 16384;                     // dense stage: B image after 256 x 64 B of A
 
 // GB = weight groups per 64-position block (1: Gw % 64 == 0, 2: Gw == 32);
-// GB = 0: dense D weights (no codes) in every main stage.
-template <class DT, int GB>
-__global__ __launch_bounds__(512, 1) void gemm_fq4_kernel(
+// GB = 0: dense D weights (no codes) in every main stage.  WMW = waves along M (1 or 2).
+template <class DT, int GB, int WMW>
+__global__ __launch_bounds__(512, 1) void gemm_fq5_kernel(
     const typename DT::T* __restrict__ A, const void* __restrict__ Bw,
     const typename DT::T* __restrict__ wscale, const typename DT::T* __restrict__ wsal,
     const typename DT::T* __restrict__ bias, typename DT::T* __restrict__ Y, int M, int N,
     int Kp, int S_pad, int Gw, int ngw, int tiles_m, int tiles_n) {
   typedef typename DT::T T;
-  __shared__ __attribute__((aligned(16))) unsigned char lds[F4_NSLOT * F4_SLOT];
+  constexpr int NWV = 8 / WMW;        // waves along N
+  constexpr int MW = 256 / WMW;       // rows per wave
+  constexpr int CW = 256 / NWV;       // weight rows (output columns) per wave
+  constexpr int I = MW / 32, J = CW / 32;
+  constexpr int GBn = GB > 0 ? GB : 1;
+  constexpr int LPG = CW / 8;         // scale-DMA lanes per group (8 scales per lane)
+  __shared__ __attribute__((aligned(16))) unsigned char lds[F5_NSLOT * F5_SLOT];
 
   int tm, tn;
   tile_coords(tiles_m, tiles_n, 4, tm, tn);
   const int m0 = tm * 256, n0 = tn * 256;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 2, wn = wave & 3;
-  const int r16 = lane & 15, q = lane >> 4;
+  const int wm = wave / NWV, wn = wave % NWV;
+  const int r32 = lane & 31, h = lane >> 5;
   const int lda = Kp + S_pad;
-  const int nkt = lda / 64;
-  const int nkd = Kp / 64;                // main (non-salient) stages
-  const int nkm = GB ? nkd : 0;           // main stages that carry int4 codes
+  const int nkm = GB ? Kp / 64 : 0;       // 64-column stages that carry int4 codes
+  const int nkt = nkm + (lda - nkm * 64) / 32;  // + 32-column dense stages
   const int Np = pad_n(N);
 
   // ---- per-lane DMA source offsets (bytes); per-instruction steps are scalar
+  // dense stage: A and B as 256 rows x 64 B, chunk c of row r at ((c ^ ((r >> 2) & 3)) << 4)
+  const int drow = 16 * wave + (lane >> 2);
+  const int dchunk = (lane & 3) ^ ((lane >> 4) & 3);
+  const uint32_t ad_off = (uint32_t)((size_t)(m0 + drow) * lda * sizeof(T) + dchunk * 16);
+  const uint32_t ad_str = (uint32_t)(128 * (size_t)lda * sizeof(T));
+  const uint32_t bd_row0 = (uint32_t)min(n0 + drow, N - 1);
+  const uint32_t bd_row1 = (uint32_t)min(n0 + drow + 128, N - 1);
   const int arow = 8 * wave + (lane >> 3);
   const uint32_t a_off = (uint32_t)((size_t)(m0 + arow) * lda * sizeof(T) +
                                     (((lane & 7) ^ ((arow >> 1) & 7)) << 4));
   const uint32_t a_str = (uint32_t)(64 * (size_t)lda * sizeof(T));
   const uint32_t b_off = (uint32_t)((size_t)(n0 + 32 * wave + (lane >> 1)) * (Kp / 2) +
                                     (((lane & 1) ^ ((lane >> 4) & 1)) << 4));
-  const int s_u = min(lane >> 3, GB > 0 ? GB - 1 : 0);
-  const uint32_t s_off = (uint32_t)((n0 + 64 * wn + (lane & 7) * 8) * sizeof(T));
+  const int s_u = min(lane / LPG, GBn - 1);
+  const uint32_t s_off = (uint32_t)((n0 + CW * wn + (lane % LPG) * 8) * sizeof(T));
 
+  // DMA of stage kt into its ring slot: codes stages (kt < nkm) 4 A + 1 B + 1 S ops,
+  // dense stages 2 A + 2 B ops per wave.
   auto issue = [&](int kt) {
-    unsigned char* slot = lds + (kt % F4_NSLOT) * F4_SLOT;
-    const unsigned char* ab = (const unsigned char*)A + (size_t)kt * 64 * sizeof(T);
+    unsigned char* slot = lds + (kt % F5_NSLOT) * F5_SLOT;
+    if (kt < nkm) {
+      const unsigned char* ab = (const unsigned char*)A + (size_t)kt * 64 * sizeof(T);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) glds16(ab + (size_t)i * a_str + a_off, slot + (i * 8 + wave) * 1024);
-    if (GB > 0 && kt < nkm) {
-      glds16((const unsigned char*)Bw + (size_t)kt * 32 + b_off, slot + F4_A + wave * 1024);
+      for (int i = 0; i < 4; ++i) glds16(ab + (size_t)i * a_str + a_off, slot + (i * 8 + wave) * 1024);
+      glds16((const unsigned char*)Bw + (size_t)kt * 32 + b_off, slot + F5_A + wave * 1024);
       const int g0 = GB == 1 ? (kt * 64) / Gw : kt * 2;
       const int g = min(g0 + s_u, ngw - 1);  // zero-code padding past the last group
       glds16((const unsigned char*)wscale + (size_t)g * Np * sizeof(T) + s_off,
-             slot + F4_A + F4_B + wave * 1024);
+             slot + F5_A + F5_B + wave * 1024);
+    } else {
+      const int col = nkm * 64 + (kt - nkm) * 32;
+      const unsigned char* ab = (const unsigned char*)A + (size_t)col * sizeof(T);
+      glds16(ab + ad_off, slot + wave * 1024);
+      glds16(ab + ad_str + ad_off, slot + (8 + wave) * 1024);
+      const bool main = col < Kp;  // dense main weights (GB == 0) or the salient slice
+      const unsigned char* bb = main ? (const unsigned char*)Bw : (const unsigned char*)wsal;
+      const uint32_t ldb = main ? (uint32_t)Kp : (uint32_t)S_pad;
+      const uint32_t c0 = (uint32_t)(main ? col : col - Kp) * sizeof(T) + dchunk * 16;
+      glds16(bb + bd_row0 * ldb * sizeof(T) + c0, slot + F5_DB + wave * 1024);
+      glds16(bb + bd_row1 * ldb * sizeof(T) + c0, slot + F5_DB + (8 + wave) * 1024);
     }
   };
 
-  f32x4 acc[8][4];
+  f32x16 acc[I][J];
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+  for (int i = 0; i < I; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < J; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  // A fragment t = 8 s + i (sub-step s, M tile i) of the current slot; rows of one wave
-  // share the swizzle (r16 >> 1) & 7, so consecutive i differ by an immediate 2 KiB.
-  const int a_row0 = (wm * 128 + r16) * 128;
-  const int a_sw = (r16 >> 1) & 7;
+  const DecK dk = make_deck();
+
+  // A fragment t = I*u + i (sub-step u, M tile i) of a slot: rows of one wave share the
+  // swizzle (r32 >> 1) & 7, so tiles differ by an immediate 4 KiB.
+  const int a_row0 = (wm * MW + r32) * 128;
+  const int a_sw = (r32 >> 1) & 7;
   auto ald = [&](const unsigned char* __restrict__ slot, int t) {
-    return *(const u32x4*)(slot + a_row0 + (t & 7) * 2048 + (((4 * (t >> 3) + q) ^ a_sw) << 4));
+    return *(const u32x4*)(slot + a_row0 + (t % I) * 4096 + (((2 * (t / I) + h) ^ a_sw) << 4));
   };
-  // 16 blocks of 4 MFMAs; the A fragment of block t+3 is read during block t and one
-  // sched_barrier per block keeps the compiler from hoisting every read (register budget:
-  // 2 waves per SIMD, 256 registers, 128 of them accumulators).
-#define SQMP_FQ4_BLOCKS(BF, HOOK)                                              \
+  // 4*I blocks of J MFMAs; the A fragment of block t+3 is read during block t, one
+  // sched_barrier per block keeps the compiler from hoisting every read, and HOOK runs
+  // the decode of the next sub-step under the MFMAs.
+#define SQMP_FQ5_BLOCKS(BF, ...)                                               \
   {                                                                            \
     u32x4 a[4];                                                                \
     a[0] = ald(slot, 0);                                                       \
     a[1] = ald(slot, 1);                                                       \
     a[2] = ald(slot, 2);                                                       \
-    _Pragma("unroll") for (int t = 0; t < 16; ++t) {                           \
-      if (t + 3 < 16) a[(t + 3) & 3] = ald(slot, t + 3);                       \
-      _Pragma("unroll") for (int j = 0; j < 4; ++j)                            \
-          Mfma<DT>::run(acc[t & 7][j], BF[t >> 3][j], a[t & 3]);               \
-      HOOK;                                                                    \
+    _Pragma("unroll") for (int t = 0; t < 4 * I; ++t) {                        \
+      if (t + 3 < 4 * I) a[(t + 3) & 3] = ald(slot, t + 3);                    \
+      _Pragma("unroll") for (int j = 0; j < J; ++j)                            \
+          Mfma32<DT>::run(acc[t % I][j], BF(t / I, j), a[t & 3]);              \
+      __VA_ARGS__;                                                             \
       __builtin_amdgcn_sched_barrier(0);                                       \
     }                                                                          \
   }
 
   auto compute_codes = [&](const unsigned char* __restrict__ slot) {
-    const unsigned char* sb = slot + F4_A;
-    const unsigned char* ss = slot + F4_A + F4_B + wave * 1024;
-    uint2 bw[4];
-    uint32_t sc[4][GB > 0 ? GB : 1];
+    const unsigned char* sb = slot + F5_A;
+    const unsigned char* ss = slot + F5_A + F5_B + wave * 1024;
+    u32x4 bw[J];
+    uint32_t sp[J][GBn];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int row = wn * 64 + 16 * j + r16;
-      bw[j] = *(const uint2*)(sb + row * 32 + ((q ^ ((r16 >> 2) & 2)) << 3));
+    for (int j = 0; j < J; ++j) {
+      const int row = wn * CW + 32 * j + r32;
+      bw[j] = *(const u32x4*)(sb + row * 32 + ((h ^ ((r32 >> 3) & 1)) << 4));
 #pragma unroll
-      for (int u = 0; u < (GB > 0 ? GB : 1); ++u) sc[j][u] = *(const uint16_t*)(ss + u * 128 + (16 * j + r16) * 2);
+      for (int g = 0; g < GBn; ++g)
+        sp[j][g] = Dec<DT>::prep(*(const uint16_t*)(ss + g * CW * 2 + (32 * j + r32) * 2));
     }
-    u32x4 bf[2][4];
+    u32x4 bf[2][J];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) bf[0][j] = Dec8<DT>::run(bw[j].x, sc[j][0]);
-    // sub-step 1's fragments are decoded under the MFMAs of blocks 1..4
-    SQMP_FQ4_BLOCKS(bf, if (t >= 1 && t <= 4) bf[1][t - 1] = Dec8<DT>::run(bw[t - 1].y, sc[t - 1][GB == 2 ? 1 : 0]));
+    for (int j = 0; j < J; ++j) bf[0][j] = Dec<DT>::run(bw[j][0], sp[j][0], dk);
+#define SQMP_BF_CODES(u, j) bf[(u) & 1][j]
+    SQMP_FQ5_BLOCKS(SQMP_BF_CODES,
+                    if (t / I < 3 && t % I >= 1 && t % I <= J) {
+                      const int un = t / I + 1, jj = t % I - 1;
+                      bf[un & 1][jj] = Dec<DT>::run(bw[jj][un], sp[jj][GB == 2 ? (un >> 1) : 0], dk);
+                    });
+#undef SQMP_BF_CODES
   };
 
-  // dense B through registers (salient tail; every stage when GB == 0); 32-bit row offsets
-  uint32_t brow[4];
+  // dense stage: two 16-element sub-steps, A and B fragments both from the slot
+  const int d_sw = (r32 >> 2) & 3;
+  auto compute_dense = [&](const unsigned char* __restrict__ slot) {
 #pragma unroll
-  for (int j = 0; j < 4; ++j) brow[j] = (uint32_t)min(n0 + wn * 64 + j * 16 + r16, N - 1);
-  auto compute_dense = [&](const unsigned char* __restrict__ slot, const T* __restrict__ Bd, uint32_t ldb, int kofs) {
-    u32x4 bf[2][4];
-    const unsigned char* bb = (const unsigned char*)(Bd + kofs + 8 * q);
+    for (int u = 0; u < 2; ++u) {
+      const int co = ((2 * u + h) ^ d_sw) << 4;
+      u32x4 bf[J];
 #pragma unroll
-    for (int s = 0; s < 2; ++s)
+      for (int j = 0; j < J; ++j) bf[j] = *(const u32x4*)(slot + F5_DB + (wn * CW + 32 * j + r32) * 64 + co);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) bf[s][j] = *(const u32x4*)(bb + (brow[j] * ldb + 32 * s) * sizeof(T));
-    SQMP_FQ4_BLOCKS(bf, (void)0);
+      for (int i = 0; i < I; ++i) {
+        const u32x4 af = *(const u32x4*)(slot + (wm * MW + 32 * i + r32) * 64 + co);
+#pragma unroll
+        for (int j = 0; j < J; ++j) Mfma32<DT>::run(acc[i][j], bf[j], af);
+      }
+    }
   };
-#undef SQMP_FQ4_BLOCKS
+#undef SQMP_FQ5_BLOCKS
 
-  // ---- the ring: stage kt lives in slot kt % 3, issued two stages ahead.  Three loops,
-  // one compute body each, so the accumulators keep their registers across iterations.
-  auto enter = [&](int kt) {
+  // ---- the ring: stage kt lives in slot kt % 3, issued two stages ahead.  One loop per
+  // compute body, so the accumulators keep their registers across iterations.
+  issue(0);
+  if (nkt > 1) issue(1);
+  int kt = 0;
+  for (; kt < nkm; ++kt) {
     // retire stage kt; the DMA of stage kt+1 (issued after it) may stay in flight
     if (kt + 1 < nkt) {
-      if (kt + 1 < nkm) vm_wait<F4_VM_CODES>();
-      else vm_wait<F4_VM_DENSE>();
+      if (kt + 1 < nkm) vm_wait<F5_VM_CODES>();
+      else vm_wait<F5_VM_DENSE>();
     } else {
       vm_wait<0>();
     }
     raw_barrier();  // every wave's DMA for stage kt has landed; slot (kt+2)%3 is free
     if (kt + 2 < nkt) issue(kt + 2);
-    return (const unsigned char*)lds + (kt % F4_NSLOT) * F4_SLOT;
-  };
-  issue(0);
-  if (nkt > 1) issue(1);
-  int kt = 0;
-  for (; kt < nkm; ++kt) compute_codes(enter(kt));
-  for (; kt < nkd; ++kt) compute_dense(enter(kt), (const T*)Bw, (uint32_t)Kp, kt * 64);
-  for (; kt < nkt; ++kt) compute_dense(enter(kt), wsal, (uint32_t)S_pad, (kt - nkd) * 64);
+    compute_codes(lds + (kt % F5_NSLOT) * F5_SLOT);
+  }
+  for (; kt < nkt; ++kt) {
+    if (kt + 1 < nkt) vm_wait<F5_VM_DENSE>();
+    else vm_wait<0>();
+    raw_barrier();
+    if (kt + 2 < nkt) issue(kt + 2);
+    compute_dense(lds + (kt % F5_NSLOT) * F5_SLOT);
+  }
 
-  // ---- epilogue: acc[i][j][r] = C[n = n0 + 64 wn + 16 j + 4 q + r][m = m0 + 128 wm + 16 i + r16]
+  // ---- epilogue: acc[i][j][4 rr + r] = C[n = n0 + CW wn + 32 j + 8 rr + 4 h + r]
+  //                                        [m = m0 + MW wm + 32 i + r32]
+  // bias: every load issued before the first use (clamped columns, one wait)
+  float bvs[J][4][4];
+  if (bias) {
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int nb = n0 + wn * 64 + j * 16 + q * 4;
-    if (nb >= N) continue;
-    float bv[4];
+    for (int j = 0; j < J; ++j)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) bv[r] = (bias && nb + r < N) ? DT::to_f(bias[nb + r]) : 0.f;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int gm = m0 + wm * 128 + i * 16 + r16;
-      if (gm >= M) continue;
-      T v[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = DT::from_f(acc[i][j][r] + bv[r]);
-      T* dst = Y + (size_t)gm * N + nb;
-      if (nb + 4 <= N && (N & 3) == 0) {
-        *(uint2*)dst = *(const uint2*)v;
-      } else {
+      for (int rr = 0; rr < 4; ++rr)
 #pragma unroll
         for (int r = 0; r < 4; ++r)
-          if (nb + r < N) dst[r] = v[r];
+          bvs[j][rr][r] = DT::to_f(bias[min(n0 + wn * CW + 32 * j + 8 * rr + 4 * h + r, N - 1)]);
+  } else {
+#pragma unroll
+    for (int j = 0; j < J; ++j)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) bvs[j][rr][r] = 0.f;
+  }
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      const int nb = n0 + wn * CW + 32 * j + 8 * rr + 4 * h;
+      if (nb >= N) continue;
+      const float* bv = bvs[j][rr];
+#pragma unroll
+      for (int i = 0; i < I; ++i) {
+        const int gm = m0 + wm * MW + 32 * i + r32;
+        if (gm >= M) continue;
+        T v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = DT::from_f(acc[i][j][4 * rr + r] + bv[r]);
+        T* dst = Y + (size_t)gm * N + nb;
+        if (nb + 4 <= N && (N & 3) == 0) {
+          *(uint2*)dst = *(const uint2*)v;
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (nb + r < N) dst[r] = v[r];
+        }
       }
     }
   }
@@ -281,7 +341,7 @@ __global__ __launch_bounds__(256, 1) void gemm_i8v2_kernel(
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         const int blk = min(ks * 4 + t, nblk - 1);
-        b[j][t] = *(const uint2*)(B4 + (size_t)nrow[j] * brow_dw + (size_t)blk * 8 + q * 2);
+        b[j][t] = *(const uint2*)(B4 + (size_t)nrow[j] * brow_dw + (size_t)blk * 8 + 4 * (q & 1) + 2 * (q >> 1));
       }
   };
   auto fold = [&](int g) {
@@ -409,37 +469,49 @@ __global__ __launch_bounds__(256, 1) void gemm_i8v2_kernel(
 }
 
 // ================================================================= launchers
-template <class DT, int GB>
-static int fq4_launch(const void* a, const void* codes, const void* wscale, const void* wsal,
+template <class DT, int GB, int WMW>
+static int fq5_launch(const void* a, const void* codes, const void* wscale, const void* wsal,
                       const void* bias, void* y, int M, int N, int Kp, int S_pad, int Gw,
                       int ngw, hipStream_t s) {
   typedef typename DT::T T;
   const int tiles_m = cdiv(M, 256), tiles_n = cdiv(N, 256);
-  gemm_fq4_kernel<DT, GB><<<dim3(tiles_m * tiles_n), dim3(512), 0, s>>>(
+  gemm_fq5_kernel<DT, GB, WMW><<<dim3(tiles_m * tiles_n), dim3(512), 0, s>>>(
       (const T*)a, codes, (const T*)wscale, (const T*)wsal, (const T*)bias, (T*)y, M, N, Kp,
       S_pad, Gw, ngw, tiles_m, tiles_n);
   SQMP_LAUNCH_CHECK();
   return SQMP_OK;
 }
 
-template <class DT>
-static int fq4_dispatch(const void* a, const void* codes, const void* wscale, const void* wsal,
+template <class DT, int WMW>
+static int fq5_dispatch(const void* a, const void* codes, const void* wscale, const void* wsal,
                         const void* bias, void* y, int M, int N, int Kp, int S_pad, int Gw,
                         int ngw, int n_bits, hipStream_t s) {
-  if (n_bits == 0) return fq4_launch<DT, 0>(a, codes, wscale, wsal, bias, y, M, N, Kp, S_pad, 1, 1, s);
+  if (n_bits == 0) return fq5_launch<DT, 0, WMW>(a, codes, wscale, wsal, bias, y, M, N, Kp, S_pad, 1, 1, s);
   if (n_bits != 4) return SQMP_EUNSUPPORTED;
-  if (Gw % 64 == 0) return fq4_launch<DT, 1>(a, codes, wscale, wsal, bias, y, M, N, Kp, S_pad, Gw, ngw, s);
-  if (Gw == 32) return fq4_launch<DT, 2>(a, codes, wscale, wsal, bias, y, M, N, Kp, S_pad, Gw, ngw, s);
+  if (Gw % 64 == 0) return fq5_launch<DT, 1, WMW>(a, codes, wscale, wsal, bias, y, M, N, Kp, S_pad, Gw, ngw, s);
+  if (Gw == 32) return fq5_launch<DT, 2, WMW>(a, codes, wscale, wsal, bias, y, M, N, Kp, S_pad, Gw, ngw, s);
   return SQMP_EUNSUPPORTED;
+}
+
+// Waves along M of the fq5 tile (tuning knob, SQMP_FQ_WAVES_M = 1 or 2).
+static int fq_waves_m() {
+  static int v = [] {
+    const char* e = getenv("SQMP_FQ_WAVES_M");
+    return (e && e[0] == '2') ? 2 : 1;
+  }();
+  return v;
 }
 
 int launch_gemm_fq_fast(int dtype, const void* a, const void* codes, const void* wscale,
                         const void* wsal, const void* bias, void* y, int M, int N, int Kp,
                         int S_pad, int Gw, int ngw, int n_bits, hipStream_t s) {
+  const bool two = fq_waves_m() == 2;
   if (dtype == SQMP_F16)
-    return fq4_dispatch<F16>(a, codes, wscale, wsal, bias, y, M, N, Kp, S_pad, Gw, ngw, n_bits, s);
+    return two ? fq5_dispatch<F16, 2>(a, codes, wscale, wsal, bias, y, M, N, Kp, S_pad, Gw, ngw, n_bits, s)
+               : fq5_dispatch<F16, 1>(a, codes, wscale, wsal, bias, y, M, N, Kp, S_pad, Gw, ngw, n_bits, s);
   if (dtype == SQMP_BF16)
-    return fq4_dispatch<BF16>(a, codes, wscale, wsal, bias, y, M, N, Kp, S_pad, Gw, ngw, n_bits, s);
+    return two ? fq5_dispatch<BF16, 2>(a, codes, wscale, wsal, bias, y, M, N, Kp, S_pad, Gw, ngw, n_bits, s)
+               : fq5_dispatch<BF16, 1>(a, codes, wscale, wsal, bias, y, M, N, Kp, S_pad, Gw, ngw, n_bits, s);
   return SQMP_EUNSUPPORTED;
 }
 

@@ -44,32 +44,65 @@ template <> struct Mfma<F32> {
   }
 };
 
-// One bpack dword (8 codes) + the raw 16-bit D scale -> the 8 D values D(code * s) of
-// one B fragment (exactly the reference's W_hat, fake_quant.py:193).
-template <class DT> struct Dec8;
-template <> struct Dec8<F16> {
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+// 32x32x16 MFMA: lane (r = l & 31, h = l >> 5) holds row r, k = 8h + e of each operand;
+// D register g holds row (g & 3) + 8 (g >> 2) + 4h, column r.
+template <class DT> struct Mfma32;
+template <> struct Mfma32<F16> {
+  __device__ static inline void run(f32x16& acc, const u32x4& a, const u32x4& b) {
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(*(const f16x8*)&a, *(const f16x8*)&b, acc, 0, 0, 0);
+  }
+};
+template <> struct Mfma32<BF16> {
+  __device__ static inline void run(f32x16& acc, const u32x4& a, const u32x4& b) {
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*(const bf16x8*)&a, *(const bf16x8*)&b, acc, 0, 0, 0);
+  }
+};
+
+// Decode constants held in VGPRs (gfx950 VOP3 takes no literal), so (x & m) | c is one
+// v_and_or_b32.  make_deck() runs once per kernel; the empty asm hides the values.
+struct DecK {
+  uint32_t m0, m1, c0, c1;
+};
+__device__ inline DecK make_deck() {
+  DecK k{0x000F000Fu, 0x00F000F0u, 0x64006400u, 0x54005400u};
+  asm volatile("" : "+v"(k.m0), "+v"(k.m1), "+v"(k.c0), "+v"(k.c1));
+  return k;
+}
+__device__ inline uint32_t and_or(uint32_t x, uint32_t m, uint32_t c) { return (x & m) | c; }
+
+// One bpack dword (8 codes of one lane's fragment) + its prepared scale -> the 8 D values
+// D(code * s) (exactly the reference's W_hat, fake_quant.py:193).
+template <class DT> struct Dec;
+template <> struct Dec<F16> {
   typedef _Float16 h2 __attribute__((ext_vector_type(2)));
-  // (0x6400 | nibble) is the half 1024 + nibble; minus 1032 gives the code exactly; the
+  __device__ static inline uint32_t prep(uint32_t sbits) { return sbits | (sbits << 16); }
+  // Nibble slot 0 of a half-word under 0x6400 is the half 1024 + n; slot 1 (bits 4..7)
+  // under 0x5400 is 64 + n (ulp 1/16); minus 1032 / 72 gives the code exactly, and the
   // packed half multiply rounds code * s once (RNE).
-  __device__ static inline u32x4 run(uint32_t w, uint32_t sbits) {
-    const uint32_t s2b = sbits | (sbits << 16);
+  __device__ static inline u32x4 run(uint32_t w, uint32_t s2b, const DecK& k) {
     const h2 s2 = *(const h2*)&s2b;
-    const h2 off = {(_Float16)1032.0f, (_Float16)1032.0f};
+    const h2 o0 = {(_Float16)1032.0f, (_Float16)1032.0f};
+    const h2 o1 = {(_Float16)72.0f, (_Float16)72.0f};
+    const uint32_t t = w >> 8;
+    const uint32_t b[4] = {and_or(w, k.m0, k.c0), and_or(w, k.m1, k.c1), and_or(t, k.m0, k.c0),
+                           and_or(t, k.m1, k.c1)};
     uint32_t o[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const uint32_t bits = ((w >> (4 * i)) & 0x000F000Fu) | 0x64006400u;
-      h2 h = *(const h2*)&bits;
-      h = (h - off) * s2;
-      o[i] = *(const uint32_t*)&h;
+      h2 hv = *(const h2*)&b[i];
+      hv = (hv - ((i & 1) ? o1 : o0)) * s2;
+      o[i] = *(const uint32_t*)&hv;
     }
     return u32x4{o[0], o[1], o[2], o[3]};
   }
 };
-template <> struct Dec8<BF16> {
+template <> struct Dec<BF16> {
+  __device__ static inline uint32_t prep(uint32_t sbits) { return sbits << 16; }
   // code * s is exact in fp32 (3-bit code x 8-bit bf16 mantissa); one RNE cast to bf16.
-  __device__ static inline u32x4 run(uint32_t w, uint32_t sbits) {
-    const float s = __uint_as_float(sbits << 16);
+  __device__ static inline u32x4 run(uint32_t w, uint32_t sf, const DecK&) {
+    const float s = __uint_as_float(sf);
     uint32_t o[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
