@@ -155,7 +155,7 @@ def main():
 
     q, x, lin = make_layer(dev, args.act, seed=1234 + rank)
     pw = q.packed()
-    use_i8 = ops.i8_eligible(pw, args.act, 4)
+    use_i8 = ops.I8_AUTO and ops.i8_eligible(pw, args.act, 4)  # what W4A4Linear(auto) runs
     stream = torch.cuda.current_stream(dev)
 
     def step():
@@ -193,6 +193,13 @@ def main():
     gemm_ms = time_events(gemm, max(10, args.steps), stream)
     quant_ms = time_events(quant, max(10, args.steps), stream)
     achieved = flops / (gemm_ms * 1e-3) / 1e12
+    # reference point: the vendor dense fp16 GEMM (hipBLASLt via torch) on the same shape,
+    # unquantized -- what the reference's F.linear costs on this GPU, without any act-quant
+    wd = lin.weight.detach()
+    dense = lambda: torch.nn.functional.linear(x, wd, lin.bias)  # noqa: E731
+    for _ in range(3):
+        dense()
+    dense_ms = time_events(dense, max(10, args.steps), stream)
     # prepass algorithmic bytes: read x (colmax) + read x (quantize) + write operand(s)
     xbytes = M * K * 2
     if use_i8:
@@ -239,9 +246,13 @@ def main():
             "unit": "TFLOP/s",
             "frac": round(achieved / PEAK_TFLOPS[kdt], 4),
             "traffic": traffic,
-            "kernel": "sqmp::gemm_i8_kernel" if use_i8 else "sqmp::gemm_fq_kernel<F16,4>",
+            "kernel": "sqmp::gemm_i8v2_kernel<F16>" if use_i8 else "sqmp::gemm_fq5_kernel<F16,1,1>",
             "avg_ms": round(gemm_ms, 4),
             "algorithmic_flops_per_launch": flops,
+        },
+        "reference_points": {
+            "torch_fp16_linear_ms": round(dense_ms, 4),
+            "torch_fp16_linear_TFLOP_per_s": round(flops / (dense_ms * 1e-3) / 1e12, 1),
         },
         "prepass": {
             "avg_ms": round(quant_ms, 4),

@@ -33,6 +33,7 @@ constexpr uint32_t G_ZERO = 0xFFFFu;  // output position holds 0 (salient / padd
 constexpr uint32_t G_PASS = 0xFFFEu;  // output position passes the input through
 
 enum { MODE_TOKEN = 0, MODE_TENSOR = 1, MODE_GROUP = 2 };
+constexpr int PFC_FP = 6;  // 16-B row chunks per thread held for the next row (K*esize <= 24 KiB)
 
 template <class DT, int MODE, int OUT>
 __global__ __launch_bounds__(256) void quant_act_kernel(
@@ -85,10 +86,32 @@ __global__ __launch_bounds__(256) void quant_act_kernel(
   __syncthreads();
 
   const bool xvec = ((K * (int)sizeof(T)) % 16 == 0) && (((uintptr_t)x) % 16 == 0);
+  // Rows of at most PFC 16-B chunks per thread are software-pipelined: the next row's
+  // chunks are loaded into registers while this row is quantized (hides HBM latency).
+  constexpr int PFC = 4;
+  const int nch = xvec ? K / VEC : 0;
+  const bool pipe = xvec && nch <= PFC * 256;
+  u32x4 nxt[PFC];
+  auto load_row = [&](int mm) {
+    const u32x4* src = (const u32x4*)(x + (size_t)mm * K);
+#pragma unroll
+    for (int i = 0; i < PFC; ++i) {
+      const int c = tid + 256 * i;
+      if (c < nch) nxt[i] = src[c];
+    }
+  };
+  if (pipe && (int)blockIdx.x < M) load_row(blockIdx.x);
   for (int m = blockIdx.x; m < M; m += gridDim.x) {
     T* xr = x + (size_t)m * K;
     // ---- stage the row
-    if (xvec) {
+    if (pipe) {
+#pragma unroll
+      for (int i = 0; i < PFC; ++i) {
+        const int c = tid + 256 * i;
+        if (c < nch) ((u32x4*)row)[c] = nxt[i];
+      }
+      if (m + (int)gridDim.x < M) load_row(m + gridDim.x);
+    } else if (xvec) {
       for (int c = tid; c < K / VEC; c += 256) ((u32x4*)row)[c] = ((const u32x4*)xr)[c];
     } else {
       for (int k = tid; k < K; k += 256) row[k] = xr[k];
@@ -208,6 +231,186 @@ __global__ __launch_bounds__(256) void quant_act_kernel(
   }
 }
 
+// ---------------------------------------------------------------- OUT_FP fast kernel
+// x_hat code of one element: rne(D(t / s)).  q = t * r with r = RN(1/s) is within ~1 fp32
+// ulp of the correctly rounded quotient, so D(q) == D(t / s) unless q lies within a few
+// ulps of a D rounding midpoint (low 13 / 16 dropped bits == half) -- then the exact
+// division decides.  |q| < 0.25 always yields a (signed) zero code.
+template <class DT>
+__device__ inline float fast_code(float t, float s, float r) {
+  if (DT::id == SQMP_F32) return __builtin_rintf(t / s);
+  const float q = t * r;
+  const uint32_t b = __float_as_uint(q);
+  constexpr int DROP = DT::id == SQMP_F16 ? 13 : 16;
+  constexpr uint32_t MASK = (1u << DROP) - 1, HALF = 1u << (DROP - 1);
+  const uint32_t lo = b & MASK;
+  const uint32_t d = lo > HALF ? lo - HALF : HALF - lo;
+  if (d <= 3u && fabsf(q) >= 0.25f) return __builtin_rintf(rd<DT>(t / s));
+  return __builtin_rintf(rd<DT>(q));
+}
+
+// Per row: stage the row in LDS (software-pipelined through registers), ONE gather pass
+// over the output positions (values kept in registers; per-group absmax by LDS atomics),
+// the group scales and reciprocals, then quantize from registers and write 16-B chunks.
+// The entry table is chunk-major (two planes of 4 entries) so lanes read consecutive
+// 16-B words.  Rows up to FCH*2048 packed positions; longer rows use quant_act_kernel.
+constexpr int FCH = 6;  // output chunks (8 positions) per thread
+template <class DT, int MODE>
+__global__ __launch_bounds__(256) void quant_fp_kernel(
+    const typename DT::T* __restrict__ x, int M, int K, int q_max, int G, int nga,
+    const int32_t* __restrict__ amap, int P, const int32_t* __restrict__ nonsal, int Kn,
+    const int32_t* __restrict__ sal, int S, int S_pad,
+    const int32_t* __restrict__ rank_by_col, const uint32_t* __restrict__ cmax,
+    typename DT::T* __restrict__ out) {
+  typedef typename DT::T T;
+  constexpr int VEC = 16 / sizeof(T);
+  static_assert(VEC == 8, "fp16 / bf16 only");
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_f[];
+  const int NCH = P / 8;                       // main chunks (P % 128 == 0)
+  const int W = P + S_pad, WCH = W / 8;        // all output chunks
+  const int rowb = (int)round_up_dev(K * (int)sizeof(T), 16);
+  T* row = (T*)smem_f;
+  u32x4* ent = (u32x4*)(smem_f + rowb);        // [2][NCH]
+  uint16_t* grp = (uint16_t*)(ent + 2 * NCH);  // K
+  const int grpb = (int)round_up_dev(K * 2, 16);
+  float2* scr = (float2*)((unsigned char*)grp + grpb);      // nga: (scale, 1/scale)
+  uint32_t* gmax = (uint32_t*)(scr + nga);                   // nga
+  uint16_t* salc = (uint16_t*)(gmax + nga);                  // S_pad: salient column or 0xFFFF
+  float* red = (float*)(salc + round_up_dev(S_pad, 8));      // 16
+  const int tid = threadIdx.x;
+  const float invG = 1.0f / (float)G;
+
+  for (int k = tid; k < K; k += 256) grp[k] = (uint16_t)G_ZERO;
+  for (int j = tid; j < S_pad; j += 256) salc[j] = j < S ? (uint16_t)sal[j] : (uint16_t)0xFFFFu;
+  __syncthreads();
+  for (int i = tid; i < Kn; i += 256) {
+    const int k = nonsal[i];
+    int g = 0;
+    if (MODE == MODE_GROUP) g = fdiv_floor_a(rank_by_col ? rank_by_col[k] : i, G, invG);
+    grp[k] = (uint16_t)g;
+  }
+  __syncthreads();
+  for (int c = tid; c < NCH; c += 256) {
+    uint32_t e[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int k = amap[c * 8 + j];
+      e[j] = k >= 0 ? (((uint32_t)grp[k] << 16) | (uint32_t)k) : (G_ZERO << 16);
+    }
+    ent[c] = u32x4{e[0], e[1], e[2], e[3]};
+    ent[NCH + c] = u32x4{e[4], e[5], e[6], e[7]};
+  }
+  float s_all = 0.f, r_all = 0.f;
+  if (MODE == MODE_TENSOR) {
+    float m = 0.f;
+    for (int i = tid; i < Kn; i += 256) m = fmaxf(m, __uint_as_float(cmax[nonsal[i]]));
+    m = block_max(m, red);
+    s_all = group_scale<DT>(m, q_max);
+    r_all = 1.0f / s_all;
+  }
+  __syncthreads();
+
+  const int nch = K / VEC;
+  u32x4 nxt[PFC_FP];
+  auto load_row = [&](int mm) {
+    const u32x4* src = (const u32x4*)(x + (size_t)mm * K);
+#pragma unroll
+    for (int i = 0; i < PFC_FP; ++i) {
+      const int c = tid + 256 * i;
+      if (c < nch) nxt[i] = src[c];
+    }
+  };
+  if ((int)blockIdx.x < M) load_row(blockIdx.x);
+  for (int m = blockIdx.x; m < M; m += gridDim.x) {
+#pragma unroll
+    for (int i = 0; i < PFC_FP; ++i) {
+      const int c = tid + 256 * i;
+      if (c < nch) ((u32x4*)row)[c] = nxt[i];
+    }
+    if (m + (int)gridDim.x < M) load_row(m + gridDim.x);
+    if (MODE == MODE_GROUP)
+      for (int g = tid; g < nga; g += 256) gmax[g] = 0u;
+    __syncthreads();
+    // ---- gather pass: values of this thread's chunks into registers + group absmax
+    uint32_t vals[FCH][4];
+    float lmax = 0.f;
+#pragma unroll
+    for (int i = 0; i < FCH; ++i) {
+      const int c = tid + 256 * i;
+      if (c < NCH) {
+        const u32x4 e0 = ent[c], e1 = ent[NCH + c];
+        const uint32_t e[8] = {e0[0], e0[1], e0[2], e0[3], e1[0], e1[1], e1[2], e1[3]};
+        T v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const uint32_t g = e[j] >> 16;
+          v[j] = g != G_ZERO ? row[e[j] & 0xFFFFu] : DT::from_f(0.f);
+          const float a = fabsf(DT::to_f(v[j]));
+          if (MODE == MODE_GROUP) {
+            if (g != G_ZERO && a > 0.f) atomicMax(&gmax[g], __float_as_uint(a));
+          } else {
+            lmax = fmaxf(lmax, a);
+          }
+        }
+#pragma unroll
+        for (int w = 0; w < 4; ++w) vals[i][w] = ((const uint32_t*)v)[w];
+      }
+    }
+    float s_row = s_all, r_row = r_all;
+    if (MODE == MODE_TOKEN) {
+      const float mx = block_max(lmax, red);
+      s_row = group_scale<DT>(mx, q_max);
+      r_row = 1.0f / s_row;
+    } else if (MODE == MODE_GROUP) {
+      __syncthreads();
+      for (int g = tid; g < nga; g += 256) {
+        const float sg = group_scale<DT>(__uint_as_float(gmax[g]), q_max);
+        scr[g] = make_float2(sg, 1.0f / sg);
+      }
+      __syncthreads();
+    }
+    // ---- quantize from registers, 16-B stores in output order
+    T* o = out + (size_t)m * W;
+#pragma unroll
+    for (int i = 0; i < FCH; ++i) {
+      const int c = tid + 256 * i;
+      if (c < NCH) {
+        const u32x4 e0 = ent[c], e1 = ent[NCH + c];
+        const uint32_t e[8] = {e0[0], e0[1], e0[2], e0[3], e1[0], e1[1], e1[2], e1[3]};
+        const T* v = (const T*)vals[i];
+        T r[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const uint32_t g = e[j] >> 16;
+          float y = 0.f;
+          if (g != G_ZERO) {
+            const float2 sr = MODE == MODE_GROUP ? scr[g] : make_float2(s_row, r_row);
+            y = fast_code<DT>(DT::to_f(v[j]), sr.x, sr.y) * sr.x;
+          }
+          r[j] = DT::from_f(y);
+        }
+        ((u32x4*)o)[c] = *(const u32x4*)r;
+      }
+    }
+    // ---- exact salient tail
+    for (int c = NCH + tid; c < WCH; c += 256) {
+      T r[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const uint32_t k = salc[(c - NCH) * 8 + j];
+        r[j] = k != 0xFFFFu ? row[k] : DT::from_f(0.f);
+      }
+      ((u32x4*)o)[c] = *(const u32x4*)r;
+    }
+    __syncthreads();  // row / gmax reuse
+  }
+}
+
+static size_t quant_fp_lds_bytes(int K, int P, int nga, int S_pad, int esize) {
+  return (size_t)round_up((long)K * esize, 16) + 4 * (size_t)P + (size_t)round_up(2L * K, 16) +
+         12 * (size_t)nga + 2 * (size_t)round_up(S_pad, 8) + 64;
+}
+
 static size_t quant_lds_bytes(int K, int P, int nga, int esize) {
   return (size_t)round_up((long)K * esize, 16) + 4 * (size_t)P + (size_t)round_up(2L * K, 16) +
          8 * (size_t)nga + 64;
@@ -234,6 +437,24 @@ static int quant_launch(void* x, int M, int K, int q_max, int G, int nga, const 
   return SQMP_OK;
 }
 
+template <class DT, int MODE>
+static int quant_fp_launch(void* x, int M, int K, int q_max, int G, int nga, const int32_t* amap,
+                           int P, const int32_t* nonsal, int Kn, const int32_t* sal, int S,
+                           int S_pad, const int32_t* rank, const uint32_t* cmax, void* out,
+                           size_t lds, hipStream_t s) {
+  typedef typename DT::T T;
+  SQMP_HIP_CHECK(hipFuncSetAttribute((const void*)quant_fp_kernel<DT, MODE>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  int per_cu = (int)((160 * 1024) / lds);
+  per_cu = per_cu < 1 ? 1 : (per_cu > 8 ? 8 : per_cu);
+  int grid = 256 * per_cu;
+  if (grid > M) grid = M;
+  quant_fp_kernel<DT, MODE><<<dim3(grid), dim3(256), lds, s>>>(
+      (const T*)x, M, K, q_max, G, nga, amap, P, nonsal, Kn, sal, S, S_pad, rank, cmax, (T*)out);
+  SQMP_LAUNCH_CHECK();
+  return SQMP_OK;
+}
+
 template <class DT>
 static int quant_dispatch(void* x, int M, int K, int amode, int q_max, int G, int nga,
                           const int32_t* amap, int P, const int32_t* nonsal, int Kn,
@@ -246,6 +467,21 @@ static int quant_dispatch(void* x, int M, int K, int amode, int q_max, int G, in
   const int mode = amode == SQMP_ACT_PER_TOKEN    ? MODE_TOKEN
                    : amode == SQMP_ACT_PER_TENSOR ? MODE_TENSOR
                                                   : MODE_GROUP;
+  if constexpr (DT::id != SQMP_F32) {
+  if (out_kind == SQMP_OUT_FP && K % 8 == 0 && K * 2 <= PFC_FP * 256 * 16 &&
+      P <= FCH * 256 * 8 && (((uintptr_t)x) % 16 == 0)) {
+    const size_t lds = quant_fp_lds_bytes(K, P, nga, S_pad, sizeof(typename DT::T));
+    if (lds <= 160 * 1024) {
+#define SQMP_QF(MODE)                                                                         \
+  quant_fp_launch<DT, MODE>(x, M, K, q_max, G, nga, amap, P, nonsal, Kn, sal, S, S_pad, rank, \
+                            cmax, out, lds, s)
+      if (mode == MODE_TOKEN) return SQMP_QF(MODE_TOKEN);
+      if (mode == MODE_TENSOR) return SQMP_QF(MODE_TENSOR);
+      return SQMP_QF(MODE_GROUP);
+#undef SQMP_QF
+    }
+  }
+  }
   if (out_kind == SQMP_OUT_FP) {
     if (mode == MODE_TOKEN) return SQMP_Q(MODE_TOKEN, SQMP_OUT_FP);
     if (mode == MODE_TENSOR) return SQMP_Q(MODE_TENSOR, SQMP_OUT_FP);
@@ -304,11 +540,13 @@ extern "C" int sqmp_quant_act(void* x, int dtype, int M, int K, int amode, int n
   }
   int st;
   if (amode == SQMP_ACT_PER_TENSOR || amode == SQMP_ACT_PER_GROUP) {
-    st = launch_colmax(x, dtype, M, K, cmax, s);
+    // one clear for the adjacent cmax and rank workspace arrays
+    SQMP_HIP_CHECK(hipMemsetAsync(workspace, 0, sqmp_act_workspace_bytes(M, K), s));
+    st = launch_colmax(x, dtype, M, K, cmax, s, false);
     if (st) return st;
   }
   if (amode == SQMP_ACT_PER_GROUP) {
-    st = launch_rank(cmax, nonsal, Kn, K, rank, s);
+    st = launch_rank(cmax, nonsal, Kn, K, rank, s, false);
     if (st) return st;
   }
   const int q_max = (1 << (n_bits - 1)) - 1;

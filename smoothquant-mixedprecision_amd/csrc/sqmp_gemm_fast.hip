@@ -25,6 +25,8 @@
 //   output columns of one row: 8-byte stores in the epilogue.
 //
 // gemm_i8v2 -- per_token / per_tensor activations on the integer MFMA (see below).
+#include <string.h>
+
 #include "sqmp_mfma.h"
 
 namespace sqmp {
@@ -49,8 +51,10 @@ constexpr int F5_VM_DENSE = 2 + 2;              // ... per 32-column dense stage
 constexpr int F5_DB = 16384;                     // dense stage: B image after 256 x 64 B of A
 
 // GB = weight groups per 64-position block (1: Gw % 64 == 0, 2: Gw == 32);
-// GB = 0: dense D weights (no codes) in every main stage.  WMW = waves along M (1 or 2).
-template <class DT, int GB, int WMW>
+// GB = 0: dense D weights (no codes) in every main stage.  WMW = waves along M (1 or 2);
+// PF = A-fragment read-ahead (blocks); NOWAIT = 1 is a timing diagnostic only (skips the
+// DMA waits, so results are garbage; every address stays in bounds).
+template <class DT, int GB, int WMW, int PF = 3, int NOWAIT = 0>
 __global__ __launch_bounds__(512, 1) void gemm_fq5_kernel(
     const typename DT::T* __restrict__ A, const void* __restrict__ Bw,
     const typename DT::T* __restrict__ wscale, const typename DT::T* __restrict__ wsal,
@@ -143,14 +147,12 @@ __global__ __launch_bounds__(512, 1) void gemm_fq5_kernel(
   // the decode of the next sub-step under the MFMAs.
 #define SQMP_FQ5_BLOCKS(BF, ...)                                               \
   {                                                                            \
-    u32x4 a[4];                                                                \
-    a[0] = ald(slot, 0);                                                       \
-    a[1] = ald(slot, 1);                                                       \
-    a[2] = ald(slot, 2);                                                       \
+    u32x4 a[PF + 1];                                                           \
+    _Pragma("unroll") for (int t = 0; t < PF; ++t) a[t] = ald(slot, t);        \
     _Pragma("unroll") for (int t = 0; t < 4 * I; ++t) {                        \
-      if (t + 3 < 4 * I) a[(t + 3) & 3] = ald(slot, t + 3);                    \
+      if (t + PF < 4 * I) a[(t + PF) % (PF + 1)] = ald(slot, t + PF);          \
       _Pragma("unroll") for (int j = 0; j < J; ++j)                            \
-          Mfma32<DT>::run(acc[t % I][j], BF(t / I, j), a[t & 3]);              \
+          Mfma32<DT>::run(acc[t % I][j], BF(t / I, j), a[t % (PF + 1)]);       \
       __VA_ARGS__;                                                             \
       __builtin_amdgcn_sched_barrier(0);                                       \
     }                                                                          \
@@ -208,18 +210,22 @@ __global__ __launch_bounds__(512, 1) void gemm_fq5_kernel(
   for (; kt < nkm; ++kt) {
     // retire stage kt; the DMA of stage kt+1 (issued after it) may stay in flight
     if (kt + 1 < nkt) {
-      if (kt + 1 < nkm) vm_wait<F5_VM_CODES>();
+      if (NOWAIT) {
+      } else if (kt + 1 < nkm) vm_wait<F5_VM_CODES>();
       else vm_wait<F5_VM_DENSE>();
     } else {
       vm_wait<0>();
     }
-    raw_barrier();  // every wave's DMA for stage kt has landed; slot (kt+2)%3 is free
+    if (NOWAIT < 2) raw_barrier();  // every wave's DMA for stage kt has landed; slot (kt+2)%3 is free
     if (kt + 2 < nkt) issue(kt + 2);
     compute_codes(lds + (kt % F5_NSLOT) * F5_SLOT);
   }
   for (; kt < nkt; ++kt) {
-    if (kt + 1 < nkt) vm_wait<F5_VM_DENSE>();
-    else vm_wait<0>();
+    if (kt + 1 < nkt) {
+      if (!NOWAIT) vm_wait<F5_VM_DENSE>();
+    } else {
+      vm_wait<0>();
+    }
     raw_barrier();
     if (kt + 2 < nkt) issue(kt + 2);
     compute_dense(lds + (kt % F5_NSLOT) * F5_SLOT);
@@ -469,13 +475,13 @@ __global__ __launch_bounds__(256, 1) void gemm_i8v2_kernel(
 }
 
 // ================================================================= launchers
-template <class DT, int GB, int WMW>
+template <class DT, int GB, int WMW, int PF = 3, int NOWAIT = 0>
 static int fq5_launch(const void* a, const void* codes, const void* wscale, const void* wsal,
                       const void* bias, void* y, int M, int N, int Kp, int S_pad, int Gw,
                       int ngw, hipStream_t s) {
   typedef typename DT::T T;
   const int tiles_m = cdiv(M, 256), tiles_n = cdiv(N, 256);
-  gemm_fq5_kernel<DT, GB, WMW><<<dim3(tiles_m * tiles_n), dim3(512), 0, s>>>(
+  gemm_fq5_kernel<DT, GB, WMW, PF, NOWAIT><<<dim3(tiles_m * tiles_n), dim3(512), 0, s>>>(
       (const T*)a, codes, (const T*)wscale, (const T*)wsal, (const T*)bias, (T*)y, M, N, Kp,
       S_pad, Gw, ngw, tiles_m, tiles_n);
   SQMP_LAUNCH_CHECK();
@@ -493,11 +499,18 @@ static int fq5_dispatch(const void* a, const void* codes, const void* wscale, co
   return SQMP_EUNSUPPORTED;
 }
 
-// Waves along M of the fq5 tile (tuning knob, SQMP_FQ_WAVES_M = 1 or 2).
-static int fq_waves_m() {
+// fq5 tile variant (tuning knob SQMP_FQ_VARIANT): "wm1" (default), "wm2" (2 x 4 waves),
+// "pf6" (wm1, 6-block A read-ahead), "nowait" / "nobar" (timing diagnostics that skip the
+// DMA waits / also the stage barrier of the codes loop: wrong results, in-bounds addresses).
+static int fq_variant() {
   static int v = [] {
-    const char* e = getenv("SQMP_FQ_WAVES_M");
-    return (e && e[0] == '2') ? 2 : 1;
+    const char* e = getenv("SQMP_FQ_VARIANT");
+    if (!e) return 0;
+    if (!strcmp(e, "wm2")) return 1;
+    if (!strcmp(e, "pf6")) return 2;
+    if (!strcmp(e, "nowait")) return 3;
+    if (!strcmp(e, "nobar")) return 4;
+    return 0;
   }();
   return v;
 }
@@ -505,13 +518,20 @@ static int fq_waves_m() {
 int launch_gemm_fq_fast(int dtype, const void* a, const void* codes, const void* wscale,
                         const void* wsal, const void* bias, void* y, int M, int N, int Kp,
                         int S_pad, int Gw, int ngw, int n_bits, hipStream_t s) {
-  const bool two = fq_waves_m() == 2;
-  if (dtype == SQMP_F16)
-    return two ? fq5_dispatch<F16, 2>(a, codes, wscale, wsal, bias, y, M, N, Kp, S_pad, Gw, ngw, n_bits, s)
-               : fq5_dispatch<F16, 1>(a, codes, wscale, wsal, bias, y, M, N, Kp, S_pad, Gw, ngw, n_bits, s);
+  const int v = fq_variant();
+  if (dtype == SQMP_F16) {
+    if (v == 2 && n_bits == 4 && Gw % 64 == 0)
+      return fq5_launch<F16, 1, 1, 6>(a, codes, wscale, wsal, bias, y, M, N, Kp, S_pad, Gw, ngw, s);
+    if (v == 3 && n_bits == 4 && Gw % 64 == 0)
+      return fq5_launch<F16, 1, 1, 3, 1>(a, codes, wscale, wsal, bias, y, M, N, Kp, S_pad, Gw, ngw, s);
+    if (v == 4 && n_bits == 4 && Gw % 64 == 0)
+      return fq5_launch<F16, 1, 1, 3, 2>(a, codes, wscale, wsal, bias, y, M, N, Kp, S_pad, Gw, ngw, s);
+    return v == 1 ? fq5_dispatch<F16, 2>(a, codes, wscale, wsal, bias, y, M, N, Kp, S_pad, Gw, ngw, n_bits, s)
+                  : fq5_dispatch<F16, 1>(a, codes, wscale, wsal, bias, y, M, N, Kp, S_pad, Gw, ngw, n_bits, s);
+  }
   if (dtype == SQMP_BF16)
-    return two ? fq5_dispatch<BF16, 2>(a, codes, wscale, wsal, bias, y, M, N, Kp, S_pad, Gw, ngw, n_bits, s)
-               : fq5_dispatch<BF16, 1>(a, codes, wscale, wsal, bias, y, M, N, Kp, S_pad, Gw, ngw, n_bits, s);
+    return v == 1 ? fq5_dispatch<BF16, 2>(a, codes, wscale, wsal, bias, y, M, N, Kp, S_pad, Gw, ngw, n_bits, s)
+                  : fq5_dispatch<BF16, 1>(a, codes, wscale, wsal, bias, y, M, N, Kp, S_pad, Gw, ngw, n_bits, s);
   return SQMP_EUNSUPPORTED;
 }
 

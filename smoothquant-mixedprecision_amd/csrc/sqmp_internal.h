@@ -6,13 +6,14 @@ namespace sqmp {
 
 // cmax[c] = bits(max_r |x[r][c]|) over a contiguous D matrix [R][C] (fp32 bits of the
 // D value; non-negative floats order like their bit patterns).  Zeroes cmax first.
-int launch_colmax(const void* x, int dtype, int R, int C, uint32_t* cmax, hipStream_t s);
+int launch_colmax(const void* x, int dtype, int R, int C, uint32_t* cmax, hipStream_t s,
+                  bool zero = true);  // zero: clear cmax first (else the caller did)
 
 // Stable ascending rank of the list cols[0..L) (NULL = identity) keyed by cmax[col]:
 // rank_by_col[cols[i]] = #{j : (cmax[cols[j]], j) < (cmax[cols[i]], i)}.  Zeroes the
 // C-entry rank_by_col first.
 int launch_rank(const uint32_t* cmax, const int32_t* cols, int L, int C,
-                int32_t* rank_by_col, hipStream_t s);
+                int32_t* rank_by_col, hipStream_t s, bool zero = true);
 
 // Index maps of a packed weight (see include/sqmp_w4a4.h).  rank_by_col == NULL keeps the
 // original column order (per_channel / per_tensor / unsorted per_group).

@@ -25,6 +25,7 @@ __global__ __launch_bounds__(256) void colmax_kernel(const typename DT::T* __res
 #pragma unroll
   for (int i = 0; i < VEC; ++i) m[i] = 0.f;
   if (c0 + VEC <= C && VEC > 1) {
+#pragma unroll 8
     for (int r = r0 + wid; r < r1; r += 4) {
       const u32x4 raw = *(const u32x4*)(x + (size_t)r * C + c0);
       const T* v = (const T*)&raw;
@@ -67,8 +68,9 @@ static void colmax_launch(const void* x, int R, int C, uint32_t* cmax, hipStream
   }
 }
 
-int launch_colmax(const void* x, int dtype, int R, int C, uint32_t* cmax, hipStream_t s) {
-  SQMP_HIP_CHECK(hipMemsetAsync(cmax, 0, sizeof(uint32_t) * (size_t)C, s));
+int launch_colmax(const void* x, int dtype, int R, int C, uint32_t* cmax, hipStream_t s,
+                  bool zero) {
+  if (zero) SQMP_HIP_CHECK(hipMemsetAsync(cmax, 0, sizeof(uint32_t) * (size_t)C, s));
   if (R <= 0 || C <= 0) return SQMP_OK;
   switch (dtype) {
     case SQMP_F32: colmax_launch<F32>(x, R, C, cmax, s); break;
@@ -81,41 +83,42 @@ int launch_colmax(const void* x, int dtype, int R, int C, uint32_t* cmax, hipStr
 }
 
 // ------------------------------------------------------------------ stable rank
-// 2-D grid of (256 owners) x (1024 competitors); each owner counts competitors with a
-// smaller composite key (value bits << 32 | list index) and adds its partial count.
-// O(L^2) compares, fully parallel, deterministic and stable by construction.
-constexpr int RANK_TILE = 1024;
+// 2-D grid of (256 owners) x (RANK_TILE competitors); each owner counts competitors that
+// order before it -- (value, list index) lexicographically, i.e. a stable ascending sort
+// -- and adds its partial count.  O(L^2) 32-bit compares over broadcast LDS reads,
+// fully parallel, deterministic and stable by construction.
+constexpr int RANK_TILE = 256;
 
 __global__ __launch_bounds__(256) void rank_kernel(const uint32_t* __restrict__ cmax,
                                                    const int32_t* __restrict__ cols, int L,
                                                    int32_t* __restrict__ rank_by_col) {
-  __shared__ uint64_t keys[RANK_TILE];
+  __shared__ uint32_t kv[RANK_TILE];
   const int j0 = blockIdx.y * RANK_TILE;
   const int jn = min(RANK_TILE, L - j0);
-  for (int t = threadIdx.x; t < RANK_TILE; t += 256) {
-    const int j = j0 + t;
-    uint64_t k = ~0ull;  // sentinel: never smaller than a real key
-    if (t < jn) {
-      const int c = cols ? cols[j] : j;
-      k = ((uint64_t)cmax[c] << 32) | (uint32_t)j;
-    }
-    keys[t] = k;
+  {
+    const int t = threadIdx.x;
+    // sentinel above every non-negative float's bits: never orders first
+    kv[t] = t < jn ? cmax[cols ? cols[j0 + t] : j0 + t] : 0xFFFFFFFFu;
   }
   __syncthreads();
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i >= L) return;
   const int ci = cols ? cols[i] : i;
-  const uint64_t mine = ((uint64_t)cmax[ci] << 32) | (uint32_t)i;
+  const uint32_t mine = cmax[ci];
+  const int lim = i - j0;  // competitors t < lim have a lower list index
   int cnt = 0;
-#pragma unroll 8
-  for (int t = 0; t < RANK_TILE; ++t) cnt += keys[t] < mine ? 1 : 0;
+#pragma unroll 16
+  for (int t = 0; t < RANK_TILE; ++t) {
+    const uint32_t k = kv[t];
+    cnt += (k < mine || (k == mine && t < lim)) ? 1 : 0;
+  }
   if (cnt) atomicAdd(&rank_by_col[ci], cnt);
 }
 
 int launch_rank(const uint32_t* cmax, const int32_t* cols, int L, int C,
-                int32_t* rank_by_col, hipStream_t s) {
+                int32_t* rank_by_col, hipStream_t s, bool zero) {
   // rank_by_col is indexed by column: clear the whole column range the list can touch.
-  SQMP_HIP_CHECK(hipMemsetAsync(rank_by_col, 0, sizeof(int32_t) * (size_t)C, s));
+  if (zero) SQMP_HIP_CHECK(hipMemsetAsync(rank_by_col, 0, sizeof(int32_t) * (size_t)C, s));
   if (L <= 0) return SQMP_OK;
   dim3 grid(cdiv(L, 256), cdiv(L, RANK_TILE));
   rank_kernel<<<grid, dim3(256), 0, s>>>(cmax, cols, L, rank_by_col);

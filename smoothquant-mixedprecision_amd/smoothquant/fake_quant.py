@@ -111,7 +111,7 @@ _PACKED_BUFFERS = ("w_codes", "w_scale", "w_salient", "w_perm", "w_amap", "w_ama
 class W4A4Linear(nn.Module):
     """Mixed-precision W4A4 linear: salient input channels in D, the rest int4/int8.
 
-    Forward kernels (chosen per layer, see `kernel`):
+    Forward kernels (chosen per layer, see `kernel`; "auto" = "fq" unless ops.I8_AUTO):
       "i8"  per_token / per_tensor activations: int8 act codes x int4 weight codes on the
             i8 MFMA with per-group fp32 folds (exact scale factorisation).
       "fq"  every act mode: dequantized activations x in-kernel-decoded weights on the D
@@ -262,7 +262,8 @@ class W4A4Linear(nn.Module):
             raise RuntimeError(f"bias dtype {bias.dtype} does not match {pw.dtype}")
         bits = self.quant_bits
         use_i8 = (self.kernel == "i8" or
-                  (self.kernel == "auto" and ops.i8_eligible(pw, self.act_quant_name, bits)))
+                  (self.kernel == "auto" and ops.I8_AUTO
+                   and ops.i8_eligible(pw, self.act_quant_name, bits)))
         if use_i8:
             a8, sa, xs = ops.quant_act_i8(xc, pw, self.act_quant_name, bits)
         else:

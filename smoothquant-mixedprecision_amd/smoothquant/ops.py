@@ -244,6 +244,11 @@ def gemm_i8(a8: torch.Tensor, sa: torch.Tensor, xs: torch.Tensor, pw: PackedWeig
     return y
 
 
+# Whether W4A4Linear(kernel="auto") takes the integer path for eligible layers.  Off: on
+# gfx950 the faithful fq GEMM is currently faster than gemm_i8 (perf log).
+I8_AUTO = False
+
+
 def i8_eligible(pw: PackedWeight, act_quant: str, act_bits: int) -> bool:
     """Whether the integer MFMA path computes this layer (exact-scale factorisation)."""
     return (act_quant in ("per_token", "per_tensor") and pw.dtype != torch.float32

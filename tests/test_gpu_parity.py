@@ -324,3 +324,39 @@ def test_full_size_config2_properties():
     W_np = to_np(W).astype(np.float16)
     w_hat = O.w4a4_from_float(W_np, "per_group", 4, Gs, sal, D)
     assert bits_equal(to_np(q.weight)[w_rows], D.f32(w_hat)[w_rows])
+
+
+# ------------------------------------------------------------------ rounding stress
+@pytest.mark.parametrize("dt", ["fp16", "bf16"])
+@pytest.mark.parametrize("act", ["per_token", "per_tensor", "per_group"])
+def test_act_quant_rounding_stress(dt, act):
+    """The activation operand x_hat = D(rne(D(x / s)) * s) is bit-exact on ~1M elements.
+    The kernel divides by multiplying with RN(1/s) and falls back to the exact division
+    only within a few fp32 ulps of a D rounding midpoint (sqmp_actquant.hip fast_code);
+    random data hits that window ~1e-3 of the time, and rows whose scale is a power of two
+    put quotients exactly on half-integers (round-half-even of the code)."""
+    dev = _dev()
+    from smoothquant import ops
+    D = O.DT(dt)
+    M, K, N, Gs = 512, 2048, 256, 128
+    g = np.random.default_rng(zlib.crc32(f"stress-{dt}-{act}".encode()))
+    x = g.standard_normal((M, K)).astype(np.float32)
+    x[:, g.permutation(K)[:20]] *= 25.0
+    # rows 0..63: absmax 7 * 2^e -> s = 2^e exactly, the rest multiples of s/2 (ties)
+    for r in range(64):
+        e = int(g.integers(-6, 3))
+        x[r] = np.round(x[r] * 2.0) / 2.0 * 2.0 ** e
+        x[r] = np.clip(x[r], -7 * 2.0 ** e, 7 * 2.0 ** e)
+        x[r, 0] = 7 * 2.0 ** e
+    x = D.rnd(x)
+    W = D.rnd(g.standard_normal((N, K)).astype(np.float32) * 0.02)
+    imp = torch.from_numpy(np.abs(g.standard_normal(K)).astype(np.float32))
+    q = make_layer(W, None, dt, dev, weight_quant="per_channel", act_quant=act,
+                   importance=imp, salient_prop=0.05, quant_bits=4, group_size=Gs)
+    pw = q.packed()
+    xt = to_t(x, dt, dev)
+    a = ops.quant_act_fp(xt, pw, act, 4, Gs)
+    got = a_operand_to_original(q, a, K)
+    sal = q.salient_indices.cpu().numpy()
+    want = O.quantize_input(x, act, 4, Gs, sal, D)
+    assert bits_equal(got, D.f32(want))

@@ -1,0 +1,37 @@
+"""Time the W4A4 GEMM alone on BASELINE config 2 (HIP events, GEMM on torch's current
+stream).  python tools/gemm_time.py [fq|i8] [iters]  -> one line: kind, avg ms, TFLOP/s."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "smoothquant-mixedprecision_amd")]
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+from smoothquant import ops  # noqa: E402
+
+kind = sys.argv[1] if len(sys.argv) > 1 else "fq"
+iters = int(sys.argv[2]) if len(sys.argv) > 2 else 50
+dev = torch.device("cuda")
+act = "per_group" if kind == "fq" else "per_token"
+q, x, lin = bench.make_layer(dev, act, seed=1)
+pw = q.packed()
+if kind == "fq":
+    a = ops.quant_act_fp(x, pw, act, 4, bench.G)
+    run = lambda: ops.gemm_fq(a, pw, lin.bias)  # noqa: E731
+else:
+    a8, sa, xs = ops.quant_act_i8(x, pw, act, 4)
+    run = lambda: ops.gemm_i8(a8, sa, xs, pw, lin.bias)  # noqa: E731
+for _ in range(5):
+    run()
+torch.cuda.synchronize()
+e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+e0.record()
+for _ in range(iters):
+    run()
+e1.record()
+torch.cuda.synchronize()
+ms = e0.elapsed_time(e1) / iters
+M, K, N = x.shape[0], x.shape[1], lin.out_features
+print(f"{kind} variant={os.environ.get('SQMP_FQ_VARIANT', 'default')} avg_ms={ms:.4f} "
+      f"TFLOP/s={2 * M * N * K / ms / 1e9:.1f}")
