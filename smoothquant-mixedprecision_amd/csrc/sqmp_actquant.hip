@@ -406,6 +406,173 @@ __global__ __launch_bounds__(256) void quant_fp_kernel(
   }
 }
 
+// ---------------------------------------------------------------- wave-per-row variant
+// Same arithmetic as quant_fp_kernel, but each wave owns whole rows: no block barrier on
+// the per-row path, so every wave of the CU streams its own rows (next row prefetched
+// into registers while this one is quantized).  RCH = 16-B row chunks per lane
+// (K * esize <= RCH * 1 KiB), VCH = 8-position output chunks per lane (P <= VCH * 512).
+// The block (4 waves) shares the entry table and the salient column list.
+template <class DT, int MODE, int RCH, int VCH>
+__global__ __launch_bounds__(256) void quant_fp_wave_kernel(
+    const typename DT::T* __restrict__ x, int M, int K, int q_max, int G, int nga,
+    const int32_t* __restrict__ amap, int P, const int32_t* __restrict__ nonsal, int Kn,
+    const int32_t* __restrict__ sal, int S, int S_pad,
+    const int32_t* __restrict__ rank_by_col, const uint32_t* __restrict__ cmax,
+    typename DT::T* __restrict__ out) {
+  typedef typename DT::T T;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_w[];
+  const int NCH = P / 8;
+  const int W = P + S_pad, WCH = W / 8;
+  const int rowb = (int)round_up_dev(K * (int)sizeof(T), 16);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  u32x4* ent = (u32x4*)smem_w;                                   // [2][NCH]
+  uint16_t* salc = (uint16_t*)(ent + 2 * NCH);                   // S_pad
+  unsigned char* wbase = (unsigned char*)(salc + round_up_dev(S_pad, 8));
+  const int wbytes = rowb + (int)round_up_dev(12 * nga, 16);
+  T* row = (T*)(wbase + wave * wbytes);                          // this wave's row
+  float2* scr = (float2*)((unsigned char*)row + rowb);           // nga
+  uint32_t* gmax = (uint32_t*)(scr + nga);                       // nga
+  uint16_t* grp = (uint16_t*)wbase;  // init scratch (K entries), aliases the row buffers
+  const float invG = 1.0f / (float)G;
+
+  // ---- block-wide tables (the only block barriers)
+  for (int k = tid; k < K; k += 256) grp[k] = (uint16_t)G_ZERO;
+  for (int j = tid; j < S_pad; j += 256) salc[j] = j < S ? (uint16_t)sal[j] : (uint16_t)0xFFFFu;
+  __syncthreads();
+  for (int i = tid; i < Kn; i += 256) {
+    const int k = nonsal[i];
+    int g = 0;
+    if (MODE == MODE_GROUP) g = fdiv_floor_a(rank_by_col ? rank_by_col[k] : i, G, invG);
+    grp[k] = (uint16_t)g;
+  }
+  __syncthreads();
+  for (int c = tid; c < NCH; c += 256) {
+    uint32_t e[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int k = amap[c * 8 + j];
+      e[j] = k >= 0 ? (((uint32_t)grp[k] << 16) | (uint32_t)k) : (G_ZERO << 16);
+    }
+    ent[c] = u32x4{e[0], e[1], e[2], e[3]};
+    ent[NCH + c] = u32x4{e[4], e[5], e[6], e[7]};
+  }
+  float s_all = 0.f, r_all = 0.f;
+  if (MODE == MODE_TENSOR) {
+    float m = 0.f;
+    for (int i = lane; i < Kn; i += 64) m = fmaxf(m, __uint_as_float(cmax[nonsal[i]]));
+    m = wave_max(m);
+    s_all = group_scale<DT>(m, q_max);
+    r_all = 1.0f / s_all;
+  }
+  __syncthreads();  // grp scratch dead from here on: row buffers are the waves' own
+
+  const int nch = K / 8;
+  const int wstride = gridDim.x * 4;
+  u32x4 nxt[RCH];
+  auto load_row = [&](int mm) {
+    const u32x4* src = (const u32x4*)(x + (size_t)mm * K);
+#pragma unroll
+    for (int i = 0; i < RCH; ++i) {
+      const int c = lane + 64 * i;
+      if (c < nch) nxt[i] = src[c];
+    }
+  };
+  int m = blockIdx.x * 4 + wave;
+  if (m < M) load_row(m);
+  for (; m < M; m += wstride) {
+#pragma unroll
+    for (int i = 0; i < RCH; ++i) {
+      const int c = lane + 64 * i;
+      if (c < nch) ((u32x4*)row)[c] = nxt[i];
+    }
+    if (m + wstride < M) load_row(m + wstride);
+    if (MODE == MODE_GROUP)
+      for (int g = lane; g < nga; g += 64) gmax[g] = 0u;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    // ---- gather pass
+    uint32_t vals[VCH][4];
+    float lmax = 0.f;
+#pragma unroll
+    for (int i = 0; i < VCH; ++i) {
+      const int c = lane + 64 * i;
+      if (c < NCH) {
+        const u32x4 e0 = ent[c], e1 = ent[NCH + c];
+        const uint32_t e[8] = {e0[0], e0[1], e0[2], e0[3], e1[0], e1[1], e1[2], e1[3]};
+        T v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const uint32_t g = e[j] >> 16;
+          v[j] = g != G_ZERO ? row[e[j] & 0xFFFFu] : DT::from_f(0.f);
+          const float a = fabsf(DT::to_f(v[j]));
+          if (MODE == MODE_GROUP) {
+            if (g != G_ZERO && a > 0.f) atomicMax(&gmax[g], __float_as_uint(a));
+          } else {
+            lmax = fmaxf(lmax, a);
+          }
+        }
+#pragma unroll
+        for (int w = 0; w < 4; ++w) vals[i][w] = ((const uint32_t*)v)[w];
+      }
+    }
+    float s_row = s_all, r_row = r_all;
+    if (MODE == MODE_TOKEN) {
+      s_row = group_scale<DT>(wave_max(lmax), q_max);
+      r_row = 1.0f / s_row;
+    } else if (MODE == MODE_GROUP) {
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      for (int g = lane; g < nga; g += 64) {
+        const float sg = group_scale<DT>(__uint_as_float(gmax[g]), q_max);
+        scr[g] = make_float2(sg, 1.0f / sg);
+      }
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    }
+    // ---- quantize from registers, 16-B stores
+    T* o = out + (size_t)m * W;
+#pragma unroll
+    for (int i = 0; i < VCH; ++i) {
+      const int c = lane + 64 * i;
+      if (c < NCH) {
+        const u32x4 e0 = ent[c], e1 = ent[NCH + c];
+        const uint32_t e[8] = {e0[0], e0[1], e0[2], e0[3], e1[0], e1[1], e1[2], e1[3]};
+        const T* v = (const T*)vals[i];
+        T r[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const uint32_t g = e[j] >> 16;
+          float y = 0.f;
+          if (g != G_ZERO) {
+            const float2 sr = MODE == MODE_GROUP ? scr[g] : make_float2(s_row, r_row);
+            y = fast_code<DT>(DT::to_f(v[j]), sr.x, sr.y) * sr.x;
+          }
+          r[j] = DT::from_f(y);
+        }
+        ((u32x4*)o)[c] = *(const u32x4*)r;
+      }
+    }
+    for (int c = NCH + lane; c < WCH; c += 64) {
+      T r[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const uint32_t k = salc[(c - NCH) * 8 + j];
+        r[j] = k != 0xFFFFu ? row[k] : DT::from_f(0.f);
+      }
+      ((u32x4*)o)[c] = *(const u32x4*)r;
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");  // row / gmax reuse
+  }
+}
+
+static size_t quant_fp_wave_lds_bytes(int K, int P, int nga, int S_pad, int esize) {
+  // entry table + salient list + 4 per-wave (row, scales, group max) regions; the
+  // init-time column->group scratch (2K bytes) lives inside the row regions
+  const size_t wb = (size_t)round_up((long)K * esize, 16) + (size_t)round_up(12L * nga, 16);
+  return 4 * (size_t)P + 2 * (size_t)round_up(S_pad, 8) + 4 * wb;
+}
+
 static size_t quant_fp_lds_bytes(int K, int P, int nga, int S_pad, int esize) {
   return (size_t)round_up((long)K * esize, 16) + 4 * (size_t)P + (size_t)round_up(2L * K, 16) +
          12 * (size_t)nga + 2 * (size_t)round_up(S_pad, 8) + 64;
@@ -433,6 +600,24 @@ static int quant_launch(void* x, int M, int K, int q_max, int G, int nga, const 
   quant_act_kernel<DT, MODE, OUT><<<dim3(grid), dim3(256), lds, s>>>(
       (T*)x, M, K, q_max, G, nga, amap, P, nonsal, Kn, sal, S, S_pad, rank, cmax, out,
       (float*)out_scale, (T*)out_xs);
+  SQMP_LAUNCH_CHECK();
+  return SQMP_OK;
+}
+
+template <class DT, int MODE, int RCH, int VCH>
+static int quant_fpw_launch(void* x, int M, int K, int q_max, int G, int nga, const int32_t* amap,
+                            int P, const int32_t* nonsal, int Kn, const int32_t* sal, int S,
+                            int S_pad, const int32_t* rank, const uint32_t* cmax, void* out,
+                            size_t lds, hipStream_t s) {
+  typedef typename DT::T T;
+  SQMP_HIP_CHECK(hipFuncSetAttribute((const void*)quant_fp_wave_kernel<DT, MODE, RCH, VCH>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  int per_cu = (int)((160 * 1024) / lds);
+  per_cu = per_cu < 1 ? 1 : (per_cu > 8 ? 8 : per_cu);
+  int grid = 256 * per_cu;
+  if (grid > cdiv(M, 4)) grid = cdiv(M, 4);
+  quant_fp_wave_kernel<DT, MODE, RCH, VCH><<<dim3(grid), dim3(256), lds, s>>>(
+      (const T*)x, M, K, q_max, G, nga, amap, P, nonsal, Kn, sal, S, S_pad, rank, cmax, (T*)out);
   SQMP_LAUNCH_CHECK();
   return SQMP_OK;
 }
@@ -468,6 +653,22 @@ static int quant_dispatch(void* x, int M, int K, int amode, int q_max, int G, in
                    : amode == SQMP_ACT_PER_TENSOR ? MODE_TENSOR
                                                   : MODE_GROUP;
   if constexpr (DT::id != SQMP_F32) {
+  if (out_kind == SQMP_OUT_FP && K % 8 == 0 && K <= 8192 && P <= 8192 &&
+      (((uintptr_t)x) % 16 == 0)) {
+    const size_t lds = quant_fp_wave_lds_bytes(K, P, nga, S_pad, sizeof(typename DT::T));
+    if (lds <= 160 * 1024) {
+      const bool small = K <= 4096 && P <= 4096;
+#define SQMP_QW(MODE)                                                                          \
+  (small ? quant_fpw_launch<DT, MODE, 8, 8>(x, M, K, q_max, G, nga, amap, P, nonsal, Kn, sal, S, \
+                                            S_pad, rank, cmax, out, lds, s)                    \
+         : quant_fpw_launch<DT, MODE, 16, 16>(x, M, K, q_max, G, nga, amap, P, nonsal, Kn, sal, \
+                                              S, S_pad, rank, cmax, out, lds, s))
+      if (mode == MODE_TOKEN) return SQMP_QW(MODE_TOKEN);
+      if (mode == MODE_TENSOR) return SQMP_QW(MODE_TENSOR);
+      return SQMP_QW(MODE_GROUP);
+#undef SQMP_QW
+    }
+  }
   if (out_kind == SQMP_OUT_FP && K % 8 == 0 && K * 2 <= PFC_FP * 256 * 16 &&
       P <= FCH * 256 * 8 && (((uintptr_t)x) % 16 == 0)) {
     const size_t lds = quant_fp_lds_bytes(K, P, nga, S_pad, sizeof(typename DT::T));
