@@ -202,6 +202,71 @@ class W4A4Linear(nn.Module):
                             m["S"], m["S_pad"], m["Kp"], m["Gw"], m["ngw"], m["n_bits"],
                             m["wmode"], m["dtype"], self.w_dense)
 
+    # ------------------------------------------------------------------ persistence
+    # Packed format (the reference persists only the dequantized weight
+    # and drops salient_indices).  state_dict() holds the packed buffers (w_codes, w_scale,
+    # w_salient, maps) plus `_extra_state`: plain ints / strings / an int64 tensor, so a
+    # checkpoint loads with torch.load(weights_only=True) and needs no recalibration.
+    EXTRA_FORMAT = "sqmp-w4a4-packed/1"
+
+    def get_extra_state(self):
+        m = self._meta
+        return {
+            "format": self.EXTRA_FORMAT,
+            "in_features": self.in_features, "out_features": self.out_features,
+            "quant_bits": self.quant_bits, "group_size": self.group_size,
+            "act_quant": self.act_quant_name, "output_quant": self.output_quant_name,
+            "weight_quant": self.weight_quant_name, "kernel": self.kernel,
+            "salient_indices": (None if self.salient_indices is None
+                                else self.salient_indices.detach().to("cpu", torch.int64)),
+            "meta": None if m is None else {k: (str(v).replace("torch.", "") if k == "dtype" else int(v))
+                                            for k, v in m.items()},
+        }
+
+    def set_extra_state(self, state):
+        if not isinstance(state, dict) or state.get("format") != self.EXTRA_FORMAT:
+            raise RuntimeError(f"W4A4Linear: unsupported extra state {type(state)}")
+        if (state["in_features"], state["out_features"]) != (self.in_features, self.out_features):
+            raise RuntimeError("W4A4Linear: checkpoint shape does not match the module")
+        self.quant_bits = state["quant_bits"]
+        self.group_size = state["group_size"]
+        act = state["act_quant"]
+        self.act_quant_name = act
+        self.act_quant = partial(_ACT_FNS[act], n_bits=self.quant_bits,
+                                 **({"group_size": self.group_size} if act == "per_group" else {}))
+        if state["output_quant"] != "None":
+            self.output_quant_name, self.output_quant = self.act_quant_name, self.act_quant
+        else:
+            self.output_quant_name, self.output_quant = "None", (lambda x: x)
+        self.weight_quant_name = state["weight_quant"]
+        self.kernel = state.get("kernel", "auto")
+        sal = state["salient_indices"]
+        self.salient_indices = None if sal is None else sal.clone()
+        meta = state["meta"]
+        if meta is not None:
+            meta = dict(meta)
+            meta["dtype"] = getattr(torch, meta["dtype"])
+            self._meta = meta
+            self._random_init = False
+
+    def _load_from_state_dict(self, state_dict, prefix, local_metadata, strict, missing_keys,
+                              unexpected_keys, error_msgs):
+        sd = state_dict
+        if prefix + "_extra_state" in sd:
+            # size the packed buffers (None in a fresh module) from the checkpoint; the
+            # default loader below then copies every key, strictly
+            for name in _PACKED_BUFFERS:
+                t = sd.get(prefix + name)
+                setattr(self, name, None if t is None else torch.empty_like(t))
+            if prefix + "bias" in sd and self.bias is not None:
+                self.bias = torch.empty_like(sd[prefix + "bias"])
+        elif prefix + "weight" in sd:
+            # a reference checkpoint (dequantized `weight` buffer): stored as given
+            self.weight = sd[prefix + "weight"]
+            sd = {k: v for k, v in sd.items() if k != prefix + "weight"}
+        super()._load_from_state_dict(sd, prefix, local_metadata, strict, missing_keys,
+                                      unexpected_keys, error_msgs)
+
     # the reference's `weight` buffer (dequantized W_hat, fake_quant.py:357-365)
     @property
     def weight(self) -> torch.Tensor:

@@ -360,3 +360,33 @@ def test_act_quant_rounding_stress(dt, act):
     sal = q.salient_indices.cpu().numpy()
     want = O.quantize_input(x, act, 4, Gs, sal, D)
     assert bits_equal(got, D.f32(want))
+
+
+# ------------------------------------------------------------------ packed checkpoints
+def test_packed_checkpoint_roundtrip(tmp_path):
+    """A quantized layer saved with its packed state reloads into a fresh module (safe
+    loader) and computes the identical output, with no re-quantization."""
+    dev = _dev()
+    import os
+    from smoothquant.checkpoint import load_quantized, save_quantized
+    from smoothquant.fake_quant import W4A4Linear
+    g = np.random.default_rng(11)
+    K, N = 512, 512
+    W = g.standard_normal((N, K)).astype(np.float32) * 0.02
+    b = g.standard_normal(N).astype(np.float32) * 0.01
+    imp = torch.from_numpy(np.abs(g.standard_normal(K)).astype(np.float32))
+    model = torch.nn.Sequential(torch.nn.Linear(K, N), torch.nn.Linear(N, N)).to(dev).half()
+    model[0] = make_layer(W, b, "fp16", dev, weight_quant="per_group", act_quant="per_group",
+                          importance=imp, salient_prop=0.05, quant_bits=4, group_size=64)
+    model[1] = make_layer(W, b, "fp16", dev, weight_quant="per_channel", act_quant="per_token",
+                          quantize_output=True, importance=imp, salient_prop=0.05)
+    x = to_t(g.standard_normal((64, K)), "fp16", dev)
+    y0 = model(x.clone())
+    p = os.path.join(tmp_path, "q.pt")
+    save_quantized(model, p)
+    fresh = torch.nn.Sequential(torch.nn.Linear(K, N), torch.nn.Linear(N, N)).to(dev).half()
+    load_quantized(fresh, p)
+    assert all(isinstance(m, W4A4Linear) for m in fresh)
+    y1 = fresh(x.clone())
+    assert bits_equal(to_np(y1), to_np(y0))
+    assert bits_equal(to_np(fresh[0].weight), to_np(model[0].weight))
