@@ -246,7 +246,7 @@ def main():
             "unit": "TFLOP/s",
             "frac": round(achieved / PEAK_TFLOPS[kdt], 4),
             "traffic": traffic,
-            "kernel": "sqmp::gemm_i8v2_kernel<F16>" if use_i8 else "sqmp::gemm_fq5_kernel<F16,1,1>",
+            "kernel": "sqmp::gemm_i8v2_kernel<F16>" if use_i8 else "sqmp::gemm_fq6_kernel<F16,1>",
             "avg_ms": round(gemm_ms, 4),
             "algorithmic_flops_per_launch": flops,
         },

@@ -12,7 +12,7 @@
 //   vector issue for 8 of its 32 cycles (16x16x32: 8 of 16), which leaves the issue
 //   slots the int4 decode needs.  Every main-loop global byte moves by LDS-DMA
 //   (global_load_lds_dwordx4) into a 3-slot LDS ring, two 64-element K-stages ahead:
-//     A  256 rows x 128 B, 16-B chunks XOR-swizzled by (row >> 1) & 7
+//     A  256 rows x 128 B, 16-B chunks permuted (bitrev3) and XOR-swizzled by (row >> 1) & 7
 //     B  256 weight rows x one 32-B bpack block; lane half h reads its 16-B half (its four
 //        sub-step fragments) with one ds_read_b128, halves swizzled by (row >> 3) & 1
 //     S  the block's group scales, 1 KiB per wave (its columns).
@@ -50,6 +50,15 @@ constexpr int F5_VM_CODES = 4 + 1 + 1;           // DMA ops per wave per codes s
 constexpr int F5_VM_DENSE = 2 + 2;              // ... per 32-column dense stage
 constexpr int F5_DB = 16384;                     // dense stage: B image after 256 x 64 B of A
 
+// LDS images of the ring, shared by the 32x32x16 (fq5) and 16x16x32 (fq6) kernels:
+//   codes-stage A: 256 rows x 128 B, logical 16-B chunk c of row r at physical chunk
+//     a_pchunk(c, r) = bitrev3(c) ^ ((r >> 1) & 7) -- conflict-free for both fragment
+//     read patterns (32x32: chunk 2u+h; 16x16: chunk 4(q&1)+2s+(q>>1));
+//   dense-stage A and B: 256 rows x 64 B, chunk c of row r at c ^ d_f((r >> 2) & 3).
+__host__ __device__ inline int bitrev3(int c) { return ((c & 1) << 2) | (c & 2) | ((c >> 2) & 1); }
+__device__ inline int a_pchunk(int c, int r) { return bitrev3(c) ^ ((r >> 1) & 7); }
+__device__ inline int d_f(int g) { return (-g) & 3; }
+
 // GB = weight groups per 64-position block (1: Gw % 64 == 0, 2: Gw == 32);
 // GB = 0: dense D weights (no codes) in every main stage.  WMW = waves along M (1 or 2);
 // PF = A-fragment read-ahead (blocks); NOWAIT = 1 is a timing diagnostic only (skips the
@@ -84,14 +93,14 @@ __global__ __launch_bounds__(512, 1) void gemm_fq5_kernel(
   // ---- per-lane DMA source offsets (bytes); per-instruction steps are scalar
   // dense stage: A and B as 256 rows x 64 B, chunk c of row r at ((c ^ ((r >> 2) & 3)) << 4)
   const int drow = 16 * wave + (lane >> 2);
-  const int dchunk = (lane & 3) ^ ((lane >> 4) & 3);
+  const int dchunk = (lane & 3) ^ d_f((lane >> 4) & 3);
   const uint32_t ad_off = (uint32_t)((size_t)(m0 + drow) * lda * sizeof(T) + dchunk * 16);
   const uint32_t ad_str = (uint32_t)(128 * (size_t)lda * sizeof(T));
   const uint32_t bd_row0 = (uint32_t)min(n0 + drow, N - 1);
   const uint32_t bd_row1 = (uint32_t)min(n0 + drow + 128, N - 1);
   const int arow = 8 * wave + (lane >> 3);
   const uint32_t a_off = (uint32_t)((size_t)(m0 + arow) * lda * sizeof(T) +
-                                    (((lane & 7) ^ ((arow >> 1) & 7)) << 4));
+                                    (bitrev3((lane & 7) ^ ((arow >> 1) & 7)) << 4));
   const uint32_t a_str = (uint32_t)(64 * (size_t)lda * sizeof(T));
   const uint32_t b_off = (uint32_t)((size_t)(n0 + 32 * wave + (lane >> 1)) * (Kp / 2) +
                                     (((lane & 1) ^ ((lane >> 4) & 1)) << 4));
@@ -140,7 +149,7 @@ __global__ __launch_bounds__(512, 1) void gemm_fq5_kernel(
   const int a_row0 = (wm * MW + r32) * 128;
   const int a_sw = (r32 >> 1) & 7;
   auto ald = [&](const unsigned char* __restrict__ slot, int t) {
-    return *(const u32x4*)(slot + a_row0 + (t % I) * 4096 + (((2 * (t / I) + h) ^ a_sw) << 4));
+    return *(const u32x4*)(slot + a_row0 + (t % I) * 4096 + ((bitrev3(2 * (t / I) + h) ^ a_sw) << 4));
   };
   // 4*I blocks of J MFMAs; the A fragment of block t+3 is read during block t, one
   // sched_barrier per block keeps the compiler from hoisting every read, and HOOK runs
@@ -184,7 +193,7 @@ __global__ __launch_bounds__(512, 1) void gemm_fq5_kernel(
   };
 
   // dense stage: two 16-element sub-steps, A and B fragments both from the slot
-  const int d_sw = (r32 >> 2) & 3;
+  const int d_sw = d_f((r32 >> 2) & 3);
   auto compute_dense = [&](const unsigned char* __restrict__ slot) {
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
@@ -273,6 +282,195 @@ __global__ __launch_bounds__(512, 1) void gemm_fq5_kernel(
           for (int r = 0; r < 4; ++r)
             if (nb + r < N) dst[r] = v[r];
         }
+      }
+    }
+  }
+}
+
+// ================================================================= gemm_fq6
+// The fq5 ring and wave layout (1 x 8 waves, 256 x 32 per wave) on v_mfma_f32_16x16x32:
+// 16 x 2 tiles of 16 x 16 per wave (128 fp32 accumulators), two 32-element sub-steps per
+// 64-element stage.  Lane (r16, q) of sub-step s takes bpack dword 2q + s of its weight
+// row (one ds_read_b64 per tile column carries both sub-steps) and A chunk
+// 4 (q & 1) + 2 s + (q >> 1) -- the positions of that dword.  Same DMA ring, waits and
+// dense stages as fq5; dense stages give lane q chunk q of both 64-B rows.
+template <class DT, int GB>
+__global__ __launch_bounds__(512, 1) void gemm_fq6_kernel(
+    const typename DT::T* __restrict__ A, const void* __restrict__ Bw,
+    const typename DT::T* __restrict__ wscale, const typename DT::T* __restrict__ wsal,
+    const typename DT::T* __restrict__ bias, typename DT::T* __restrict__ Y, int M, int N,
+    int Kp, int S_pad, int Gw, int ngw, int tiles_m, int tiles_n) {
+  typedef typename DT::T T;
+  constexpr int CW = 32;                // weight rows (output columns) per wave
+  constexpr int I = 16, J = 2;          // 16 x 16 tiles per wave
+  constexpr int GBn = GB > 0 ? GB : 1;
+  constexpr int LPG = CW / 8;
+  constexpr int PF = 3;
+  __shared__ __attribute__((aligned(16))) unsigned char lds[F5_NSLOT * F5_SLOT];
+
+  int tm, tn;
+  tile_coords(tiles_m, tiles_n, 4, tm, tn);
+  const int m0 = tm * 256, n0 = tn * 256;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wn = wave;
+  const int r16 = lane & 15, q = lane >> 4;
+  const int lda = Kp + S_pad;
+  const int nkm = GB ? Kp / 64 : 0;
+  const int nkt = nkm + (lda - nkm * 64) / 32;
+  const int Np = pad_n(N);
+
+  const int drow = 16 * wave + (lane >> 2);
+  const int dchunk = (lane & 3) ^ d_f((lane >> 4) & 3);
+  const uint32_t ad_off = (uint32_t)((size_t)(m0 + drow) * lda * sizeof(T) + dchunk * 16);
+  const uint32_t ad_str = (uint32_t)(128 * (size_t)lda * sizeof(T));
+  const uint32_t bd_row0 = (uint32_t)min(n0 + drow, N - 1);
+  const uint32_t bd_row1 = (uint32_t)min(n0 + drow + 128, N - 1);
+  const int arow = 8 * wave + (lane >> 3);
+  const uint32_t a_off = (uint32_t)((size_t)(m0 + arow) * lda * sizeof(T) +
+                                    (bitrev3((lane & 7) ^ ((arow >> 1) & 7)) << 4));
+  const uint32_t a_str = (uint32_t)(64 * (size_t)lda * sizeof(T));
+  const uint32_t b_off = (uint32_t)((size_t)(n0 + 32 * wave + (lane >> 1)) * (Kp / 2) +
+                                    (((lane & 1) ^ ((lane >> 4) & 1)) << 4));
+  const int s_u = min(lane / LPG, GBn - 1);
+  const uint32_t s_off = (uint32_t)((n0 + CW * wn + (lane % LPG) * 8) * sizeof(T));
+
+  auto issue = [&](int kt) {
+    unsigned char* slot = lds + (kt % F5_NSLOT) * F5_SLOT;
+    if (kt < nkm) {
+      const unsigned char* ab = (const unsigned char*)A + (size_t)kt * 64 * sizeof(T);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) glds16(ab + (size_t)i * a_str + a_off, slot + (i * 8 + wave) * 1024);
+      glds16((const unsigned char*)Bw + (size_t)kt * 32 + b_off, slot + F5_A + wave * 1024);
+      const int g0 = GB == 1 ? (kt * 64) / Gw : kt * 2;
+      const int g = min(g0 + s_u, ngw - 1);
+      glds16((const unsigned char*)wscale + (size_t)g * Np * sizeof(T) + s_off,
+             slot + F5_A + F5_B + wave * 1024);
+    } else {
+      const int col = nkm * 64 + (kt - nkm) * 32;
+      const unsigned char* ab = (const unsigned char*)A + (size_t)col * sizeof(T);
+      glds16(ab + ad_off, slot + wave * 1024);
+      glds16(ab + ad_str + ad_off, slot + (8 + wave) * 1024);
+      const bool main = col < Kp;
+      const unsigned char* bb = main ? (const unsigned char*)Bw : (const unsigned char*)wsal;
+      const uint32_t ldb = main ? (uint32_t)Kp : (uint32_t)S_pad;
+      const uint32_t c0 = (uint32_t)(main ? col : col - Kp) * sizeof(T) + dchunk * 16;
+      glds16(bb + bd_row0 * ldb * sizeof(T) + c0, slot + F5_DB + wave * 1024);
+      glds16(bb + bd_row1 * ldb * sizeof(T) + c0, slot + F5_DB + (8 + wave) * 1024);
+    }
+  };
+
+  f32x4 acc[I][J];
+#pragma unroll
+  for (int i = 0; i < I; ++i)
+#pragma unroll
+    for (int j = 0; j < J; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const DecK dk = make_deck();
+  const int a_row0 = r16 * 128;
+  const int a_sw = (r16 >> 1) & 7;
+  // A fragment of block t = I*s + i: row 16 i + r16, chunk 4 (q&1) + 2 s + (q>>1)
+  auto ald = [&](const unsigned char* __restrict__ slot, int t) {
+    const int c = 4 * (q & 1) + 2 * (t / I) + (q >> 1);
+    return *(const u32x4*)(slot + a_row0 + (t % I) * 2048 + ((bitrev3(c) ^ a_sw) << 4));
+  };
+#define SQMP_FQ6_BLOCKS(BF, ...)                                               \
+  {                                                                            \
+    u32x4 a[PF + 1];                                                           \
+    _Pragma("unroll") for (int t = 0; t < PF; ++t) a[t] = ald(slot, t);        \
+    _Pragma("unroll") for (int t = 0; t < 2 * I; ++t) {                        \
+      if (t + PF < 2 * I) a[(t + PF) % (PF + 1)] = ald(slot, t + PF);          \
+      _Pragma("unroll") for (int j = 0; j < J; ++j)                            \
+          Mfma<DT>::run(acc[t % I][j], BF(t / I, j), a[t % (PF + 1)]);         \
+      __VA_ARGS__;                                                             \
+      __builtin_amdgcn_sched_barrier(0);                                       \
+    }                                                                          \
+  }
+
+  auto compute_codes = [&](const unsigned char* __restrict__ slot) {
+    const unsigned char* sb = slot + F5_A;
+    const unsigned char* ss = slot + F5_A + F5_B + wave * 1024;
+    uint2 bw[J];
+    uint32_t sp[J];
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      const int row = wn * CW + 16 * j + r16;
+      bw[j] = *(const uint2*)(sb + row * 32 + (((q >> 1) ^ ((r16 >> 3) & 1)) << 4) + (q & 1) * 8);
+      // group of this lane's dwords: 0 for GB == 1; q & 1 for Gw == 32 (positions 32(q&1)..)
+      const int g = GB == 2 ? (q & 1) : 0;
+      sp[j] = Dec<DT>::prep(*(const uint16_t*)(ss + g * CW * 2 + (16 * j + r16) * 2));
+    }
+    u32x4 bf[2][J];
+#pragma unroll
+    for (int j = 0; j < J; ++j) bf[0][j] = Dec<DT>::run(bw[j].x, sp[j], dk);
+#define SQMP_BF6(s, j) bf[s][j]
+    SQMP_FQ6_BLOCKS(SQMP_BF6,
+                    if (t >= 1 && t <= J) bf[1][t - 1] = Dec<DT>::run(bw[t - 1].y, sp[t - 1], dk));
+#undef SQMP_BF6
+  };
+#undef SQMP_FQ6_BLOCKS
+
+  const int d_sw = d_f((r16 >> 2) & 3);
+  auto compute_dense = [&](const unsigned char* __restrict__ slot) {
+    const int co = (q ^ d_sw) << 4;
+    u32x4 bf[J];
+#pragma unroll
+    for (int j = 0; j < J; ++j) bf[j] = *(const u32x4*)(slot + F5_DB + (wn * CW + 16 * j + r16) * 64 + co);
+#pragma unroll
+    for (int i = 0; i < I; ++i) {
+      const u32x4 af = *(const u32x4*)(slot + (16 * i + r16) * 64 + co);
+#pragma unroll
+      for (int j = 0; j < J; ++j) Mfma<DT>::run(acc[i][j], bf[j], af);
+    }
+  };
+
+  issue(0);
+  if (nkt > 1) issue(1);
+  int kt = 0;
+  for (; kt < nkm; ++kt) {
+    if (kt + 1 < nkt) {
+      if (kt + 1 < nkm) vm_wait<F5_VM_CODES>();
+      else vm_wait<F5_VM_DENSE>();
+    } else {
+      vm_wait<0>();
+    }
+    raw_barrier();
+    if (kt + 2 < nkt) issue(kt + 2);
+    compute_codes(lds + (kt % F5_NSLOT) * F5_SLOT);
+  }
+  for (; kt < nkt; ++kt) {
+    if (kt + 1 < nkt) vm_wait<F5_VM_DENSE>();
+    else vm_wait<0>();
+    raw_barrier();
+    if (kt + 2 < nkt) issue(kt + 2);
+    compute_dense(lds + (kt % F5_NSLOT) * F5_SLOT);
+  }
+
+  // ---- epilogue: acc[i][j][r] = C[n = n0 + 32 wn + 16 j + 4 q + r][m = m0 + 16 i + r16]
+  float bvs[J][4];
+#pragma unroll
+  for (int j = 0; j < J; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      bvs[j][r] = bias ? DT::to_f(bias[min(n0 + wn * CW + 16 * j + 4 * q + r, N - 1)]) : 0.f;
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    const int nb = n0 + wn * CW + 16 * j + 4 * q;
+    if (nb >= N) continue;
+#pragma unroll
+    for (int i = 0; i < I; ++i) {
+      const int gm = m0 + 16 * i + r16;
+      if (gm >= M) continue;
+      T v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = DT::from_f(acc[i][j][r] + bvs[j][r]);
+      T* dst = Y + (size_t)gm * N + nb;
+      if (nb + 4 <= N && (N & 3) == 0) {
+        *(uint2*)dst = *(const uint2*)v;
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (nb + r < N) dst[r] = v[r];
       }
     }
   }
@@ -499,18 +697,44 @@ static int fq5_dispatch(const void* a, const void* codes, const void* wscale, co
   return SQMP_EUNSUPPORTED;
 }
 
-// fq5 tile variant (tuning knob SQMP_FQ_VARIANT): "wm1" (default), "wm2" (2 x 4 waves),
-// "pf6" (wm1, 6-block A read-ahead), "nowait" / "nobar" (timing diagnostics that skip the
-// DMA waits / also the stage barrier of the codes loop: wrong results, in-bounds addresses).
+template <class DT, int GB>
+static int fq6_launch(const void* a, const void* codes, const void* wscale, const void* wsal,
+                      const void* bias, void* y, int M, int N, int Kp, int S_pad, int Gw,
+                      int ngw, hipStream_t s) {
+  typedef typename DT::T T;
+  const int tiles_m = cdiv(M, 256), tiles_n = cdiv(N, 256);
+  gemm_fq6_kernel<DT, GB><<<dim3(tiles_m * tiles_n), dim3(512), 0, s>>>(
+      (const T*)a, codes, (const T*)wscale, (const T*)wsal, (const T*)bias, (T*)y, M, N, Kp,
+      S_pad, Gw, ngw, tiles_m, tiles_n);
+  SQMP_LAUNCH_CHECK();
+  return SQMP_OK;
+}
+
+template <class DT>
+static int fq6_dispatch(const void* a, const void* codes, const void* wscale, const void* wsal,
+                        const void* bias, void* y, int M, int N, int Kp, int S_pad, int Gw,
+                        int ngw, int n_bits, hipStream_t s) {
+  if (n_bits == 0) return fq6_launch<DT, 0>(a, codes, wscale, wsal, bias, y, M, N, Kp, S_pad, 1, 1, s);
+  if (n_bits != 4) return SQMP_EUNSUPPORTED;
+  if (Gw % 64 == 0) return fq6_launch<DT, 1>(a, codes, wscale, wsal, bias, y, M, N, Kp, S_pad, Gw, ngw, s);
+  if (Gw == 32) return fq6_launch<DT, 2>(a, codes, wscale, wsal, bias, y, M, N, Kp, S_pad, Gw, ngw, s);
+  return SQMP_EUNSUPPORTED;
+}
+
+// GEMM variant (tuning knob SQMP_FQ_VARIANT): default "fq6" (16x16x32, 1 x 8 waves);
+// "wm1" = fq5 (32x32x16, 1 x 8), "wm2" = fq5 (2 x 4), "pf6" = fq5 with a 6-block A
+// read-ahead, "nowait" / "nobar" = fq5 timing diagnostics that skip the DMA waits / also
+// the stage barrier of the codes loop (wrong results, in-bounds addresses).
 static int fq_variant() {
   static int v = [] {
     const char* e = getenv("SQMP_FQ_VARIANT");
-    if (!e) return 0;
+    if (!e || !strcmp(e, "fq6")) return 5;
+    if (!strcmp(e, "wm1") || !strcmp(e, "fq5")) return 0;
     if (!strcmp(e, "wm2")) return 1;
     if (!strcmp(e, "pf6")) return 2;
     if (!strcmp(e, "nowait")) return 3;
     if (!strcmp(e, "nobar")) return 4;
-    return 0;
+    return 5;
   }();
   return v;
 }
@@ -519,6 +743,13 @@ int launch_gemm_fq_fast(int dtype, const void* a, const void* codes, const void*
                         const void* wsal, const void* bias, void* y, int M, int N, int Kp,
                         int S_pad, int Gw, int ngw, int n_bits, hipStream_t s) {
   const int v = fq_variant();
+  if (v == 5) {
+    if (dtype == SQMP_F16)
+      return fq6_dispatch<F16>(a, codes, wscale, wsal, bias, y, M, N, Kp, S_pad, Gw, ngw, n_bits, s);
+    if (dtype == SQMP_BF16)
+      return fq6_dispatch<BF16>(a, codes, wscale, wsal, bias, y, M, N, Kp, S_pad, Gw, ngw, n_bits, s);
+    return SQMP_EUNSUPPORTED;
+  }
   if (dtype == SQMP_F16) {
     if (v == 2 && n_bits == 4 && Gw % 64 == 0)
       return fq5_launch<F16, 1, 1, 6>(a, codes, wscale, wsal, bias, y, M, N, Kp, S_pad, Gw, ngw, s);

@@ -1,5 +1,5 @@
 """Run only the W4A4 GEMM (and optionally the prepass) of BASELINE config 2 -- a target
-for rocprofv3 counter passes.  python tools/gemm_only.py [fq|i8] [iters] [prepass]"""
+for rocprofv3 counter passes.  python tools/gemm_only.py [fq|i8] [iters] [per_group|per_token] [prepass]"""
 import os
 import sys
 
@@ -12,9 +12,10 @@ from smoothquant import ops  # noqa: E402
 
 kind = sys.argv[1] if len(sys.argv) > 1 else "fq"
 iters = int(sys.argv[2]) if len(sys.argv) > 2 else 10
-prepass = len(sys.argv) > 3 and sys.argv[3] == "prepass"
+extra = sys.argv[3:]
+prepass = "prepass" in extra
 dev = torch.device("cuda")
-act = "per_group" if kind == "fq" else "per_token"
+act = next((a for a in extra if a.startswith("per_")), "per_group" if kind == "fq" else "per_token")
 q, x, lin = bench.make_layer(dev, act, seed=1)
 pw = q.packed()
 if kind == "fq":
