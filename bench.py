@@ -200,6 +200,14 @@ def main():
     for _ in range(3):
         dense()
     dense_ms = time_events(dense, max(10, args.steps), stream)
+    # reference point: the reference's own fake-quant forward (restated in PyTorch ops,
+    # tools/torch_fakequant.py) on this GPU, same layer and input
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from torch_fakequant import TorchFakeQuantLinear
+    ref = TorchFakeQuantLinear(q.weight, lin.bias.detach(), q.salient_indices, args.act, 4, G)
+    y_ref, y_ours = ref(x), q(x.clone())
+    ref_rel = float((y_ref.float() - y_ours.float()).norm() / y_ref.float().norm())
+    ref_ms = time_events(lambda: ref(x), max(5, args.steps // 5), stream)
     # prepass algorithmic bytes: read x (colmax) + read x (quantize) + write operand(s)
     xbytes = M * K * 2
     if use_i8:
@@ -251,8 +259,14 @@ def main():
             "algorithmic_flops_per_launch": flops,
         },
         "reference_points": {
+            "reference_fakequant_forward_ms": round(ref_ms, 4),
+            "reference_fakequant_TFLOP_per_s": round(flops / (ref_ms * 1e-3) / 1e12, 1),
+            "speedup_vs_reference_fakequant": round(ref_ms / ms_per_step, 2),
+            "reference_vs_ours_rel_err": ref_rel,
             "torch_fp16_linear_ms": round(dense_ms, 4),
             "torch_fp16_linear_TFLOP_per_s": round(flops / (dense_ms * 1e-3) / 1e12, 1),
+            "note": "reference fake-quant forward restated in PyTorch ops (tools/torch_fakequant.py) on "
+                    "this GPU; fp16 F.linear = unquantized hipBLASLt GEMM of the same shape",
         },
         "prepass": {
             "avg_ms": round(quant_ms, 4),

@@ -25,10 +25,11 @@
  *   Np        = roundup(N, 256): codes are allocated with Np rows (rows >= N are never
  *             stored to y) and wscale rows have stride Np.
  *   codes     4-bit weights: "bpack", uint8 [Np][Kp/2].  Per row, per 64-position block,
- *             8 dwords; dword (q*2 + s) holds the 8 codes of positions 32s + 8q + e
- *             (e = 0..7): even e in nibble e/2, odd e in nibble 4 + e/2; nibble =
- *             code + 8 (code in [-7, 7]).  One 8-byte read per MFMA lane group q is
- *             exactly its two 16x16x32 B fragments (s = 0, 1), or its 16x16x64 i8 one.
+ *             8 dwords; dword (h*4 + u) holds the 8 codes of positions 16u + 8h + e
+ *             (e = 0..7): even e in nibble e/2 of the low half-word, odd e in nibble e/2
+ *             of the high half-word; nibble = code + 8 (code in [-7, 7]).  A 16-byte half
+ *             h is one 32x32x16 lane half's four sub-step fragments; dwords 2q, 2q+1 are
+ *             one 16x16x32 lane group's two sub-steps (and its 16x16x64 i8 fragment).
  *             8-bit weights: int8 [N][Kp] row-major.  Salient columns and padding hold 0.
  *   wscale    D [ngw][Np]: per-(group, row) scale; group of position p is p / Gw.
  *   wsal      D [N][S_pad]: the salient weight columns, exact (fake_quant.py:363-365),
@@ -96,7 +97,7 @@ int sqmp_weight_geometry(int K, int S, int wmode, int group_size, int* Kp, int* 
                          int* ngw, int* S_pad);
 
 size_t sqmp_pack_workspace_bytes(int N, int K);
-size_t sqmp_act_workspace_bytes(int M, int K);
+size_t sqmp_act_workspace_bytes(int M, int K, int Kp);  /* Kp: packed length (K for INPLACE) */
 
 /* Offline weight quantization + packing: W4A4Linear.from_float (fake_quant.py:324-371)
  * with quantize_weight_per_{channel,tensor}_absmax (:9-26), quantize_weight_per_group_

@@ -406,6 +406,41 @@ __global__ __launch_bounds__(256) void quant_fp_kernel(
   }
 }
 
+// ---------------------------------------------------------------- entry table
+// Once per call: for every packed position p, ent = (group << 16) | column (G_ZERO for
+// salient / padding positions), written in the wave kernel's LDS image order (two planes
+// of 4 entries per 8-position chunk), and rank_by_col[column] for the block kernels.
+// The list index of column k is found by binary search in the ascending `nonsal`; its
+// rank is the sum of the rank_partial tiles (per_group), the list index itself otherwise.
+__global__ __launch_bounds__(256) void build_ent_kernel(
+    const int32_t* __restrict__ amap, int P, const int32_t* __restrict__ nonsal, int Kn,
+    const int32_t* __restrict__ part, int ntile, int ld, int mode, int G,
+    uint32_t* __restrict__ ent, int32_t* __restrict__ rank_by_col) {
+  const int p = blockIdx.x * 256 + threadIdx.x;
+  if (p >= P) return;
+  const int k = amap[p];
+  uint32_t e = G_ZERO << 16;
+  if (k >= 0 && Kn > 0) {
+    int lo = 0, hi = Kn - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (nonsal[mid] < k) lo = mid + 1; else hi = mid;
+    }
+    int r = lo;
+    if (part) {
+      r = 0;
+      for (int t = 0; t < ntile; ++t) r += part[(size_t)t * ld + lo];
+      if (rank_by_col) rank_by_col[k] = r;
+    }
+    const int g = mode == MODE_GROUP ? r / G : 0;
+    e = ((uint32_t)g << 16) | (uint32_t)k;
+  }
+  if (ent) {
+    const int c = p >> 3, j = p & 7;
+    ent[(size_t)(j >> 2) * (P / 2) + c * 4 + (j & 3)] = e;
+  }
+}
+
 // ---------------------------------------------------------------- wave-per-row variant
 // Same arithmetic as quant_fp_kernel, but each wave owns whole rows: no block barrier on
 // the per-row path, so every wave of the CU streams its own rows (next row prefetched
@@ -414,10 +449,9 @@ __global__ __launch_bounds__(256) void quant_fp_kernel(
 // The block (4 waves) shares the entry table and the salient column list.
 template <class DT, int MODE, int RCH, int VCH>
 __global__ __launch_bounds__(256) void quant_fp_wave_kernel(
-    const typename DT::T* __restrict__ x, int M, int K, int q_max, int G, int nga,
-    const int32_t* __restrict__ amap, int P, const int32_t* __restrict__ nonsal, int Kn,
-    const int32_t* __restrict__ sal, int S, int S_pad,
-    const int32_t* __restrict__ rank_by_col, const uint32_t* __restrict__ cmax,
+    const typename DT::T* __restrict__ x, int M, int K, int q_max, int nga,
+    const u32x4* __restrict__ ent_g, int P, const int32_t* __restrict__ nonsal, int Kn,
+    const int32_t* __restrict__ sal, int S, int S_pad, const uint32_t* __restrict__ cmax,
     typename DT::T* __restrict__ out) {
   typedef typename DT::T T;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_w[];
@@ -432,30 +466,10 @@ __global__ __launch_bounds__(256) void quant_fp_wave_kernel(
   T* row = (T*)(wbase + wave * wbytes);                          // this wave's row
   float2* scr = (float2*)((unsigned char*)row + rowb);           // nga
   uint32_t* gmax = (uint32_t*)(scr + nga);                       // nga
-  uint16_t* grp = (uint16_t*)wbase;  // init scratch (K entries), aliases the row buffers
-  const float invG = 1.0f / (float)G;
 
-  // ---- block-wide tables (the only block barriers)
-  for (int k = tid; k < K; k += 256) grp[k] = (uint16_t)G_ZERO;
+  // ---- the call's entry table (build_ent_kernel): one coalesced copy
+  for (int c = tid; c < 2 * NCH; c += 256) ent[c] = ent_g[c];
   for (int j = tid; j < S_pad; j += 256) salc[j] = j < S ? (uint16_t)sal[j] : (uint16_t)0xFFFFu;
-  __syncthreads();
-  for (int i = tid; i < Kn; i += 256) {
-    const int k = nonsal[i];
-    int g = 0;
-    if (MODE == MODE_GROUP) g = fdiv_floor_a(rank_by_col ? rank_by_col[k] : i, G, invG);
-    grp[k] = (uint16_t)g;
-  }
-  __syncthreads();
-  for (int c = tid; c < NCH; c += 256) {
-    uint32_t e[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int k = amap[c * 8 + j];
-      e[j] = k >= 0 ? (((uint32_t)grp[k] << 16) | (uint32_t)k) : (G_ZERO << 16);
-    }
-    ent[c] = u32x4{e[0], e[1], e[2], e[3]};
-    ent[NCH + c] = u32x4{e[4], e[5], e[6], e[7]};
-  }
   float s_all = 0.f, r_all = 0.f;
   if (MODE == MODE_TENSOR) {
     float m = 0.f;
@@ -464,7 +478,7 @@ __global__ __launch_bounds__(256) void quant_fp_wave_kernel(
     s_all = group_scale<DT>(m, q_max);
     r_all = 1.0f / s_all;
   }
-  __syncthreads();  // grp scratch dead from here on: row buffers are the waves' own
+  __syncthreads();  // tables complete; row buffers are the waves' own
 
   const int nch = K / 8;
   const int wstride = gridDim.x * 4;
@@ -567,8 +581,7 @@ __global__ __launch_bounds__(256) void quant_fp_wave_kernel(
 }
 
 static size_t quant_fp_wave_lds_bytes(int K, int P, int nga, int S_pad, int esize) {
-  // entry table + salient list + 4 per-wave (row, scales, group max) regions; the
-  // init-time column->group scratch (2K bytes) lives inside the row regions
+  // entry table + salient list + 4 per-wave (row, scales, group max) regions
   const size_t wb = (size_t)round_up((long)K * esize, 16) + (size_t)round_up(12L * nga, 16);
   return 4 * (size_t)P + 2 * (size_t)round_up(S_pad, 8) + 4 * wb;
 }
@@ -605,10 +618,9 @@ static int quant_launch(void* x, int M, int K, int q_max, int G, int nga, const 
 }
 
 template <class DT, int MODE, int RCH, int VCH>
-static int quant_fpw_launch(void* x, int M, int K, int q_max, int G, int nga, const int32_t* amap,
-                            int P, const int32_t* nonsal, int Kn, const int32_t* sal, int S,
-                            int S_pad, const int32_t* rank, const uint32_t* cmax, void* out,
-                            size_t lds, hipStream_t s) {
+static int quant_fpw_launch(void* x, int M, int K, int q_max, int nga, const uint32_t* ent, int P,
+                            const int32_t* nonsal, int Kn, const int32_t* sal, int S, int S_pad,
+                            const uint32_t* cmax, void* out, size_t lds, hipStream_t s) {
   typedef typename DT::T T;
   SQMP_HIP_CHECK(hipFuncSetAttribute((const void*)quant_fp_wave_kernel<DT, MODE, RCH, VCH>,
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
@@ -617,7 +629,8 @@ static int quant_fpw_launch(void* x, int M, int K, int q_max, int G, int nga, co
   int grid = 256 * per_cu;
   if (grid > cdiv(M, 4)) grid = cdiv(M, 4);
   quant_fp_wave_kernel<DT, MODE, RCH, VCH><<<dim3(grid), dim3(256), lds, s>>>(
-      (const T*)x, M, K, q_max, G, nga, amap, P, nonsal, Kn, sal, S, S_pad, rank, cmax, (T*)out);
+      (const T*)x, M, K, q_max, nga, (const u32x4*)ent, P, nonsal, Kn, sal, S, S_pad, cmax,
+      (T*)out);
   SQMP_LAUNCH_CHECK();
   return SQMP_OK;
 }
@@ -644,8 +657,8 @@ template <class DT>
 static int quant_dispatch(void* x, int M, int K, int amode, int q_max, int G, int nga,
                           const int32_t* amap, int P, const int32_t* nonsal, int Kn,
                           const int32_t* sal, int S, int S_pad, const int32_t* rank,
-                          const uint32_t* cmax, int out_kind, void* out, void* out_scale,
-                          void* out_xs, hipStream_t s) {
+                          const uint32_t* cmax, const uint32_t* ent, int out_kind, void* out,
+                          void* out_scale, void* out_xs, hipStream_t s) {
 #define SQMP_Q(MODE, OUTK)                                                                  \
   quant_launch<DT, MODE, OUTK>(x, M, K, q_max, G, nga, amap, P, nonsal, Kn, sal, S, S_pad, \
                                rank, cmax, out, out_scale, out_xs, s)
@@ -653,20 +666,21 @@ static int quant_dispatch(void* x, int M, int K, int amode, int q_max, int G, in
                    : amode == SQMP_ACT_PER_TENSOR ? MODE_TENSOR
                                                   : MODE_GROUP;
   if constexpr (DT::id != SQMP_F32) {
-  if (out_kind == SQMP_OUT_FP && K % 8 == 0 && K <= 8192 && P <= 8192 &&
+  if (ent && out_kind == SQMP_OUT_FP && K % 8 == 0 && K <= 12288 && P <= 12288 &&
       (((uintptr_t)x) % 16 == 0)) {
     const size_t lds = quant_fp_wave_lds_bytes(K, P, nga, S_pad, sizeof(typename DT::T));
     if (lds <= 160 * 1024) {
-      const bool small = K <= 4096 && P <= 4096;
-#define SQMP_QW(MODE)                                                                          \
-  (small ? quant_fpw_launch<DT, MODE, 8, 8>(x, M, K, q_max, G, nga, amap, P, nonsal, Kn, sal, S, \
-                                            S_pad, rank, cmax, out, lds, s)                    \
-         : quant_fpw_launch<DT, MODE, 16, 16>(x, M, K, q_max, G, nga, amap, P, nonsal, Kn, sal, \
-                                              S, S_pad, rank, cmax, out, lds, s))
+      const int sz = (K <= 4096 && P <= 4096) ? 0 : (K <= 8192 && P <= 8192) ? 1 : 2;
+#define SQMP_QW1(MODE, R)                                                                   \
+  quant_fpw_launch<DT, MODE, R, R>(x, M, K, q_max, nga, ent, P, nonsal, Kn, sal, S, S_pad, cmax, \
+                                   out, lds, s)
+#define SQMP_QW(MODE) \
+  (sz == 0 ? SQMP_QW1(MODE, 8) : sz == 1 ? SQMP_QW1(MODE, 16) : SQMP_QW1(MODE, 24))
       if (mode == MODE_TOKEN) return SQMP_QW(MODE_TOKEN);
       if (mode == MODE_TENSOR) return SQMP_QW(MODE_TENSOR);
       return SQMP_QW(MODE_GROUP);
 #undef SQMP_QW
+#undef SQMP_QW1
     }
   }
   if (out_kind == SQMP_OUT_FP && K % 8 == 0 && K * 2 <= PFC_FP * 256 * 16 &&
@@ -703,9 +717,13 @@ static int quant_dispatch(void* x, int M, int K, int amode, int q_max, int G, in
 
 using namespace sqmp;
 
-extern "C" size_t sqmp_act_workspace_bytes(int M, int K) {
+// Workspace: cmax u32 [K64] | rank_by_col i32 [K64] | rank partials i32 [tiles][K64] |
+// entry table u32 [Kp].  Only cmax is cleared per call.
+static size_t ws_k64(int K) { return (size_t)round_up(K > 0 ? K : 1, 64); }
+extern "C" size_t sqmp_act_workspace_bytes(int M, int K, int Kp) {
   (void)M;
-  return 2 * sizeof(uint32_t) * (size_t)round_up(K > 0 ? K : 1, 64);
+  const size_t k64 = ws_k64(K);
+  return sizeof(uint32_t) * (k64 * (2 + (size_t)rank_tiles(K)) + (size_t)round_up(Kp > K ? Kp : K, 64));
 }
 
 extern "C" int sqmp_quant_act(void* x, int dtype, int M, int K, int amode, int n_bits,
@@ -731,9 +749,12 @@ extern "C" int sqmp_quant_act(void* x, int dtype, int M, int K, int amode, int n
   const bool group = amode == SQMP_ACT_PER_GROUP || amode == SQMP_ACT_PER_GROUP_UNSORTED;
   if (group && (group_size <= 0 || group_size > 65000)) return SQMP_EINVAL;
   if (M == 0) return SQMP_OK;
-  if (ws_bytes < sqmp_act_workspace_bytes(M, K) || !workspace) return SQMP_EWORKSPACE;
+  if (ws_bytes < sqmp_act_workspace_bytes(M, K, Kp) || !workspace) return SQMP_EWORKSPACE;
+  const size_t k64 = ws_k64(K);
   uint32_t* cmax = (uint32_t*)workspace;
-  int32_t* rank = (int32_t*)((char*)workspace + sizeof(uint32_t) * round_up(K, 64));
+  int32_t* rank = (int32_t*)(cmax + k64);
+  int32_t* part = rank + k64;
+  uint32_t* ent = (uint32_t*)(part + k64 * (size_t)rank_tiles(K));
   const int Kn = K - S;
   if (Kn == 0) {
     // every channel salient: the reference skips quantization entirely (:299)
@@ -741,30 +762,41 @@ extern "C" int sqmp_quant_act(void* x, int dtype, int M, int K, int amode, int n
   }
   int st;
   if (amode == SQMP_ACT_PER_TENSOR || amode == SQMP_ACT_PER_GROUP) {
-    // one clear for the adjacent cmax and rank workspace arrays
-    SQMP_HIP_CHECK(hipMemsetAsync(workspace, 0, sqmp_act_workspace_bytes(M, K), s));
+    SQMP_HIP_CHECK(hipMemsetAsync(cmax, 0, sizeof(uint32_t) * k64, s));
     st = launch_colmax(x, dtype, M, K, cmax, s, false);
     if (st) return st;
   }
-  if (amode == SQMP_ACT_PER_GROUP) {
-    st = launch_rank(cmax, nonsal, Kn, K, rank, s, false);
+  const bool sorted = amode == SQMP_ACT_PER_GROUP;
+  if (sorted) {
+    st = launch_rank_partial(cmax, nonsal, Kn, (int)k64, part, s);
     if (st) return st;
+  }
+  // entry table (read by the wave kernel) and rank_by_col (read by the block kernels)
+  const int mode_e = group ? MODE_GROUP : MODE_TOKEN;
+  const int Pe = out_kind == SQMP_OUT_INPLACE ? K : Kp;
+  const bool need_ent = out_kind == SQMP_OUT_FP && Pe % 8 == 0;
+  if (need_ent || sorted) {
+    build_ent_kernel<<<dim3(cdiv(Pe, 256)), dim3(256), 0, s>>>(
+        amap, Pe, nonsal, Kn, sorted ? part : nullptr, rank_tiles(Kn), (int)k64, mode_e,
+        group ? group_size : 1, need_ent ? ent : nullptr, sorted ? rank : nullptr);
+    SQMP_LAUNCH_CHECK();
   }
   const int q_max = (1 << (n_bits - 1)) - 1;
   const int nga = group ? (Kn > 0 ? cdiv(Kn, group_size) : 1) : 1;
-  const int32_t* rk = amode == SQMP_ACT_PER_GROUP ? rank : nullptr;
+  const int32_t* rk = sorted ? rank : nullptr;
+  const uint32_t* entp = need_ent ? ent : nullptr;
   switch (dtype) {
     case SQMP_F32:
       return quant_dispatch<F32>(x, M, K, amode, q_max, group_size, nga, amap, Kp, nonsal,
-                                 Kn, salient, S, S_pad, rk, cmax, out_kind, out, out_scale,
+                                 Kn, salient, S, S_pad, rk, cmax, entp, out_kind, out, out_scale,
                                  out_xs, s);
     case SQMP_F16:
       return quant_dispatch<F16>(x, M, K, amode, q_max, group_size, nga, amap, Kp, nonsal,
-                                 Kn, salient, S, S_pad, rk, cmax, out_kind, out, out_scale,
+                                 Kn, salient, S, S_pad, rk, cmax, entp, out_kind, out, out_scale,
                                  out_xs, s);
     default:
       return quant_dispatch<BF16>(x, M, K, amode, q_max, group_size, nga, amap, Kp, nonsal,
-                                  Kn, salient, S, S_pad, rk, cmax, out_kind, out, out_scale,
+                                  Kn, salient, S, S_pad, rk, cmax, entp, out_kind, out, out_scale,
                                   out_xs, s);
   }
 }

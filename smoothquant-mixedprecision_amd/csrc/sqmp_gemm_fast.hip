@@ -294,7 +294,7 @@ __global__ __launch_bounds__(512, 1) void gemm_fq5_kernel(
 // row (one ds_read_b64 per tile column carries both sub-steps) and A chunk
 // 4 (q & 1) + 2 s + (q >> 1) -- the positions of that dword.  Same DMA ring, waits and
 // dense stages as fq5; dense stages give lane q chunk q of both 64-B rows.
-template <class DT, int GB>
+template <class DT, int GB, int TM>
 __global__ __launch_bounds__(512, 1) void gemm_fq6_kernel(
     const typename DT::T* __restrict__ A, const void* __restrict__ Bw,
     const typename DT::T* __restrict__ wscale, const typename DT::T* __restrict__ wsal,
@@ -302,7 +302,9 @@ __global__ __launch_bounds__(512, 1) void gemm_fq6_kernel(
     int Kp, int S_pad, int Gw, int ngw, int tiles_m, int tiles_n) {
   typedef typename DT::T T;
   constexpr int CW = 32;                // weight rows (output columns) per wave
-  constexpr int I = 16, J = 2;          // 16 x 16 tiles per wave
+  constexpr int I = TM / 16, J = 2;     // 16 x 16 tiles per wave (TM rows x 32 columns)
+  constexpr int NA = TM / 64;           // codes-stage A DMA ops per wave (64 rows each)
+  constexpr int VM_CODES = NA + 1 + 1, VM_DENSE = TM / 128 + 2;
   constexpr int GBn = GB > 0 ? GB : 1;
   constexpr int LPG = CW / 8;
   constexpr int PF = 3;
@@ -310,7 +312,7 @@ __global__ __launch_bounds__(512, 1) void gemm_fq6_kernel(
 
   int tm, tn;
   tile_coords(tiles_m, tiles_n, 4, tm, tn);
-  const int m0 = tm * 256, n0 = tn * 256;
+  const int m0 = tm * TM, n0 = tn * 256;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wn = wave;
@@ -340,7 +342,7 @@ __global__ __launch_bounds__(512, 1) void gemm_fq6_kernel(
     if (kt < nkm) {
       const unsigned char* ab = (const unsigned char*)A + (size_t)kt * 64 * sizeof(T);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) glds16(ab + (size_t)i * a_str + a_off, slot + (i * 8 + wave) * 1024);
+      for (int i = 0; i < NA; ++i) glds16(ab + (size_t)i * a_str + a_off, slot + (i * 8 + wave) * 1024);
       glds16((const unsigned char*)Bw + (size_t)kt * 32 + b_off, slot + F5_A + wave * 1024);
       const int g0 = GB == 1 ? (kt * 64) / Gw : kt * 2;
       const int g = min(g0 + s_u, ngw - 1);
@@ -350,7 +352,7 @@ __global__ __launch_bounds__(512, 1) void gemm_fq6_kernel(
       const int col = nkm * 64 + (kt - nkm) * 32;
       const unsigned char* ab = (const unsigned char*)A + (size_t)col * sizeof(T);
       glds16(ab + ad_off, slot + wave * 1024);
-      glds16(ab + ad_str + ad_off, slot + (8 + wave) * 1024);
+      if (TM == 256) glds16(ab + ad_str + ad_off, slot + (8 + wave) * 1024);
       const bool main = col < Kp;
       const unsigned char* bb = main ? (const unsigned char*)Bw : (const unsigned char*)wsal;
       const uint32_t ldb = main ? (uint32_t)Kp : (uint32_t)S_pad;
@@ -429,8 +431,8 @@ __global__ __launch_bounds__(512, 1) void gemm_fq6_kernel(
   int kt = 0;
   for (; kt < nkm; ++kt) {
     if (kt + 1 < nkt) {
-      if (kt + 1 < nkm) vm_wait<F5_VM_CODES>();
-      else vm_wait<F5_VM_DENSE>();
+      if (kt + 1 < nkm) vm_wait<VM_CODES>();
+      else vm_wait<VM_DENSE>();
     } else {
       vm_wait<0>();
     }
@@ -439,7 +441,7 @@ __global__ __launch_bounds__(512, 1) void gemm_fq6_kernel(
     compute_codes(lds + (kt % F5_NSLOT) * F5_SLOT);
   }
   for (; kt < nkt; ++kt) {
-    if (kt + 1 < nkt) vm_wait<F5_VM_DENSE>();
+    if (kt + 1 < nkt) vm_wait<VM_DENSE>();
     else vm_wait<0>();
     raw_barrier();
     if (kt + 2 < nkt) issue(kt + 2);
@@ -697,13 +699,13 @@ static int fq5_dispatch(const void* a, const void* codes, const void* wscale, co
   return SQMP_EUNSUPPORTED;
 }
 
-template <class DT, int GB>
+template <class DT, int GB, int TM>
 static int fq6_launch(const void* a, const void* codes, const void* wscale, const void* wsal,
                       const void* bias, void* y, int M, int N, int Kp, int S_pad, int Gw,
                       int ngw, hipStream_t s) {
   typedef typename DT::T T;
-  const int tiles_m = cdiv(M, 256), tiles_n = cdiv(N, 256);
-  gemm_fq6_kernel<DT, GB><<<dim3(tiles_m * tiles_n), dim3(512), 0, s>>>(
+  const int tiles_m = cdiv(M, TM), tiles_n = cdiv(N, 256);
+  gemm_fq6_kernel<DT, GB, TM><<<dim3(tiles_m * tiles_n), dim3(512), 0, s>>>(
       (const T*)a, codes, (const T*)wscale, (const T*)wsal, (const T*)bias, (T*)y, M, N, Kp,
       S_pad, Gw, ngw, tiles_m, tiles_n);
   SQMP_LAUNCH_CHECK();
@@ -714,11 +716,17 @@ template <class DT>
 static int fq6_dispatch(const void* a, const void* codes, const void* wscale, const void* wsal,
                         const void* bias, void* y, int M, int N, int Kp, int S_pad, int Gw,
                         int ngw, int n_bits, hipStream_t s) {
-  if (n_bits == 0) return fq6_launch<DT, 0>(a, codes, wscale, wsal, bias, y, M, N, Kp, S_pad, 1, 1, s);
+  // 128-row tiles when 256-row tiles would leave the chip under two workgroups per CU
+  const bool small = (long)cdiv(M, 256) * cdiv(N, 256) < 2L * 256;
+#define SQMP_FQ6(GB, GW, NGW)                                                                   \
+  (small ? fq6_launch<DT, GB, 128>(a, codes, wscale, wsal, bias, y, M, N, Kp, S_pad, GW, NGW, s) \
+         : fq6_launch<DT, GB, 256>(a, codes, wscale, wsal, bias, y, M, N, Kp, S_pad, GW, NGW, s))
+  if (n_bits == 0) return SQMP_FQ6(0, 1, 1);
   if (n_bits != 4) return SQMP_EUNSUPPORTED;
-  if (Gw % 64 == 0) return fq6_launch<DT, 1>(a, codes, wscale, wsal, bias, y, M, N, Kp, S_pad, Gw, ngw, s);
-  if (Gw == 32) return fq6_launch<DT, 2>(a, codes, wscale, wsal, bias, y, M, N, Kp, S_pad, Gw, ngw, s);
+  if (Gw % 64 == 0) return SQMP_FQ6(1, Gw, ngw);
+  if (Gw == 32) return SQMP_FQ6(2, Gw, ngw);
   return SQMP_EUNSUPPORTED;
+#undef SQMP_FQ6
 }
 
 // GEMM variant (tuning knob SQMP_FQ_VARIANT): default "fq6" (16x16x32, 1 x 8 waves);

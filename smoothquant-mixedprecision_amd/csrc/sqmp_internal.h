@@ -14,6 +14,11 @@ int launch_colmax(const void* x, int dtype, int R, int C, uint32_t* cmax, hipStr
 // C-entry rank_by_col first.
 int launch_rank(const uint32_t* cmax, const int32_t* cols, int L, int C,
                 int32_t* rank_by_col, hipStream_t s, bool zero = true);
+// Atomic-free variant: part[tile][i] = competitors of tile `tile` ordered before list
+// entry i (tiles of 256); rank(i) = sum over the rank_tiles(L) tiles.  ld = row stride.
+int rank_tiles(int L);
+int launch_rank_partial(const uint32_t* cmax, const int32_t* cols, int L, int ld,
+                        int32_t* part, hipStream_t s);
 
 // Index maps of a packed weight (see include/sqmp_w4a4.h).  rank_by_col == NULL keeps the
 // original column order (per_channel / per_tensor / unsorted per_group).

@@ -126,6 +126,44 @@ int launch_rank(const uint32_t* cmax, const int32_t* cols, int L, int C,
   return SQMP_OK;
 }
 
+// Same counts without atomics: block (bx, by) writes the count of competitor tile by for
+// its 256 owners to part[by][owner]; the consumer sums the cdiv(L, RANK_TILE) partials.
+// Every (tile, owner) slot is written, so the buffer needs no clearing.
+__global__ __launch_bounds__(256) void rank_partial_kernel(const uint32_t* __restrict__ cmax,
+                                                           const int32_t* __restrict__ cols, int L,
+                                                           int ld, int32_t* __restrict__ part) {
+  __shared__ uint32_t kv[RANK_TILE];
+  const int j0 = blockIdx.y * RANK_TILE;
+  const int jn = min(RANK_TILE, L - j0);
+  {
+    const int t = threadIdx.x;
+    kv[t] = t < jn ? cmax[cols ? cols[j0 + t] : j0 + t] : 0xFFFFFFFFu;
+  }
+  __syncthreads();
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= L) return;
+  const uint32_t mine = cmax[cols ? cols[i] : i];
+  const int lim = i - j0;
+  int cnt = 0;
+#pragma unroll 16
+  for (int t = 0; t < RANK_TILE; ++t) {
+    const uint32_t k = kv[t];
+    cnt += (k < mine || (k == mine && t < lim)) ? 1 : 0;
+  }
+  part[(size_t)blockIdx.y * ld + i] = cnt;
+}
+
+int rank_tiles(int L) { return L > 0 ? cdiv(L, RANK_TILE) : 0; }
+
+int launch_rank_partial(const uint32_t* cmax, const int32_t* cols, int L, int ld,
+                        int32_t* part, hipStream_t s) {
+  if (L <= 0) return SQMP_OK;
+  dim3 grid(cdiv(L, 256), cdiv(L, RANK_TILE));
+  rank_partial_kernel<<<grid, dim3(256), 0, s>>>(cmax, cols, L, ld, part);
+  SQMP_LAUNCH_CHECK();
+  return SQMP_OK;
+}
+
 // ------------------------------------------------------------------ index maps
 // One workgroup.  flag[k] marks salient columns; the non-salient list is an ordered
 // compaction (block-wide exclusive scan over per-thread chunk counts).

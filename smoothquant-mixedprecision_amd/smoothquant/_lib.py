@@ -28,7 +28,7 @@ SIGNATURES = {
     "sqmp_status_string": (ctypes.c_char_p, [_i]),
     "sqmp_weight_geometry": (_i, [_i, _i, _i, _i, _ip, _ip, _ip, _ip]),
     "sqmp_pack_workspace_bytes": (_sz, [_i, _i]),
-    "sqmp_act_workspace_bytes": (_sz, [_i, _i]),
+    "sqmp_act_workspace_bytes": (_sz, [_i, _i, _i]),
     "sqmp_pack_weight": (_i, [_vp, _i, _i, _i, _i, _i, _i, _vp, _i, _vp, _vp, _vp, _vp, _vp,
                               _vp, _vp, _vp, _sz, _vp]),
     "sqmp_dequant_weight": (_i, [_vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _i,

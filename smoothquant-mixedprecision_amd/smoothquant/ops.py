@@ -171,8 +171,8 @@ def _pad_rows(M: int) -> int:
     return max(256, (M + 255) // 256 * 256)
 
 
-def _act_workspace(M: int, K: int, device):
-    n = load().sqmp_act_workspace_bytes(M, K)
+def _act_workspace(M: int, K: int, Kp: int, device):
+    n = load().sqmp_act_workspace_bytes(M, K, Kp)
     return torch.empty(n, dtype=torch.uint8, device=device), n
 
 
@@ -180,12 +180,12 @@ def quant_act_fp(x2: torch.Tensor, pw: PackedWeight, act_quant: str, n_bits: int
                  group_size: int) -> torch.Tensor:
     """x [M, K] -> A [M, Kp + S_pad] in D: x_hat in packed order + exact salient tail.
 
-    The returned tensor is an M-row view of an allocation padded to a multiple of 128 rows
-    (the GEMM stages whole 128-row tiles by LDS-DMA; rows >= M are never stored)."""
+    The returned tensor is an M-row view of an allocation padded to a multiple of 256 rows
+    (the GEMM stages whole 256-row tiles by LDS-DMA; rows >= M are never stored)."""
     _require_gpu(x2, "quant_act")
     M, K = x2.shape
     a = torch.empty((_pad_rows(M), pw.Kp + pw.S_pad), dtype=x2.dtype, device=x2.device)[:M]
-    ws, nb = _act_workspace(M, K, x2.device)
+    ws, nb = _act_workspace(M, K, pw.Kp, x2.device)
     check(load().sqmp_quant_act(_p(x2), _dtype_code(x2.dtype), M, K, ACT_MODES[act_quant], n_bits,
                                 group_size, _p(pw.amap), pw.Kp, _p(pw.nonsal), _p(pw.salient), pw.S,
                                 pw.S_pad, _lib.OUT_FP, _p(a), None, None, _p(ws), nb,
@@ -202,7 +202,7 @@ def quant_act_i8(x2: torch.Tensor, pw: PackedWeight, act_quant: str, n_bits: int
     a8 = torch.empty((Mp, (pw.Kp + 255) // 256 * 256), dtype=torch.int8, device=x2.device)[:M]
     sa = torch.empty((M,), dtype=torch.float32, device=x2.device)
     xs = torch.empty((Mp, pw.S_pad), dtype=x2.dtype, device=x2.device)[:M]
-    ws, nb = _act_workspace(M, K, x2.device)
+    ws, nb = _act_workspace(M, K, pw.Kp, x2.device)
     check(load().sqmp_quant_act(_p(x2), _dtype_code(x2.dtype), M, K, ACT_MODES[act_quant], n_bits,
                                 0, _p(pw.amap), pw.Kp, _p(pw.nonsal), _p(pw.salient), pw.S,
                                 pw.S_pad, _lib.OUT_I8, _p(a8), _p(sa), _p(xs) if pw.S_pad else None,
@@ -215,7 +215,7 @@ def fake_quant_inplace(t2: torch.Tensor, act_quant: str, n_bits: int, group_size
     """Fake-quantize t [M, C] in place; columns marked -2 in amap_fq pass through."""
     _require_gpu(t2, "fake_quant")
     M, C = t2.shape
-    ws, nb = _act_workspace(M, C, t2.device)
+    ws, nb = _act_workspace(M, C, C, t2.device)
     check(load().sqmp_quant_act(_p(t2), _dtype_code(t2.dtype), M, C, ACT_MODES[act_quant], n_bits,
                                 group_size, _p(amap_fq), C, _p(nonsal), None, S, 0,
                                 _lib.OUT_INPLACE, None, None, None, _p(ws), nb, _stream(t2)),

@@ -65,7 +65,7 @@ def test_weight_geometry(lib):
 
 
 def test_workspace_queries(lib):
-    assert lib.sqmp_act_workspace_bytes(16384, 4096) >= 2 * 4 * 4096
+    assert lib.sqmp_act_workspace_bytes(16384, 4096, 4096) >= 2 * 4 * 4096 + 4 * 4096
     assert lib.sqmp_pack_workspace_bytes(4096, 11008) >= 2 * 4 * 11008
 
 
