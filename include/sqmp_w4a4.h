@@ -58,12 +58,16 @@ extern "C" {
 enum sqmp_dtype { SQMP_F32 = 0, SQMP_F16 = 1, SQMP_BF16 = 2 };
 
 /* act_quant (fake_quant.py:246-256); PER_GROUP is the sorted variant the reference
- * binds (:104-154); PER_GROUP_UNSORTED is the unwired :77-101 variant. */
+ * binds (:104-154); PER_GROUP_UNSORTED is the unwired :77-101 variant;
+ * PER_GROUP_MEAN3STD sorts the columns by mean|x| + 3 std|x| over the batch instead of
+ * the column absmax (the README.md:36 "statistical sorting", absent from the reference's
+ * code -- defined by this library, parity unpinned). */
 enum sqmp_act_mode {
   SQMP_ACT_PER_TOKEN = 0,
   SQMP_ACT_PER_TENSOR = 1,
   SQMP_ACT_PER_GROUP = 2,
-  SQMP_ACT_PER_GROUP_UNSORTED = 3
+  SQMP_ACT_PER_GROUP_UNSORTED = 3,
+  SQMP_ACT_PER_GROUP_MEAN3STD = 4
 };
 
 /* weight_quant (fake_quant.py:348-361); PER_GROUP = sorted (:156-207). */
@@ -72,8 +76,10 @@ enum sqmp_weight_mode {
   SQMP_W_PER_TENSOR = 1,
   SQMP_W_PER_GROUP = 2,
   SQMP_W_PER_GROUP_UNSORTED = 3,
-  SQMP_W_NONE = 4  /* no weight quantization: `codes` holds dense D [N][Kp] (a directly
-                      constructed W4A4Linear, fake_quant.py:227-235); GEMM n_bits = 0 */
+  SQMP_W_NONE = 4,  /* no weight quantization: `codes` holds dense D [N][Kp] (a directly
+                       constructed W4A4Linear, fake_quant.py:227-235); GEMM n_bits = 0 */
+  SQMP_W_PER_GROUP_MEAN3STD = 5  /* groups over columns sorted by mean|W| + 3 std|W| over
+                                    the N rows (see SQMP_ACT_PER_GROUP_MEAN3STD) */
 };
 
 /* Output of sqmp_quant_act. */

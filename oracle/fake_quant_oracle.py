@@ -35,7 +35,8 @@ __all__ = [
     "quantize_activation_per_tensor_absmax", "quantize_activation_per_group_absmax",
     "quantize_activation_per_group_absmax_sort", "quantize_weight_per_group_absmax_sort",
     "select_salient", "w4a4_from_float", "w4a4_forward", "linear", "act_quant_fn",
-    "weight_quant_fn",
+    "weight_quant_fn", "mean3std_key", "quantize_activation_per_group_mean3std_sort",
+    "quantize_weight_per_group_mean3std_sort",
 ]
 
 
@@ -155,10 +156,26 @@ def stable_argsort(keys) -> np.ndarray:
     return np.argsort(np.asarray(keys, dtype=np.float64), kind="stable")
 
 
-def _sorted_group_quant(t2, n_bits, group_size, dt: DT):
+def mean3std_key(t2, dt: DT):
+    """The mean + 3 sigma column key (README.md:36 "statistical sorting"; absent from the
+    reference's code, so defined here -- PARITY UNPINNED): mean|x| + 3 std|x| over the
+    rows (population std) from fp64 sums of |x| and x^2, rounded once to fp32.  The HIP
+    key kernel (sqmp_stats.hip) computes the same formula with the same rounding points."""
+    a = np.abs(dt.f32(t2)).astype(np.float64)
+    R = a.shape[0]
+    mean = a.sum(axis=0) / R
+    var = np.maximum((a * a).sum(axis=0) / R - mean * mean, 0.0)
+    return (mean + 3.0 * np.sqrt(var)).astype(np.float32)
+
+
+def _sorted_group_quant(t2, n_bits, group_size, dt: DT, key: str = "max"):
     """Shared body of fake_quant.py:104-154 and :156-207: sort columns ascending by
-    column absmax, group, quantize, unsort.  Returns (dequant, codes, scales, perm)."""
-    col_max = np.abs(t2).max(axis=0)                    # :113 / :164
+    column absmax, group, quantize, unsort.  Returns (dequant, codes, scales, perm).
+    key="mean3std" sorts by mean3std_key instead (the config-5 extension)."""
+    if key == "mean3std":
+        col_max = mean3std_key(t2, dt)
+    else:
+        col_max = np.abs(t2).max(axis=0)                # :113 / :164
     perm = stable_argsort(dt.f32(col_max))              # :116 / :167
     deq, code, s = _group_quant_rows(t2[:, perm], n_bits, group_size, dt)
     inv = np.argsort(perm, kind="stable")               # :150 / :204
@@ -176,25 +193,46 @@ def quantize_weight_per_group_absmax_sort(w, n_bits, dt: DT, group_size=128):
     return _sorted_group_quant(w, n_bits, group_size, dt)[0]
 
 
+def quantize_activation_per_group_mean3std_sort(t, n_bits, dt: DT, group_size=128):
+    """Config-5 extension: :104-154 with the mean3std_key sort (parity unpinned)."""
+    t2 = t.reshape(-1, t.shape[-1])
+    return _sorted_group_quant(t2, n_bits, group_size, dt, "mean3std")[0].reshape(t.shape)
+
+
+def quantize_weight_per_group_mean3std_sort(w, n_bits, dt: DT, group_size=128):
+    """Config-5 extension: :156-207 with the mean3std_key sort (parity unpinned)."""
+    return _sorted_group_quant(w, n_bits, group_size, dt, "mean3std")[0]
+
+
 def act_quant_fn(name: str, n_bits: int, group_size: int, dt: DT):
-    """The `act_quant` binding of W4A4Linear.__init__ (fake_quant.py:246-256)."""
+    """The `act_quant` binding of W4A4Linear.__init__ (fake_quant.py:246-256), plus the
+    config-5 rebindings: "per_group_unsorted" = :77-101, "per_group_mean3std"."""
     if name == "per_token":
         return lambda t: quantize_activation_per_token_absmax(t, n_bits, dt)
     if name == "per_tensor":
         return lambda t: quantize_activation_per_tensor_absmax(t, n_bits, dt)
     if name == "per_group":
         return lambda t: quantize_activation_per_group_absmax_sort(t, n_bits, dt, group_size)
+    if name == "per_group_unsorted":
+        return lambda t: quantize_activation_per_group_absmax(t, n_bits, dt, group_size)
+    if name == "per_group_mean3std":
+        return lambda t: quantize_activation_per_group_mean3std_sort(t, n_bits, dt, group_size)
     raise ValueError(f"Invalid act_quant: {name}")
 
 
 def weight_quant_fn(name: str, n_bits: int, group_size: int, dt: DT):
-    """The weight quantizer choice of from_float (fake_quant.py:348-361)."""
+    """The weight quantizer choice of from_float (fake_quant.py:348-361), plus the
+    config-5 compositions: "per_group_unsorted" = :29-53, "per_group_mean3std"."""
     if name == "per_channel":
         return lambda w: quantize_weight_per_channel_absmax(w, n_bits, dt)
     if name == "per_tensor":
         return lambda w: quantize_weight_per_tensor_absmax(w, n_bits, dt)
     if name == "per_group":
         return lambda w: quantize_weight_per_group_absmax_sort(w, n_bits, dt, group_size)
+    if name == "per_group_unsorted":
+        return lambda w: quantize_weight_per_group_absmax(w, n_bits, dt, group_size)
+    if name == "per_group_mean3std":
+        return lambda w: quantize_weight_per_group_mean3std_sort(w, n_bits, dt, group_size)
     raise ValueError(f"Invalid weight_quant: {name}")
 
 
@@ -246,14 +284,17 @@ def quantize_input(x2, act_quant, n_bits, group_size, salient, dt: DT):
 
 
 def w4a4_forward(x, w_hat, bias, act_quant, n_bits, group_size, salient,
-                 quantize_output, dt: DT):
-    """fake_quant.py:279-322 (forward) with the weights already fake-quantized."""
+                 quantize_output, dt: DT, act_bits=None):
+    """fake_quant.py:279-322 (forward) with the weights already fake-quantized.
+    act_bits: the activation quantizer's n_bits when it was rebound (W4A8, config 5);
+    output quantization keeps the constructor's binding (n_bits), as in the reference."""
     shape = x.shape
     if len(shape) not in (2, 3):
         raise ValueError(f"Unsupported input shape: {shape}")
     K = shape[-1]
     x2 = dt.rnd(dt.f32(x.reshape(-1, K)))
-    q_x = quantize_input(x2, act_quant, n_bits, group_size, salient, dt)
+    q_x = quantize_input(x2, act_quant, n_bits if act_bits is None else act_bits, group_size,
+                         salient, dt)
     y = linear(q_x, w_hat, bias, dt)
     if quantize_output and salient is not None:
         mask = np.ones(K, dtype=bool)

@@ -718,12 +718,16 @@ static int quant_dispatch(void* x, int M, int K, int amode, int q_max, int G, in
 using namespace sqmp;
 
 // Workspace: cmax u32 [K64] | rank_by_col i32 [K64] | rank partials i32 [tiles][K64] |
-// entry table u32 [Kp].  Only cmax is cleared per call.
+// entry table u32 [Kp64] | fp64 column sums [2][K64] (mean + 3 sigma key).  Only cmax (or
+// the sums) is cleared per call.
 static size_t ws_k64(int K) { return (size_t)round_up(K > 0 ? K : 1, 64); }
+static size_t ws_u32_words(int K, int Kp) {
+  const size_t k64 = ws_k64(K);
+  return k64 * (2 + (size_t)rank_tiles(K)) + (size_t)round_up(Kp > K ? Kp : K, 64);
+}
 extern "C" size_t sqmp_act_workspace_bytes(int M, int K, int Kp) {
   (void)M;
-  const size_t k64 = ws_k64(K);
-  return sizeof(uint32_t) * (k64 * (2 + (size_t)rank_tiles(K)) + (size_t)round_up(Kp > K ? Kp : K, 64));
+  return sizeof(uint32_t) * ws_u32_words(K, Kp) + 2 * sizeof(double) * ws_k64(K);
 }
 
 extern "C" int sqmp_quant_act(void* x, int dtype, int M, int K, int amode, int n_bits,
@@ -733,7 +737,7 @@ extern "C" int sqmp_quant_act(void* x, int dtype, int M, int K, int amode, int n
                               void* workspace, size_t ws_bytes, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   if (dtype < SQMP_F32 || dtype > SQMP_BF16 || M < 0 || K <= 0 || K > 65000) return SQMP_EINVAL;
-  if (amode < SQMP_ACT_PER_TOKEN || amode > SQMP_ACT_PER_GROUP_UNSORTED) return SQMP_EINVAL;
+  if (amode < SQMP_ACT_PER_TOKEN || amode > SQMP_ACT_PER_GROUP_MEAN3STD) return SQMP_EINVAL;
   if (n_bits < 2 || n_bits > 8) return SQMP_EUNSUPPORTED;
   if (S < 0 || S > K || !x || !amap || (K - S > 0 && !nonsal)) return SQMP_EINVAL;
   if (out_kind == SQMP_OUT_INPLACE) {
@@ -746,7 +750,8 @@ extern "C" int sqmp_quant_act(void* x, int dtype, int M, int K, int amode, int n
   } else {
     return SQMP_EINVAL;
   }
-  const bool group = amode == SQMP_ACT_PER_GROUP || amode == SQMP_ACT_PER_GROUP_UNSORTED;
+  const bool group = amode == SQMP_ACT_PER_GROUP || amode == SQMP_ACT_PER_GROUP_UNSORTED ||
+                     amode == SQMP_ACT_PER_GROUP_MEAN3STD;
   if (group && (group_size <= 0 || group_size > 65000)) return SQMP_EINVAL;
   if (M == 0) return SQMP_OK;
   if (ws_bytes < sqmp_act_workspace_bytes(M, K, Kp) || !workspace) return SQMP_EWORKSPACE;
@@ -755,6 +760,7 @@ extern "C" int sqmp_quant_act(void* x, int dtype, int M, int K, int amode, int n
   int32_t* rank = (int32_t*)(cmax + k64);
   int32_t* part = rank + k64;
   uint32_t* ent = (uint32_t*)(part + k64 * (size_t)rank_tiles(K));
+  double* sums = (double*)((uint32_t*)workspace + ws_u32_words(K, Kp));
   const int Kn = K - S;
   if (Kn == 0) {
     // every channel salient: the reference skips quantization entirely (:299)
@@ -765,8 +771,11 @@ extern "C" int sqmp_quant_act(void* x, int dtype, int M, int K, int amode, int n
     SQMP_HIP_CHECK(hipMemsetAsync(cmax, 0, sizeof(uint32_t) * k64, s));
     st = launch_colmax(x, dtype, M, K, cmax, s, false);
     if (st) return st;
+  } else if (amode == SQMP_ACT_PER_GROUP_MEAN3STD) {
+    st = launch_colkey_mean3std(x, dtype, M, K, sums, cmax, s);
+    if (st) return st;
   }
-  const bool sorted = amode == SQMP_ACT_PER_GROUP;
+  const bool sorted = amode == SQMP_ACT_PER_GROUP || amode == SQMP_ACT_PER_GROUP_MEAN3STD;
   if (sorted) {
     st = launch_rank_partial(cmax, nonsal, Kn, (int)k64, part, s);
     if (st) return st;

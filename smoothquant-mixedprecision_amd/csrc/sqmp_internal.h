@@ -9,6 +9,11 @@ namespace sqmp {
 int launch_colmax(const void* x, int dtype, int R, int C, uint32_t* cmax, hipStream_t s,
                   bool zero = true);  // zero: clear cmax first (else the caller did)
 
+// key[c] = bits(fp32(mean|x| + 3 std|x|)) over the R rows (the mean + 3 sigma sort key);
+// `sums` is a 2*C fp64 scratch (cleared here).
+int launch_colkey_mean3std(const void* x, int dtype, int R, int C, double* sums,
+                           uint32_t* key, hipStream_t s);
+
 // Stable ascending rank of the list cols[0..L) (NULL = identity) keyed by cmax[col]:
 // rank_by_col[cols[i]] = #{j : (cmax[cols[j]], j) < (cmax[cols[i]], i)}.  Zeroes the
 // C-entry rank_by_col first.

@@ -213,7 +213,8 @@ extern "C" int sqmp_weight_geometry(int K, int S, int wmode, int group_size, int
                                     int* Gw, int* ngw, int* S_pad) {
   if (K <= 0 || K > 65000 || S < 0 || S > K) return SQMP_EINVAL;
   int kp, gw, ng;
-  if (wmode == SQMP_W_PER_GROUP || wmode == SQMP_W_PER_GROUP_UNSORTED) {
+  if (wmode == SQMP_W_PER_GROUP || wmode == SQMP_W_PER_GROUP_UNSORTED ||
+      wmode == SQMP_W_PER_GROUP_MEAN3STD) {
     if (group_size <= 0 || group_size > 65000) return SQMP_EINVAL;
     ng = cdiv(K, group_size);
     gw = group_size;
@@ -234,9 +235,10 @@ extern "C" int sqmp_weight_geometry(int K, int S, int wmode, int group_size, int
   return SQMP_OK;
 }
 
+// Workspace: key u32 [K64] | rank i32 [K64] | fp64 column sums [2][K64] (mean + 3 sigma).
 extern "C" size_t sqmp_pack_workspace_bytes(int N, int K) {
   (void)N;
-  return 2 * sizeof(uint32_t) * (size_t)round_up(K > 0 ? K : 1, 64);
+  return (2 * sizeof(uint32_t) + 2 * sizeof(double)) * (size_t)round_up(K > 0 ? K : 1, 64);
 }
 
 extern "C" int sqmp_pack_weight(const void* w, int dtype, int N, int K, int wmode,
@@ -256,9 +258,14 @@ extern "C" int sqmp_pack_weight(const void* w, int dtype, int N, int K, int wmod
   if (ws_bytes < sqmp_pack_workspace_bytes(N, K) || !workspace) return SQMP_EWORKSPACE;
   uint32_t* cmax = (uint32_t*)workspace;
   int32_t* rank = (int32_t*)((char*)workspace + sizeof(uint32_t) * round_up(K, 64));
-  const bool sorted = wmode == SQMP_W_PER_GROUP;
+  double* sums = (double*)((char*)workspace + 2 * sizeof(uint32_t) * round_up(K, 64));
+  const bool mean3std = wmode == SQMP_W_PER_GROUP_MEAN3STD;
+  const bool sorted = wmode == SQMP_W_PER_GROUP || mean3std;
   const bool per_tensor = wmode == SQMP_W_PER_TENSOR;
-  if (sorted || per_tensor) {
+  if (mean3std) {
+    st = launch_colkey_mean3std(w, dtype, N, K, sums, cmax, s);
+    if (st) return st;
+  } else if (sorted || per_tensor) {
     st = launch_colmax(w, dtype, N, K, cmax, s);
     if (st) return st;
   }

@@ -82,6 +82,112 @@ int launch_colmax(const void* x, int dtype, int R, int C, uint32_t* cmax, hipStr
   return SQMP_OK;
 }
 
+// ------------------------------------------------------------------ mean + 3 sigma key
+// The "statistical sorting (mean + 3*STD)" strategy of the reference's README (README.md:36;
+// absent from its code, so this key is defined here -- parity unpinned): per column,
+// key = mean|x| + 3 * std|x| over the R rows (population std), computed from fp64 sums of
+// |x| and x^2 and rounded once to fp32.  Stored as fp32 bits in the same slot as the
+// absmax key, so the stable rank kernels order both the same way.
+template <class DT, int VEC>
+__global__ __launch_bounds__(256) void colsum_kernel(const typename DT::T* __restrict__ x,
+                                                     int R, int C, int rows_per_block,
+                                                     double* __restrict__ s1,
+                                                     double* __restrict__ s2) {
+  typedef typename DT::T T;
+  __shared__ double red[2][4][64 * VEC];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int c0 = (blockIdx.x * 64 + lane) * VEC;
+  const int r0 = blockIdx.y * rows_per_block;
+  const int r1 = min(R, r0 + rows_per_block);
+  double a[VEC], q[VEC];
+#pragma unroll
+  for (int i = 0; i < VEC; ++i) a[i] = q[i] = 0.0;
+  if (c0 + VEC <= C && VEC > 1) {
+    for (int r = r0 + wid; r < r1; r += 4) {
+      const u32x4 raw = *(const u32x4*)(x + (size_t)r * C + c0);
+      const T* v = (const T*)&raw;
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) {
+        const double d = fabs((double)DT::to_f(v[i]));
+        a[i] = __dadd_rn(a[i], d);
+        q[i] = __dadd_rn(q[i], __dmul_rn(d, d));
+      }
+    }
+  } else if (c0 < C) {
+    for (int r = r0 + wid; r < r1; r += 4)
+#pragma unroll
+      for (int i = 0; i < VEC; ++i)
+        if (c0 + i < C) {
+          const double d = fabs((double)DT::to_f(x[(size_t)r * C + c0 + i]));
+          a[i] = __dadd_rn(a[i], d);
+          q[i] = __dadd_rn(q[i], __dmul_rn(d, d));
+        }
+  }
+#pragma unroll
+  for (int i = 0; i < VEC; ++i) {
+    red[0][wid][lane * VEC + i] = a[i];
+    red[1][wid][lane * VEC + i] = q[i];
+  }
+  __syncthreads();
+  for (int t = threadIdx.x; t < 64 * VEC; t += 256) {
+    const int c = blockIdx.x * 64 * VEC + t;
+    if (c >= C) continue;
+    const double va = (red[0][0][t] + red[0][1][t]) + (red[0][2][t] + red[0][3][t]);
+    const double vq = (red[1][0][t] + red[1][1][t]) + (red[1][2][t] + red[1][3][t]);
+    if (va != 0.0) atomicAdd(&s1[c], va);
+    if (vq != 0.0) atomicAdd(&s2[c], vq);
+  }
+}
+
+__global__ __launch_bounds__(256) void mean3std_key_kernel(const double* __restrict__ s1,
+                                                           const double* __restrict__ s2,
+                                                           int R, int C,
+                                                           uint32_t* __restrict__ key) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  const double mean = __ddiv_rn(s1[c], (double)R);
+  double var = __dsub_rn(__ddiv_rn(s2[c], (double)R), __dmul_rn(mean, mean));
+  var = var > 0.0 ? var : 0.0;
+  const double k = __dadd_rn(mean, __dmul_rn(3.0, __dsqrt_rn(var)));
+  key[c] = __float_as_uint(__double2float_rn(k));
+}
+
+template <class DT>
+static void colsum_launch(const void* x, int R, int C, double* s1, double* s2, hipStream_t s) {
+  typedef typename DT::T T;
+  constexpr int VEC = 16 / sizeof(T);
+  const bool vec_ok = ((C * sizeof(T)) % 16 == 0) && (((uintptr_t)x) % 16 == 0);
+  int rows_per_block = 128;
+  const int cblocks_v = cdiv(C, 64 * VEC);
+  while (rows_per_block > 16 && (long)cblocks_v * cdiv(R, rows_per_block) < 1024)
+    rows_per_block >>= 1;
+  if (vec_ok) {
+    colsum_kernel<DT, VEC><<<dim3(cblocks_v, cdiv(R, rows_per_block)), dim3(256), 0, s>>>(
+        (const T*)x, R, C, rows_per_block, s1, s2);
+  } else {
+    colsum_kernel<DT, 1><<<dim3(cdiv(C, 64), cdiv(R, rows_per_block)), dim3(256), 0, s>>>(
+        (const T*)x, R, C, rows_per_block, s1, s2);
+  }
+}
+
+int launch_colkey_mean3std(const void* x, int dtype, int R, int C, double* sums,
+                           uint32_t* key, hipStream_t s) {
+  SQMP_HIP_CHECK(hipMemsetAsync(sums, 0, 2 * sizeof(double) * (size_t)C, s));
+  if (R <= 0 || C <= 0) return SQMP_OK;
+  double* s1 = sums;
+  double* s2 = sums + C;
+  switch (dtype) {
+    case SQMP_F32: colsum_launch<F32>(x, R, C, s1, s2, s); break;
+    case SQMP_F16: colsum_launch<F16>(x, R, C, s1, s2, s); break;
+    case SQMP_BF16: colsum_launch<BF16>(x, R, C, s1, s2, s); break;
+    default: return SQMP_EINVAL;
+  }
+  SQMP_LAUNCH_CHECK();
+  mean3std_key_kernel<<<dim3(cdiv(C, 256)), dim3(256), 0, s>>>(s1, s2, R, C, key);
+  SQMP_LAUNCH_CHECK();
+  return SQMP_OK;
+}
+
 // ------------------------------------------------------------------ stable rank
 // 2-D grid of (256 owners) x (RANK_TILE competitors); each owner counts competitors that
 // order before it -- (value, list index) lexicographically, i.e. a stable ascending sort

@@ -16,7 +16,9 @@ SQMP_OK, SQMP_EINVAL, SQMP_EUNSUPPORTED, SQMP_EHIP, SQMP_EWORKSPACE = 0, -1, -2,
 
 F32, F16, BF16 = 0, 1, 2
 ACT_PER_TOKEN, ACT_PER_TENSOR, ACT_PER_GROUP, ACT_PER_GROUP_UNSORTED = 0, 1, 2, 3
+ACT_PER_GROUP_MEAN3STD = 4
 W_PER_CHANNEL, W_PER_TENSOR, W_PER_GROUP, W_PER_GROUP_UNSORTED, W_NONE = 0, 1, 2, 3, 4
+W_PER_GROUP_MEAN3STD = 5
 OUT_FP, OUT_I8, OUT_INPLACE = 0, 1, 2
 
 _vp, _i, _sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t

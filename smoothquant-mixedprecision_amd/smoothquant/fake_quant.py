@@ -16,6 +16,7 @@ Reference map (file:line in fake_quant.py):
 """
 from __future__ import annotations
 
+import inspect
 from functools import partial
 from typing import Optional
 
@@ -27,6 +28,12 @@ from .ops import PackedWeight
 
 _ACT = ("per_token", "per_tensor", "per_group")
 _WEIGHT = ("per_channel", "per_tensor", "per_group")
+# Sort-strategy extensions (BASELINE config 5; not accepted by the reference, which only
+# wires max-sorted groups): "_unsorted" = the reference's unwired unsorted quantizers
+# (fake_quant.py:29-53, :77-101); "_mean3std" = columns sorted by mean|x| + 3 std|x| (the
+# README.md:36 "statistical sorting", absent from the reference's code; parity unpinned).
+_ACT_EXT = _ACT + ("per_group_unsorted", "per_group_mean3std")
+_WEIGHT_EXT = _WEIGHT + ("per_group_unsorted", "per_group_mean3std")
 
 
 # ----------------------------------------------------------------------------------------
@@ -67,6 +74,15 @@ def quantize_activation_per_group_absmax_sort(t, n_bits, group_size=128):
     return out.view(t.shape)
 
 
+@torch.no_grad()
+def quantize_activation_per_group_mean3std_sort(t, n_bits, group_size=128):
+    """As :104-154 with the columns sorted by mean|x| + 3 std|x| over the batch instead of
+    the column absmax (README.md:36; not in the reference's code -- parity unpinned)."""
+    out = t.contiguous().clone()
+    _fq_act(out, "per_group_mean3std", n_bits, group_size)
+    return out.view(t.shape)
+
+
 def _fq_weight(w: torch.Tensor, mode: str, n_bits: int, group_size: int) -> torch.Tensor:
     return ops.dequant_weight(ops.pack_weight(w, mode, n_bits, group_size, None))
 
@@ -97,9 +113,61 @@ def quantize_weight_per_group_absmax_sort(w, n_bits, group_size=128):
     return _fq_weight(w, "per_group", n_bits, group_size)
 
 
+@torch.no_grad()
+def quantize_weight_per_group_mean3std_sort(w, n_bits, group_size=128):
+    """As :156-207 with the columns sorted by mean|W| + 3 std|W| (parity unpinned)."""
+    return _fq_weight(w, "per_group_mean3std", n_bits, group_size)
+
+
 _ACT_FNS = {"per_token": quantize_activation_per_token_absmax,
             "per_tensor": quantize_activation_per_tensor_absmax,
-            "per_group": quantize_activation_per_group_absmax_sort}
+            "per_group": quantize_activation_per_group_absmax_sort,
+            "per_group_unsorted": quantize_activation_per_group_absmax,
+            "per_group_mean3std": quantize_activation_per_group_mean3std_sort}
+_FN_MODE = {fn: mode for mode, fn in _ACT_FNS.items()}
+_GROUPED = ("per_group", "per_group_unsorted", "per_group_mean3std")
+
+
+def _bind_act(mode: str, n_bits: int, group_size: int):
+    """The act_quant partial of fake_quant.py:246-256 for `mode`."""
+    kw = {"group_size": group_size} if mode in _GROUPED else {}
+    return partial(_ACT_FNS[mode], n_bits=n_bits, **kw)
+
+
+def resolve_quantizer(fn):
+    """(mode, n_bits, group_size) of an act/output quantizer callable, or None for the
+    identity.  Accepts what the reference binds (fake_quant.py:246-263) and what its users
+    rebind (e.g. W4A8: ``q.act_quant = partial(quantize_activation_per_group_absmax_sort,
+    n_bits=8, group_size=G)``): a functools.partial over one of this module's activation
+    quantizers.  Any other callable raises -- the HIP operator cannot run arbitrary Python
+    quantizers, and silently ignoring one would change the numerics."""
+    if fn is None or getattr(fn, "_sqmp_identity", False):
+        return None
+    base, args, kw = fn, (), {}
+    if isinstance(fn, partial):
+        base, args, kw = fn.func, fn.args, dict(fn.keywords or {})
+    mode = _FN_MODE.get(base)
+    if mode is None:
+        raise NotImplementedError(
+            f"W4A4Linear: unsupported quantizer callable {fn!r}; bind one of "
+            f"{sorted(f.__name__ for f in _FN_MODE)} with functools.partial")
+    bound = inspect.signature(base).bind_partial(None, *args, **kw)
+    bound.apply_defaults()
+    n_bits = bound.arguments.get("n_bits")
+    if n_bits is None:
+        raise TypeError(f"{base.__name__}: missing n_bits")
+    return mode, int(n_bits), int(bound.arguments.get("group_size", 128))
+
+
+def _identity(x):
+    return x
+
+
+def _spec_list(spec):
+    return None if spec is None else [spec[0], int(spec[1]), int(spec[2])]
+
+
+_identity._sqmp_identity = True
 
 _PACKED_BUFFERS = ("w_codes", "w_scale", "w_salient", "w_perm", "w_amap", "w_amap_fq",
                    "w_nonsal", "salient_i32", "w_dense", "out_amap_fq", "out_nonsal")
@@ -126,17 +194,16 @@ class W4A4Linear(nn.Module):
         self.out_features = out_features
         self.group_size = group_size
         self.quant_bits = quant_bits
-        if act_quant not in _ACT:
+        if act_quant not in _ACT_EXT:
             raise ValueError(f"Invalid act_quant: {act_quant}")     # fake_quant.py:256
         self.act_quant_name = act_quant
-        self.act_quant = partial(_ACT_FNS[act_quant], n_bits=quant_bits,
-                                 **({"group_size": group_size} if act_quant == "per_group" else {}))
+        self.act_quant = _bind_act(act_quant, quant_bits, group_size)
         if quantize_output:
             self.output_quant_name = self.act_quant_name
             self.output_quant = self.act_quant
         else:
             self.output_quant_name = "None"
-            self.output_quant = lambda x: x
+            self.output_quant = _identity
         self.salient_indices = None
         if importance is not None and salient_prop > 0:             # :265-270
             sorted_idx = torch.argsort(importance, descending=True, stable=True)
@@ -181,7 +248,7 @@ class W4A4Linear(nn.Module):
                 raise RuntimeError("W4A4Linear packing needs a ROCm GPU (no CPU implementation)")
             wg = wg.to("cuda")
         sal = self.salient_indices
-        pw = ops.pack_weight(wg, weight_quant if weight_quant in _WEIGHT else "none",
+        pw = ops.pack_weight(wg, weight_quant if weight_quant in _WEIGHT_EXT else "none",
                              self.quant_bits, self.group_size, sal)
         self._install(pw, weight_quant)
         if dev.type != "cuda":
@@ -216,6 +283,9 @@ class W4A4Linear(nn.Module):
             "in_features": self.in_features, "out_features": self.out_features,
             "quant_bits": self.quant_bits, "group_size": self.group_size,
             "act_quant": self.act_quant_name, "output_quant": self.output_quant_name,
+            # the bound quantizers themselves (they may have been rebound, e.g. W4A8)
+            "act_spec": _spec_list(resolve_quantizer(self.act_quant)),
+            "output_spec": _spec_list(resolve_quantizer(self.output_quant)),
             "weight_quant": self.weight_quant_name, "kernel": self.kernel,
             "salient_indices": (None if self.salient_indices is None
                                 else self.salient_indices.detach().to("cpu", torch.int64)),
@@ -232,12 +302,16 @@ class W4A4Linear(nn.Module):
         self.group_size = state["group_size"]
         act = state["act_quant"]
         self.act_quant_name = act
-        self.act_quant = partial(_ACT_FNS[act], n_bits=self.quant_bits,
-                                 **({"group_size": self.group_size} if act == "per_group" else {}))
+        spec = state.get("act_spec")
+        self.act_quant = (_bind_act(spec[0], spec[1], spec[2]) if spec
+                          else _bind_act(act, self.quant_bits, self.group_size))
         if state["output_quant"] != "None":
-            self.output_quant_name, self.output_quant = self.act_quant_name, self.act_quant
+            ospec = state.get("output_spec")
+            self.output_quant_name = state["output_quant"]
+            self.output_quant = (_bind_act(ospec[0], ospec[1], ospec[2]) if ospec
+                                 else self.act_quant)
         else:
-            self.output_quant_name, self.output_quant = "None", (lambda x: x)
+            self.output_quant_name, self.output_quant = "None", _identity
         self.weight_quant_name = state["weight_quant"]
         self.kernel = state.get("kernel", "auto")
         sal = state["salient_indices"]
@@ -319,37 +393,39 @@ class W4A4Linear(nn.Module):
         pw = self.packed()
         if x2.dtype != pw.dtype:
             raise RuntimeError(f"expected input dtype {pw.dtype}, got {x2.dtype}")
-        mutate_input = (self.salient_indices is None and self.act_quant_name != "per_group"
+        # the bound quantizers (fake_quant.py:246-263), honouring a rebinding such as W4A8
+        amode, bits, ag = resolve_quantizer(self.act_quant)
+        ospec = resolve_quantizer(self.output_quant)
+        # per_token / per_tensor quantize the caller's activation in place when no channel
+        # is salient (:304 -> :56-75); the grouped quantizers return new tensors
+        mutate_input = (self.salient_indices is None and amode in ("per_token", "per_tensor")
                         and x2.data_ptr() == x.data_ptr() and x2.is_contiguous())
         xc = x2.contiguous()
         bias = None if self.bias is None else self.bias.reshape(-1)
         if bias is not None and bias.dtype != pw.dtype:
             raise RuntimeError(f"bias dtype {bias.dtype} does not match {pw.dtype}")
-        bits = self.quant_bits
         use_i8 = (self.kernel == "i8" or
-                  (self.kernel == "auto" and ops.I8_AUTO
-                   and ops.i8_eligible(pw, self.act_quant_name, bits)))
+                  (self.kernel == "auto" and ops.I8_AUTO and ops.i8_eligible(pw, amode, bits)))
         if use_i8:
-            a8, sa, xs = ops.quant_act_i8(xc, pw, self.act_quant_name, bits)
+            a8, sa, xs = ops.quant_act_i8(xc, pw, amode, bits)
         else:
-            a = ops.quant_act_fp(xc, pw, self.act_quant_name, bits, self.group_size)
+            a = ops.quant_act_fp(xc, pw, amode, bits, ag)
         if mutate_input:
-            # the reference quantizes the caller's activation in place here (:304 -> :56-75)
-            ops.fake_quant_inplace(xc, self.act_quant_name, bits, self.group_size, pw.amap_fq,
-                                   pw.nonsal, 0)
+            ops.fake_quant_inplace(xc, amode, bits, ag, pw.amap_fq, pw.nonsal, 0)
         y = ops.gemm_i8(a8, sa, xs, pw, bias) if use_i8 else ops.gemm_fq(a, pw, bias)
-        if self.output_quant_name != "None":                                 # :308-316
+        if ospec is not None:                                                # :308-316
+            omode, obits, og = ospec
             if self.salient_indices is not None:
                 if pw.N != pw.K:
                     raise IndexError(
                         f"The shape of the mask [{pw.K}] at index 0 does not match the shape "
                         f"of the indexed tensor [{y.shape[0]}, {pw.N}] at index 1")
                 if pw.K - pw.S > 0:
-                    ops.fake_quant_inplace(y, self.output_quant_name, bits, self.group_size,
-                                           pw.amap_fq, pw.nonsal, pw.S)
+                    ops.fake_quant_inplace(y, omode, obits, og, pw.amap_fq, pw.nonsal, pw.S)
             else:
-                ops.fake_quant_inplace(y, self.output_quant_name, bits, self.group_size,
-                                       self.out_amap_fq, self.out_nonsal, 0)
+                if self.out_amap_fq is None:
+                    _, _, self.out_amap_fq, self.out_nonsal = ops.build_maps(pw.N, None, y.device)
+                ops.fake_quant_inplace(y, omode, obits, og, self.out_amap_fq, self.out_nonsal, 0)
         if len(x_shape) == 3:
             return y.view(x_shape[0], x_shape[1], -1)
         return y
@@ -365,7 +441,7 @@ class W4A4Linear(nn.Module):
                                 quantize_output=quantize_output, importance=importance,
                                 salient_prop=salient_prop, quant_bits=quant_bits,
                                 group_size=group_size)
-        if weight_quant not in _WEIGHT:
+        if weight_quant not in _WEIGHT_EXT:
             raise ValueError(f"Invalid weight_quant: {weight_quant}")         # :361
         new_module._pack_from(module.weight.data, weight_quant)
         if module.bias is not None:

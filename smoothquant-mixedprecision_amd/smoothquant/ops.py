@@ -16,10 +16,11 @@ from ._lib import check, load
 
 DTYPE_CODE = {torch.float32: _lib.F32, torch.float16: _lib.F16, torch.bfloat16: _lib.BF16}
 ACT_MODES = {"per_token": _lib.ACT_PER_TOKEN, "per_tensor": _lib.ACT_PER_TENSOR,
-             "per_group": _lib.ACT_PER_GROUP, "per_group_unsorted": _lib.ACT_PER_GROUP_UNSORTED}
+             "per_group": _lib.ACT_PER_GROUP, "per_group_unsorted": _lib.ACT_PER_GROUP_UNSORTED,
+             "per_group_mean3std": _lib.ACT_PER_GROUP_MEAN3STD}
 WEIGHT_MODES = {"per_channel": _lib.W_PER_CHANNEL, "per_tensor": _lib.W_PER_TENSOR,
                 "per_group": _lib.W_PER_GROUP, "per_group_unsorted": _lib.W_PER_GROUP_UNSORTED,
-                "none": _lib.W_NONE}
+                "per_group_mean3std": _lib.W_PER_GROUP_MEAN3STD, "none": _lib.W_NONE}
 
 
 def _p(t: Optional[torch.Tensor]):
