@@ -142,6 +142,24 @@ int sqmp_quant_act(void* x, int dtype, int M, int K, int amode, int n_bits,
                    void* out_scale, void* out_xs, void* workspace, size_t ws_bytes,
                    void* stream);
 
+/* sqmp_quant_act_v2 flags. */
+#define SQMP_QA_CLEAN_WS 1    /* the workspace's statistics regions are zero on entry (a
+                                 persistent workspace, first allocated zeroed); the call
+                                 leaves them zero again, so no per-call memset is needed */
+#define SQMP_QA_REUSE_STATS 2 /* the workspace still holds the sorted column order of THIS
+                                 batch x and non-salient list (a previous call on the same
+                                 input, e.g. q/k/v or gate/up sharing x): skip the column
+                                 statistics and the rank (sorted per_group modes only) */
+
+/* sqmp_quant_act with the per-weight map posmap (int32 [K]: packed position of column k,
+ * the inverse of perm; NULL = derive it per call) and flags.  With posmap, OUT_FP on
+ * fp16/bf16 runs column statistics -> rank -> table -> the lane-contiguous quantizer. */
+int sqmp_quant_act_v2(void* x, int dtype, int M, int K, int amode, int n_bits,
+                      int group_size, const int32_t* amap, int Kp, const int32_t* nonsal,
+                      const int32_t* salient, int S, int S_pad, const int32_t* posmap,
+                      int flags, int out_kind, void* out, void* out_scale, void* out_xs,
+                      void* workspace, size_t ws_bytes, void* stream);
+
 /* GEMM operand allocation rule: the activation operands (a / a8 / xs) are read in whole
  * 256-row tiles by LDS-DMA, so their allocations must hold roundup(M, 256) rows (rows
  * >= M may hold anything; they never reach y).  a8 rows are roundup(Kp, 256) bytes.

@@ -18,6 +18,8 @@
 // LDS tables once (column -> group, output position -> (group, column)), then per row:
 // stage the row in LDS, per-(row, group) absmax with LDS atomics, scales, and writes the
 // output row in OUTPUT order with 16-B coalesced stores (gathering from the LDS row).
+#include <stdlib.h>
+
 #include "sqmp_internal.h"
 
 namespace sqmp {
@@ -415,8 +417,12 @@ __global__ __launch_bounds__(256) void quant_fp_kernel(
 __global__ __launch_bounds__(256) void build_ent_kernel(
     const int32_t* __restrict__ amap, int P, const int32_t* __restrict__ nonsal, int Kn,
     const int32_t* __restrict__ part, int ntile, int ld, int mode, int G,
-    uint32_t* __restrict__ ent, int32_t* __restrict__ rank_by_col) {
+    uint32_t* __restrict__ ent, int32_t* __restrict__ rank_by_col, uint32_t* __restrict__ lctab,
+    int lc_len, uint32_t lc_none, int32_t* __restrict__ colsorted) {
   const int p = blockIdx.x * 256 + threadIdx.x;
+  // ranks [Kn, lc_len) of the lane-contiguous table: (zero word, sink word) entries
+  if (lctab)
+    for (int r = Kn + p; r < lc_len; r += P) lctab[r] = lc_none;
   if (p >= P) return;
   const int k = amap[p];
   uint32_t e = G_ZERO << 16;
@@ -431,14 +437,53 @@ __global__ __launch_bounds__(256) void build_ent_kernel(
       r = 0;
       for (int t = 0; t < ntile; ++t) r += part[(size_t)t * ld + lo];
       if (rank_by_col) rank_by_col[k] = r;
+      if (colsorted) colsorted[r] = k;  // the sorted order, for SQMP_QA_REUSE_STATS
     }
     const int g = mode == MODE_GROUP ? r / G : 0;
     e = ((uint32_t)g << 16) | (uint32_t)k;
+    // rank-ordered (column, packed position) table of the lane-contiguous quantizer
+    if (lctab) lctab[r] = (uint32_t)k | ((uint32_t)p << 16);
   }
   if (ent) {
     const int c = p >> 3, j = p & 7;
     ent[(size_t)(j >> 2) * (P / 2) + c * 4 + (j & 3)] = e;
   }
+}
+
+// ---------------------------------------------------------------- lane-contiguous table
+// Per call, one thread per non-salient list entry i (column nonsal[i]):
+//   TAB_COUNTS  r = counts[col] (the stable rank), counts[col] = 0 afterwards, and the
+//               sorted column list colsorted[r] = col is kept for sibling layers;
+//   TAB_SORTED  col = colsorted[i], r = i (statistics reused from a previous call);
+//   TAB_LIST    r = i (unsorted groups / per_token / per_tensor).
+// lctab[r] = col | posmap[col] << 16, ranks [Kn, lc_len) get the (zero word, sink word)
+// entry, and key[0..K) is cleared when given (clean-workspace protocol).
+enum { TAB_COUNTS = 0, TAB_SORTED = 1, TAB_LIST = 2 };
+__global__ __launch_bounds__(256) void lc_table_kernel(
+    int mode, const int32_t* __restrict__ nonsal, int Kn, int K,
+    const int32_t* __restrict__ posmap, int32_t* __restrict__ counts,
+    int32_t* __restrict__ colsorted, uint32_t* __restrict__ key, uint32_t* __restrict__ lctab,
+    int lc_len, uint32_t lc_none) {
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  const int nt = gridDim.x * 256;
+  if (t < Kn) {
+    int col, r;
+    if (mode == TAB_SORTED) {
+      col = colsorted[t];
+      r = t;
+    } else {
+      col = nonsal[t];
+      r = t;
+      if (mode == TAB_COUNTS) {
+        r = counts[col];
+        counts[col] = 0;
+        colsorted[r] = col;
+      }
+    }
+    lctab[r] = (uint32_t)col | ((uint32_t)posmap[col] << 16);
+  }
+  if (key && t < K) key[t] = 0u;
+  for (int r = Kn + t; r < lc_len; r += nt) lctab[r] = lc_none;
 }
 
 // ---------------------------------------------------------------- wave-per-row variant
@@ -718,28 +763,32 @@ static int quant_dispatch(void* x, int M, int K, int amode, int q_max, int G, in
 using namespace sqmp;
 
 // Workspace: cmax u32 [K64] | rank_by_col i32 [K64] | rank partials i32 [tiles][K64] |
-// entry table u32 [Kp64] | fp64 column sums [2][K64] (mean + 3 sigma key).  Only cmax (or
-// the sums) is cleared per call.
+// entry table u32 [Kp64] | lane-contiguous table u32 [roundup(K, 4096)] | rank counts
+// i32 [K64] | sorted column list i32 [K64] | fp64 column sums [2][K64] (mean + 3 sigma).
+// Without SQMP_QA_CLEAN_WS only what a call reads before writing is cleared per call.
 static size_t ws_k64(int K) { return (size_t)round_up(K > 0 ? K : 1, 64); }
 static size_t ws_u32_words(int K, int Kp) {
   const size_t k64 = ws_k64(K);
-  return k64 * (2 + (size_t)rank_tiles(K)) + (size_t)round_up(Kp > K ? Kp : K, 64);
+  return k64 * (4 + (size_t)rank_tiles(K)) + (size_t)round_up(Kp > K ? Kp : K, 64) +
+         (size_t)round_up(K > 0 ? K : 1, 4096);
 }
 extern "C" size_t sqmp_act_workspace_bytes(int M, int K, int Kp) {
   (void)M;
   return sizeof(uint32_t) * ws_u32_words(K, Kp) + 2 * sizeof(double) * ws_k64(K);
 }
 
-extern "C" int sqmp_quant_act(void* x, int dtype, int M, int K, int amode, int n_bits,
-                              int group_size, const int32_t* amap, int Kp,
-                              const int32_t* nonsal, const int32_t* salient, int S, int S_pad,
-                              int out_kind, void* out, void* out_scale, void* out_xs,
-                              void* workspace, size_t ws_bytes, void* stream) {
+extern "C" int sqmp_quant_act_v2(void* x, int dtype, int M, int K, int amode, int n_bits,
+                                 int group_size, const int32_t* amap, int Kp,
+                                 const int32_t* nonsal, const int32_t* salient, int S,
+                                 int S_pad, const int32_t* posmap, int flags, int out_kind,
+                                 void* out, void* out_scale, void* out_xs, void* workspace,
+                                 size_t ws_bytes, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   if (dtype < SQMP_F32 || dtype > SQMP_BF16 || M < 0 || K <= 0 || K > 65000) return SQMP_EINVAL;
   if (amode < SQMP_ACT_PER_TOKEN || amode > SQMP_ACT_PER_GROUP_MEAN3STD) return SQMP_EINVAL;
   if (n_bits < 2 || n_bits > 8) return SQMP_EUNSUPPORTED;
   if (S < 0 || S > K || !x || !amap || (K - S > 0 && !nonsal)) return SQMP_EINVAL;
+  if (flags & ~(SQMP_QA_CLEAN_WS | SQMP_QA_REUSE_STATS)) return SQMP_EINVAL;
   if (out_kind == SQMP_OUT_INPLACE) {
     if (Kp != K) return SQMP_EINVAL;
   } else if (out_kind == SQMP_OUT_FP || out_kind == SQMP_OUT_I8) {
@@ -755,11 +804,15 @@ extern "C" int sqmp_quant_act(void* x, int dtype, int M, int K, int amode, int n
   if (group && (group_size <= 0 || group_size > 65000)) return SQMP_EINVAL;
   if (M == 0) return SQMP_OK;
   if (ws_bytes < sqmp_act_workspace_bytes(M, K, Kp) || !workspace) return SQMP_EWORKSPACE;
+  const bool clean = (flags & SQMP_QA_CLEAN_WS) != 0;
   const size_t k64 = ws_k64(K);
   uint32_t* cmax = (uint32_t*)workspace;
   int32_t* rank = (int32_t*)(cmax + k64);
   int32_t* part = rank + k64;
   uint32_t* ent = (uint32_t*)(part + k64 * (size_t)rank_tiles(K));
+  uint32_t* lctab = ent + round_up(Kp > K ? Kp : K, 64);
+  int32_t* counts = (int32_t*)(lctab + round_up(K, 4096));
+  int32_t* colsorted = counts + k64;
   double* sums = (double*)((uint32_t*)workspace + ws_u32_words(K, Kp));
   const int Kn = K - S;
   if (Kn == 0) {
@@ -767,15 +820,56 @@ extern "C" int sqmp_quant_act(void* x, int dtype, int M, int K, int amode, int n
     if (out_kind == SQMP_OUT_INPLACE) return SQMP_OK;
   }
   int st;
+  const bool sorted = amode == SQMP_ACT_PER_GROUP || amode == SQMP_ACT_PER_GROUP_MEAN3STD;
+  const int q_max = (1 << (n_bits - 1)) - 1;
+  // SQMP_DISABLE_LC=1 selects the previous row kernels (A/B timing diagnostics only)
+  static const bool lc_off = getenv("SQMP_DISABLE_LC") != nullptr;
+  const bool use_lc = out_kind == SQMP_OUT_FP && !lc_off &&
+                      quant_lc_supported(dtype, M, K, group, group_size, Kn, Kp, S_pad, x, out);
+  const int lmode = group ? 2 : amode == SQMP_ACT_PER_TENSOR ? 1 : 0;
+  const uint32_t lc_none = (uint32_t)(Kp + S_pad) | ((uint32_t)(Kp + S_pad + 1) << 16);
+  const int lc_len = (int)round_up(K, 4096);
+
+  // ---- fast path: lane-contiguous quantizer fed by the per-weight column -> position map;
+  // at most colmax + rank + table + quantizer launches, none of them a memset in the
+  // clean-workspace protocol, and only table + quantizer when the statistics are reused.
+  if (use_lc && posmap && amode != SQMP_ACT_PER_TENSOR) {
+    int tmode = TAB_LIST;
+    if (sorted) {
+      if (flags & SQMP_QA_REUSE_STATS) {
+        tmode = TAB_SORTED;
+      } else {
+        tmode = TAB_COUNTS;
+        if (amode == SQMP_ACT_PER_GROUP) {
+          if (!clean) SQMP_HIP_CHECK(hipMemsetAsync(cmax, 0, sizeof(uint32_t) * k64, s));
+          st = launch_colmax(x, dtype, M, K, cmax, s, false);
+        } else {
+          st = launch_colkey_mean3std(x, dtype, M, K, sums, cmax, s, clean);
+        }
+        if (st) return st;
+        if (!clean) SQMP_HIP_CHECK(hipMemsetAsync(counts, 0, sizeof(int32_t) * k64, s));
+        st = launch_rank_count(cmax, nonsal, Kn, counts, s);
+        if (st) return st;
+      }
+    }
+    const int nthr = K > Kn ? K : (Kn > 0 ? Kn : 1);
+    lc_table_kernel<<<dim3(cdiv(nthr, 256)), dim3(256), 0, s>>>(
+        tmode, nonsal, Kn, K, posmap, counts, colsorted, tmode == TAB_COUNTS ? cmax : nullptr,
+        lctab, lc_len, lc_none);
+    SQMP_LAUNCH_CHECK();
+    return launch_quant_lc(dtype, lmode, x, M, K, q_max, group_size, lctab, Kn, amap, Kp,
+                           salient, S, S_pad, cmax, nonsal, out, s);
+  }
+
+  // ---- general path (fp32, 8-bit int output, in-place output quant, large rows)
   if (amode == SQMP_ACT_PER_TENSOR || amode == SQMP_ACT_PER_GROUP) {
     SQMP_HIP_CHECK(hipMemsetAsync(cmax, 0, sizeof(uint32_t) * k64, s));
     st = launch_colmax(x, dtype, M, K, cmax, s, false);
     if (st) return st;
   } else if (amode == SQMP_ACT_PER_GROUP_MEAN3STD) {
-    st = launch_colkey_mean3std(x, dtype, M, K, sums, cmax, s);
+    st = launch_colkey_mean3std(x, dtype, M, K, sums, cmax, s, clean);
     if (st) return st;
   }
-  const bool sorted = amode == SQMP_ACT_PER_GROUP || amode == SQMP_ACT_PER_GROUP_MEAN3STD;
   if (sorted) {
     st = launch_rank_partial(cmax, nonsal, Kn, (int)k64, part, s);
     if (st) return st;
@@ -784,28 +878,50 @@ extern "C" int sqmp_quant_act(void* x, int dtype, int M, int K, int amode, int n
   const int mode_e = group ? MODE_GROUP : MODE_TOKEN;
   const int Pe = out_kind == SQMP_OUT_INPLACE ? K : Kp;
   const bool need_ent = out_kind == SQMP_OUT_FP && Pe % 8 == 0;
-  if (need_ent || sorted) {
+  if (need_ent || sorted || use_lc) {
     build_ent_kernel<<<dim3(cdiv(Pe, 256)), dim3(256), 0, s>>>(
         amap, Pe, nonsal, Kn, sorted ? part : nullptr, rank_tiles(Kn), (int)k64, mode_e,
-        group ? group_size : 1, need_ent ? ent : nullptr, sorted ? rank : nullptr);
+        group ? group_size : 1, need_ent && !use_lc ? ent : nullptr, sorted ? rank : nullptr,
+        use_lc ? lctab : nullptr, lc_len, lc_none, sorted ? colsorted : nullptr);
     SQMP_LAUNCH_CHECK();
   }
-  const int q_max = (1 << (n_bits - 1)) - 1;
-  const int nga = group ? (Kn > 0 ? cdiv(Kn, group_size) : 1) : 1;
-  const int32_t* rk = sorted ? rank : nullptr;
-  const uint32_t* entp = need_ent ? ent : nullptr;
-  switch (dtype) {
-    case SQMP_F32:
-      return quant_dispatch<F32>(x, M, K, amode, q_max, group_size, nga, amap, Kp, nonsal,
-                                 Kn, salient, S, S_pad, rk, cmax, entp, out_kind, out, out_scale,
+  if (use_lc) {
+    st = launch_quant_lc(dtype, lmode, x, M, K, q_max, group_size, lctab, Kn, amap, Kp,
+                         salient, S, S_pad, cmax, nonsal, out, s);
+  } else {
+    const int nga = group ? (Kn > 0 ? cdiv(Kn, group_size) : 1) : 1;
+    const int32_t* rk = sorted ? rank : nullptr;
+    const uint32_t* entp = need_ent ? ent : nullptr;
+    switch (dtype) {
+      case SQMP_F32:
+        st = quant_dispatch<F32>(x, M, K, amode, q_max, group_size, nga, amap, Kp, nonsal, Kn,
+                                 salient, S, S_pad, rk, cmax, entp, out_kind, out, out_scale,
                                  out_xs, s);
-    case SQMP_F16:
-      return quant_dispatch<F16>(x, M, K, amode, q_max, group_size, nga, amap, Kp, nonsal,
-                                 Kn, salient, S, S_pad, rk, cmax, entp, out_kind, out, out_scale,
+        break;
+      case SQMP_F16:
+        st = quant_dispatch<F16>(x, M, K, amode, q_max, group_size, nga, amap, Kp, nonsal, Kn,
+                                 salient, S, S_pad, rk, cmax, entp, out_kind, out, out_scale,
                                  out_xs, s);
-    default:
-      return quant_dispatch<BF16>(x, M, K, amode, q_max, group_size, nga, amap, Kp, nonsal,
-                                  Kn, salient, S, S_pad, rk, cmax, entp, out_kind, out, out_scale,
+        break;
+      default:
+        st = quant_dispatch<BF16>(x, M, K, amode, q_max, group_size, nga, amap, Kp, nonsal, Kn,
+                                  salient, S, S_pad, rk, cmax, entp, out_kind, out, out_scale,
                                   out_xs, s);
+    }
   }
+  if (st) return st;
+  // the general path leaves the column keys behind: restore the clean-workspace invariant
+  if (clean && (amode == SQMP_ACT_PER_TENSOR || sorted))
+    SQMP_HIP_CHECK(hipMemsetAsync(cmax, 0, sizeof(uint32_t) * k64, s));
+  return SQMP_OK;
+}
+
+extern "C" int sqmp_quant_act(void* x, int dtype, int M, int K, int amode, int n_bits,
+                              int group_size, const int32_t* amap, int Kp,
+                              const int32_t* nonsal, const int32_t* salient, int S, int S_pad,
+                              int out_kind, void* out, void* out_scale, void* out_xs,
+                              void* workspace, size_t ws_bytes, void* stream) {
+  return sqmp_quant_act_v2(x, dtype, M, K, amode, n_bits, group_size, amap, Kp, nonsal,
+                           salient, S, S_pad, nullptr, 0, out_kind, out, out_scale, out_xs,
+                           workspace, ws_bytes, stream);
 }

@@ -1,0 +1,348 @@
+// Lane-contiguous activation quantizer (OUT_FP, fp16 / bf16): the pre-GEMM half of
+// W4A4Linear.forward (/root/reference/smoothquant/fake_quant.py:291-304) with the bound
+// act quantizer (:56-75 per_token / per_tensor, :77-101 unsorted and :104-154 sorted
+// per_group), producing the faithful GEMM's A operand [M][P + S_pad]:
+//   positions p < P (packed weight order): x_hat of column amap[p], 0 at salient/padding;
+//   positions P + j: the exact salient column sal[j], 0 beyond S.
+//
+// Layout of the work (one workgroup = NW waves, two rows at a time):
+//   * LDS holds the two rows INTERLEAVED: word k = (x[m][k], x[m+1][k]) as two D halves,
+//     so every 32-bit LDS access moves both rows' values of one column.
+//   * Thread t owns the RPL consecutive activation ranks [RPL t, RPL (t+1)) (its entries
+//     of the per-call table: column | packed position << 16 in rank order, built by
+//     build_ent_kernel).  A per_group group is G consecutive ranks, so for G >= RPL a
+//     thread's values lie in one group (G / RPL lanes per group, combined by lane
+//     shuffles; groups never straddle waves) and for G < RPL a thread holds RPL / G whole
+//     groups: the group absmax needs no LDS atomics.
+//   * Per row pair: 16-B global loads (prefetched one row pair ahead) -> interleave into
+//     LDS -> gather the thread's RPL column pairs (ds_read_b32) -> group absmax on the
+//     packed magnitudes (v_pk_max_u16) -> scales -> quantize both rows at once with packed
+//     math -> scatter to the packed positions in the same LDS buffer (ds_write_b32) ->
+//     de-interleave 16-B chunks -> 16-B global stores of both rows.
+// Numerics (bit-exact with the reference, signed zeros included):
+//   scale s = D(D(clamp(absmax, 1e-5)) / q_max), r = fp32(1 / s) correctly rounded;
+//   q = fl32(x / s) by Markstein's correction (q0 = x r, e = fma(-q0, s, x) exact,
+//   q = fma(e, r, q0) is the correctly rounded quotient); code = rne(D(q)) (fp16: the
+//   1536 magic add, exact for |q| < 512); x_hat = D(code * s) (one correctly rounded D
+//   product) with the sign of x (the reference's -0.0 for small negative values).
+#include "sqmp_internal.h"
+
+namespace sqmp {
+
+namespace {
+
+constexpr int LC_MODE_TOKEN = 0, LC_MODE_TENSOR = 1, LC_MODE_GROUP = 2;
+constexpr int LC_CH = 4;    // 16-B input chunks per thread per row
+constexpr int LC_MAXW = 16;  // waves per workgroup (1024 threads)
+
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef _Float16 h16x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 b16x2 __attribute__((ext_vector_type(2)));
+
+__device__ inline uint32_t pk_absmax(uint32_t a, uint32_t b) {
+  // both halves are D values; their magnitudes order like unsigned 16-bit integers
+  const u16x2 x = __builtin_bit_cast(u16x2, a & 0x7FFF7FFFu);
+  const u16x2 y = __builtin_bit_cast(u16x2, b & 0x7FFF7FFFu);
+  return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(x, y));
+}
+
+template <class DT>
+__device__ inline float half_lo(uint32_t w) {
+  return DT::to_f(__builtin_bit_cast(typename DT::T, (uint16_t)(w & 0xFFFFu)));
+}
+template <class DT>
+__device__ inline float half_hi(uint32_t w) {
+  return DT::to_f(__builtin_bit_cast(typename DT::T, (uint16_t)(w >> 16)));
+}
+
+// lane-xor max of both halves over `width` lanes (width a power of two <= 64)
+__device__ inline uint32_t xor_max(uint32_t v, int width) {
+  for (int o = 1; o < width; o <<= 1) v = pk_absmax(v, (uint32_t)__shfl_xor((int)v, o, 64));
+  return v;
+}
+
+// the two rows' scales of one group
+struct PairScale {
+  f32x2 s, r;     // D scale (as fp32) and its correctly rounded reciprocal
+  uint32_t sd;    // both scales as D bit patterns
+};
+
+template <class DT>
+__device__ inline PairScale pair_scale(uint32_t mx, int q_max) {
+  PairScale c;
+  c.s[0] = group_scale<DT>(half_lo<DT>(mx), q_max);
+  c.s[1] = group_scale<DT>(half_hi<DT>(mx), q_max);
+  c.r[0] = 1.0f / c.s[0];
+  c.r[1] = 1.0f / c.s[1];
+  c.sd = (uint32_t)__builtin_bit_cast(uint16_t, DT::from_f(c.s[0])) |
+         ((uint32_t)__builtin_bit_cast(uint16_t, DT::from_f(c.s[1])) << 16);
+  return c;
+}
+
+template <class DT>
+__device__ inline uint32_t quant_pair(uint32_t v, const PairScale& c);
+
+template <>
+__device__ inline uint32_t quant_pair<F16>(uint32_t v, const PairScale& c) {
+  const f32x2 t = __builtin_convertvector(__builtin_bit_cast(h16x2, v), f32x2);
+  const f32x2 q0 = t * c.r;
+  const f32x2 e = __builtin_elementwise_fma(-q0, c.s, t);
+  const f32x2 q = __builtin_elementwise_fma(e, c.r, q0);
+  const h16x2 d = __builtin_convertvector(q, h16x2);
+  const h16x2 magic = {(_Float16)1536.0f, (_Float16)1536.0f};
+  const h16x2 code = (d + magic) - magic;
+  const h16x2 y = code * __builtin_bit_cast(h16x2, c.sd);
+  return __builtin_bit_cast(uint32_t, y) | (v & 0x80008000u);
+}
+
+template <>
+__device__ inline uint32_t quant_pair<BF16>(uint32_t v, const PairScale& c) {
+  f32x2 t;
+  t[0] = __uint_as_float(v << 16);
+  t[1] = __uint_as_float(v & 0xFFFF0000u);
+  const f32x2 q0 = t * c.r;
+  const f32x2 e = __builtin_elementwise_fma(-q0, c.s, t);
+  const f32x2 q = __builtin_elementwise_fma(e, c.r, q0);
+  const uint32_t db = __builtin_bit_cast(uint32_t, __builtin_convertvector(q, b16x2));
+  f32x2 d;
+  d[0] = __uint_as_float(db << 16);
+  d[1] = __uint_as_float(db & 0xFFFF0000u);
+  const f32x2 y = __builtin_elementwise_roundeven(d) * c.s;  // code * s: exact in fp32
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(y, b16x2)) | (v & 0x80008000u);
+}
+
+}  // namespace
+
+// RPL = ranks per thread; GS = the group size when it is below RPL (RPL / GS groups per
+// thread), else 0.  blockDim = 64 * NW.
+template <class DT, int MODE, int RPL, int GS>
+__global__ __launch_bounds__(1024) void quant_lc_kernel(
+    const typename DT::T* __restrict__ x, int M, int K, int q_max, int G,
+    const uint32_t* __restrict__ lctab, int Kn, const int32_t* __restrict__ amap, int P,
+    const int32_t* __restrict__ sal, int S, int S_pad, const uint32_t* __restrict__ cmax,
+    const int32_t* __restrict__ nonsal, typename DT::T* __restrict__ out) {
+  typedef typename DT::T T;
+  extern __shared__ __attribute__((aligned(16))) uint32_t lc_buf[];  // [W + 8] column pairs
+  __shared__ float lc_red[2][LC_MAXW];
+  const int nthr = blockDim.x;
+  const int NW = nthr >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int W = P + S_pad;          // output row length (multiple of 8)
+  const int nchk = K / 8;           // 16-B input chunks per row
+  const int ochk = W / 8;           // 16-B output chunks per row
+  const int rb = RPL * tid;         // this thread's first rank
+
+  // ---- once per workgroup: salient-position mask, zeroed buffer (+ two spare words: W =
+  // a zero read by padding table entries, W + 1 = a write-only sink for their scatter)
+  const int zp0 = 64 * tid;
+  uint64_t zmask = 0;
+  for (int i = 0; i < 64; ++i) {
+    const int p = zp0 + i;
+    if (p < K && amap[p] < 0) zmask |= 1ull << i;
+  }
+  for (int c = tid; c < W + 2; c += nthr) lc_buf[c] = 0u;
+  PairScale tens;
+  if (MODE == LC_MODE_TENSOR) {
+    float m = 0.f;
+    for (int i = tid; i < Kn; i += nthr) m = fmaxf(m, __uint_as_float(cmax[nonsal[i]]));
+    m = wave_max(m);
+    if (lane == 0) lc_red[0][wave] = m;
+    __syncthreads();
+    m = 0.f;
+    for (int w = 0; w < NW; ++w) m = fmaxf(m, lc_red[0][w]);
+    const uint32_t mb = (uint32_t)__builtin_bit_cast(uint16_t, DT::from_f(m));
+    tens = pair_scale<DT>(mb | (mb << 16), q_max);
+  }
+  __syncthreads();
+
+  const int npair = (M + 1) / 2;
+  u32x4 nx0[LC_CH], nx1[LC_CH];
+  auto load_pair = [&](int rp) {
+    const int m0 = 2 * rp;
+    const bool has1 = m0 + 1 < M;
+    const u32x4* s0 = (const u32x4*)(x + (size_t)m0 * K);
+    const u32x4* s1 = (const u32x4*)(x + (size_t)(has1 ? m0 + 1 : m0) * K);
+#pragma unroll
+    for (int i = 0; i < LC_CH; ++i) {
+      const int c = tid + nthr * i;
+      if (c < nchk) {
+        nx0[i] = s0[c];
+        nx1[i] = has1 ? s1[c] : u32x4{0u, 0u, 0u, 0u};
+      }
+    }
+  };
+  int rp = blockIdx.x;
+  if (rp < npair) load_pair(rp);
+  for (; rp < npair; rp += gridDim.x) {
+    const int m0 = 2 * rp;
+    const bool has1 = m0 + 1 < M;
+    // ---- interleave the two rows into LDS: word k = (x[m0][k], x[m0+1][k])
+#pragma unroll
+    for (int i = 0; i < LC_CH; ++i) {
+      const int c = tid + nthr * i;
+      if (c < nchk) {
+        u32x4 w0, w1;
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+          w0[2 * k] = __builtin_amdgcn_perm(nx1[i][k], nx0[i][k], 0x05040100u);
+          w0[2 * k + 1] = __builtin_amdgcn_perm(nx1[i][k], nx0[i][k], 0x07060302u);
+          w1[2 * k] = __builtin_amdgcn_perm(nx1[i][k + 2], nx0[i][k + 2], 0x05040100u);
+          w1[2 * k + 1] = __builtin_amdgcn_perm(nx1[i][k + 2], nx0[i][k + 2], 0x07060302u);
+        }
+        ((u32x4*)lc_buf)[2 * c] = w0;
+        ((u32x4*)lc_buf)[2 * c + 1] = w1;
+      }
+    }
+    __syncthreads();
+
+    // ---- this thread's RPL table entries (L1/L2-resident, padded to whole rounds with
+    // (W, W + 1) entries), gather; exact salient columns into the tail (>= K)
+    uint32_t tab[RPL];
+    int toff = rb;
+    asm volatile("" : "+v"(toff));  // re-read per pair (no loop-invariant hoisting)
+#pragma unroll
+    for (int i = 0; i < RPL / 4; ++i) {
+      const u32x4 e = ((const u32x4*)(lctab + toff))[i];
+      tab[4 * i] = e[0]; tab[4 * i + 1] = e[1]; tab[4 * i + 2] = e[2]; tab[4 * i + 3] = e[3];
+    }
+    uint32_t v[RPL];
+#pragma unroll
+    for (int i = 0; i < RPL; ++i) v[i] = lc_buf[tab[i] & 0xFFFFu];
+    for (int j = tid; j < S; j += nthr) lc_buf[P + j] = lc_buf[sal[j]];
+
+    // ---- scales, then quantize + scatter
+    if (MODE == LC_MODE_GROUP && GS > 0) {
+      __syncthreads();  // every gather done before the scatter below
+#pragma unroll
+      for (int g = 0; g < RPL / (GS > 0 ? GS : RPL); ++g) {
+        uint32_t mx = 0u;
+#pragma unroll
+        for (int i = g * GS; i < (g + 1) * GS; ++i) mx = pk_absmax(mx, v[i]);
+        const PairScale c = pair_scale<DT>(mx, q_max);
+#pragma unroll
+        for (int i = g * GS; i < (g + 1) * GS; ++i) lc_buf[tab[i] >> 16] = quant_pair<DT>(v[i], c);
+      }
+    } else {
+      PairScale c = tens;
+      if (MODE != LC_MODE_TENSOR) {
+        uint32_t mx = 0u;
+#pragma unroll
+        for (int i = 0; i < RPL; ++i) mx = pk_absmax(mx, v[i]);
+        if (MODE == LC_MODE_GROUP) {
+          mx = xor_max(mx, G / RPL);
+        } else {
+          mx = xor_max(mx, 64);
+          if (lane == 0) {
+            lc_red[0][wave] = half_lo<DT>(mx);
+            lc_red[1][wave] = half_hi<DT>(mx);
+          }
+        }
+        __syncthreads();  // every gather done before the scatter below (+ token maxima)
+        if (MODE == LC_MODE_TOKEN) {
+          float m0f = 0.f, m1f = 0.f;
+          for (int w = 0; w < NW; ++w) {
+            m0f = fmaxf(m0f, lc_red[0][w]);
+            m1f = fmaxf(m1f, lc_red[1][w]);
+          }
+          mx = (uint32_t)__builtin_bit_cast(uint16_t, DT::from_f(m0f)) |
+               ((uint32_t)__builtin_bit_cast(uint16_t, DT::from_f(m1f)) << 16);
+        }
+        c = pair_scale<DT>(mx, q_max);
+      } else {
+        __syncthreads();
+      }
+#pragma unroll
+      for (int i = 0; i < RPL; ++i) lc_buf[tab[i] >> 16] = quant_pair<DT>(v[i], c);
+    }
+    // salient columns' own packed positions hold 0 (their weight codes are 0 too)
+    for (uint64_t zm = zmask; zm; zm &= zm - 1) lc_buf[zp0 + __builtin_ctzll(zm)] = 0u;
+    if (rp + (int)gridDim.x < npair) load_pair(rp + gridDim.x);  // prefetch the next pair
+    __syncthreads();
+
+    // ---- de-interleave 16-B chunks and store both rows
+    T* o0 = out + (size_t)m0 * W;
+    T* o1 = out + (size_t)(m0 + 1) * W;
+    for (int c = tid; c < ochk; c += nthr) {
+      const u32x4 a = ((const u32x4*)lc_buf)[2 * c];
+      const u32x4 b = ((const u32x4*)lc_buf)[2 * c + 1];
+      u32x4 y0, y1;
+      y0[0] = __builtin_amdgcn_perm(a[1], a[0], 0x05040100u);
+      y0[1] = __builtin_amdgcn_perm(a[3], a[2], 0x05040100u);
+      y0[2] = __builtin_amdgcn_perm(b[1], b[0], 0x05040100u);
+      y0[3] = __builtin_amdgcn_perm(b[3], b[2], 0x05040100u);
+      y1[0] = __builtin_amdgcn_perm(a[1], a[0], 0x07060302u);
+      y1[1] = __builtin_amdgcn_perm(a[3], a[2], 0x07060302u);
+      y1[2] = __builtin_amdgcn_perm(b[1], b[0], 0x07060302u);
+      y1[3] = __builtin_amdgcn_perm(b[3], b[2], 0x07060302u);
+      ((u32x4*)o0)[c] = y0;
+      if (has1) ((u32x4*)o1)[c] = y1;
+    }
+    __syncthreads();  // the buffer is rewritten by the next pair
+  }
+}
+
+constexpr int LC_RPL = 16;
+
+static int lc_waves(int K, int Kn) {
+  const int a = Kn > 0 ? cdiv(Kn, 64 * LC_RPL) : 1;
+  const int b = cdiv(K / 8, 64 * LC_CH);
+  return a > b ? a : b;
+}
+
+template <class DT, int MODE, int GS>
+static int quant_lc_launch(const void* x, int M, int K, int q_max, int G, const uint32_t* lctab,
+                           int Kn, const int32_t* amap, int P, const int32_t* sal, int S,
+                           int S_pad, const uint32_t* cmax, const int32_t* nonsal, void* out,
+                           hipStream_t s) {
+  typedef typename DT::T T;
+  const int nw = lc_waves(K, Kn);
+  const size_t lds = sizeof(uint32_t) * (size_t)(P + S_pad + 8);
+  SQMP_HIP_CHECK(hipFuncSetAttribute((const void*)quant_lc_kernel<DT, MODE, LC_RPL, GS>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  int per_cu = (int)((150 * 1024) / lds);
+  const int by_waves = 32 / nw;
+  per_cu = per_cu < 1 ? 1 : (per_cu > by_waves ? by_waves : per_cu);
+  int grid = 256 * per_cu;
+  const int npair = (M + 1) / 2;
+  if (grid > npair) grid = npair;
+  quant_lc_kernel<DT, MODE, LC_RPL, GS><<<dim3(grid), dim3(64 * nw), lds, s>>>(
+      (const T*)x, M, K, q_max, G, lctab, Kn, amap, P, sal, S, S_pad, cmax, nonsal, (T*)out);
+  SQMP_LAUNCH_CHECK();
+  return SQMP_OK;
+}
+
+bool quant_lc_supported(int dtype, int M, int K, int amode_group, int G, int Kn, int P,
+                        int S_pad, const void* x, const void* out) {
+  if (dtype != SQMP_F16 && dtype != SQMP_BF16) return false;
+  if (M <= 0 || K % 8 != 0 || K > 16384 || Kn > 16384 || P + S_pad >= 65536) return false;
+  if (((uintptr_t)x) % 16 != 0 || ((uintptr_t)out) % 16 != 0) return false;
+  if ((size_t)4 * (P + S_pad + 8) > 150 * 1024) return false;
+  if (lc_waves(K, Kn) > LC_MAXW) return false;
+  if (amode_group) {
+    // power-of-two groups that never straddle a wave's 64 * RPL ranks; below RPL only 8
+    if (G < 8 || G > 64 * LC_RPL || (G & (G - 1)) != 0) return false;
+  }
+  return true;
+}
+
+int launch_quant_lc(int dtype, int mode, const void* x, int M, int K, int q_max, int G,
+                    const uint32_t* lctab, int Kn, const int32_t* amap, int P,
+                    const int32_t* sal, int S, int S_pad, const uint32_t* cmax,
+                    const int32_t* nonsal, void* out, hipStream_t s) {
+#define SQMP_LC(DTT, MD, GSV)                                                            \
+  quant_lc_launch<DTT, MD, GSV>(x, M, K, q_max, G, lctab, Kn, amap, P, sal, S, S_pad, cmax, \
+                                nonsal, out, s)
+#define SQMP_LC_MODE(DTT)                                           \
+  (mode == LC_MODE_TOKEN ? SQMP_LC(DTT, LC_MODE_TOKEN, 0)            \
+   : mode == LC_MODE_TENSOR ? SQMP_LC(DTT, LC_MODE_TENSOR, 0)        \
+   : G < LC_RPL ? SQMP_LC(DTT, LC_MODE_GROUP, 8) : SQMP_LC(DTT, LC_MODE_GROUP, 0))
+  if (dtype == SQMP_F16) return SQMP_LC_MODE(F16);
+  if (dtype == SQMP_BF16) return SQMP_LC_MODE(BF16);
+  return SQMP_EUNSUPPORTED;
+#undef SQMP_LC_MODE
+#undef SQMP_LC
+}
+
+}  // namespace sqmp

@@ -11,8 +11,12 @@ int launch_colmax(const void* x, int dtype, int R, int C, uint32_t* cmax, hipStr
 
 // key[c] = bits(fp32(mean|x| + 3 std|x|)) over the R rows (the mean + 3 sigma sort key);
 // `sums` is a 2*C fp64 scratch (cleared here).
+// clean: `sums` is zero on entry (no memset) and is left zero.
 int launch_colkey_mean3std(const void* x, int dtype, int R, int C, double* sums,
-                           uint32_t* key, hipStream_t s);
+                           uint32_t* key, hipStream_t s, bool clean = false);
+// counts[cols[i]] += stable rank of list entry i (counts zero on entry).
+int launch_rank_count(const uint32_t* cmax, const int32_t* cols, int L, int32_t* counts,
+                      hipStream_t s);
 
 // Stable ascending rank of the list cols[0..L) (NULL = identity) keyed by cmax[col]:
 // rank_by_col[cols[i]] = #{j : (cmax[cols[j]], j) < (cmax[cols[i]], i)}.  Zeroes the
@@ -30,6 +34,15 @@ int launch_rank_partial(const uint32_t* cmax, const int32_t* cols, int L, int ld
 int launch_build_maps(int K, int Kp, const int32_t* rank_by_col, const int32_t* salient,
                       int S, int32_t* perm, int32_t* amap, int32_t* amap_fq,
                       int32_t* nonsal, hipStream_t s);
+
+// Lane-contiguous OUT_FP quantizer (sqmp_actquant_lc.hip).  mode: 0 token, 1 tensor,
+// 2 group (any rank order: sorted / unsorted / mean3std -- lctab carries it).
+bool quant_lc_supported(int dtype, int M, int K, int amode_group, int G, int Kn, int P,
+                        int S_pad, const void* x, const void* out);
+int launch_quant_lc(int dtype, int mode, const void* x, int M, int K, int q_max, int G,
+                    const uint32_t* lctab, int Kn, const int32_t* amap, int P,
+                    const int32_t* sal, int S, int S_pad, const uint32_t* cmax,
+                    const int32_t* nonsal, void* out, hipStream_t s);
 
 // Fast GEMMs (sqmp_gemm_fast.hip); SQMP_EUNSUPPORTED when the shape has no fast kernel.
 int launch_gemm_fq_fast(int dtype, const void* a, const void* codes, const void* wscale,

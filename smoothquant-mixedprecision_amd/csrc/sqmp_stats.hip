@@ -139,14 +139,17 @@ __global__ __launch_bounds__(256) void colsum_kernel(const typename DT::T* __res
   }
 }
 
-__global__ __launch_bounds__(256) void mean3std_key_kernel(const double* __restrict__ s1,
-                                                           const double* __restrict__ s2,
+__global__ __launch_bounds__(256) void mean3std_key_kernel(double* __restrict__ s1,
+                                                           double* __restrict__ s2,
                                                            int R, int C,
-                                                           uint32_t* __restrict__ key) {
+                                                           uint32_t* __restrict__ key,
+                                                           int clear) {
   const int c = blockIdx.x * 256 + threadIdx.x;
   if (c >= C) return;
-  const double mean = __ddiv_rn(s1[c], (double)R);
-  double var = __dsub_rn(__ddiv_rn(s2[c], (double)R), __dmul_rn(mean, mean));
+  const double a1 = s1[c], a2 = s2[c];
+  if (clear) s1[c] = s2[c] = 0.0;  // leave the sums zero for the next call
+  const double mean = __ddiv_rn(a1, (double)R);
+  double var = __dsub_rn(__ddiv_rn(a2, (double)R), __dmul_rn(mean, mean));
   var = var > 0.0 ? var : 0.0;
   const double k = __dadd_rn(mean, __dmul_rn(3.0, __dsqrt_rn(var)));
   key[c] = __float_as_uint(__double2float_rn(k));
@@ -171,8 +174,8 @@ static void colsum_launch(const void* x, int R, int C, double* s1, double* s2, h
 }
 
 int launch_colkey_mean3std(const void* x, int dtype, int R, int C, double* sums,
-                           uint32_t* key, hipStream_t s) {
-  SQMP_HIP_CHECK(hipMemsetAsync(sums, 0, 2 * sizeof(double) * (size_t)C, s));
+                           uint32_t* key, hipStream_t s, bool clean) {
+  if (!clean) SQMP_HIP_CHECK(hipMemsetAsync(sums, 0, 2 * sizeof(double) * (size_t)C, s));
   if (R <= 0 || C <= 0) return SQMP_OK;
   double* s1 = sums;
   double* s2 = sums + C;
@@ -183,7 +186,7 @@ int launch_colkey_mean3std(const void* x, int dtype, int R, int C, double* sums,
     default: return SQMP_EINVAL;
   }
   SQMP_LAUNCH_CHECK();
-  mean3std_key_kernel<<<dim3(cdiv(C, 256)), dim3(256), 0, s>>>(s1, s2, R, C, key);
+  mean3std_key_kernel<<<dim3(cdiv(C, 256)), dim3(256), 0, s>>>(s1, s2, R, C, key, clean ? 1 : 0);
   SQMP_LAUNCH_CHECK();
   return SQMP_OK;
 }
@@ -219,6 +222,39 @@ __global__ __launch_bounds__(256) void rank_kernel(const uint32_t* __restrict__ 
     cnt += (k < mine || (k == mine && t < lim)) ? 1 : 0;
   }
   if (cnt) atomicAdd(&rank_by_col[ci], cnt);
+}
+
+// Counting rank with 128-competitor tiles (more, shorter blocks than rank_kernel): adds
+// into counts[cols[i]], which the caller guarantees to be zero (clean workspace).
+__global__ __launch_bounds__(256) void rank_count_kernel(const uint32_t* __restrict__ cmax,
+                                                         const int32_t* __restrict__ cols, int L,
+                                                         int32_t* __restrict__ counts) {
+  __shared__ uint32_t kv[128];
+  const int j0 = blockIdx.y * 128;
+  const int jn = min(128, L - j0);
+  if (threadIdx.x < 128)
+    kv[threadIdx.x] = (int)threadIdx.x < jn ? cmax[cols[j0 + threadIdx.x]] : 0xFFFFFFFFu;
+  __syncthreads();
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= L) return;
+  const int ci = cols[i];
+  const uint32_t mine = cmax[ci];
+  const int lim = i - j0;
+  int c0 = 0, c1 = 0;
+#pragma unroll 16
+  for (int t = 0; t < 128; t += 2) {
+    c0 += (kv[t] < mine || (kv[t] == mine && t < lim)) ? 1 : 0;
+    c1 += (kv[t + 1] < mine || (kv[t + 1] == mine && t + 1 < lim)) ? 1 : 0;
+  }
+  if (c0 + c1) atomicAdd(&counts[ci], c0 + c1);
+}
+
+int launch_rank_count(const uint32_t* cmax, const int32_t* cols, int L, int32_t* counts,
+                      hipStream_t s) {
+  if (L <= 0) return SQMP_OK;
+  rank_count_kernel<<<dim3(cdiv(L, 256), cdiv(L, 128)), dim3(256), 0, s>>>(cmax, cols, L, counts);
+  SQMP_LAUNCH_CHECK();
+  return SQMP_OK;
 }
 
 int launch_rank(const uint32_t* cmax, const int32_t* cols, int L, int C,

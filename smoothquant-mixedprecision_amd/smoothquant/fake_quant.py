@@ -214,6 +214,9 @@ class W4A4Linear(nn.Module):
         self._meta = None
         for name in _PACKED_BUFFERS:
             self.register_buffer(name, None)
+        # column -> packed position (inverse of w_perm), derived: not part of checkpoints
+        self.register_buffer("w_posmap", None, persistent=False)
+        self._sal_key = None
         if bias:
             self.register_buffer("bias", torch.zeros((1, out_features), dtype=torch.float16))
         else:
@@ -233,6 +236,8 @@ class W4A4Linear(nn.Module):
         self.w_nonsal = pw.nonsal
         self.salient_i32 = pw.salient
         self.w_dense = pw.dense
+        self.w_posmap = pw.posmap
+        self._sal_key = pw.sal_key
         self._meta = dict(N=pw.N, K=pw.K, S=pw.S, S_pad=pw.S_pad, Kp=pw.Kp, Gw=pw.Gw,
                           ngw=pw.ngw, n_bits=pw.n_bits, wmode=pw.wmode, dtype=pw.dtype)
         self.weight_quant_name = weight_quant
@@ -264,10 +269,14 @@ class W4A4Linear(nn.Module):
                             device="cuda")
             self._pack_from(w, "None")
         m = self._meta
+        if self.w_posmap is None or self.w_posmap.device != self.w_perm.device:
+            self.w_posmap = ops.build_posmap(self.w_perm, m["K"])  # e.g. after a checkpoint load
+        if self._sal_key is None:
+            self._sal_key = ops.salient_key(m["K"], self.salient_i32)
         return PackedWeight(self.w_codes, self.w_scale, self.w_salient, self.w_perm, self.w_amap,
                             self.w_amap_fq, self.w_nonsal, self.salient_i32, m["N"], m["K"],
                             m["S"], m["S_pad"], m["Kp"], m["Gw"], m["ngw"], m["n_bits"],
-                            m["wmode"], m["dtype"], self.w_dense)
+                            m["wmode"], m["dtype"], self.w_dense, self.w_posmap, self._sal_key)
 
     # ------------------------------------------------------------------ persistence
     # Packed format (the reference persists only the dequantized weight
@@ -316,6 +325,7 @@ class W4A4Linear(nn.Module):
         self.kernel = state.get("kernel", "auto")
         sal = state["salient_indices"]
         self.salient_indices = None if sal is None else sal.clone()
+        self.w_posmap, self._sal_key = None, None  # re-derived from the loaded buffers
         meta = state["meta"]
         if meta is not None:
             meta = dict(meta)
@@ -409,7 +419,7 @@ class W4A4Linear(nn.Module):
         if use_i8:
             a8, sa, xs = ops.quant_act_i8(xc, pw, amode, bits)
         else:
-            a = ops.quant_act_fp(xc, pw, amode, bits, ag)
+            a = ops.quant_act_fp(xc, pw, amode, bits, ag, stats_of=x)
         if mutate_input:
             ops.fake_quant_inplace(xc, amode, bits, ag, pw.amap_fq, pw.nonsal, 0)
         y = ops.gemm_i8(a8, sa, xs, pw, bias) if use_i8 else ops.gemm_fq(a, pw, bias)
