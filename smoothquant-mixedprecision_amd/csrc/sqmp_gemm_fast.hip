@@ -27,6 +27,8 @@
 // gemm_i8v2 -- per_token / per_tensor activations on the integer MFMA (see below).
 #include <string.h>
 
+#include <type_traits>
+
 #include "sqmp_mfma.h"
 
 namespace sqmp {
@@ -49,6 +51,7 @@ constexpr int F5_NSLOT = 3;                      // 147456 B of 160 KiB
 constexpr int F5_VM_CODES = 4 + 1 + 1;           // DMA ops per wave per codes stage
 constexpr int F5_VM_DENSE = 2 + 2;              // ... per 32-column dense stage
 constexpr int F5_DB = 16384;                     // dense stage: B image after 256 x 64 B of A
+constexpr int F5_DN = 16384;                     // fq6 dense stage: B after 128 x 128 B of A
 
 // LDS images of the ring, shared by the 32x32x16 (fq5) and 16x16x32 (fq6) kernels:
 //   codes-stage A: 256 rows x 128 B, logical 16-B chunk c of row r at physical chunk
@@ -292,8 +295,12 @@ __global__ __launch_bounds__(512, 1) void gemm_fq5_kernel(
 // 16 x 2 tiles of 16 x 16 per wave (128 fp32 accumulators), two 32-element sub-steps per
 // 64-element stage.  Lane (r16, q) of sub-step s takes bpack dword 2q + s of its weight
 // row (one ds_read_b64 per tile column carries both sub-steps) and A chunk
-// 4 (q & 1) + 2 s + (q >> 1) -- the positions of that dword.  Same DMA ring, waits and
-// dense stages as fq5; dense stages give lane q chunk q of both 64-B rows.
+// 4 (q & 1) + 2 s + (q >> 1) -- the positions of that dword.  Same DMA ring and waits as
+// fq5.  Dense stages (the exact salient slice; every stage for dense weights) are 64
+// columns wide over 128 rows of the tile (two half-height stages per 64-column block when
+// TM = 256): A 128 rows x 128 B + B 256 weight rows x 128 B fill one 48 KiB slot, every
+// DMA moves whole 128-B lines, both images use the codes-stage A swizzle, and lane
+// (r16, q) of sub-step s reads chunk 4 (q & 1) + 2 s + (q >> 1) of A and B alike.
 template <class DT, int GB, int TM>
 __global__ __launch_bounds__(512, 1) void gemm_fq6_kernel(
     const typename DT::T* __restrict__ A, const void* __restrict__ Bw,
@@ -304,7 +311,8 @@ __global__ __launch_bounds__(512, 1) void gemm_fq6_kernel(
   constexpr int CW = 32;                // weight rows (output columns) per wave
   constexpr int I = TM / 16, J = 2;     // 16 x 16 tiles per wave (TM rows x 32 columns)
   constexpr int NA = TM / 64;           // codes-stage A DMA ops per wave (64 rows each)
-  constexpr int VM_CODES = NA + 1 + 1, VM_DENSE = TM / 128 + 2;
+  constexpr int HALVES = TM / 128;      // dense stages per 64-column block (128 rows each)
+  constexpr int VM_CODES = NA + 1 + 1, VM_DENSE = 2 + 4;
   constexpr int GBn = GB > 0 ? GB : 1;
   constexpr int LPG = CW / 8;
   constexpr int PF = 3;
@@ -319,19 +327,17 @@ __global__ __launch_bounds__(512, 1) void gemm_fq6_kernel(
   const int r16 = lane & 15, q = lane >> 4;
   const int lda = Kp + S_pad;
   const int nkm = GB ? Kp / 64 : 0;
-  const int nkt = nkm + (lda - nkm * 64) / 32;
+  const int nkt = nkm + ((lda - nkm * 64) / 64) * HALVES;
   const int Np = pad_n(N);
 
-  const int drow = 16 * wave + (lane >> 2);
-  const int dchunk = (lane & 3) ^ d_f((lane >> 4) & 3);
-  const uint32_t ad_off = (uint32_t)((size_t)(m0 + drow) * lda * sizeof(T) + dchunk * 16);
-  const uint32_t ad_str = (uint32_t)(128 * (size_t)lda * sizeof(T));
-  const uint32_t bd_row0 = (uint32_t)min(n0 + drow, N - 1);
-  const uint32_t bd_row1 = (uint32_t)min(n0 + drow + 128, N - 1);
   const int arow = 8 * wave + (lane >> 3);
-  const uint32_t a_off = (uint32_t)((size_t)(m0 + arow) * lda * sizeof(T) +
-                                    (bitrev3((lane & 7) ^ ((arow >> 1) & 7)) << 4));
+  const uint32_t lchunk = (uint32_t)(bitrev3((lane & 7) ^ ((arow >> 1) & 7)) << 4);
+  const uint32_t a_off = (uint32_t)((size_t)(m0 + arow) * lda * sizeof(T)) + lchunk;
   const uint32_t a_str = (uint32_t)(64 * (size_t)lda * sizeof(T));
+  const uint32_t ah_str = (uint32_t)(128 * (size_t)lda * sizeof(T));  // dense half-tile step
+  uint32_t bd_row[4];  // dense-stage B rows of this lane (clamped: wsal has N rows)
+#pragma unroll
+  for (int i = 0; i < 4; ++i) bd_row[i] = (uint32_t)min(n0 + arow + 64 * i, N - 1);
   const uint32_t b_off = (uint32_t)((size_t)(n0 + 32 * wave + (lane >> 1)) * (Kp / 2) +
                                     (((lane & 1) ^ ((lane >> 4) & 1)) << 4));
   const int s_u = min(lane / LPG, GBn - 1);
@@ -349,16 +355,19 @@ __global__ __launch_bounds__(512, 1) void gemm_fq6_kernel(
       glds16((const unsigned char*)wscale + (size_t)g * Np * sizeof(T) + s_off,
              slot + F5_A + F5_B + wave * 1024);
     } else {
-      const int col = nkm * 64 + (kt - nkm) * 32;
-      const unsigned char* ab = (const unsigned char*)A + (size_t)col * sizeof(T);
-      glds16(ab + ad_off, slot + wave * 1024);
-      if (TM == 256) glds16(ab + ad_str + ad_off, slot + (8 + wave) * 1024);
+      const int d = kt - nkm;
+      const int col = nkm * 64 + (d / HALVES) * 64;
+      const int h = d % HALVES;
+      const unsigned char* ab = (const unsigned char*)A + (size_t)col * sizeof(T) + h * ah_str;
+      glds16(ab + a_off, slot + wave * 1024);
+      glds16(ab + a_str + a_off, slot + (8 + wave) * 1024);
       const bool main = col < Kp;
       const unsigned char* bb = main ? (const unsigned char*)Bw : (const unsigned char*)wsal;
       const uint32_t ldb = main ? (uint32_t)Kp : (uint32_t)S_pad;
-      const uint32_t c0 = (uint32_t)(main ? col : col - Kp) * sizeof(T) + dchunk * 16;
-      glds16(bb + bd_row0 * ldb * sizeof(T) + c0, slot + F5_DB + wave * 1024);
-      glds16(bb + bd_row1 * ldb * sizeof(T) + c0, slot + F5_DB + (8 + wave) * 1024);
+      const unsigned char* bc = bb + (size_t)(main ? col : col - Kp) * sizeof(T) + lchunk;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        glds16(bc + (size_t)bd_row[i] * ldb * sizeof(T), slot + F5_DN + (i * 8 + wave) * 1024);
     }
   };
 
@@ -412,17 +421,34 @@ __global__ __launch_bounds__(512, 1) void gemm_fq6_kernel(
   };
 #undef SQMP_FQ6_BLOCKS
 
-  const int d_sw = d_f((r16 >> 2) & 3);
-  auto compute_dense = [&](const unsigned char* __restrict__ slot) {
-    const int co = (q ^ d_sw) << 4;
-    u32x4 bf[J];
+  // dense stage: rows 128 h .. 128 h + 127 of the tile (accumulator blocks 8 h ..)
+  auto compute_dense = [&](const unsigned char* __restrict__ slot, auto hc) {
+    constexpr int H = decltype(hc)::value;
+    constexpr int I2 = 8;
+    u32x4 bf[2][J];
 #pragma unroll
-    for (int j = 0; j < J; ++j) bf[j] = *(const u32x4*)(slot + F5_DB + (wn * CW + 16 * j + r16) * 64 + co);
+    for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
-    for (int i = 0; i < I; ++i) {
-      const u32x4 af = *(const u32x4*)(slot + (16 * i + r16) * 64 + co);
+      for (int j = 0; j < J; ++j) {
+        const int c = 4 * (q & 1) + 2 * s2 + (q >> 1);
+        bf[s2][j] = *(const u32x4*)(slot + F5_DN + (wn * CW + 16 * j + r16) * 128 +
+                                    ((bitrev3(c) ^ a_sw) << 4));
+      }
+    // A fragments read PF blocks ahead, one sched_barrier per block (as the codes loop)
+    auto ald2 = [&](int t) {
+      const int c = 4 * (q & 1) + 2 * (t / I2) + (q >> 1);
+      return *(const u32x4*)(slot + a_row0 + (t % I2) * 2048 + ((bitrev3(c) ^ a_sw) << 4));
+    };
+    u32x4 a[PF + 1];
 #pragma unroll
-      for (int j = 0; j < J; ++j) Mfma<DT>::run(acc[i][j], bf[j], af);
+    for (int t = 0; t < PF; ++t) a[t] = ald2(t);
+#pragma unroll
+    for (int t = 0; t < 2 * I2; ++t) {
+      if (t + PF < 2 * I2) a[(t + PF) % (PF + 1)] = ald2(t + PF);
+#pragma unroll
+      for (int j = 0; j < J; ++j)
+        Mfma<DT>::run(acc[H * I2 + t % I2][j], bf[t / I2][j], a[t % (PF + 1)]);
+      __builtin_amdgcn_sched_barrier(0);
     }
   };
 
@@ -445,7 +471,11 @@ __global__ __launch_bounds__(512, 1) void gemm_fq6_kernel(
     else vm_wait<0>();
     raw_barrier();
     if (kt + 2 < nkt) issue(kt + 2);
-    compute_dense(lds + (kt % F5_NSLOT) * F5_SLOT);
+    unsigned char* slot = lds + (kt % F5_NSLOT) * F5_SLOT;
+    if (HALVES == 1 || (kt - nkm) % HALVES == 0)
+      compute_dense(slot, std::integral_constant<int, 0>());
+    else
+      compute_dense(slot, std::integral_constant<int, HALVES - 1>());
   }
 
   // ---- epilogue: acc[i][j][r] = C[n = n0 + 32 wn + 16 j + 4 q + r][m = m0 + 16 i + r16]
