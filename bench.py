@@ -44,8 +44,10 @@ HBM_PEAK_GBS = 8000.0
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=10)
+    # defaults long enough for the chip to settle at the clock it holds under this load
+    # (DVFS, MI355X_MICROARCH.md): ~0.14 s of warmup and of timed steps
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=200)
     ap.add_argument("--act", default="per_group", choices=["per_group", "per_token"])
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--cpu-rows", type=int, default=16384)
@@ -188,7 +190,7 @@ def main():
         gemm = lambda: ops.gemm_fq(a, pw, lin.bias)  # noqa: E731
         quant = lambda: ops.quant_act_fp(x, pw, args.act, 4, G)  # noqa: E731
         kdt = "f16"
-    for _ in range(3):
+    for _ in range(max(3, args.warmup)):
         gemm()
     gemm_ms = time_events(gemm, max(10, args.steps), stream)
     quant_ms = time_events(quant, max(10, args.steps), stream)
@@ -197,7 +199,7 @@ def main():
     # unquantized -- what the reference's F.linear costs on this GPU, without any act-quant
     wd = lin.weight.detach()
     dense = lambda: torch.nn.functional.linear(x, wd, lin.bias)  # noqa: E731
-    for _ in range(3):
+    for _ in range(max(3, args.warmup)):
         dense()
     dense_ms = time_events(dense, max(10, args.steps), stream)
     # reference point: the reference's own fake-quant forward (restated in PyTorch ops,

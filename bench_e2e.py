@@ -1,0 +1,214 @@
+"""End-to-end W4A4 prefill benchmarks of BASELINE.json configs 3 and 4 on 1 MI355X.
+
+    python bench_e2e.py --model llama2-7b [--layers 32] [--windows 8] [--seq 2048] [--group 64]
+                        [--salient 0.05] [--act per_group] [--weight per_group] [--cal-blocks 4]
+    python bench_e2e.py --model opt-1.3b   (config 3: G=128, 5 % salient, quantize_opt with
+                                            its default bmm-input output quantization)
+
+The architecture of the named model with random-init fp16 weights built directly on the
+GPU (there are no checkpoints offline), random token windows.  Importance: the reference's
+mean|x| calibration features (smoothquant.calibration.get_calib_feat) on synthetic
+512-token blocks; quantization: the reference's entry point (quantize_llama_like /
+quantize_opt, fake_quant.py:377-561) with every nn.Linear of the decoder becoming a HIP
+W4A4Linear.  Timing: Evaluator-style prefill (run_experiments.py:86-123), batch 1, wall
+clock around the whole window loop after one warm-up window, for (1) the fp16 model,
+(2) the W4A4 model, (3) the reference's fake-quant forward restated in PyTorch ops
+(tools/torch_fakequant.py) on the same W_hat and salient sets, with the fp16 GEMM, and
+(4) the same with an fp32 GEMM -- (3) vs (4) is the reference's own sensitivity to GEMM
+accumulation order, the noise floor against which the W4A4 kernel's PPL delta reads.
+Perplexities are of a random model: only differences are meaningful.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for _p in (ROOT, os.path.join(ROOT, "smoothquant-mixedprecision_amd"), os.path.join(ROOT, "tools")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import torch  # noqa: E402
+import torch.nn as nn  # noqa: E402
+
+MODELS = {
+    # name: (family, config kwargs, default group size, linear FLOP/token per layer factor)
+    "llama2-7b": ("llama", dict(vocab_size=32000, hidden_size=4096, intermediate_size=11008,
+                                num_hidden_layers=32, num_attention_heads=32,
+                                num_key_value_heads=32, max_position_embeddings=4096,
+                                rms_norm_eps=1e-5), 64),
+    "opt-1.3b": ("opt", dict(vocab_size=50272, hidden_size=2048, ffn_dim=8192,
+                             num_hidden_layers=24, num_attention_heads=16,
+                             max_position_embeddings=2048, word_embed_proj_dim=2048,
+                             do_layer_norm_before=True), 128),
+}
+
+
+def parse(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default="llama2-7b", choices=sorted(MODELS))
+    ap.add_argument("--layers", type=int, default=None)
+    ap.add_argument("--windows", type=int, default=8)
+    ap.add_argument("--seq", type=int, default=2048)
+    ap.add_argument("--group", type=int, default=None)
+    ap.add_argument("--salient", type=float, default=0.05)
+    ap.add_argument("--act", default="per_group")
+    ap.add_argument("--weight", default="per_group")
+    ap.add_argument("--act-bits", type=int, default=4, help="8 = W4A8 (act_quant rebound)")
+    ap.add_argument("--cal-blocks", type=int, default=4)
+    ap.add_argument("--no-ref", action="store_true", help="skip the reference fake-quant legs")
+    return ap.parse_args(argv)
+
+
+@torch.no_grad()
+def run_windows(model, ids, seq, n):
+    """Evaluator loop (run_experiments.py:86-123): returns (ppl, seconds for n windows)."""
+    nlls = []
+    model(ids[:, :seq])  # warm-up window (kernel selection, allocator)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(n):
+        batch = ids[:, i * seq:(i + 1) * seq]
+        logits = model(batch).logits
+        sl = logits[:, :-1, :].contiguous().float()
+        loss = nn.CrossEntropyLoss()(sl.view(-1, sl.size(-1)), batch[:, 1:].reshape(-1))
+        nlls.append(loss.float() * seq)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    return float(torch.exp(torch.stack(nlls).sum() / (n * seq))), dt
+
+
+def build(name, layers):
+    family, cfg_kw, _ = MODELS[name]
+    cfg_kw = dict(cfg_kw)
+    if layers:
+        cfg_kw["num_hidden_layers"] = layers
+    if family == "llama":
+        from transformers import LlamaConfig, LlamaForCausalLM
+        cfg, cls = LlamaConfig(attn_implementation="sdpa", **cfg_kw), LlamaForCausalLM
+    else:
+        from transformers import OPTConfig, OPTForCausalLM
+        cfg, cls = OPTConfig(attn_implementation="sdpa", **cfg_kw), OPTForCausalLM
+    prev = torch.get_default_dtype()
+    torch.set_default_dtype(torch.float16)
+    with torch.device("cuda"):
+        model = cls(cfg).eval()
+    torch.set_default_dtype(prev)
+    return family, cfg, model
+
+
+def linear_flops_per_token(model):
+    return 2 * sum(m.in_features * m.out_features for n, m in model.named_modules()
+                   if isinstance(m, nn.Linear) and "lm_head" not in n)
+
+
+class RefLinear(nn.Module):
+    """A W4A4Linear replaced by the reference's fake-quant forward on its W_hat / salient
+    set and bound quantizers (tools/torch_fakequant.py)."""
+
+    def __init__(self, q, accum32):
+        super().__init__()
+        from smoothquant.fake_quant import resolve_quantizer
+        from torch_fakequant import TorchFakeQuantLinear
+        b = None if q.bias is None else q.bias.reshape(-1)
+        mode, bits, g = resolve_quantizer(q.act_quant)
+        self.f = TorchFakeQuantLinear(q.weight, b, q.salient_indices, mode, bits, g,
+                                      accum32=accum32,
+                                      output_quant=resolve_quantizer(q.output_quant))
+
+    def forward(self, x):
+        return self.f(x)
+
+
+def swap_reference(model, accum32):
+    """Every W4A4Linear -> RefLinear; existing RefLinears switch their GEMM accumulation."""
+    from smoothquant.fake_quant import W4A4Linear
+    for _, m in list(model.named_modules()):
+        for attr, child in list(m.named_children()):
+            if isinstance(child, W4A4Linear):
+                setattr(m, attr, RefLinear(child, accum32))
+            elif isinstance(child, RefLinear):
+                child.f.accum32 = accum32
+
+
+def main(argv=None):
+    args = parse(argv)
+    from functools import partial
+
+    from smoothquant import fake_quant as FQ
+    from smoothquant.calibration import get_calib_feat
+    family, cfg, model = build(args.model, args.layers)
+    G = args.group or MODELS[args.model][2]
+    dev = torch.device("cuda")
+    torch.manual_seed(0)
+    g = torch.Generator(device=dev).manual_seed(1)
+    ids = torch.randint(0, cfg.vocab_size, (1, args.windows * args.seq), generator=g, device=dev)
+    cal = [torch.randint(0, cfg.vocab_size, (1, 512), generator=g, device=dev)
+           for _ in range(args.cal_blocks)]
+    flops_tok = linear_flops_per_token(model)
+
+    ppl16, dt16 = run_windows(model, ids, args.seq, args.windows)
+
+    t_q = time.perf_counter()
+    feat = get_calib_feat(model, None, samples=cal, device=dev)
+    qfn = FQ.quantize_llama_like if family == "llama" else FQ.quantize_opt
+    model = qfn(model, weight_quant=args.weight, act_quant=args.act, input_feat=feat,
+                salient_prop=args.salient, quant_bits=4, group_size=G)
+    if args.act_bits != 4:
+        # W4A8 (config 5): rebind the bound activation quantizer, as a reference user would
+        fn = FQ._ACT_FNS[args.act]
+        kw = {"group_size": G} if args.act.startswith("per_group") else {}
+        for m in model.modules():
+            if isinstance(m, FQ.W4A4Linear):
+                m.act_quant = partial(fn, n_bits=args.act_bits, **kw)
+    torch.cuda.synchronize()
+    t_q = time.perf_counter() - t_q
+    n_w4 = sum(isinstance(m, FQ.W4A4Linear) for m in model.modules())
+    ppl4, dt4 = run_windows(model, ids, args.seq, args.windows)
+
+    tokens = args.windows * args.seq
+    out = {
+        "metric": f"{args.model} W4A4 prefill tokens/s (1 GPU)",
+        "value": round(tokens / dt4, 1),
+        "unit": "tokens/s",
+        "higher_is_better": True,
+        "n_gpus": 1,
+        "fp16_tokens_per_s": round(tokens / dt16, 1),
+        "w4a4_over_fp16": round(dt16 / dt4, 4),
+        "ppl_fp16": round(ppl16, 4),
+        "ppl_w4a4": round(ppl4, 4),
+        "linear_TFLOP_per_s_w4a4": round(flops_tok * tokens / dt4 / 1e12, 1),
+    }
+    if not args.no_ref:
+        swap_reference(model, accum32=False)
+        pplr, dtr = run_windows(model, ids, args.seq, args.windows)
+        swap_reference(model, accum32=True)
+        pplr32, _ = run_windows(model, ids, args.seq, args.windows)
+        out.update({
+            "reference_fakequant_tokens_per_s": round(tokens / dtr, 1),
+            "speedup_vs_reference_fakequant": round(dtr / dt4, 2),
+            "ppl_reference_fakequant": round(pplr, 4),
+            "ppl_reference_fakequant_fp32_gemm": round(pplr32, 4),
+            "ppl_delta_vs_reference": round(ppl4 - pplr, 4),
+            "reference_gemm_order_noise": round(pplr32 - pplr, 4),
+        })
+    out.update({
+        "data": "synthetic: random-init fp16 weights of the named architecture, random tokens; "
+                "PPL values are of a random model -- only differences are meaningful",
+        "config": {"workload": f"{args.model} prefill, batch 1", "layers": cfg.num_hidden_layers,
+                   "seq_len": args.seq, "windows": args.windows, "group_size": G,
+                   "salient_prop": args.salient, "weight_quant": args.weight,
+                   "act_quant": args.act, "act_bits": args.act_bits, "w4a4_linears": n_w4,
+                   "quantizer": qfn.__name__,
+                   "calibration": f"{args.cal_blocks} x 512 random tokens"},
+        "setup_s": {"calibrate_and_quantize": round(t_q, 1)},
+    })
+    print(json.dumps(out), flush=True)
+    return out
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,94 @@
+"""Config 5 of BASELINE.json: Llama-2-7B (random-init, architecture-exact) W4A4 / W4A8 x
+group size {64, 128, 256, 1024} x channel sort {none, max, mean+3sigma} on 1 MI355X.
+
+    python bench_sweep.py [--layers 32] [--windows 2] [--bits 4,8] [--groups 64,128,256,1024]
+                          [--sorts none,max,mean3std] [--salient 0.05]
+
+For every combination: quantize a copy of the fp16 model with quantize_llama_like
+(weight and activation per_group with the given sort; W4A8 rebinds the bound act
+quantizer to 8 bits), time Evaluator-style prefill windows and report
+tokens/s, perplexity, the perplexity of the reference's fake-quant forward on the same
+W_hat / salient sets (tools/torch_fakequant.py) and the difference.  Random weights and
+tokens: perplexities are of a random model, only differences are meaningful.  Prints one
+JSON object per combination and a summary line.
+"""
+from __future__ import annotations
+
+import argparse
+import copy
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for _p in (ROOT, os.path.join(ROOT, "smoothquant-mixedprecision_amd"), os.path.join(ROOT, "tools")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import torch  # noqa: E402
+
+import bench_e2e  # noqa: E402
+
+SORTS = {"none": "per_group_unsorted", "max": "per_group", "mean3std": "per_group_mean3std"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--layers", type=int, default=32)
+    ap.add_argument("--windows", type=int, default=2)
+    ap.add_argument("--seq", type=int, default=2048)
+    ap.add_argument("--bits", default="4,8")
+    ap.add_argument("--groups", default="64,128,256,1024")
+    ap.add_argument("--sorts", default="none,max,mean3std")
+    ap.add_argument("--salient", type=float, default=0.05)
+    args = ap.parse_args()
+    from functools import partial
+
+    from smoothquant import fake_quant as FQ
+    from smoothquant.calibration import get_calib_feat
+
+    family, cfg, base = bench_e2e.build("llama2-7b", args.layers)
+    dev = torch.device("cuda")
+    g = torch.Generator(device=dev).manual_seed(1)
+    ids = torch.randint(0, cfg.vocab_size, (1, args.windows * args.seq), generator=g, device=dev)
+    cal = [torch.randint(0, cfg.vocab_size, (1, 512), generator=g, device=dev) for _ in range(4)]
+    ppl16, dt16 = bench_e2e.run_windows(base, ids, args.seq, args.windows)
+    feat = get_calib_feat(base, None, samples=cal, device=dev)
+    tokens = args.windows * args.seq
+    rows = []
+    for bits in [int(b) for b in args.bits.split(",")]:
+        for G in [int(x) for x in args.groups.split(",")]:
+            for sort in args.sorts.split(","):
+                mode = SORTS[sort]
+                model = copy.deepcopy(base)
+                model = FQ.quantize_llama_like(model, weight_quant=mode, act_quant=mode,
+                                               input_feat=feat, salient_prop=args.salient,
+                                               quant_bits=4, group_size=G)
+                if bits != 4:
+                    for m in model.modules():
+                        if isinstance(m, FQ.W4A4Linear):
+                            m.act_quant = partial(FQ._ACT_FNS[mode], n_bits=bits, group_size=G)
+                ppl, dt = bench_e2e.run_windows(model, ids, args.seq, args.windows)
+                bench_e2e.swap_reference(model, accum32=False)
+                pplr, dtr = bench_e2e.run_windows(model, ids, args.seq, args.windows)
+                row = {"w_bits": 4, "a_bits": bits, "group_size": G, "sort": sort,
+                       "tokens_per_s": round(tokens / dt, 1),
+                       "reference_fakequant_tokens_per_s": round(tokens / dtr, 1),
+                       "ppl": round(ppl, 4), "ppl_reference_fakequant": round(pplr, 4),
+                       "ppl_delta_vs_reference": round(ppl - pplr, 4),
+                       "ppl_delta_vs_fp16": round(ppl - ppl16, 4)}
+                print(json.dumps(row), flush=True)
+                rows.append(row)
+                del model
+                torch.cuda.empty_cache()
+    print(json.dumps({"metric": "Llama-2-7B W4A4/W4A8 sweep (config 5), 1 GPU",
+                      "fp16_tokens_per_s": round(tokens / dt16, 1), "ppl_fp16": round(ppl16, 4),
+                      "combinations": len(rows), "layers": cfg.num_hidden_layers,
+                      "windows": args.windows, "seq_len": args.seq,
+                      "data": "synthetic: random-init weights and tokens (only differences "
+                              "are meaningful)"}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -480,7 +480,7 @@ __global__ __launch_bounds__(256) void lc_table_kernel(
         colsorted[r] = col;
       }
     }
-    lctab[r] = (uint32_t)col | ((uint32_t)posmap[col] << 16);
+    lctab[r] = (uint32_t)col | ((uint32_t)(posmap ? posmap[col] : col) << 16);
   }
   if (key && t < K) key[t] = 0u;
   for (int r = Kn + t; r < lc_len; r += nt) lctab[r] = lc_none;
@@ -861,7 +861,36 @@ extern "C" int sqmp_quant_act_v2(void* x, int dtype, int M, int K, int amode, in
                            salient, S, S_pad, cmax, nonsal, out, s);
   }
 
-  // ---- general path (fp32, 8-bit int output, in-place output quant, large rows)
+  // ---- in-place output quantization (fake_quant.py:308-316) on the same kernels: the
+  // "packed" order is the identity, salient columns keep their values (no zeroing, no
+  // tail), and the row is written back over itself.
+  if (out_kind == SQMP_OUT_INPLACE && !lc_off && amode != SQMP_ACT_PER_TENSOR &&
+      quant_lc_supported(dtype, M, K, group, group_size, Kn, K, 0, x, x)) {
+    int tmode = TAB_LIST;
+    if (sorted) {
+      tmode = TAB_COUNTS;
+      if (amode == SQMP_ACT_PER_GROUP) {
+        if (!clean) SQMP_HIP_CHECK(hipMemsetAsync(cmax, 0, sizeof(uint32_t) * k64, s));
+        st = launch_colmax(x, dtype, M, K, cmax, s, false);
+      } else {
+        st = launch_colkey_mean3std(x, dtype, M, K, sums, cmax, s, clean);
+      }
+      if (st) return st;
+      if (!clean) SQMP_HIP_CHECK(hipMemsetAsync(counts, 0, sizeof(int32_t) * k64, s));
+      st = launch_rank_count(cmax, nonsal, Kn, counts, s);
+      if (st) return st;
+    }
+    const int nthr = K > Kn ? K : (Kn > 0 ? Kn : 1);
+    const uint32_t none_ip = (uint32_t)K | ((uint32_t)(K + 1) << 16);
+    lc_table_kernel<<<dim3(cdiv(nthr, 256)), dim3(256), 0, s>>>(
+        tmode, nonsal, Kn, K, nullptr, counts, colsorted, tmode == TAB_COUNTS ? cmax : nullptr,
+        lctab, lc_len, none_ip);
+    SQMP_LAUNCH_CHECK();
+    return launch_quant_lc(dtype, lmode, x, M, K, q_max, group_size, lctab, Kn, nullptr, K,
+                           salient, 0, 0, cmax, nonsal, x, s);
+  }
+
+  // ---- general path (fp32, 8-bit int output, large rows, other group sizes)
   if (amode == SQMP_ACT_PER_TENSOR || amode == SQMP_ACT_PER_GROUP) {
     SQMP_HIP_CHECK(hipMemsetAsync(cmax, 0, sizeof(uint32_t) * k64, s));
     st = launch_colmax(x, dtype, M, K, cmax, s, false);

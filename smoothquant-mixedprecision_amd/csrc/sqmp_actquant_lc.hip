@@ -118,10 +118,12 @@ __device__ inline uint32_t quant_pair<BF16>(uint32_t v, const PairScale& c) {
 // thread), else 0.  blockDim = 64 * NW.
 template <class DT, int MODE, int RPL, int GS>
 __global__ __launch_bounds__(1024) void quant_lc_kernel(
-    const typename DT::T* __restrict__ x, int M, int K, int q_max, int G,
+    const typename DT::T* x, int M, int K, int q_max, int G,
     const uint32_t* __restrict__ lctab, int Kn, const int32_t* __restrict__ amap, int P,
     const int32_t* __restrict__ sal, int S, int S_pad, const uint32_t* __restrict__ cmax,
-    const int32_t* __restrict__ nonsal, typename DT::T* __restrict__ out) {
+    const int32_t* __restrict__ nonsal, typename DT::T* out) {
+  // x and out alias for in-place output quantization (every row is read before it is
+  // written: a workgroup stores a pair only after loading it)
   typedef typename DT::T T;
   extern __shared__ __attribute__((aligned(16))) uint32_t lc_buf[];  // [W + 8] column pairs
   __shared__ float lc_red[2][LC_MAXW];
@@ -138,10 +140,11 @@ __global__ __launch_bounds__(1024) void quant_lc_kernel(
   // a zero read by padding table entries, W + 1 = a write-only sink for their scatter)
   const int zp0 = 64 * tid;
   uint64_t zmask = 0;
-  for (int i = 0; i < 64; ++i) {
-    const int p = zp0 + i;
-    if (p < K && amap[p] < 0) zmask |= 1ull << i;
-  }
+  if (amap)  // NULL: in-place output quantization, salient columns pass through
+    for (int i = 0; i < 64; ++i) {
+      const int p = zp0 + i;
+      if (p < K && amap[p] < 0) zmask |= 1ull << i;
+    }
   for (int c = tid; c < W + 2; c += nthr) lc_buf[c] = 0u;
   PairScale tens;
   if (MODE == LC_MODE_TENSOR) {

@@ -311,8 +311,11 @@ __global__ __launch_bounds__(512, 1) void gemm_fq6_kernel(
   constexpr int CW = 32;                // weight rows (output columns) per wave
   constexpr int I = TM / 16, J = 2;     // 16 x 16 tiles per wave (TM rows x 32 columns)
   constexpr int NA = TM / 64;           // codes-stage A DMA ops per wave (64 rows each)
-  constexpr int HALVES = TM / 128;      // dense stages per 64-column block (128 rows each)
-  constexpr int VM_CODES = NA + 1 + 1, VM_DENSE = 2 + 4;
+  // dense stages: TM = 128 -> 64 columns x 128 rows (A 16 KiB + B 32 KiB, 128-B lines);
+  // TM = 256 -> 32 columns x 256 rows (A 16 KiB + B 16 KiB, 64-B row pieces: measured
+  // faster there than 64-column half-height stages, which move B twice)
+  constexpr int DW = TM == 128 ? 64 : 32;
+  constexpr int VM_CODES = NA + 1 + 1, VM_DENSE = DW == 64 ? 2 + 4 : 2 + 2;
   constexpr int GBn = GB > 0 ? GB : 1;
   constexpr int LPG = CW / 8;
   constexpr int PF = 3;
@@ -327,17 +330,23 @@ __global__ __launch_bounds__(512, 1) void gemm_fq6_kernel(
   const int r16 = lane & 15, q = lane >> 4;
   const int lda = Kp + S_pad;
   const int nkm = GB ? Kp / 64 : 0;
-  const int nkt = nkm + ((lda - nkm * 64) / 64) * HALVES;
+  const int nkt = nkm + (lda - nkm * 64) / DW;
   const int Np = pad_n(N);
 
   const int arow = 8 * wave + (lane >> 3);
   const uint32_t lchunk = (uint32_t)(bitrev3((lane & 7) ^ ((arow >> 1) & 7)) << 4);
   const uint32_t a_off = (uint32_t)((size_t)(m0 + arow) * lda * sizeof(T)) + lchunk;
   const uint32_t a_str = (uint32_t)(64 * (size_t)lda * sizeof(T));
-  const uint32_t ah_str = (uint32_t)(128 * (size_t)lda * sizeof(T));  // dense half-tile step
-  uint32_t bd_row[4];  // dense-stage B rows of this lane (clamped: wsal has N rows)
+  uint32_t bd_row[4];  // 64-column dense-stage B rows of this lane (clamped: wsal has N rows)
 #pragma unroll
   for (int i = 0; i < 4; ++i) bd_row[i] = (uint32_t)min(n0 + arow + 64 * i, N - 1);
+  // 32-column dense stages: 4 lanes per 64-B row piece, chunks swizzled by (row >> 2) & 3
+  const int drow = 16 * wave + (lane >> 2);
+  const int dchunk = (lane & 3) ^ d_f((lane >> 4) & 3);
+  const uint32_t ad_off = (uint32_t)((size_t)(m0 + drow) * lda * sizeof(T) + dchunk * 16);
+  const uint32_t ad_str = (uint32_t)(128 * (size_t)lda * sizeof(T));
+  const uint32_t bd_row0 = (uint32_t)min(n0 + drow, N - 1);
+  const uint32_t bd_row1 = (uint32_t)min(n0 + drow + 128, N - 1);
   const uint32_t b_off = (uint32_t)((size_t)(n0 + 32 * wave + (lane >> 1)) * (Kp / 2) +
                                     (((lane & 1) ^ ((lane >> 4) & 1)) << 4));
   const int s_u = min(lane / LPG, GBn - 1);
@@ -354,11 +363,9 @@ __global__ __launch_bounds__(512, 1) void gemm_fq6_kernel(
       const int g = min(g0 + s_u, ngw - 1);
       glds16((const unsigned char*)wscale + (size_t)g * Np * sizeof(T) + s_off,
              slot + F5_A + F5_B + wave * 1024);
-    } else {
-      const int d = kt - nkm;
-      const int col = nkm * 64 + (d / HALVES) * 64;
-      const int h = d % HALVES;
-      const unsigned char* ab = (const unsigned char*)A + (size_t)col * sizeof(T) + h * ah_str;
+    } else if (DW == 64) {
+      const int col = nkm * 64 + (kt - nkm) * 64;
+      const unsigned char* ab = (const unsigned char*)A + (size_t)col * sizeof(T);
       glds16(ab + a_off, slot + wave * 1024);
       glds16(ab + a_str + a_off, slot + (8 + wave) * 1024);
       const bool main = col < Kp;
@@ -368,6 +375,17 @@ __global__ __launch_bounds__(512, 1) void gemm_fq6_kernel(
 #pragma unroll
       for (int i = 0; i < 4; ++i)
         glds16(bc + (size_t)bd_row[i] * ldb * sizeof(T), slot + F5_DN + (i * 8 + wave) * 1024);
+    } else {
+      const int col = nkm * 64 + (kt - nkm) * 32;
+      const unsigned char* ab = (const unsigned char*)A + (size_t)col * sizeof(T);
+      glds16(ab + ad_off, slot + wave * 1024);
+      glds16(ab + ad_str + ad_off, slot + (8 + wave) * 1024);
+      const bool main = col < Kp;
+      const unsigned char* bb = main ? (const unsigned char*)Bw : (const unsigned char*)wsal;
+      const uint32_t ldb = main ? (uint32_t)Kp : (uint32_t)S_pad;
+      const uint32_t c0 = (uint32_t)(main ? col : col - Kp) * sizeof(T) + dchunk * 16;
+      glds16(bb + bd_row0 * ldb * sizeof(T) + c0, slot + F5_DB + wave * 1024);
+      glds16(bb + bd_row1 * ldb * sizeof(T) + c0, slot + F5_DB + (8 + wave) * 1024);
     }
   };
 
@@ -421,7 +439,21 @@ __global__ __launch_bounds__(512, 1) void gemm_fq6_kernel(
   };
 #undef SQMP_FQ6_BLOCKS
 
-  // dense stage: rows 128 h .. 128 h + 127 of the tile (accumulator blocks 8 h ..)
+  // 32-column dense stage over all TM rows
+  const int d_sw = d_f((r16 >> 2) & 3);
+  auto compute_dense32 = [&](const unsigned char* __restrict__ slot) {
+    const int co = (q ^ d_sw) << 4;
+    u32x4 bf[J];
+#pragma unroll
+    for (int j = 0; j < J; ++j) bf[j] = *(const u32x4*)(slot + F5_DB + (wn * CW + 16 * j + r16) * 64 + co);
+#pragma unroll
+    for (int i = 0; i < I; ++i) {
+      const u32x4 af = *(const u32x4*)(slot + (16 * i + r16) * 64 + co);
+#pragma unroll
+      for (int j = 0; j < J; ++j) Mfma<DT>::run(acc[i][j], bf[j], af);
+    }
+  };
+  // 64-column dense stage over 128 rows (TM = 128)
   auto compute_dense = [&](const unsigned char* __restrict__ slot, auto hc) {
     constexpr int H = decltype(hc)::value;
     constexpr int I2 = 8;
@@ -472,10 +504,10 @@ __global__ __launch_bounds__(512, 1) void gemm_fq6_kernel(
     raw_barrier();
     if (kt + 2 < nkt) issue(kt + 2);
     unsigned char* slot = lds + (kt % F5_NSLOT) * F5_SLOT;
-    if (HALVES == 1 || (kt - nkm) % HALVES == 0)
+    if constexpr (DW == 64)
       compute_dense(slot, std::integral_constant<int, 0>());
     else
-      compute_dense(slot, std::integral_constant<int, HALVES - 1>());
+      compute_dense32(slot);
   }
 
   // ---- epilogue: acc[i][j][r] = C[n = n0 + 32 wn + 16 j + 4 q + r][m = m0 + 16 i + r16]

@@ -284,11 +284,18 @@ def fake_quant_inplace(t2: torch.Tensor, act_quant: str, n_bits: int, group_size
     """Fake-quantize t [M, C] in place; columns marked -2 in amap_fq pass through."""
     _require_gpu(t2, "fake_quant")
     M, C = t2.shape
-    ws, nb = _act_workspace(M, C, C, t2.device)
-    check(load().sqmp_quant_act(_p(t2), _dtype_code(t2.dtype), M, C, ACT_MODES[act_quant], n_bits,
-                                group_size, _p(amap_fq), C, _p(nonsal), None, S, 0,
-                                _lib.OUT_INPLACE, None, None, None, _p(ws), nb, _stream(t2)),
-          "fake_quant")
+    lib = load()
+    nb = lib.sqmp_act_workspace_bytes(M, C, C)
+    stream = torch.cuda.current_stream(t2.device).cuda_stream
+    e = _act_ws(t2.device, stream, C, C, nb)
+    status = lib.sqmp_quant_act_v2(_p(t2), _dtype_code(t2.dtype), M, C, ACT_MODES[act_quant],
+                                   n_bits, group_size, _p(amap_fq), C, _p(nonsal), None, S, 0,
+                                   None, _lib.QA_CLEAN_WS, _lib.OUT_INPLACE, None, None, None,
+                                   _p(e["buf"]), e["buf"].numel(), ctypes.c_void_p(stream))
+    if status != _lib.SQMP_OK:
+        _WS.pop((t2.device.index, stream, C, C), None)
+        check(status, "fake_quant")
+    e["stats"] = None  # the sorted-column list now describes t2, not a layer input
     return t2
 
 

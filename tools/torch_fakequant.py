@@ -8,7 +8,11 @@ Follows /root/reference/smoothquant/fake_quant.py:
                                  F.linear with the stored dequantized weight)
   per_group (sorted)   :104-154 (batch column absmax, argsort, pad to G, per-(row, group)
                                  scales, round, unsort)
-  per_token            :56-64
+  per_token / tensor   :56-75
+  output quantization  :308-316 (OPT q/k/v with quantize_bmm_input)
+plus the config-5 variants (unsorted groups :77-101, the mean+3sigma sort key).
+`accum32` runs F.linear on fp32 copies: the same fake-quant math with a different GEMM
+accumulation order (the noise floor of PPL comparisons).
 """
 import torch
 import torch.nn.functional as F
@@ -22,10 +26,29 @@ def act_per_token(t, n_bits):
 
 
 @torch.no_grad()
-def act_per_group_sorted(t, n_bits, group_size):
+def act_per_tensor(t, n_bits):
+    q_max = 2 ** (n_bits - 1) - 1
+    s = t.abs().max().clamp(min=1e-5).div(q_max)
+    return t.div(s).round().mul(s)
+
+
+def _mean3std(t):
+    a = t.abs().double()
+    mean = a.mean(0)
+    var = ((a * a).mean(0) - mean * mean).clamp(min=0)
+    return (mean + 3 * var.sqrt()).float()
+
+
+@torch.no_grad()
+def act_per_group_sorted(t, n_bits, group_size, key="max"):
     q_max = 2 ** (n_bits - 1) - 1
     M, C = t.shape
-    idx = torch.argsort(t.abs().max(dim=0)[0], stable=True)
+    if key == "none":
+        idx = torch.arange(C, device=t.device)
+    elif key == "mean3std":
+        idx = torch.argsort(_mean3std(t), stable=True)
+    else:
+        idx = torch.argsort(t.abs().max(dim=0)[0], stable=True)
     ts = t[:, idx]
     pad = (-C) % group_size
     if pad:
@@ -42,8 +65,11 @@ def act_per_group_sorted(t, n_bits, group_size):
 class TorchFakeQuantLinear:
     """The reference forward on given W_hat (dequantized weight), bias, salient set."""
 
-    def __init__(self, w_hat, bias, salient, act_quant="per_group", n_bits=4, group_size=128):
+    def __init__(self, w_hat, bias, salient, act_quant="per_group", n_bits=4, group_size=128,
+                 accum32=False, output_quant=None):
         self.w = w_hat
+        self.accum32 = accum32
+        self.out_spec = output_quant  # (mode, bits, group) or None
         self.b = bias
         K = w_hat.shape[1]
         self.mask = None
@@ -54,10 +80,20 @@ class TorchFakeQuantLinear:
         self.n_bits = n_bits
         self.G = group_size
 
+    @staticmethod
+    def _quant(t, mode, bits, G):
+        if mode == "per_group":
+            return act_per_group_sorted(t, bits, G)
+        if mode == "per_group_unsorted":
+            return act_per_group_sorted(t, bits, G, "none")
+        if mode == "per_group_mean3std":
+            return act_per_group_sorted(t, bits, G, "mean3std")
+        if mode == "per_tensor":
+            return act_per_tensor(t, bits)
+        return act_per_token(t, bits)
+
     def _aq(self, t):
-        if self.act == "per_group":
-            return act_per_group_sorted(t, self.n_bits, self.G)
-        return act_per_token(t, self.n_bits)
+        return self._quant(t, self.act, self.n_bits, self.G)
 
     @torch.no_grad()
     def __call__(self, x):
@@ -67,5 +103,16 @@ class TorchFakeQuantLinear:
             q_x[:, self.mask] = self._aq(x2[:, self.mask])
         else:
             q_x = self._aq(x2)
-        y = F.linear(q_x, self.w, self.b)
+        if self.accum32:
+            y = F.linear(q_x.float(), self.w.float(),
+                         None if self.b is None else self.b.float()).to(q_x.dtype)
+        else:
+            y = F.linear(q_x, self.w, self.b)
+        if self.out_spec is not None:
+            mode, bits, G = self.out_spec
+            if self.mask is not None:
+                y = y.clone()
+                y[:, self.mask] = self._quant(y[:, self.mask], mode, bits, G)
+            else:
+                y = self._quant(y, mode, bits, G)
         return y.view(*x.shape[:-1], -1)
