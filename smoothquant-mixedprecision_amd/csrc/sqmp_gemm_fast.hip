@@ -25,6 +25,7 @@
 //   output columns of one row: 8-byte stores in the epilogue.
 //
 // gemm_i8v2 -- per_token / per_tensor activations on the integer MFMA (see below).
+#include <stdlib.h>
 #include <string.h>
 
 #include <type_traits>
@@ -301,21 +302,28 @@ __global__ __launch_bounds__(512, 1) void gemm_fq5_kernel(
 // TM = 256): A 128 rows x 128 B + B 256 weight rows x 128 B fill one 48 KiB slot, every
 // DMA moves whole 128-B lines, both images use the codes-stage A swizzle, and lane
 // (r16, q) of sub-step s reads chunk 4 (q & 1) + 2 s + (q >> 1) of A and B alike.
-template <class DT, int GB, int TM>
+// PRIO (tuning knob): 0 none; 1 = one s_setprio 1 for the younger half (waves 4-7) before
+// the main loop; 2 = s_setprio 1 / 0 around each stage's compute (MI355X guide T5).
+// WM = waves along M (1: 1 x 8 waves of TM x 32; 2: 2 x 4 waves of TM/2 x 64).
+template <class DT, int GB, int TM, int PRIO = 0, int WM = 1, int SCALE_PRED = 0>
 __global__ __launch_bounds__(512, 1) void gemm_fq6_kernel(
     const typename DT::T* __restrict__ A, const void* __restrict__ Bw,
     const typename DT::T* __restrict__ wscale, const typename DT::T* __restrict__ wsal,
     const typename DT::T* __restrict__ bias, typename DT::T* __restrict__ Y, int M, int N,
     int Kp, int S_pad, int Gw, int ngw, int tiles_m, int tiles_n) {
   typedef typename DT::T T;
-  constexpr int CW = 32;                // weight rows (output columns) per wave
-  constexpr int I = TM / 16, J = 2;     // 16 x 16 tiles per wave (TM rows x 32 columns)
+  constexpr int NWN = 8 / WM;           // waves along N
+  constexpr int CW = 256 / NWN;         // weight rows (output columns) per wave
+  constexpr int MW = TM / WM;           // rows per wave
+  constexpr int I = MW / 16, J = CW / 16;  // 16 x 16 tiles per wave
   constexpr int NA = TM / 64;           // codes-stage A DMA ops per wave (64 rows each)
   // dense stages: TM = 128 -> 64 columns x 128 rows (A 16 KiB + B 32 KiB, 128-B lines);
   // TM = 256 -> 32 columns x 256 rows (A 16 KiB + B 16 KiB, 64-B row pieces: measured
   // faster there than 64-column half-height stages, which move B twice)
   constexpr int DW = TM == 128 ? 64 : 32;
-  constexpr int VM_CODES = NA + 1 + 1, VM_DENSE = DW == 64 ? 2 + 4 : 2 + 2;
+  // dense A ops per wave: 2 (64-col or TM = 256), 1 (TM = 64: one 128-row op, upper half unused)
+  constexpr int NAD = DW == 64 ? 2 : (TM == 256 ? 2 : 1);
+  constexpr int VM_CODES = NA + 1 + 1, VM_DENSE = DW == 64 ? 2 + 4 : NAD + 2;
   constexpr int GBn = GB > 0 ? GB : 1;
   constexpr int LPG = CW / 8;
   constexpr int PF = 3;
@@ -326,7 +334,7 @@ __global__ __launch_bounds__(512, 1) void gemm_fq6_kernel(
   const int m0 = tm * TM, n0 = tn * 256;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wn = wave;
+  const int wm = wave / NWN, wn = wave % NWN;
   const int r16 = lane & 15, q = lane >> 4;
   const int lda = Kp + S_pad;
   const int nkm = GB ? Kp / 64 : 0;
@@ -361,8 +369,11 @@ __global__ __launch_bounds__(512, 1) void gemm_fq6_kernel(
       glds16((const unsigned char*)Bw + (size_t)kt * 32 + b_off, slot + F5_A + wave * 1024);
       const int g0 = GB == 1 ? (kt * 64) / Gw : kt * 2;
       const int g = min(g0 + s_u, ngw - 1);
-      glds16((const unsigned char*)wscale + (size_t)g * Np * sizeof(T) + s_off,
-             slot + F5_A + F5_B + wave * 1024);
+      // only the lanes that carry distinct scales move bytes (GBn groups x CW columns);
+      // the instruction still issues once per wave, so the vmcnt counts stay the same
+      if (SCALE_PRED == 0 || lane < GBn * LPG)
+        glds16((const unsigned char*)wscale + (size_t)g * Np * sizeof(T) + s_off,
+               slot + F5_A + F5_B + wave * 1024);
     } else if (DW == 64) {
       const int col = nkm * 64 + (kt - nkm) * 64;
       const unsigned char* ab = (const unsigned char*)A + (size_t)col * sizeof(T);
@@ -379,7 +390,7 @@ __global__ __launch_bounds__(512, 1) void gemm_fq6_kernel(
       const int col = nkm * 64 + (kt - nkm) * 32;
       const unsigned char* ab = (const unsigned char*)A + (size_t)col * sizeof(T);
       glds16(ab + ad_off, slot + wave * 1024);
-      glds16(ab + ad_str + ad_off, slot + (8 + wave) * 1024);
+      if (NAD == 2) glds16(ab + ad_str + ad_off, slot + (8 + wave) * 1024);
       const bool main = col < Kp;
       const unsigned char* bb = main ? (const unsigned char*)Bw : (const unsigned char*)wsal;
       const uint32_t ldb = main ? (uint32_t)Kp : (uint32_t)S_pad;
@@ -396,7 +407,7 @@ __global__ __launch_bounds__(512, 1) void gemm_fq6_kernel(
     for (int j = 0; j < J; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const DecK dk = make_deck();
-  const int a_row0 = r16 * 128;
+  const int a_row0 = (wm * MW + r16) * 128;
   const int a_sw = (r16 >> 1) & 7;
   // A fragment of block t = I*s + i: row 16 i + r16, chunk 4 (q&1) + 2 s + (q>>1)
   auto ald = [&](const unsigned char* __restrict__ slot, int t) {
@@ -433,8 +444,10 @@ __global__ __launch_bounds__(512, 1) void gemm_fq6_kernel(
 #pragma unroll
     for (int j = 0; j < J; ++j) bf[0][j] = Dec<DT>::run(bw[j].x, sp[j], dk);
 #define SQMP_BF6(s, j) bf[s][j]
+    // sub-step 1 fragments decoded under the first J blocks (used from block I on)
+    static_assert(J <= I, "sub-step 1 decode must finish before block I");
     SQMP_FQ6_BLOCKS(SQMP_BF6,
-                    if (t >= 1 && t <= J) bf[1][t - 1] = Dec<DT>::run(bw[t - 1].y, sp[t - 1], dk));
+                    if (t < J) bf[1][t] = Dec<DT>::run(bw[t].y, sp[t], dk));
 #undef SQMP_BF6
   };
 #undef SQMP_FQ6_BLOCKS
@@ -448,7 +461,7 @@ __global__ __launch_bounds__(512, 1) void gemm_fq6_kernel(
     for (int j = 0; j < J; ++j) bf[j] = *(const u32x4*)(slot + F5_DB + (wn * CW + 16 * j + r16) * 64 + co);
 #pragma unroll
     for (int i = 0; i < I; ++i) {
-      const u32x4 af = *(const u32x4*)(slot + (16 * i + r16) * 64 + co);
+      const u32x4 af = *(const u32x4*)(slot + (wm * MW + 16 * i + r16) * 64 + co);
 #pragma unroll
       for (int j = 0; j < J; ++j) Mfma<DT>::run(acc[i][j], bf[j], af);
     }
@@ -456,7 +469,7 @@ __global__ __launch_bounds__(512, 1) void gemm_fq6_kernel(
   // 64-column dense stage over 128 rows (TM = 128)
   auto compute_dense = [&](const unsigned char* __restrict__ slot, auto hc) {
     constexpr int H = decltype(hc)::value;
-    constexpr int I2 = 8;
+    constexpr int I2 = I;
     u32x4 bf[2][J];
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2)
@@ -486,6 +499,7 @@ __global__ __launch_bounds__(512, 1) void gemm_fq6_kernel(
 
   issue(0);
   if (nkt > 1) issue(1);
+  if (PRIO == 1 && wave >= 4) __builtin_amdgcn_s_setprio(1);
   int kt = 0;
   for (; kt < nkm; ++kt) {
     if (kt + 1 < nkt) {
@@ -496,7 +510,9 @@ __global__ __launch_bounds__(512, 1) void gemm_fq6_kernel(
     }
     raw_barrier();
     if (kt + 2 < nkt) issue(kt + 2);
+    if (PRIO == 2) __builtin_amdgcn_s_setprio(1);
     compute_codes(lds + (kt % F5_NSLOT) * F5_SLOT);
+    if (PRIO == 2) __builtin_amdgcn_s_setprio(0);
   }
   for (; kt < nkt; ++kt) {
     if (kt + 1 < nkt) vm_wait<VM_DENSE>();
@@ -504,13 +520,16 @@ __global__ __launch_bounds__(512, 1) void gemm_fq6_kernel(
     raw_barrier();
     if (kt + 2 < nkt) issue(kt + 2);
     unsigned char* slot = lds + (kt % F5_NSLOT) * F5_SLOT;
+    if (PRIO == 2) __builtin_amdgcn_s_setprio(1);
     if constexpr (DW == 64)
       compute_dense(slot, std::integral_constant<int, 0>());
     else
       compute_dense32(slot);
+    if (PRIO == 2) __builtin_amdgcn_s_setprio(0);
   }
+  if (PRIO == 1) __builtin_amdgcn_s_setprio(0);
 
-  // ---- epilogue: acc[i][j][r] = C[n = n0 + 32 wn + 16 j + 4 q + r][m = m0 + 16 i + r16]
+  // ---- epilogue: acc[i][j][r] = C[n = n0 + CW wn + 16 j + 4 q + r][m = m0 + MW wm + 16 i + r16]
   float bvs[J][4];
 #pragma unroll
   for (int j = 0; j < J; ++j)
@@ -523,7 +542,7 @@ __global__ __launch_bounds__(512, 1) void gemm_fq6_kernel(
     if (nb >= N) continue;
 #pragma unroll
     for (int i = 0; i < I; ++i) {
-      const int gm = m0 + 16 * i + r16;
+      const int gm = m0 + wm * MW + 16 * i + r16;
       if (gm >= M) continue;
       T v[4];
 #pragma unroll
@@ -761,15 +780,48 @@ static int fq5_dispatch(const void* a, const void* codes, const void* wscale, co
   return SQMP_EUNSUPPORTED;
 }
 
+static int fq6_prio() {
+  static int v = [] {
+    const char* e = getenv("SQMP_FQ6_PRIO");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+static int fq6_wm() {
+  static int v = [] {
+    const char* e = getenv("SQMP_FQ6_WM");
+    return e ? atoi(e) : 1;
+  }();
+  return v;
+}
+
 template <class DT, int GB, int TM>
 static int fq6_launch(const void* a, const void* codes, const void* wscale, const void* wsal,
                       const void* bias, void* y, int M, int N, int Kp, int S_pad, int Gw,
                       int ngw, hipStream_t s) {
   typedef typename DT::T T;
   const int tiles_m = cdiv(M, TM), tiles_n = cdiv(N, 256);
-  gemm_fq6_kernel<DT, GB, TM><<<dim3(tiles_m * tiles_n), dim3(512), 0, s>>>(
-      (const T*)a, codes, (const T*)wscale, (const T*)wsal, (const T*)bias, (T*)y, M, N, Kp,
-      S_pad, Gw, ngw, tiles_m, tiles_n);
+#define SQMP_FQ6_L(PR, WMV)                                                                   \
+  gemm_fq6_kernel<DT, GB, TM, PR, WMV><<<dim3(tiles_m * tiles_n), dim3(512), 0, s>>>(         \
+      (const T*)a, codes, (const T*)wscale, (const T*)wsal, (const T*)bias, (T*)y, M, N, Kp, \
+      S_pad, Gw, ngw, tiles_m, tiles_n)
+  const int pr = fq6_prio();
+  bool done = false;
+  if constexpr (TM >= 128) {
+    if (fq6_wm() == 2) {
+      SQMP_FQ6_L(0, 2);
+      done = true;
+    }
+  }
+  if (done) {
+  } else if (pr == 1) SQMP_FQ6_L(1, 1);
+  else if (pr == 2) SQMP_FQ6_L(2, 1);
+  else if (pr == 3)  // diagnostic: every lane moves a (duplicate) scale chunk
+    gemm_fq6_kernel<DT, GB, TM, 0, 1, 0><<<dim3(tiles_m * tiles_n), dim3(512), 0, s>>>(
+        (const T*)a, codes, (const T*)wscale, (const T*)wsal, (const T*)bias, (T*)y, M, N, Kp,
+        S_pad, Gw, ngw, tiles_m, tiles_n);
+  else SQMP_FQ6_L(0, 1);
+#undef SQMP_FQ6_L
   SQMP_LAUNCH_CHECK();
   return SQMP_OK;
 }
@@ -778,11 +830,15 @@ template <class DT>
 static int fq6_dispatch(const void* a, const void* codes, const void* wscale, const void* wsal,
                         const void* bias, void* y, int M, int N, int Kp, int S_pad, int Gw,
                         int ngw, int n_bits, hipStream_t s) {
-  // 128-row tiles when 256-row tiles would leave the chip under two workgroups per CU
-  const bool small = (long)cdiv(M, 256) * cdiv(N, 256) < 2L * 256;
-#define SQMP_FQ6(GB, GW, NGW)                                                                   \
-  (small ? fq6_launch<DT, GB, 128>(a, codes, wscale, wsal, bias, y, M, N, Kp, S_pad, GW, NGW, s) \
-         : fq6_launch<DT, GB, 256>(a, codes, wscale, wsal, bias, y, M, N, Kp, S_pad, GW, NGW, s))
+  // 128-row tiles when 256-row tiles would leave the chip under two workgroups per CU;
+  // 64-row tiles when even 128-row tiles would leave CUs idle (e.g. OPT-1.3B's 2048-wide
+  // layers at 2048 tokens: 128 tiles of 128 x 256)
+  const long t256 = (long)cdiv(M, 256) * cdiv(N, 256), t128 = (long)cdiv(M, 128) * cdiv(N, 256);
+  const int tm = t256 >= 2L * 256 ? 256 : (t128 >= 256 || M <= 64 ? 128 : 64);
+#define SQMP_FQ6(GB, GW, NGW)                                                                     \
+  (tm == 256 ? fq6_launch<DT, GB, 256>(a, codes, wscale, wsal, bias, y, M, N, Kp, S_pad, GW, NGW, s) \
+   : tm == 128 ? fq6_launch<DT, GB, 128>(a, codes, wscale, wsal, bias, y, M, N, Kp, S_pad, GW, NGW, s) \
+               : fq6_launch<DT, GB, 64>(a, codes, wscale, wsal, bias, y, M, N, Kp, S_pad, GW, NGW, s))
   if (n_bits == 0) return SQMP_FQ6(0, 1, 1);
   if (n_bits != 4) return SQMP_EUNSUPPORTED;
   if (Gw % 64 == 0) return SQMP_FQ6(1, Gw, ngw);
