@@ -486,6 +486,80 @@ __global__ __launch_bounds__(256) void lc_table_kernel(
   for (int r = Kn + t; r < lc_len; r += nt) lctab[r] = lc_none;
 }
 
+// ---------------------------------------------------------------- rank + table, one launch
+// For lists up to RT_MAX entries: every workgroup stages all L keys key[nonsal[j]] in LDS
+// and ranks 256 / TPO owners, TPO lanes per owner splitting the competitors (16-B LDS
+// reads, interleaved so the TPO lanes hit consecutive chunks), then reduces the TPO
+// partial counts by lane shuffles.  The stable rank of owner i is
+//   #{j : key_j < key_i} + #{j < i : key_j == key_i}
+// (the reference's stable argsort, fake_quant.py:113), counted as key_j < thr with
+// thr = key_i + 1 on 4-entry chunks wholly below i, key_i elsewhere, plus the equal keys
+// of i's own chunk below i.  Writes colsorted[r] and lctab[r] = col | posmap[col] << 16,
+// and the (zero, sink) entries of ranks [L, lc_len).  The keys are NOT cleared here (other
+// workgroups may still read them): the quantizer launched next clears them.
+constexpr int RT_MAX = 8192;
+template <int TPO>
+__global__ __launch_bounds__(256) void rank_table_kernel(
+    const uint32_t* __restrict__ key, const int32_t* __restrict__ nonsal, int L,
+    const int32_t* __restrict__ posmap, int32_t* __restrict__ colsorted,
+    uint32_t* __restrict__ lctab, int lc_len, uint32_t lc_none) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t rt_kv[];  // roundup(L, 4 TPO)
+  const int tid = threadIdx.x;
+  const int L4 = (int)round_up_dev(L, 4 * TPO) >> 2;
+  for (int j = tid; j < 4 * L4; j += 256) rt_kv[j] = j < L ? key[nonsal[j]] : 0xFFFFFFFFu;
+  const int nt = gridDim.x * 256;
+  for (int r = L + blockIdx.x * 256 + tid; r < lc_len; r += nt) lctab[r] = lc_none;
+  __syncthreads();
+  const int sub = tid % TPO;
+  const int owner = blockIdx.x * (256 / TPO) + tid / TPO;
+  const int oi = owner < L ? owner : L - 1;
+  const uint32_t mine = rt_kv[oi];
+  const int ochunk = oi >> 2;
+  uint32_t c0 = 0, c1 = 0;
+  const u32x4* kv4 = (const u32x4*)rt_kv;
+#pragma unroll 4
+  for (int j4 = sub; j4 < L4; j4 += TPO) {
+    const u32x4 k = kv4[j4];
+    const uint32_t thr = j4 < ochunk ? mine + 1u : mine;  // keys never reach 0xFFFFFFFF
+    c0 += (k[0] < thr ? 1u : 0u) + (k[1] < thr ? 1u : 0u);
+    c1 += (k[2] < thr ? 1u : 0u) + (k[3] < thr ? 1u : 0u);
+  }
+  uint32_t cnt = c0 + c1;
+  if (sub == (ochunk % TPO))
+    for (int e = 0; e < (oi & 3); ++e) cnt += rt_kv[4 * ochunk + e] == mine ? 1u : 0u;
+#pragma unroll
+  for (int o = 1; o < TPO; o <<= 1) cnt += (uint32_t)__shfl_xor((int)cnt, o, 64);
+  if (sub == 0 && owner < L) {
+    const int col = nonsal[owner];
+    colsorted[cnt] = col;
+    lctab[cnt] = (uint32_t)col | ((uint32_t)(posmap ? posmap[col] : col) << 16);
+  }
+}
+
+// SQMP_RANK_TABLE_OFF=1 keeps rank_count + lc_table (A/B diagnostics).
+static bool rank_table_fits(int L) {
+  static const bool off = getenv("SQMP_RANK_TABLE_OFF") != nullptr;
+  return !off && L > 0 && L <= RT_MAX;
+}
+
+static int launch_rank_table(const uint32_t* key, const int32_t* nonsal, int L,
+                             const int32_t* posmap, int32_t* colsorted, uint32_t* lctab,
+                             int lc_len, uint32_t lc_none, hipStream_t s) {
+  // about 128-256 competitors per lane (SQMP_RT_TPO=16/32 overrides, tuning only)
+  static const int tpo_env = getenv("SQMP_RT_TPO") ? atoi(getenv("SQMP_RT_TPO")) : 0;
+  const int tpo = tpo_env == 16 || tpo_env == 32 ? tpo_env : (L <= 2048 ? 16 : 32);
+  const int grid = cdiv((long)L * tpo, 256);
+  const size_t lds = sizeof(uint32_t) * (size_t)round_up(L, 4 * tpo);
+  if (tpo == 16)
+    rank_table_kernel<16><<<dim3(grid), dim3(256), lds, s>>>(key, nonsal, L, posmap, colsorted,
+                                                              lctab, lc_len, lc_none);
+  else
+    rank_table_kernel<32><<<dim3(grid), dim3(256), lds, s>>>(key, nonsal, L, posmap, colsorted,
+                                                              lctab, lc_len, lc_none);
+  SQMP_LAUNCH_CHECK();
+  return SQMP_OK;
+}
+
 // ---------------------------------------------------------------- wave-per-row variant
 // Same arithmetic as quant_fp_kernel, but each wave owns whole rows: no block barrier on
 // the per-row path, so every wave of the CU streams its own rows (next row prefetched
@@ -830,35 +904,50 @@ extern "C" int sqmp_quant_act_v2(void* x, int dtype, int M, int K, int amode, in
   const uint32_t lc_none = (uint32_t)(Kp + S_pad) | ((uint32_t)(Kp + S_pad + 1) << 16);
   const int lc_len = (int)round_up(K, 4096);
 
-  // ---- fast path: lane-contiguous quantizer fed by the per-weight column -> position map;
-  // at most colmax + rank + table + quantizer launches, none of them a memset in the
-  // clean-workspace protocol, and only table + quantizer when the statistics are reused.
-  if (use_lc && posmap && amode != SQMP_ACT_PER_TENSOR) {
+  // ---- lane-contiguous quantizer: statistics, then the rank-ordered (column, position)
+  // table -- one rank_table launch for lists up to RT_MAX, else rank_count + lc_table; no
+  // memsets in the clean-workspace protocol, only the table when statistics are reused.
+  auto lc_prepare = [&](const int32_t* pm, uint32_t none, bool reuse,
+                        uint32_t*& key_clear) -> int {
+    key_clear = nullptr;
     int tmode = TAB_LIST;
     if (sorted) {
-      if (flags & SQMP_QA_REUSE_STATS) {
+      if (reuse) {
         tmode = TAB_SORTED;
       } else {
         tmode = TAB_COUNTS;
+        int st2;
         if (amode == SQMP_ACT_PER_GROUP) {
           if (!clean) SQMP_HIP_CHECK(hipMemsetAsync(cmax, 0, sizeof(uint32_t) * k64, s));
-          st = launch_colmax(x, dtype, M, K, cmax, s, false);
+          st2 = launch_colmax(x, dtype, M, K, cmax, s, false);
         } else {
-          st = launch_colkey_mean3std(x, dtype, M, K, sums, cmax, s, clean);
+          st2 = launch_colkey_mean3std(x, dtype, M, K, sums, cmax, s, clean);
         }
-        if (st) return st;
+        if (st2) return st2;
+        if (rank_table_fits(Kn)) {
+          key_clear = cmax;  // cleared by the quantizer, after every rank_table read
+          return launch_rank_table(cmax, nonsal, Kn, pm, colsorted, lctab, lc_len, none, s);
+        }
         if (!clean) SQMP_HIP_CHECK(hipMemsetAsync(counts, 0, sizeof(int32_t) * k64, s));
-        st = launch_rank_count(cmax, nonsal, Kn, counts, s);
-        if (st) return st;
+        st2 = launch_rank_count(cmax, nonsal, Kn, counts, s);
+        if (st2) return st2;
       }
     }
     const int nthr = K > Kn ? K : (Kn > 0 ? Kn : 1);
     lc_table_kernel<<<dim3(cdiv(nthr, 256)), dim3(256), 0, s>>>(
-        tmode, nonsal, Kn, K, posmap, counts, colsorted, tmode == TAB_COUNTS ? cmax : nullptr,
-        lctab, lc_len, lc_none);
+        tmode, nonsal, Kn, K, pm, counts, colsorted, tmode == TAB_COUNTS ? cmax : nullptr,
+        lctab, lc_len, none);
     SQMP_LAUNCH_CHECK();
+    return SQMP_OK;
+  };
+
+  // fast path: the table maps ranks straight to packed positions (per-weight posmap)
+  if (use_lc && posmap && amode != SQMP_ACT_PER_TENSOR) {
+    uint32_t* kc;
+    st = lc_prepare(posmap, lc_none, (flags & SQMP_QA_REUSE_STATS) != 0, kc);
+    if (st) return st;
     return launch_quant_lc(dtype, lmode, x, M, K, q_max, group_size, lctab, Kn, amap, Kp,
-                           salient, S, S_pad, cmax, nonsal, out, s);
+                           salient, S, S_pad, cmax, nonsal, out, kc, (int)k64, s);
   }
 
   // ---- in-place output quantization (fake_quant.py:308-316) on the same kernels: the
@@ -866,28 +955,11 @@ extern "C" int sqmp_quant_act_v2(void* x, int dtype, int M, int K, int amode, in
   // tail), and the row is written back over itself.
   if (out_kind == SQMP_OUT_INPLACE && !lc_off && amode != SQMP_ACT_PER_TENSOR &&
       quant_lc_supported(dtype, M, K, group, group_size, Kn, K, 0, x, x)) {
-    int tmode = TAB_LIST;
-    if (sorted) {
-      tmode = TAB_COUNTS;
-      if (amode == SQMP_ACT_PER_GROUP) {
-        if (!clean) SQMP_HIP_CHECK(hipMemsetAsync(cmax, 0, sizeof(uint32_t) * k64, s));
-        st = launch_colmax(x, dtype, M, K, cmax, s, false);
-      } else {
-        st = launch_colkey_mean3std(x, dtype, M, K, sums, cmax, s, clean);
-      }
-      if (st) return st;
-      if (!clean) SQMP_HIP_CHECK(hipMemsetAsync(counts, 0, sizeof(int32_t) * k64, s));
-      st = launch_rank_count(cmax, nonsal, Kn, counts, s);
-      if (st) return st;
-    }
-    const int nthr = K > Kn ? K : (Kn > 0 ? Kn : 1);
-    const uint32_t none_ip = (uint32_t)K | ((uint32_t)(K + 1) << 16);
-    lc_table_kernel<<<dim3(cdiv(nthr, 256)), dim3(256), 0, s>>>(
-        tmode, nonsal, Kn, K, nullptr, counts, colsorted, tmode == TAB_COUNTS ? cmax : nullptr,
-        lctab, lc_len, none_ip);
-    SQMP_LAUNCH_CHECK();
+    uint32_t* kc;
+    st = lc_prepare(nullptr, (uint32_t)K | ((uint32_t)(K + 1) << 16), false, kc);
+    if (st) return st;
     return launch_quant_lc(dtype, lmode, x, M, K, q_max, group_size, lctab, Kn, nullptr, K,
-                           salient, 0, 0, cmax, nonsal, x, s);
+                           salient, 0, 0, cmax, nonsal, x, kc, (int)k64, s);
   }
 
   // ---- general path (fp32, 8-bit int output, large rows, other group sizes)
@@ -916,7 +988,7 @@ extern "C" int sqmp_quant_act_v2(void* x, int dtype, int M, int K, int amode, in
   }
   if (use_lc) {
     st = launch_quant_lc(dtype, lmode, x, M, K, q_max, group_size, lctab, Kn, amap, Kp,
-                         salient, S, S_pad, cmax, nonsal, out, s);
+                         salient, S, S_pad, cmax, nonsal, out, nullptr, 0, s);
   } else {
     const int nga = group ? (Kn > 0 ? cdiv(Kn, group_size) : 1) : 1;
     const int32_t* rk = sorted ? rank : nullptr;

@@ -121,7 +121,8 @@ __global__ __launch_bounds__(1024) void quant_lc_kernel(
     const typename DT::T* x, int M, int K, int q_max, int G,
     const uint32_t* __restrict__ lctab, int Kn, const int32_t* __restrict__ amap, int P,
     const int32_t* __restrict__ sal, int S, int S_pad, const uint32_t* __restrict__ cmax,
-    const int32_t* __restrict__ nonsal, typename DT::T* out) {
+    const int32_t* __restrict__ nonsal, typename DT::T* out, uint32_t* __restrict__ key_clear,
+    int clear_words) {
   // x and out alias for in-place output quantization (every row is read before it is
   // written: a workgroup stores a pair only after loading it)
   typedef typename DT::T T;
@@ -136,30 +137,7 @@ __global__ __launch_bounds__(1024) void quant_lc_kernel(
   const int ochk = W / 8;           // 16-B output chunks per row
   const int rb = RPL * tid;         // this thread's first rank
 
-  // ---- once per workgroup: salient-position mask, zeroed buffer (+ two spare words: W =
-  // a zero read by padding table entries, W + 1 = a write-only sink for their scatter)
-  const int zp0 = 64 * tid;
-  uint64_t zmask = 0;
-  if (amap)  // NULL: in-place output quantization, salient columns pass through
-    for (int i = 0; i < 64; ++i) {
-      const int p = zp0 + i;
-      if (p < K && amap[p] < 0) zmask |= 1ull << i;
-    }
-  for (int c = tid; c < W + 2; c += nthr) lc_buf[c] = 0u;
-  PairScale tens;
-  if (MODE == LC_MODE_TENSOR) {
-    float m = 0.f;
-    for (int i = tid; i < Kn; i += nthr) m = fmaxf(m, __uint_as_float(cmax[nonsal[i]]));
-    m = wave_max(m);
-    if (lane == 0) lc_red[0][wave] = m;
-    __syncthreads();
-    m = 0.f;
-    for (int w = 0; w < NW; ++w) m = fmaxf(m, lc_red[0][w]);
-    const uint32_t mb = (uint32_t)__builtin_bit_cast(uint16_t, DT::from_f(m));
-    tens = pair_scale<DT>(mb | (mb << 16), q_max);
-  }
-  __syncthreads();
-
+  // the first row pair's loads go out before the prologue (their latency covers it)
   const int npair = (M + 1) / 2;
   u32x4 nx0[LC_CH], nx1[LC_CH];
   auto load_pair = [&](int rp) {
@@ -178,9 +156,59 @@ __global__ __launch_bounds__(1024) void quant_lc_kernel(
   };
   int rp = blockIdx.x;
   if (rp < npair) load_pair(rp);
+
+  // ---- once per workgroup: salient-position mask, zeroed buffer (+ two spare words: W =
+  // a zero read by padding table entries, W + 1 = a write-only sink for their scatter)
+  const int zp0 = 64 * tid;
+  uint64_t zmask = 0;
+  if (amap) {  // NULL: in-place output quantization, salient columns pass through
+    if (zp0 + 64 <= K && ((uintptr_t)amap & 15) == 0) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const u32x4 e = ((const u32x4*)(amap + zp0))[i];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) zmask |= (uint64_t)(e[j] >> 31) << (4 * i + j);
+      }
+    } else {
+      for (int i = 0; i < 64; ++i) {
+        const int p = zp0 + i;
+        if (p < K && amap[p] < 0) zmask |= 1ull << i;
+      }
+    }
+  }
+  for (int c = tid; c < W + 2; c += nthr) lc_buf[c] = 0u;
+  // the column statistics of this call, read by the (completed) table kernel: restore the
+  // clean-workspace zeros
+  if (key_clear)
+    for (int c = blockIdx.x * nthr + tid; c < (clear_words >> 2); c += gridDim.x * nthr)
+      ((u32x4*)key_clear)[c] = u32x4{0u, 0u, 0u, 0u};
+  PairScale tens;
+  if (MODE == LC_MODE_TENSOR) {
+    float m = 0.f;
+    for (int i = tid; i < Kn; i += nthr) m = fmaxf(m, __uint_as_float(cmax[nonsal[i]]));
+    m = wave_max(m);
+    if (lane == 0) lc_red[0][wave] = m;
+    __syncthreads();
+    m = 0.f;
+    for (int w = 0; w < NW; ++w) m = fmaxf(m, lc_red[0][w]);
+    const uint32_t mb = (uint32_t)__builtin_bit_cast(uint16_t, DT::from_f(m));
+    tens = pair_scale<DT>(mb | (mb << 16), q_max);
+  }
+  __syncthreads();
+
   for (; rp < npair; rp += gridDim.x) {
     const int m0 = 2 * rp;
     const bool has1 = m0 + 1 < M;
+    // ---- this thread's RPL table entries (L1/L2-resident, padded to whole rounds with
+    // (W, W + 1) entries), issued first so their latency overlaps the interleave
+    uint32_t tab[RPL];
+    int toff = rb;
+    asm volatile("" : "+v"(toff));  // re-read per pair (no loop-invariant hoisting)
+#pragma unroll
+    for (int i = 0; i < RPL / 4; ++i) {
+      const u32x4 e = ((const u32x4*)(lctab + toff))[i];
+      tab[4 * i] = e[0]; tab[4 * i + 1] = e[1]; tab[4 * i + 2] = e[2]; tab[4 * i + 3] = e[3];
+    }
     // ---- interleave the two rows into LDS: word k = (x[m0][k], x[m0+1][k])
 #pragma unroll
     for (int i = 0; i < LC_CH; ++i) {
@@ -200,16 +228,7 @@ __global__ __launch_bounds__(1024) void quant_lc_kernel(
     }
     __syncthreads();
 
-    // ---- this thread's RPL table entries (L1/L2-resident, padded to whole rounds with
-    // (W, W + 1) entries), gather; exact salient columns into the tail (>= K)
-    uint32_t tab[RPL];
-    int toff = rb;
-    asm volatile("" : "+v"(toff));  // re-read per pair (no loop-invariant hoisting)
-#pragma unroll
-    for (int i = 0; i < RPL / 4; ++i) {
-      const u32x4 e = ((const u32x4*)(lctab + toff))[i];
-      tab[4 * i] = e[0]; tab[4 * i + 1] = e[1]; tab[4 * i + 2] = e[2]; tab[4 * i + 3] = e[3];
-    }
+    // ---- gather; exact salient columns into the tail (>= K)
     uint32_t v[RPL];
 #pragma unroll
     for (int i = 0; i < RPL; ++i) v[i] = lc_buf[tab[i] & 0xFFFFu];
@@ -298,7 +317,7 @@ template <class DT, int MODE, int GS>
 static int quant_lc_launch(const void* x, int M, int K, int q_max, int G, const uint32_t* lctab,
                            int Kn, const int32_t* amap, int P, const int32_t* sal, int S,
                            int S_pad, const uint32_t* cmax, const int32_t* nonsal, void* out,
-                           hipStream_t s) {
+                           uint32_t* key_clear, int clear_words, hipStream_t s) {
   typedef typename DT::T T;
   const int nw = lc_waves(K, Kn);
   const size_t lds = sizeof(uint32_t) * (size_t)(P + S_pad + 8);
@@ -311,7 +330,8 @@ static int quant_lc_launch(const void* x, int M, int K, int q_max, int G, const 
   const int npair = (M + 1) / 2;
   if (grid > npair) grid = npair;
   quant_lc_kernel<DT, MODE, LC_RPL, GS><<<dim3(grid), dim3(64 * nw), lds, s>>>(
-      (const T*)x, M, K, q_max, G, lctab, Kn, amap, P, sal, S, S_pad, cmax, nonsal, (T*)out);
+      (const T*)x, M, K, q_max, G, lctab, Kn, amap, P, sal, S, S_pad, cmax, nonsal, (T*)out,
+      key_clear, clear_words);
   SQMP_LAUNCH_CHECK();
   return SQMP_OK;
 }
@@ -333,10 +353,11 @@ bool quant_lc_supported(int dtype, int M, int K, int amode_group, int G, int Kn,
 int launch_quant_lc(int dtype, int mode, const void* x, int M, int K, int q_max, int G,
                     const uint32_t* lctab, int Kn, const int32_t* amap, int P,
                     const int32_t* sal, int S, int S_pad, const uint32_t* cmax,
-                    const int32_t* nonsal, void* out, hipStream_t s) {
+                    const int32_t* nonsal, void* out, uint32_t* key_clear, int clear_words,
+                    hipStream_t s) {
 #define SQMP_LC(DTT, MD, GSV)                                                            \
   quant_lc_launch<DTT, MD, GSV>(x, M, K, q_max, G, lctab, Kn, amap, P, sal, S, S_pad, cmax, \
-                                nonsal, out, s)
+                                nonsal, out, key_clear, clear_words, s)
 #define SQMP_LC_MODE(DTT)                                           \
   (mode == LC_MODE_TOKEN ? SQMP_LC(DTT, LC_MODE_TOKEN, 0)            \
    : mode == LC_MODE_TENSOR ? SQMP_LC(DTT, LC_MODE_TENSOR, 0)        \

@@ -351,7 +351,10 @@ __global__ __launch_bounds__(512, 1) void gemm_fq6_kernel(
   // 32-column dense stages: 4 lanes per 64-B row piece, chunks swizzled by (row >> 2) & 3
   const int drow = 16 * wave + (lane >> 2);
   const int dchunk = (lane & 3) ^ d_f((lane >> 4) & 3);
-  const uint32_t ad_off = (uint32_t)((size_t)(m0 + drow) * lda * sizeof(T) + dchunk * 16);
+  // TM = 64: the op's upper 64 rows repeat the tile's (unused there) -- never past the
+  // tile, whose rows the operand's roundup(M, 256) allocation covers
+  const int darow = TM == 64 ? (drow & 63) : drow;
+  const uint32_t ad_off = (uint32_t)((size_t)(m0 + darow) * lda * sizeof(T) + dchunk * 16);
   const uint32_t ad_str = (uint32_t)(128 * (size_t)lda * sizeof(T));
   const uint32_t bd_row0 = (uint32_t)min(n0 + drow, N - 1);
   const uint32_t bd_row1 = (uint32_t)min(n0 + drow + 128, N - 1);

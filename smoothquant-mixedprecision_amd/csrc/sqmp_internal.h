@@ -42,7 +42,8 @@ bool quant_lc_supported(int dtype, int M, int K, int amode_group, int G, int Kn,
 int launch_quant_lc(int dtype, int mode, const void* x, int M, int K, int q_max, int G,
                     const uint32_t* lctab, int Kn, const int32_t* amap, int P,
                     const int32_t* sal, int S, int S_pad, const uint32_t* cmax,
-                    const int32_t* nonsal, void* out, hipStream_t s);
+                    const int32_t* nonsal, void* out, uint32_t* key_clear, int clear_words,
+                    hipStream_t s);  // key_clear: zeroed (clear_words % 4 == 0), may be NULL
 
 // Fast GEMMs (sqmp_gemm_fast.hip); SQMP_EUNSUPPORTED when the shape has no fast kernel.
 int launch_gemm_fq_fast(int dtype, const void* a, const void* codes, const void* wscale,

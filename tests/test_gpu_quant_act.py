@@ -102,3 +102,42 @@ def test_sibling_layers_share_statistics(act):
     x.mul_(-0.5).add_(0.25)
     y1 = layers[1](x)
     assert torch.equal(y1, layers[1](x.clone()))
+
+
+TIE_CASES = [
+    # M, K, dtype, salient_prop  (list lengths select every sort-table block shape)
+    (4, 1024, "fp16", 0.0), (3, 2048, "bf16", 0.05), (4, 4096, "fp16", 0.05),
+    (2, 8192, "bf16", 0.05), (5, 11008, "fp16", 0.05), (2, 16384, "fp16", 0.02),
+]
+
+
+@pytest.mark.parametrize("case", TIE_CASES, ids=[f"{c[0]}x{c[1]}-{c[2]}-p{c[3]}" for c in TIE_CASES])
+def test_sorted_groups_tie_order(case):
+    """Small-integer activations over few rows: most column maxima tie, so the group
+    assignment depends on the stable tie rule of the reference's argsort (fake_quant.py:113,
+    equal keys keep column order).  Bit-exact A operand against the oracle."""
+    dev = _dev()
+    from smoothquant import ops
+    from smoothquant.fake_quant import W4A4Linear
+    M, K, dtn, p = case
+    dt = O.DT(dtn)
+    g = np.random.default_rng(K + M)
+    x = dt.rnd(np.round(g.standard_normal((M, K)) * 2.0).astype(np.float32))
+    x[:, g.permutation(K)[:8]] = 0.0
+    imp = (np.abs(x).mean(0) + g.random(K) * 1e-3).astype(np.float32)
+    lin = torch.nn.Linear(K, 128, bias=False).to(dev, TORCH_DT[dtn])
+    q = W4A4Linear.from_float(lin, weight_quant="per_group", act_quant="per_group",
+                              importance=torch.from_numpy(imp), salient_prop=p, group_size=64)
+    pw = q.packed()
+    a = ops.quant_act_fp(torch.from_numpy(x).to(dev, TORCH_DT[dtn]), pw, "per_group", 4, 64)
+    a = a.float().cpu().numpy()
+    sal = O.select_salient(imp, p)
+    qx = O.quantize_input(x, "per_group", 4, 64, sal, dt)
+    amap = pw.amap.cpu().numpy()
+    want = np.zeros_like(a)
+    v = amap >= 0
+    want[:, :pw.Kp][:, v] = qx[:, amap[v]]
+    if sal is not None:
+        want[:, pw.Kp:pw.Kp + pw.S] = qx[:, sal]
+    bad = np.argwhere(_bits(a, dtn) != _bits(want, dtn))
+    assert len(bad) == 0, f"{len(bad)} of {a.size} differ; first {bad[:5].tolist()}"
