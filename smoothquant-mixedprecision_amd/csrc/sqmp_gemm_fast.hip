@@ -40,7 +40,21 @@ __device__ inline void vm_wait() {
 }
 __device__ inline void raw_barrier() {
   __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");  // no LDS read moves above the barrier
   __builtin_amdgcn_sched_barrier(0);
+}
+
+// LDS-DMA of 16 B per lane (LDS destination = wave-uniform base + 16 * lane) issued from
+// inline asm.  Through the builtin, hipcc (ROCm 7.2) models the pending DMA as an LDS
+// write and then waits lgkmcnt(0) before EVERY ds_read that follows in the k-loop instead
+// of the counted lgkmcnt(N) of the A-fragment read-ahead (measured: 14 full drains per
+// 64 MFMAs).  The asm form is invisible to that analysis, so every kernel using it waits
+// for its DMAs itself (vm_wait) and never relies on __syncthreads() to drain them.
+__device__ inline void glds16a(const void* src, unsigned char* lds_dst) {
+  const uint32_t m0v = __builtin_amdgcn_readfirstlane(
+      (uint32_t)(size_t)(__attribute__((address_space(3))) unsigned char*)lds_dst);
+  asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(m0v), "v"(src)
+               : "memory", "m0");
 }
 
 // ----------------------------------------------------------------- LDS ring geometry
@@ -368,38 +382,38 @@ __global__ __launch_bounds__(512, 1) void gemm_fq6_kernel(
     if (kt < nkm) {
       const unsigned char* ab = (const unsigned char*)A + (size_t)kt * 64 * sizeof(T);
 #pragma unroll
-      for (int i = 0; i < NA; ++i) glds16(ab + (size_t)i * a_str + a_off, slot + (i * 8 + wave) * 1024);
-      glds16((const unsigned char*)Bw + (size_t)kt * 32 + b_off, slot + F5_A + wave * 1024);
+      for (int i = 0; i < NA; ++i) glds16a(ab + (size_t)i * a_str + a_off, slot + (i * 8 + wave) * 1024);
+      glds16a((const unsigned char*)Bw + (size_t)kt * 32 + b_off, slot + F5_A + wave * 1024);
       const int g0 = GB == 1 ? (kt * 64) / Gw : kt * 2;
       const int g = min(g0 + s_u, ngw - 1);
       // only the lanes that carry distinct scales move bytes (GBn groups x CW columns);
       // the instruction still issues once per wave, so the vmcnt counts stay the same
       if (SCALE_PRED == 0 || lane < GBn * LPG)
-        glds16((const unsigned char*)wscale + (size_t)g * Np * sizeof(T) + s_off,
+        glds16a((const unsigned char*)wscale + (size_t)g * Np * sizeof(T) + s_off,
                slot + F5_A + F5_B + wave * 1024);
     } else if (DW == 64) {
       const int col = nkm * 64 + (kt - nkm) * 64;
       const unsigned char* ab = (const unsigned char*)A + (size_t)col * sizeof(T);
-      glds16(ab + a_off, slot + wave * 1024);
-      glds16(ab + a_str + a_off, slot + (8 + wave) * 1024);
+      glds16a(ab + a_off, slot + wave * 1024);
+      glds16a(ab + a_str + a_off, slot + (8 + wave) * 1024);
       const bool main = col < Kp;
       const unsigned char* bb = main ? (const unsigned char*)Bw : (const unsigned char*)wsal;
       const uint32_t ldb = main ? (uint32_t)Kp : (uint32_t)S_pad;
       const unsigned char* bc = bb + (size_t)(main ? col : col - Kp) * sizeof(T) + lchunk;
 #pragma unroll
       for (int i = 0; i < 4; ++i)
-        glds16(bc + (size_t)bd_row[i] * ldb * sizeof(T), slot + F5_DN + (i * 8 + wave) * 1024);
+        glds16a(bc + (size_t)bd_row[i] * ldb * sizeof(T), slot + F5_DN + (i * 8 + wave) * 1024);
     } else {
       const int col = nkm * 64 + (kt - nkm) * 32;
       const unsigned char* ab = (const unsigned char*)A + (size_t)col * sizeof(T);
-      glds16(ab + ad_off, slot + wave * 1024);
-      if (NAD == 2) glds16(ab + ad_str + ad_off, slot + (8 + wave) * 1024);
+      glds16a(ab + ad_off, slot + wave * 1024);
+      if (NAD == 2) glds16a(ab + ad_str + ad_off, slot + (8 + wave) * 1024);
       const bool main = col < Kp;
       const unsigned char* bb = main ? (const unsigned char*)Bw : (const unsigned char*)wsal;
       const uint32_t ldb = main ? (uint32_t)Kp : (uint32_t)S_pad;
       const uint32_t c0 = (uint32_t)(main ? col : col - Kp) * sizeof(T) + dchunk * 16;
-      glds16(bb + bd_row0 * ldb * sizeof(T) + c0, slot + F5_DB + wave * 1024);
-      glds16(bb + bd_row1 * ldb * sizeof(T) + c0, slot + F5_DB + (8 + wave) * 1024);
+      glds16a(bb + bd_row0 * ldb * sizeof(T) + c0, slot + F5_DB + wave * 1024);
+      glds16a(bb + bd_row1 * ldb * sizeof(T) + c0, slot + F5_DB + (8 + wave) * 1024);
     }
   };
 

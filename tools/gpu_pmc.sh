@@ -15,6 +15,7 @@ for name in $P; do
     *_b) C="SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_WAIT_ANY SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE" ;;
     *_c) C="FETCH_SIZE" ;;
     *_d) C="WRITE_SIZE TCC_HIT_sum TCC_MISS_sum" ;;
+    *_e) C="SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT SQ_INSTS_SALU SQ_WAIT_INST_LDS SQ_INST_CYCLES_VMEM SQ_BUSY_CU_CYCLES" ;;
   esac
   KIND=${name%%_*} run $name $C || exit 1
 done
