@@ -319,7 +319,7 @@ __global__ __launch_bounds__(512, 1) void gemm_fq5_kernel(
 // PRIO (tuning knob): 0 none; 1 = one s_setprio 1 for the younger half (waves 4-7) before
 // the main loop; 2 = s_setprio 1 / 0 around each stage's compute (MI355X guide T5).
 // WM = waves along M (1: 1 x 8 waves of TM x 32; 2: 2 x 4 waves of TM/2 x 64).
-template <class DT, int GB, int TM, int PRIO = 0, int WM = 1, int SCALE_PRED = 0>
+template <class DT, int GB, int TM, int PRIO = 0, int WM = 1, int PF = 3>
 __global__ __launch_bounds__(512, 1) void gemm_fq6_kernel(
     const typename DT::T* __restrict__ A, const void* __restrict__ Bw,
     const typename DT::T* __restrict__ wscale, const typename DT::T* __restrict__ wsal,
@@ -339,8 +339,6 @@ __global__ __launch_bounds__(512, 1) void gemm_fq6_kernel(
   constexpr int NAD = DW == 64 ? 2 : (TM == 256 ? 2 : 1);
   constexpr int VM_CODES = NA + 1 + 1, VM_DENSE = DW == 64 ? 2 + 4 : NAD + 2;
   constexpr int GBn = GB > 0 ? GB : 1;
-  constexpr int LPG = CW / 8;
-  constexpr int PF = 3;
   __shared__ __attribute__((aligned(16))) unsigned char lds[F5_NSLOT * F5_SLOT];
 
   int tm, tn;
@@ -374,23 +372,25 @@ __global__ __launch_bounds__(512, 1) void gemm_fq6_kernel(
   const uint32_t bd_row1 = (uint32_t)min(n0 + drow + 128, N - 1);
   const uint32_t b_off = (uint32_t)((size_t)(n0 + 32 * wave + (lane >> 1)) * (Kp / 2) +
                                     (((lane & 1) ^ ((lane >> 4) & 1)) << 4));
+  constexpr int LPG = CW / 8;  // scale-DMA lanes per group (8 scales per lane)
   const int s_u = min(lane / LPG, GBn - 1);
   const uint32_t s_off = (uint32_t)((n0 + CW * wn + (lane % LPG) * 8) * sizeof(T));
 
   auto issue = [&](int kt) {
     unsigned char* slot = lds + (kt % F5_NSLOT) * F5_SLOT;
     if (kt < nkm) {
-      const unsigned char* ab = (const unsigned char*)A + (size_t)kt * 64 * sizeof(T);
+      // PRIO 6 (diagnostic): every codes stage re-reads stage 0's bytes (L2-resident)
+      const int ks = PRIO == 6 ? 0 : kt;
+      const unsigned char* ab = (const unsigned char*)A + (size_t)ks * 64 * sizeof(T);
 #pragma unroll
       for (int i = 0; i < NA; ++i) glds16a(ab + (size_t)i * a_str + a_off, slot + (i * 8 + wave) * 1024);
-      glds16a((const unsigned char*)Bw + (size_t)kt * 32 + b_off, slot + F5_A + wave * 1024);
+      glds16a((const unsigned char*)Bw + (size_t)ks * 32 + b_off, slot + F5_A + wave * 1024);
       const int g0 = GB == 1 ? (kt * 64) / Gw : kt * 2;
       const int g = min(g0 + s_u, ngw - 1);
-      // only the lanes that carry distinct scales move bytes (GBn groups x CW columns);
-      // the instruction still issues once per wave, so the vmcnt counts stay the same
-      if (SCALE_PRED == 0 || lane < GBn * LPG)
-        glds16a((const unsigned char*)wscale + (size_t)g * Np * sizeof(T) + s_off,
-               slot + F5_A + F5_B + wave * 1024);
+      // GBn groups x CW columns of scales (the other lanes repeat them: same lines; one
+      // wave moving all 256 columns instead measured no faster)
+      glds16a((const unsigned char*)wscale + (size_t)g * Np * sizeof(T) + s_off,
+              slot + F5_A + F5_B + wave * 1024);
     } else if (DW == 64) {
       const int col = nkm * 64 + (kt - nkm) * 64;
       const unsigned char* ab = (const unsigned char*)A + (size_t)col * sizeof(T);
@@ -514,28 +514,33 @@ __global__ __launch_bounds__(512, 1) void gemm_fq6_kernel(
     }
   };
 
+  // PRIO 4 / 5 are timing diagnostics (garbage results, in-bounds addresses): 4 keeps
+  // the DMA but skips every wait on it, 5 moves no bytes after the first two stages.
+  constexpr bool DIAG_NOWAIT = PRIO == 4 || PRIO == 5;
   issue(0);
   if (nkt > 1) issue(1);
   if (PRIO == 1 && wave >= 4) __builtin_amdgcn_s_setprio(1);
   int kt = 0;
   for (; kt < nkm; ++kt) {
-    if (kt + 1 < nkt) {
+    if (DIAG_NOWAIT && kt >= 2) {
+    } else if (kt + 1 < nkt) {
       if (kt + 1 < nkm) vm_wait<VM_CODES>();
       else vm_wait<VM_DENSE>();
     } else {
       vm_wait<0>();
     }
     raw_barrier();
-    if (kt + 2 < nkt) issue(kt + 2);
+    if (kt + 2 < nkt && PRIO != 5) issue(kt + 2);
     if (PRIO == 2) __builtin_amdgcn_s_setprio(1);
     compute_codes(lds + (kt % F5_NSLOT) * F5_SLOT);
     if (PRIO == 2) __builtin_amdgcn_s_setprio(0);
   }
   for (; kt < nkt; ++kt) {
-    if (kt + 1 < nkt) vm_wait<VM_DENSE>();
+    if (DIAG_NOWAIT && kt + 1 < nkt) {
+    } else if (kt + 1 < nkt) vm_wait<VM_DENSE>();
     else vm_wait<0>();
     raw_barrier();
-    if (kt + 2 < nkt) issue(kt + 2);
+    if (kt + 2 < nkt && PRIO != 5) issue(kt + 2);
     unsigned char* slot = lds + (kt % F5_NSLOT) * F5_SLOT;
     if (PRIO == 2) __builtin_amdgcn_s_setprio(1);
     if constexpr (DW == 64)
@@ -833,8 +838,11 @@ static int fq6_launch(const void* a, const void* codes, const void* wscale, cons
   if (done) {
   } else if (pr == 1) SQMP_FQ6_L(1, 1);
   else if (pr == 2) SQMP_FQ6_L(2, 1);
-  else if (pr == 3)  // diagnostic: every lane moves a (duplicate) scale chunk
-    gemm_fq6_kernel<DT, GB, TM, 0, 1, 0><<<dim3(tiles_m * tiles_n), dim3(512), 0, s>>>(
+  else if (pr == 4) SQMP_FQ6_L(4, 1);  // diagnostics (wrong results): no DMA waits
+  else if (pr == 5) SQMP_FQ6_L(5, 1);  // ... no DMA after the first two stages
+  else if (pr == 6) SQMP_FQ6_L(6, 1);  // ... codes stages re-read stage 0 (L2 hits)
+  else if (pr == 3)  // A-fragment read-ahead of 5 blocks (tuning)
+    gemm_fq6_kernel<DT, GB, TM, 0, 1, 5><<<dim3(tiles_m * tiles_n), dim3(512), 0, s>>>(
         (const T*)a, codes, (const T*)wscale, (const T*)wsal, (const T*)bias, (T*)y, M, N, Kp,
         S_pad, Gw, ngw, tiles_m, tiles_n);
   else SQMP_FQ6_L(0, 1);
