@@ -33,7 +33,7 @@
  *             8-bit weights: int8 [N][Kp] row-major.  Salient columns and padding hold 0.
  *   wscale    D [ngw][Np]: per-(group, row) scale; group of position p is p / Gw.
  *   wsal      D [N][S_pad]: the salient weight columns, exact (fake_quant.py:363-365),
- *             in salient_indices order, zero padded to S_pad (multiple of 128).
+ *             in salient_indices order, zero padded to S_pad (multiple of 64).
  *   perm      int32 [Kp]: original column at packed position p, -1 for padding.
  *   amap      int32 [Kp]: perm with salient columns replaced by -1 (GEMM A-operand map).
  *   amap_fq   int32 [K]:  k, or -2 for salient k (in-place output-quant map).

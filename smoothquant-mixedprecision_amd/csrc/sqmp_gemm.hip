@@ -204,7 +204,7 @@ using namespace sqmp;
 static int check_gemm_geometry(int dtype, int M, int N, int Kp, int S_pad, int Gw, int ngw,
                                int n_bits) {
   if (dtype < SQMP_F32 || dtype > SQMP_BF16 || M < 0 || N <= 0) return SQMP_EINVAL;
-  if (Kp <= 0 || Kp % 128 != 0 || S_pad < 0 || S_pad % 128 != 0) return SQMP_EINVAL;
+  if (Kp <= 0 || Kp % 128 != 0 || S_pad < 0 || S_pad % 64 != 0) return SQMP_EINVAL;
   if (n_bits == 0) return SQMP_OK;  // dense operand: no groups
   if (Gw <= 0 || ngw <= 0 || (long)(ngw - 1) * Gw >= Kp) return SQMP_EINVAL;
   if (n_bits != 4 && n_bits != 8) return SQMP_EUNSUPPORTED;

@@ -589,15 +589,21 @@ __global__ __launch_bounds__(512, 1) void gemm_fq6_kernel(
 // 64-code block) reads chunk 4 t + q; the activation codes were written in the K order
 // that matches unpack_i8 of the bpack dword pair of lane group q.
 struct StageA256 {
-  uint32_t off, stride16;
+  uint32_t off, off_half, stride16;
   __device__ inline void init(int m0, size_t lda_b, int wave, int lane) {
     const int rin = 4 * wave + (lane >> 4);
-    off = (uint32_t)((size_t)(m0 + rin) * lda_b + (((lane & 15) ^ (rin & 15)) << 4));
+    const int c = (lane & 15) ^ (rin & 15);
+    off = (uint32_t)((size_t)(m0 + rin) * lda_b + (c << 4));
+    // a half stage (the last 64 salient columns when S_pad % 128 == 64): the upper 8
+    // chunks re-read the lower ones (in bounds; those sub-steps are skipped)
+    off_half = (uint32_t)((size_t)(m0 + rin) * lda_b + ((c & 7) << 4));
     stride16 = (uint32_t)(16 * lda_b);
   }
-  __device__ inline void issue(const unsigned char* base, unsigned char* st, int wave) const {
+  __device__ inline void issue(const unsigned char* base, unsigned char* st, int wave,
+                               bool half = false) const {
+    const uint32_t o = half ? off_half : off;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) glds16(base + (size_t)i * stride16 + off, st + (i * 4 + wave) * 1024);
+    for (int i = 0; i < 8; ++i) glds16(base + (size_t)i * stride16 + o, st + (i * 4 + wave) * 1024);
   }
 };
 
@@ -624,7 +630,8 @@ __global__ __launch_bounds__(256, 1) void gemm_i8v2_kernel(
   const int wm = wave >> 1, wn = wave & 1;
   const int r16 = lane & 15, q = lane >> 4;
   const int nkm = (Kp + 255) / 256;    // 256-code stages (the last may be partial)
-  const int nks = S_pad / 128;         // 128-element salient stages
+  const int nks = (S_pad + 127) / 128;  // 128-element salient stages (the last may be 64)
+  const bool tail_half = (S_pad & 127) != 0;
   const int nblk = Kp / 64;
   const int Np = pad_n(N);
 
@@ -729,14 +736,18 @@ __global__ __launch_bounds__(256, 1) void gemm_i8v2_kernel(
     StageA256 sx;
     sx.init(m0, (size_t)S_pad * sizeof(T), wave, lane);
     const unsigned char* Xb = (const unsigned char*)XS;
-    sx.issue(Xb, lds, wave);
+    sx.issue(Xb, lds, wave, tail_half && nks == 1);
     __syncthreads();
     for (int ks = 0; ks < nks; ++ks) {
       const int cur = ks & 1;
-      if (ks + 1 < nks) sx.issue(Xb + (size_t)(ks + 1) * 128 * sizeof(T), lds + (cur ^ 1) * ST, wave);
+      if (ks + 1 < nks)
+        sx.issue(Xb + (size_t)(ks + 1) * 128 * sizeof(T), lds + (cur ^ 1) * ST, wave,
+                 tail_half && ks + 2 == nks);
       const unsigned char* st = lds + cur * ST;
+      const int nsub = tail_half && ks + 1 == nks ? 2 : 4;
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
+        if (s >= nsub) break;
         u32x4 bf[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j)

@@ -231,7 +231,7 @@ extern "C" int sqmp_weight_geometry(int K, int S, int wmode, int group_size, int
   if (Kp) *Kp = kp;
   if (Gw) *Gw = gw;
   if (ngw) *ngw = ng;
-  if (S_pad) *S_pad = (int)round_up(S, 128);
+  if (S_pad) *S_pad = (int)round_up(S, 64);  // the GEMMs' dense stages are 32 / 64 wide
   return SQMP_OK;
 }
 

@@ -51,13 +51,14 @@ def _geom(lib, K, S, wmode, G):
 
 
 def test_weight_geometry(lib):
-    # per_group (sorted): groups over all K columns, padded to the 128-code K tile
-    assert _geom(lib, 4096, 409, 2, 128) == (0, (4096, 128, 32, 512))
-    assert _geom(lib, 11008, 550, 2, 64) == (0, (11008, 64, 172, 640))
+    # per_group (sorted): groups over all K columns, padded to the 128-code K tile; the
+    # salient tail padded to 64
+    assert _geom(lib, 4096, 409, 2, 128) == (0, (4096, 128, 32, 448))
+    assert _geom(lib, 11008, 550, 2, 64) == (0, (11008, 64, 172, 576))
     # G=1024 on K=11008: 11 groups, 256 zero-padding columns in the last (fake_quant.py:176-180)
     assert _geom(lib, 11008, 0, 2, 1024) == (0, (11264, 1024, 11, 0))
     # per_channel: one group spanning the padded row
-    assert _geom(lib, 160, 16, 0, 128) == (0, (256, 256, 1, 128))
+    assert _geom(lib, 160, 16, 0, 128) == (0, (256, 256, 1, 64))
     assert _geom(lib, 100, 0, 2, 32)[1] == (128, 32, 4, 0)
     assert _geom(lib, 0, 0, 2, 32)[0] == -1          # bad K
     assert _geom(lib, 64, 0, 7, 32)[0] == -1         # bad mode

@@ -10,7 +10,7 @@ cd $R
 timeout -k 10 400 python bench.py > $O/${TAG}_bench_per_group.json 2> $O/bench_pg.err || { tail -5 $O/bench_pg.err; exit 1; }
 timeout -k 10 400 python bench.py --act per_token > $O/${TAG}_bench_per_token.json 2> $O/bench_pt.err || { tail -5 $O/bench_pt.err; exit 1; }
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/ks -o run -- python $R/bench.py --no-cpu --steps 20 --warmup 5 > $O/ks.log 2>&1 || { tail -5 $O/ks.log; exit 1; }
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/ks -o run -- python $R/bench.py --no-cpu > $O/ks.log 2>&1 || { tail -5 $O/ks.log; exit 1; }
 for act in per_group per_token; do
   kind=fq
   timeout -k 10 240 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv -d $O/f_$act -o run -- python $R/tools/gemm_only.py fq 5 $act > $O/f_$act.log 2>&1 || { tail -5 $O/f_$act.log; exit 1; }
