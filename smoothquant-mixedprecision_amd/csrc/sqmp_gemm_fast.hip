@@ -57,6 +57,29 @@ __device__ inline void glds16a(const void* src, unsigned char* lds_dst) {
                : "memory", "m0");
 }
 
+// The same LDS-DMA through a buffer resource: 32-bit per-lane offset (constant across the
+// k-loop) + a scalar offset per stage, so issuing a piece costs no vector address math
+// and moves 4 address bytes per lane instead of 8.  num_records = 0xFFFFFFFF (no range
+// check; every offset stays inside the operand).
+typedef int i32x4r __attribute__((ext_vector_type(4)));
+__device__ inline i32x4r buf_rsrc(const void* base) {
+  const uint64_t a = (uint64_t)(size_t)base;
+  i32x4r r;
+  r[0] = (int)__builtin_amdgcn_readfirstlane((uint32_t)a);
+  r[1] = (int)__builtin_amdgcn_readfirstlane((uint32_t)(a >> 32) & 0xFFFFu);
+  r[2] = -1;
+  r[3] = 0x00020000;
+  return r;
+}
+__device__ inline void blds16(const i32x4r& rsrc, uint32_t voff, uint32_t soff,
+                              unsigned char* lds_dst) {
+  const uint32_t m0v = __builtin_amdgcn_readfirstlane(
+      (uint32_t)(size_t)(__attribute__((address_space(3))) unsigned char*)lds_dst);
+  asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds" ::"s"(m0v),
+               "v"(voff), "s"(rsrc), "s"(__builtin_amdgcn_readfirstlane(soff))
+               : "memory", "m0");
+}
+
 // ----------------------------------------------------------------- LDS ring geometry
 constexpr int F5_A = 32768;                      // 256 rows x 128 B
 constexpr int F5_B = 8192;                       // 256 rows x 32 B
@@ -355,65 +378,80 @@ __global__ __launch_bounds__(512, 1) void gemm_fq6_kernel(
 
   const int arow = 8 * wave + (lane >> 3);
   const uint32_t lchunk = (uint32_t)(bitrev3((lane & 7) ^ ((arow >> 1) & 7)) << 4);
-  const uint32_t a_off = (uint32_t)((size_t)(m0 + arow) * lda * sizeof(T)) + lchunk;
+  // buffer resources: A at the tile's first row, B codes at the tile's first weight row,
+  // scales at the tile's first column; dense-stage B by absolute (clamped) row
+  const i32x4r rA = buf_rsrc(A + (size_t)m0 * lda);
+  const i32x4r rB = buf_rsrc((const unsigned char*)Bw + (size_t)n0 * (Kp / 2));
+  const i32x4r rS = buf_rsrc(wscale + n0);
+  const i32x4r rBd = buf_rsrc(Bw);
+  const i32x4r rSal = buf_rsrc(wsal);
+  const uint32_t a_off = (uint32_t)((size_t)arow * lda * sizeof(T)) + lchunk;
   const uint32_t a_str = (uint32_t)(64 * (size_t)lda * sizeof(T));
-  uint32_t bd_row[4];  // 64-column dense-stage B rows of this lane (clamped: wsal has N rows)
+  // 64-column dense-stage B rows of this lane (clamped: wsal has N rows), for the salient
+  // tail (ldb = S_pad) and, dense weights only, the main stages (ldb = Kp)
+  uint32_t bd_tail[4], bd_main[4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) bd_row[i] = (uint32_t)min(n0 + arow + 64 * i, N - 1);
+  for (int i = 0; i < 4; ++i) {
+    const uint32_t r = (uint32_t)min(n0 + arow + 64 * i, N - 1);
+    bd_tail[i] = r * (uint32_t)S_pad * sizeof(T) + lchunk;
+    bd_main[i] = GB == 0 ? r * (uint32_t)Kp * sizeof(T) + lchunk : 0u;
+  }
   // 32-column dense stages: 4 lanes per 64-B row piece, chunks swizzled by (row >> 2) & 3
   const int drow = 16 * wave + (lane >> 2);
   const int dchunk = (lane & 3) ^ d_f((lane >> 4) & 3);
   // TM = 64: the op's upper 64 rows repeat the tile's (unused there) -- never past the
   // tile, whose rows the operand's roundup(M, 256) allocation covers
   const int darow = TM == 64 ? (drow & 63) : drow;
-  const uint32_t ad_off = (uint32_t)((size_t)(m0 + darow) * lda * sizeof(T) + dchunk * 16);
+  const uint32_t ad_off = (uint32_t)((size_t)darow * lda * sizeof(T) + dchunk * 16);
   const uint32_t ad_str = (uint32_t)(128 * (size_t)lda * sizeof(T));
-  const uint32_t bd_row0 = (uint32_t)min(n0 + drow, N - 1);
-  const uint32_t bd_row1 = (uint32_t)min(n0 + drow + 128, N - 1);
-  const uint32_t b_off = (uint32_t)((size_t)(n0 + 32 * wave + (lane >> 1)) * (Kp / 2) +
+  const uint32_t bd_r0 = (uint32_t)min(n0 + drow, N - 1), bd_r1 = (uint32_t)min(n0 + drow + 128, N - 1);
+  const uint32_t b32_tail0 = bd_r0 * (uint32_t)S_pad * sizeof(T) + dchunk * 16;
+  const uint32_t b32_tail1 = bd_r1 * (uint32_t)S_pad * sizeof(T) + dchunk * 16;
+  const uint32_t b32_main0 = GB == 0 ? bd_r0 * (uint32_t)Kp * sizeof(T) + dchunk * 16 : 0u;
+  const uint32_t b32_main1 = GB == 0 ? bd_r1 * (uint32_t)Kp * sizeof(T) + dchunk * 16 : 0u;
+  const uint32_t b_off = (uint32_t)((32 * wave + (lane >> 1)) * (Kp / 2) +
                                     (((lane & 1) ^ ((lane >> 4) & 1)) << 4));
   constexpr int LPG = CW / 8;  // scale-DMA lanes per group (8 scales per lane)
+  // lane's group within the block (GB = 2: groups 2 kt, 2 kt + 1) goes in the per-lane
+  // offset; the block's first group in the scalar one
   const int s_u = min(lane / LPG, GBn - 1);
-  const uint32_t s_off = (uint32_t)((n0 + CW * wn + (lane % LPG) * 8) * sizeof(T));
+  const uint32_t s_off = (uint32_t)((CW * wn + (lane % LPG) * 8 + s_u * Np) * sizeof(T));
 
   auto issue = [&](int kt) {
     unsigned char* slot = lds + (kt % F5_NSLOT) * F5_SLOT;
     if (kt < nkm) {
       // PRIO 6 (diagnostic): every codes stage re-reads stage 0's bytes (L2-resident)
       const int ks = PRIO == 6 ? 0 : kt;
-      const unsigned char* ab = (const unsigned char*)A + (size_t)ks * 64 * sizeof(T);
+      const uint32_t sa = (uint32_t)ks * 64 * sizeof(T);
 #pragma unroll
-      for (int i = 0; i < NA; ++i) glds16a(ab + (size_t)i * a_str + a_off, slot + (i * 8 + wave) * 1024);
-      glds16a((const unsigned char*)Bw + (size_t)ks * 32 + b_off, slot + F5_A + wave * 1024);
-      const int g0 = GB == 1 ? (kt * 64) / Gw : kt * 2;
-      const int g = min(g0 + s_u, ngw - 1);
+      for (int i = 0; i < NA; ++i)
+        if (PRIO != 8 || kt < 2) blds16(rA, a_off, sa + i * a_str, slot + (i * 8 + wave) * 1024);
+      blds16(rB, b_off, (uint32_t)ks * 32, slot + F5_A + wave * 1024);
+      // GB = 2 blocks hold groups 2 kt and 2 kt + 1 < ngw exactly
+      const int g0 = GB == 1 ? min((kt * 64) / Gw, ngw - 1) : kt * 2;
       // GBn groups x CW columns of scales (the other lanes repeat them: same lines; one
       // wave moving all 256 columns instead measured no faster)
-      glds16a((const unsigned char*)wscale + (size_t)g * Np * sizeof(T) + s_off,
-              slot + F5_A + F5_B + wave * 1024);
+      blds16(rS, s_off, (uint32_t)g0 * Np * sizeof(T), slot + F5_A + F5_B + wave * 1024);
     } else if (DW == 64) {
       const int col = nkm * 64 + (kt - nkm) * 64;
-      const unsigned char* ab = (const unsigned char*)A + (size_t)col * sizeof(T);
-      glds16a(ab + a_off, slot + wave * 1024);
-      glds16a(ab + a_str + a_off, slot + (8 + wave) * 1024);
-      const bool main = col < Kp;
-      const unsigned char* bb = main ? (const unsigned char*)Bw : (const unsigned char*)wsal;
-      const uint32_t ldb = main ? (uint32_t)Kp : (uint32_t)S_pad;
-      const unsigned char* bc = bb + (size_t)(main ? col : col - Kp) * sizeof(T) + lchunk;
+      const uint32_t sa = (uint32_t)col * sizeof(T);
+      blds16(rA, a_off, sa, slot + wave * 1024);
+      blds16(rA, a_off, sa + a_str, slot + (8 + wave) * 1024);
+      const bool main = GB == 0 && col < Kp;
+      const uint32_t sb = (uint32_t)(main ? col : col - Kp) * sizeof(T);
 #pragma unroll
       for (int i = 0; i < 4; ++i)
-        glds16a(bc + (size_t)bd_row[i] * ldb * sizeof(T), slot + F5_DN + (i * 8 + wave) * 1024);
+        blds16(main ? rBd : rSal, main ? bd_main[i] : bd_tail[i], sb,
+               slot + F5_DN + (i * 8 + wave) * 1024);
     } else {
       const int col = nkm * 64 + (kt - nkm) * 32;
-      const unsigned char* ab = (const unsigned char*)A + (size_t)col * sizeof(T);
-      glds16a(ab + ad_off, slot + wave * 1024);
-      if (NAD == 2) glds16a(ab + ad_str + ad_off, slot + (8 + wave) * 1024);
-      const bool main = col < Kp;
-      const unsigned char* bb = main ? (const unsigned char*)Bw : (const unsigned char*)wsal;
-      const uint32_t ldb = main ? (uint32_t)Kp : (uint32_t)S_pad;
-      const uint32_t c0 = (uint32_t)(main ? col : col - Kp) * sizeof(T) + dchunk * 16;
-      glds16a(bb + bd_row0 * ldb * sizeof(T) + c0, slot + F5_DB + wave * 1024);
-      glds16a(bb + bd_row1 * ldb * sizeof(T) + c0, slot + F5_DB + (8 + wave) * 1024);
+      const uint32_t sa = (uint32_t)col * sizeof(T);
+      blds16(rA, ad_off, sa, slot + wave * 1024);
+      if (NAD == 2) blds16(rA, ad_off, sa + ad_str, slot + (8 + wave) * 1024);
+      const bool main = GB == 0 && col < Kp;
+      const uint32_t sb = (uint32_t)(main ? col : col - Kp) * sizeof(T);
+      blds16(main ? rBd : rSal, main ? b32_main0 : b32_tail0, sb, slot + F5_DB + wave * 1024);
+      blds16(main ? rBd : rSal, main ? b32_main1 : b32_tail1, sb, slot + F5_DB + (8 + wave) * 1024);
     }
   };
 
@@ -516,7 +554,7 @@ __global__ __launch_bounds__(512, 1) void gemm_fq6_kernel(
 
   // PRIO 4 / 5 are timing diagnostics (garbage results, in-bounds addresses): 4 keeps
   // the DMA but skips every wait on it, 5 moves no bytes after the first two stages.
-  constexpr bool DIAG_NOWAIT = PRIO == 4 || PRIO == 5;
+  constexpr bool DIAG_NOWAIT = PRIO == 4 || PRIO == 5 || PRIO == 8;  // 8: no A DMA in the loop
   issue(0);
   if (nkt > 1) issue(1);
   if (PRIO == 1 && wave >= 4) __builtin_amdgcn_s_setprio(1);
@@ -852,6 +890,7 @@ static int fq6_launch(const void* a, const void* codes, const void* wscale, cons
   else if (pr == 4) SQMP_FQ6_L(4, 1);  // diagnostics (wrong results): no DMA waits
   else if (pr == 5) SQMP_FQ6_L(5, 1);  // ... no DMA after the first two stages
   else if (pr == 6) SQMP_FQ6_L(6, 1);  // ... codes stages re-read stage 0 (L2 hits)
+  else if (pr == 8) SQMP_FQ6_L(8, 1);  // ... codes stages move B and S only
   else if (pr == 3)  // A-fragment read-ahead of 5 blocks (tuning)
     gemm_fq6_kernel<DT, GB, TM, 0, 1, 5><<<dim3(tiles_m * tiles_n), dim3(512), 0, s>>>(
         (const T*)a, codes, (const T*)wscale, (const T*)wsal, (const T*)bias, (T*)y, M, N, Kp,
