@@ -89,8 +89,13 @@ enum sqmp_act_out {
   SQMP_OUT_I8 = 1,      /* out: int8 codes [M][roundup(Kp,256)] in the i8 GEMM's K order
                            (sqmp_actquant.hip); out_scale: fp32 [M] (the D scale);
                            out_xs: D [M][S_pad] exact salient x (operand of sqmp_gemm_i8) */
-  SQMP_OUT_INPLACE = 2  /* fake-quantize `x` in place through amap_fq (output quant,
+  SQMP_OUT_INPLACE = 2, /* fake-quantize `x` in place through amap_fq (output quant,
                            fake_quant.py:308-316) */
+  SQMP_OUT_F8 = 3       /* per_token / per_tensor, n_bits <= 4, sqmp_quant_act_v2 with
+                           posmap only: out = OCP e4m3 integer codes [M][Kp] (bytes) in
+                           packed order (0 at salient / padding positions); out_scale: fp32
+                           [M] (the D scale); out_xs: D [M][S_pad] exact salient x
+                           (operands of sqmp_gemm_f8) */
 };
 
 /* Library identity. */
@@ -181,6 +186,21 @@ int sqmp_gemm_i8(const int8_t* a8, const float* ascale, const void* xs,
                  const void* codes, const void* wscale, const void* wsal,
                  const void* bias, void* y, int dtype, int M, int N, int Kp, int S_pad,
                  int Gw, int ngw, int n_bits, void* stream);
+
+/* e4m3 operands of sqmp_gemm_f8 from a packed 4-bit weight: w8 = the int4 codes as OCP
+ * e4m3 bytes [Np][Kp] in packed order, ws32 = the D group scales as fp32 [ngw][Np]
+ * (Np = roundup(N, 256)).  Once per layer. */
+int sqmp_pack_f8(const void* codes, const void* wscale, int dtype, int N, int Kp, int ngw,
+                 void* w8, float* ws32, void* stream);
+
+/* Low-precision GEMM for per_token / per_tensor activations with 4-bit codes (operands of
+ * SQMP_OUT_F8 and sqmp_pack_f8): e4m3 codes x e4m3 codes on the block-scaled FP8 MFMA
+ * (exact integer block sums in fp32), per-weight-group fold, per-row act scale, exact
+ * salient tail on the D MFMA, bias, one rounding to D.  Gw % 64 == 0, fp16/bf16.
+ * a8 and xs: roundup(M, 256) rows allocated (operand allocation rule above). */
+int sqmp_gemm_f8(const void* a8, const float* ascale, const void* xs, const void* w8,
+                 const float* ws32, const void* wsal, const void* bias, void* y, int dtype,
+                 int M, int N, int Kp, int S_pad, int Gw, int ngw, void* stream);
 
 #ifdef __cplusplus
 }

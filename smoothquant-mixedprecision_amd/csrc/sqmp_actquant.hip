@@ -865,8 +865,14 @@ extern "C" int sqmp_quant_act_v2(void* x, int dtype, int M, int K, int amode, in
   if (flags & ~(SQMP_QA_CLEAN_WS | SQMP_QA_REUSE_STATS)) return SQMP_EINVAL;
   if (out_kind == SQMP_OUT_INPLACE) {
     if (Kp != K) return SQMP_EINVAL;
-  } else if (out_kind == SQMP_OUT_FP || out_kind == SQMP_OUT_I8) {
+  } else if (out_kind == SQMP_OUT_FP || out_kind == SQMP_OUT_I8 || out_kind == SQMP_OUT_F8) {
     if (Kp < K || Kp % 128 != 0 || S_pad < S || S_pad % 64 != 0 || !out) return SQMP_EINVAL;
+    if (out_kind == SQMP_OUT_F8) {
+      if (!out_scale || (S_pad > 0 && !out_xs)) return SQMP_EINVAL;
+      // e4m3 holds every integer code up to 16 exactly; one scale per row
+      if (n_bits > 4 || (amode != SQMP_ACT_PER_TOKEN && amode != SQMP_ACT_PER_TENSOR))
+        return SQMP_EUNSUPPORTED;
+    }
     if (S > 0 && !salient) return SQMP_EINVAL;
     if (out_kind == SQMP_OUT_I8 && (!out_scale || (S_pad > 0 && !out_xs))) return SQMP_EINVAL;
     if (out_kind == SQMP_OUT_I8 && n_bits > 8) return SQMP_EUNSUPPORTED;
@@ -940,6 +946,30 @@ extern "C" int sqmp_quant_act_v2(void* x, int dtype, int M, int K, int amode, in
     SQMP_LAUNCH_CHECK();
     return SQMP_OK;
   };
+
+  // e4m3 codes for the f8 GEMM (token / tensor scales): list-order table, lc quantizer
+  if (out_kind == SQMP_OUT_F8) {
+    if (!posmap || lc_off || !quant_lc_supported(dtype, M, K, false, 0, Kn, Kp, S_pad, x, out) ||
+        ((uintptr_t)out_xs) % 16 != 0)
+      return SQMP_EUNSUPPORTED;
+    if (amode == SQMP_ACT_PER_TENSOR) {
+      if (!clean) SQMP_HIP_CHECK(hipMemsetAsync(cmax, 0, sizeof(uint32_t) * k64, s));
+      st = launch_colmax(x, dtype, M, K, cmax, s, false);
+      if (st) return st;
+    }
+    const int nthr = K > Kn ? K : (Kn > 0 ? Kn : 1);
+    lc_table_kernel<<<dim3(cdiv(nthr, 256)), dim3(256), 0, s>>>(
+        TAB_LIST, nonsal, Kn, K, posmap, counts, colsorted, nullptr, lctab, lc_len, lc_none);
+    SQMP_LAUNCH_CHECK();
+    st = launch_quant_lc(dtype, amode == SQMP_ACT_PER_TENSOR ? 1 : 0, x, M, K, q_max, 1, lctab,
+                         Kn, amap, Kp, salient, S, S_pad, cmax, nonsal, out, nullptr, 0, s,
+                         (float*)out_scale, out_xs);
+    if (st) return st;
+    // the per-tensor maximum was read by every workgroup: clear it after the launch
+    if (clean && amode == SQMP_ACT_PER_TENSOR)
+      SQMP_HIP_CHECK(hipMemsetAsync(cmax, 0, sizeof(uint32_t) * k64, s));
+    return SQMP_OK;
+  }
 
   // fast path: the table maps ranks straight to packed positions (per-weight posmap)
   if (use_lc && posmap && amode != SQMP_ACT_PER_TENSOR) {

@@ -112,17 +112,55 @@ __device__ inline uint32_t quant_pair<BF16>(uint32_t v, const PairScale& c) {
   return __builtin_bit_cast(uint32_t, __builtin_convertvector(y, b16x2)) | (v & 0x80008000u);
 }
 
+// F8 output: the two rows' integer codes (the same D(x/s) and round-half-even as
+// quant_pair) as OCP e4m3 bytes, row m0 in byte 0, row m0 + 1 in byte 2 -- exact for
+// |code| <= 15, so every 4-bit code.
+template <class DT>
+__device__ inline uint32_t f8_pair(uint32_t v, const PairScale& c);
+
+template <>
+__device__ inline uint32_t f8_pair<F16>(uint32_t v, const PairScale& c) {
+  const f32x2 t = __builtin_convertvector(__builtin_bit_cast(h16x2, v), f32x2);
+  const f32x2 q0 = t * c.r;
+  const f32x2 e = __builtin_elementwise_fma(-q0, c.s, t);
+  const f32x2 q = __builtin_elementwise_fma(e, c.r, q0);
+  const h16x2 d = __builtin_convertvector(q, h16x2);
+  const h16x2 magic = {(_Float16)1536.0f, (_Float16)1536.0f};
+  const f32x2 code = __builtin_convertvector((d + magic) - magic, f32x2);
+  const int w = __builtin_amdgcn_cvt_pk_fp8_f32(code[0], 0.f, 0, false);
+  return (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(code[1], 0.f, w, true);
+}
+
+template <>
+__device__ inline uint32_t f8_pair<BF16>(uint32_t v, const PairScale& c) {
+  f32x2 t;
+  t[0] = __uint_as_float(v << 16);
+  t[1] = __uint_as_float(v & 0xFFFF0000u);
+  const f32x2 q0 = t * c.r;
+  const f32x2 e = __builtin_elementwise_fma(-q0, c.s, t);
+  const f32x2 q = __builtin_elementwise_fma(e, c.r, q0);
+  const uint32_t db = __builtin_bit_cast(uint32_t, __builtin_convertvector(q, b16x2));
+  f32x2 d;
+  d[0] = __uint_as_float(db << 16);
+  d[1] = __uint_as_float(db & 0xFFFF0000u);
+  const f32x2 code = __builtin_elementwise_roundeven(d);
+  const int w = __builtin_amdgcn_cvt_pk_fp8_f32(code[0], 0.f, 0, false);
+  return (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(code[1], 0.f, w, true);
+}
+
 }  // namespace
 
 // RPL = ranks per thread; GS = the group size when it is below RPL (RPL / GS groups per
-// thread), else 0.  blockDim = 64 * NW.
-template <class DT, int MODE, int RPL, int GS>
+// thread), else 0.  blockDim = 64 * NW.  F8 = 1 (token / tensor modes): out is e4m3 codes
+// [M][P] (bytes), out_scale the fp32 row scales, out_xs the exact salient columns [M][S_pad].
+template <class DT, int MODE, int RPL, int GS, int F8 = 0>
 __global__ __launch_bounds__(1024) void quant_lc_kernel(
     const typename DT::T* x, int M, int K, int q_max, int G,
     const uint32_t* __restrict__ lctab, int Kn, const int32_t* __restrict__ amap, int P,
     const int32_t* __restrict__ sal, int S, int S_pad, const uint32_t* __restrict__ cmax,
     const int32_t* __restrict__ nonsal, typename DT::T* out, uint32_t* __restrict__ key_clear,
-    int clear_words) {
+    int clear_words, float* __restrict__ out_scale, typename DT::T* __restrict__ out_xs) {
+  static_assert(!F8 || MODE != LC_MODE_GROUP, "F8 codes need one scale per row");
   // x and out alias for in-place output quantization (every row is read before it is
   // written: a workgroup stores a pair only after loading it)
   typedef typename DT::T T;
@@ -275,14 +313,64 @@ __global__ __launch_bounds__(1024) void quant_lc_kernel(
       } else {
         __syncthreads();
       }
+      if (F8) {
 #pragma unroll
-      for (int i = 0; i < RPL; ++i) lc_buf[tab[i] >> 16] = quant_pair<DT>(v[i], c);
+        for (int i = 0; i < RPL; ++i) lc_buf[tab[i] >> 16] = f8_pair<DT>(v[i], c);
+        if (tid == 0) {
+          out_scale[m0] = c.s[0];
+          if (has1) out_scale[m0 + 1] = c.s[1];
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < RPL; ++i) lc_buf[tab[i] >> 16] = quant_pair<DT>(v[i], c);
+      }
     }
     // salient columns' own packed positions hold 0 (their weight codes are 0 too)
     for (uint64_t zm = zmask; zm; zm &= zm - 1) lc_buf[zp0 + __builtin_ctzll(zm)] = 0u;
     if (rp + (int)gridDim.x < npair) load_pair(rp + gridDim.x);  // prefetch the next pair
     __syncthreads();
 
+    if (F8) {
+      // codes: 16 positions per chunk, byte 0 / byte 2 of each word -> rows m0 / m0 + 1
+      unsigned char* b0 = (unsigned char*)out + (size_t)m0 * P;
+      unsigned char* b1 = (unsigned char*)out + (size_t)(m0 + 1) * P;
+      for (int c = tid; c < P / 16; c += nthr) {
+        u32x4 y0, y1;
+#pragma unroll
+        for (int h = 0; h < 4; ++h) {
+          const u32x4 w = ((const u32x4*)lc_buf)[4 * c + h];
+          // v_perm_b32 selector bytes: 0-3 = lo operand, 4-7 = hi operand, 0x0c = 0x00
+          const uint32_t a0 = __builtin_amdgcn_perm(w[1], w[0], 0x0c0c0400u);
+          const uint32_t a1 = __builtin_amdgcn_perm(w[3], w[2], 0x04000c0cu);
+          const uint32_t c0 = __builtin_amdgcn_perm(w[1], w[0], 0x0c0c0602u);
+          const uint32_t c1 = __builtin_amdgcn_perm(w[3], w[2], 0x06020c0cu);
+          y0[h] = a0 | a1;
+          y1[h] = c0 | c1;
+        }
+        ((u32x4*)b0)[c] = y0;
+        if (has1) ((u32x4*)b1)[c] = y1;
+      }
+      // exact salient columns -> out_xs [M][S_pad]
+      T* x0 = out_xs + (size_t)m0 * S_pad;
+      T* x1 = out_xs + (size_t)(m0 + 1) * S_pad;
+      for (int c = tid; c < S_pad / 8; c += nthr) {
+        const u32x4 a = ((const u32x4*)lc_buf)[2 * (P / 8 + c)];
+        const u32x4 b = ((const u32x4*)lc_buf)[2 * (P / 8 + c) + 1];
+        u32x4 z0, z1;
+        z0[0] = __builtin_amdgcn_perm(a[1], a[0], 0x05040100u);
+        z0[1] = __builtin_amdgcn_perm(a[3], a[2], 0x05040100u);
+        z0[2] = __builtin_amdgcn_perm(b[1], b[0], 0x05040100u);
+        z0[3] = __builtin_amdgcn_perm(b[3], b[2], 0x05040100u);
+        z1[0] = __builtin_amdgcn_perm(a[1], a[0], 0x07060302u);
+        z1[1] = __builtin_amdgcn_perm(a[3], a[2], 0x07060302u);
+        z1[2] = __builtin_amdgcn_perm(b[1], b[0], 0x07060302u);
+        z1[3] = __builtin_amdgcn_perm(b[3], b[2], 0x07060302u);
+        ((u32x4*)x0)[c] = z0;
+        if (has1) ((u32x4*)x1)[c] = z1;
+      }
+      __syncthreads();  // the buffer is rewritten by the next pair
+      continue;
+    }
     // ---- de-interleave 16-B chunks and store both rows
     T* o0 = out + (size_t)m0 * W;
     T* o1 = out + (size_t)(m0 + 1) * W;
@@ -313,15 +401,16 @@ static int lc_waves(int K, int Kn) {
   return a > b ? a : b;
 }
 
-template <class DT, int MODE, int GS>
+template <class DT, int MODE, int GS, int F8>
 static int quant_lc_launch(const void* x, int M, int K, int q_max, int G, const uint32_t* lctab,
                            int Kn, const int32_t* amap, int P, const int32_t* sal, int S,
                            int S_pad, const uint32_t* cmax, const int32_t* nonsal, void* out,
-                           uint32_t* key_clear, int clear_words, hipStream_t s) {
+                           uint32_t* key_clear, int clear_words, float* out_scale,
+                           void* out_xs, hipStream_t s) {
   typedef typename DT::T T;
   const int nw = lc_waves(K, Kn);
   const size_t lds = sizeof(uint32_t) * (size_t)(P + S_pad + 8);
-  SQMP_HIP_CHECK(hipFuncSetAttribute((const void*)quant_lc_kernel<DT, MODE, LC_RPL, GS>,
+  SQMP_HIP_CHECK(hipFuncSetAttribute((const void*)quant_lc_kernel<DT, MODE, LC_RPL, GS, F8>,
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   int per_cu = (int)((150 * 1024) / lds);
   const int by_waves = 32 / nw;
@@ -329,9 +418,9 @@ static int quant_lc_launch(const void* x, int M, int K, int q_max, int G, const 
   int grid = 256 * per_cu;
   const int npair = (M + 1) / 2;
   if (grid > npair) grid = npair;
-  quant_lc_kernel<DT, MODE, LC_RPL, GS><<<dim3(grid), dim3(64 * nw), lds, s>>>(
+  quant_lc_kernel<DT, MODE, LC_RPL, GS, F8><<<dim3(grid), dim3(64 * nw), lds, s>>>(
       (const T*)x, M, K, q_max, G, lctab, Kn, amap, P, sal, S, S_pad, cmax, nonsal, (T*)out,
-      key_clear, clear_words);
+      key_clear, clear_words, out_scale, (T*)out_xs);
   SQMP_LAUNCH_CHECK();
   return SQMP_OK;
 }
@@ -354,14 +443,18 @@ int launch_quant_lc(int dtype, int mode, const void* x, int M, int K, int q_max,
                     const uint32_t* lctab, int Kn, const int32_t* amap, int P,
                     const int32_t* sal, int S, int S_pad, const uint32_t* cmax,
                     const int32_t* nonsal, void* out, uint32_t* key_clear, int clear_words,
-                    hipStream_t s) {
-#define SQMP_LC(DTT, MD, GSV)                                                            \
-  quant_lc_launch<DTT, MD, GSV>(x, M, K, q_max, G, lctab, Kn, amap, P, sal, S, S_pad, cmax, \
-                                nonsal, out, key_clear, clear_words, s)
-#define SQMP_LC_MODE(DTT)                                           \
-  (mode == LC_MODE_TOKEN ? SQMP_LC(DTT, LC_MODE_TOKEN, 0)            \
-   : mode == LC_MODE_TENSOR ? SQMP_LC(DTT, LC_MODE_TENSOR, 0)        \
-   : G < LC_RPL ? SQMP_LC(DTT, LC_MODE_GROUP, 8) : SQMP_LC(DTT, LC_MODE_GROUP, 0))
+                    hipStream_t s, float* out_scale, void* out_xs) {
+#define SQMP_LC(DTT, MD, GSV, F8V)                                                           \
+  quant_lc_launch<DTT, MD, GSV, F8V>(x, M, K, q_max, G, lctab, Kn, amap, P, sal, S, S_pad,   \
+                                     cmax, nonsal, out, key_clear, clear_words, out_scale,  \
+                                     out_xs, s)
+#define SQMP_LC_MODE(DTT)                                                                  \
+  (out_scale ? (mode == LC_MODE_TOKEN    ? SQMP_LC(DTT, LC_MODE_TOKEN, 0, 1)               \
+                : mode == LC_MODE_TENSOR ? SQMP_LC(DTT, LC_MODE_TENSOR, 0, 1)              \
+                                         : SQMP_EUNSUPPORTED)                              \
+   : mode == LC_MODE_TOKEN ? SQMP_LC(DTT, LC_MODE_TOKEN, 0, 0)                             \
+   : mode == LC_MODE_TENSOR ? SQMP_LC(DTT, LC_MODE_TENSOR, 0, 0)                           \
+   : G < LC_RPL ? SQMP_LC(DTT, LC_MODE_GROUP, 8, 0) : SQMP_LC(DTT, LC_MODE_GROUP, 0, 0))
   if (dtype == SQMP_F16) return SQMP_LC_MODE(F16);
   if (dtype == SQMP_BF16) return SQMP_LC_MODE(BF16);
   return SQMP_EUNSUPPORTED;

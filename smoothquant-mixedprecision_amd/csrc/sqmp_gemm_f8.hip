@@ -1,0 +1,334 @@
+// W4A4 GEMM for per_token / per_tensor activations on the block-scaled FP8 MFMA
+// (v_mfma_scale_f32_32x32x64_f8f6f4, e4m3 operands, unit block scales): the integer
+// contraction of fake_quant.py:306 for the activation modes whose scale is one per row
+// (:56-75), where x_hat[m,k] * W_hat[n,k] = sa[m] * ws[n,g(k)] * ca[m,k] * cw[n,k].
+//
+//   y[m][n] = D( sa[m] * sum_g ws[n][g] * (sum_{k in g} ca[m][k] cw[n][k])
+//               + sum_j xs[m][j] wsal[n][j] + bias[n] )
+//
+// Both code operands are small integers (|c| <= 7), exact in e4m3; each 64-position block
+// lies in one weight group (Gw % 64 == 0), so one MFMA per 32 x 32 tile and block gives
+// the exact integer block sum in fp32 and the fold tot += tmp * ws[n][g] is one fp32 FMA
+// per element (versus a convert + FMA per element on the i8 MFMA).  The e4m3 instruction
+// runs at twice the f16 MFMA rate.  The numerics differ from the reference's
+// F.linear(D(ca sa), D(cw ws)) only by the D() roundings of the two dequantized operands
+// (relative 2^-11 per element), as the i8 path.
+//
+// Tile 256 (m) x 256 (n) per 512-thread workgroup; 8 waves, wave w owns columns
+// [32 w, 32 w + 32) over all 256 rows (8 tiles of 32 x 32).  MFMA A = activation rows,
+// B = weight columns, so a lane's 16 results share one weight column (one scale per
+// fold).  K-stages: 64-position code blocks (A and B 256 rows x 64 B of e4m3), then the
+// exact salient tail in 32-column f16 stages (v_mfma_f32_32x32x16_f16, same 256 x 64 B
+// images) after the accumulators are scaled by sa.  Every stage moves 2 A + 2 B 1-KiB
+// LDS-DMA pieces per wave through buffer resources into a 4-slot ring (3 stages ahead);
+// wave 0 also moves the stage's 256 fp32 weight scales (code stages) or the tile's 256
+// row scales (first tail stage).  LDS rows are 64 B with 16-B chunk c of row r at
+// c ^ ((r >> 2) & 3): conflict-free for the ds_read_b128 lane groups.
+#include <stdlib.h>
+
+#include "sqmp_mfma.h"
+
+namespace sqmp {
+
+namespace {
+
+typedef int i32x4b __attribute__((ext_vector_type(4)));
+typedef int i32x8b __attribute__((ext_vector_type(8)));
+
+constexpr int F8_A = 0, F8_B = 16384, F8_S = 32768;
+constexpr int F8_SLOT = 33792;  // A 16 KiB + B 16 KiB + S 1 KiB
+constexpr int F8_NSLOT = 4;     // 135168 B of LDS
+
+__device__ inline i32x4b rsrc_of(const void* base, uint32_t nrec) {
+  const uint64_t a = (uint64_t)(size_t)base;
+  i32x4b r;
+  r[0] = (int)__builtin_amdgcn_readfirstlane((uint32_t)a);
+  r[1] = (int)__builtin_amdgcn_readfirstlane((uint32_t)(a >> 32) & 0xFFFFu);
+  r[2] = (int)nrec;
+  r[3] = 0x00020000;
+  return r;
+}
+
+// 16 B per lane to LDS (wave-uniform destination + 16 * lane), issued from asm so the
+// compiler's LDS wait analysis does not see a pending DMA (see sqmp_gemm_fast.hip).
+__device__ inline void dma16(const i32x4b& rsrc, uint32_t voff, uint32_t soff,
+                             unsigned char* lds_dst) {
+  const uint32_t m0v = __builtin_amdgcn_readfirstlane(
+      (uint32_t)(size_t)(__attribute__((address_space(3))) unsigned char*)lds_dst);
+  // s_nop 4: scalar operand fresh from v_readfirstlane -> buffer soffset / descriptor;
+  // s_nop 0: M0 write -> LDS-DMA (hazard table, MI355X asm guide §4.1)
+  asm volatile("s_nop 4\n\ts_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
+               ::"s"(m0v), "v"(voff), "s"(rsrc), "s"(__builtin_amdgcn_readfirstlane(soff))
+               : "memory", "m0");
+}
+
+template <int N>
+__device__ inline void vmw() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+__device__ inline int sw64(int r, int c) { return (r << 6) + (((c ^ (r >> 2)) & 3) << 4); }
+
+}  // namespace
+
+template <class DT>
+__global__ __launch_bounds__(512, 1) void gemm_f8_kernel(
+    const unsigned char* __restrict__ A8, const float* __restrict__ ascale,
+    const typename DT::T* __restrict__ XS, const unsigned char* __restrict__ W8,
+    const float* __restrict__ ws32, const typename DT::T* __restrict__ wsal,
+    const typename DT::T* __restrict__ bias, typename DT::T* __restrict__ Y, int M, int N,
+    int Kp, int S_pad, int Gw, int ngw, int tiles_m, int tiles_n) {
+  typedef typename DT::T T;
+  __shared__ __attribute__((aligned(16))) unsigned char lds[F8_NSLOT * F8_SLOT];
+
+  int tm, tn;
+  tile_coords(tiles_m, tiles_n, 4, tm, tn);
+  const int m0 = tm * 256, n0 = tn * 256;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int l32 = lane & 31, h = lane >> 5;
+  const int nk8 = Kp / 64, nkt = nk8 + S_pad / 32;
+  const int Np = pad_n(N);
+
+  // ---- DMA geometry: piece j of a wave covers rows 16 (2 wave + j) + (lane >> 2), the
+  // lane's physical chunk lane & 3 holds logical chunk (lane & 3) ^ ((row >> 2) & 3)
+  uint32_t va8[2], vw8[2], vxs[2], vsal[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int r = 16 * (2 * wave + j) + (lane >> 2);
+    const int c = ((lane & 3) ^ (r >> 2)) & 3;
+    va8[j] = (uint32_t)r * Kp + c * 16;
+    vw8[j] = (uint32_t)r * Kp + c * 16;
+    vxs[j] = (uint32_t)r * S_pad * sizeof(T) + c * 16;
+    vsal[j] = (uint32_t)min(n0 + r, N - 1) * S_pad * sizeof(T) + c * 16;
+  }
+  const i32x4b rA = rsrc_of(A8 + (size_t)m0 * Kp, 0xFFFFFFFFu);
+  const i32x4b rW = rsrc_of(W8 + (size_t)n0 * Kp, 0xFFFFFFFFu);
+  const i32x4b rX = rsrc_of(XS + (size_t)m0 * S_pad, 0xFFFFFFFFu);
+  const i32x4b rL = rsrc_of(wsal, 0xFFFFFFFFu);
+  const i32x4b rS = rsrc_of(ws32 + n0, 0xFFFFFFFFu);
+  // row scales of rows m0 .. m0 + 255 (range-checked: rows >= M read 0)
+  const i32x4b rR = rsrc_of(ascale + m0, (uint32_t)(M - m0) * 4u);
+
+  auto issue = [&](int kt) {
+    unsigned char* slot = lds + (kt % F8_NSLOT) * F8_SLOT;
+    if (kt < nk8) {
+      const uint32_t so = (uint32_t)kt * 64;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) dma16(rA, va8[j], so, slot + F8_A + (2 * wave + j) * 1024);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) dma16(rW, vw8[j], so, slot + F8_B + (2 * wave + j) * 1024);
+      if (wave == 0) {
+        const int g = min((kt * 64) / Gw, ngw - 1);
+        dma16(rS, (uint32_t)lane * 16, (uint32_t)g * Np * 4, slot + F8_S);
+      }
+    } else {
+      const uint32_t so = (uint32_t)(kt - nk8) * 32 * sizeof(T);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) dma16(rX, vxs[j], so, slot + F8_A + (2 * wave + j) * 1024);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) dma16(rL, vsal[j], so, slot + F8_B + (2 * wave + j) * 1024);
+      if (wave == 0) dma16(rR, (uint32_t)lane * 16, 0u, slot + F8_S);
+    }
+  };
+
+  f32x16 tot[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) tot[i][r] = 0.f;
+
+  const int brow = 32 * wave + l32;
+  // code stage: e4m3 A (rows 32 i + l32) x e4m3 B (column brow), k half h of the block
+  auto compute_f8 = [&](const unsigned char* __restrict__ slot) {
+    const float s = *(const float*)(slot + F8_S + brow * 4);
+    i32x8b b;
+    {
+      const u32x4 b0 = *(const u32x4*)(slot + F8_B + sw64(brow, 2 * h));
+      const u32x4 b1 = *(const u32x4*)(slot + F8_B + sw64(brow, 2 * h + 1));
+      b = i32x8b{(int)b0[0], (int)b0[1], (int)b0[2], (int)b0[3],
+                 (int)b1[0], (int)b1[1], (int)b1[2], (int)b1[3]};
+    }
+    const f32x16 zero = {};
+    auto ald = [&](int i) {
+      const int ar = 32 * i + l32;
+      const u32x4 a0 = *(const u32x4*)(slot + F8_A + sw64(ar, 2 * h));
+      const u32x4 a1 = *(const u32x4*)(slot + F8_A + sw64(ar, 2 * h + 1));
+      return i32x8b{(int)a0[0], (int)a0[1], (int)a0[2], (int)a0[3],
+                    (int)a1[0], (int)a1[1], (int)a1[2], (int)a1[3]};
+    };
+    // software pipeline: A fragments read two tiles ahead, the MFMA of tile i + 1 issued
+    // before the fold of tile i (which waits for its own MFMA's result); sched barriers
+    // keep that order (left alone, hipcc folds each tile right after its MFMA)
+    i32x8b a[2];
+    a[0] = ald(0);
+    a[1] = ald(1);
+    f32x16 t[2];
+    t[0] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a[0], b, zero, 0, 0, 0, 127, 0, 127);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      if (i + 1 < 8) {
+        const i32x8b an = a[(i + 1) & 1];
+        if (i + 2 < 8) a[i & 1] = ald(i + 2);
+        t[(i + 1) & 1] =
+            __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(an, b, zero, 0, 0, 0, 127, 0, 127);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) tot[i][r] = __builtin_fmaf(t[i & 1][r], s, tot[i][r]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  // first tail stage: scale the integer part by the row scales (rows 32 i + (r & 3) +
+  // 8 (r >> 2) + 4 h of the tile, from the stage's S image)
+  auto apply_row_scales = [&](const unsigned char* __restrict__ slot) {
+    const float* rs = (const float*)(slot + F8_S);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int r4 = 0; r4 < 4; ++r4) {
+        const f32x4 v = *(const f32x4*)(rs + 32 * i + 8 * r4 + 4 * h);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) tot[i][4 * r4 + e] *= v[e];
+      }
+  };
+  // tail stage: exact D salient columns, 32 per stage, on the 32x32x16 D MFMA
+  auto compute_tail = [&](const unsigned char* __restrict__ slot) {
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      const u32x4 b = *(const u32x4*)(slot + F8_B + sw64(brow, 2 * st + h));
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const u32x4 a = *(const u32x4*)(slot + F8_A + sw64(32 * i + l32, 2 * st + h));
+        Mfma32<DT>::run(tot[i], a, b);
+      }
+    }
+  };
+
+  // ---- 4-slot ring, 3 stages in flight; per stage and wave 4 DMA ops (+1 on wave 0)
+  const int npre = nkt < 3 ? nkt : 3;
+  for (int k = 0; k < npre; ++k) issue(k);
+  auto stage_top = [&](int kt) {
+    const int ahead = nkt - 1 - kt;  // stages issued after kt that may stay in flight
+    if (wave == 0) {
+      if (ahead >= 2) vmw<10>();
+      else if (ahead == 1) vmw<5>();
+      else vmw<0>();
+    } else {
+      if (ahead >= 2) vmw<8>();
+      else if (ahead == 1) vmw<4>();
+      else vmw<0>();
+    }
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    if (kt + 3 < nkt) issue(kt + 3);
+    return (const unsigned char*)(lds + (kt % F8_NSLOT) * F8_SLOT);
+  };
+  int kt = 0;
+  for (; kt < nk8; ++kt) compute_f8(stage_top(kt));
+  for (; kt < nkt; ++kt) {
+    const unsigned char* slot = stage_top(kt);
+    if (kt == nk8) apply_row_scales(slot);
+    compute_tail(slot);
+  }
+  if (nkt == nk8) {  // no salient tail: row scales straight from global memory
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int gm = m0 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;
+        tot[i][r] *= gm < M ? ascale[gm] : 0.f;
+      }
+  }
+
+  // ---- epilogue: lane = column n0 + brow, rows 32 i + (r & 3) + 8 (r >> 2) + 4 h
+  const int gn = n0 + brow;
+  if (gn >= N) return;
+  const float bv = bias ? DT::to_f(bias[gn]) : 0.f;
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int gm = m0 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;
+      if (gm < M) Y[(size_t)gm * N + gn] = DT::from_f(tot[i][r] + bv);
+    }
+}
+
+// bpack int4 codes -> e4m3 bytes [Np][Kp] (natural packed order), D scales -> fp32.
+template <class DT>
+__global__ __launch_bounds__(256) void pack_f8_kernel(const uint32_t* __restrict__ codes,
+                                                      const typename DT::T* __restrict__ wscale,
+                                                      int Np, int Kp, int ngw,
+                                                      uint32_t* __restrict__ w8,
+                                                      float* __restrict__ ws32) {
+  const size_t t = (size_t)blockIdx.x * 256 + threadIdx.x;
+  const size_t words = (size_t)Np * (Kp / 4);  // 4 output bytes per thread
+  if (t < words) {
+    const int n = (int)(t / (Kp / 4));
+    const int p0 = (int)(t % (Kp / 4)) * 4;
+    uint32_t out = 0;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int p = p0 + e;
+      const uint32_t wd = codes[(size_t)n * (Kp / 8) + bpack_dword(p)];
+      const int c = (int)((wd >> bpack_shift(p)) & 0xFu) - 8;
+      const uint32_t b = (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32((float)c, 0.f, 0, false) & 0xFFu;
+      out |= b << (8 * e);
+    }
+    w8[t] = out;
+  }
+  if (t < (size_t)ngw * Np) ws32[t] = DT::to_f(wscale[t]);
+}
+
+}  // namespace sqmp
+
+using namespace sqmp;
+
+extern "C" int sqmp_pack_f8(const void* codes, const void* wscale, int dtype, int N, int Kp,
+                            int ngw, void* w8, float* ws32, void* stream) {
+  if (!codes || !wscale || !w8 || !ws32 || N <= 0 || Kp <= 0 || Kp % 128 != 0 || ngw <= 0)
+    return SQMP_EINVAL;
+  if (dtype != SQMP_F16 && dtype != SQMP_BF16) return SQMP_EUNSUPPORTED;
+  hipStream_t s = (hipStream_t)stream;
+  const int Np = pad_n(N);
+  const size_t words = (size_t)Np * (Kp / 4);
+  const size_t n = words > (size_t)ngw * Np ? words : (size_t)ngw * Np;
+  const dim3 grid((unsigned)((n + 255) / 256));
+  if (dtype == SQMP_F16)
+    pack_f8_kernel<F16><<<grid, dim3(256), 0, s>>>((const uint32_t*)codes,
+                                                    (const F16::T*)wscale, Np, Kp, ngw,
+                                                    (uint32_t*)w8, ws32);
+  else
+    pack_f8_kernel<BF16><<<grid, dim3(256), 0, s>>>((const uint32_t*)codes,
+                                                     (const BF16::T*)wscale, Np, Kp, ngw,
+                                                     (uint32_t*)w8, ws32);
+  SQMP_LAUNCH_CHECK();
+  return SQMP_OK;
+}
+
+extern "C" int sqmp_gemm_f8(const void* a8, const float* ascale, const void* xs, const void* w8,
+                            const float* ws32, const void* wsal, const void* bias, void* y,
+                            int dtype, int M, int N, int Kp, int S_pad, int Gw, int ngw,
+                            void* stream) {
+  if (M < 0 || N <= 0 || Kp <= 0 || Kp % 128 != 0 || S_pad < 0 || S_pad % 64 != 0)
+    return SQMP_EINVAL;
+  if (!a8 || !ascale || !w8 || !ws32 || !y || (S_pad > 0 && (!xs || !wsal))) return SQMP_EINVAL;
+  if (Gw <= 0 || Gw % 64 != 0 || ngw <= 0) return SQMP_EUNSUPPORTED;
+  if (dtype != SQMP_F16 && dtype != SQMP_BF16) return SQMP_EUNSUPPORTED;
+  if (M == 0) return SQMP_OK;
+  hipStream_t s = (hipStream_t)stream;
+  const int tiles_m = cdiv(M, 256), tiles_n = cdiv(N, 256);
+  const dim3 grid(tiles_m * tiles_n), block(512);
+#define SQMP_F8L(DTT)                                                                        \
+  gemm_f8_kernel<DTT><<<grid, block, 0, s>>>(                                                \
+      (const unsigned char*)a8, ascale, (const DTT::T*)xs, (const unsigned char*)w8, ws32,   \
+      (const DTT::T*)wsal, (const DTT::T*)bias, (DTT::T*)y, M, N, Kp, S_pad, Gw, ngw, tiles_m, \
+      tiles_n)
+  if (dtype == SQMP_F16) SQMP_F8L(F16);
+  else SQMP_F8L(BF16);
+#undef SQMP_F8L
+  SQMP_LAUNCH_CHECK();
+  return SQMP_OK;
+}

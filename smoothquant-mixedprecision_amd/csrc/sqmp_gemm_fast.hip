@@ -53,7 +53,9 @@ __device__ inline void raw_barrier() {
 __device__ inline void glds16a(const void* src, unsigned char* lds_dst) {
   const uint32_t m0v = __builtin_amdgcn_readfirstlane(
       (uint32_t)(size_t)(__attribute__((address_space(3))) unsigned char*)lds_dst);
-  asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(m0v), "v"(src)
+  // s_nop 0: M0 write -> LDS-DMA wait state (MI355X asm guide §4.1)
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(m0v),
+               "v"(src)
                : "memory", "m0");
 }
 
@@ -75,8 +77,11 @@ __device__ inline void blds16(const i32x4r& rsrc, uint32_t voff, uint32_t soff,
                               unsigned char* lds_dst) {
   const uint32_t m0v = __builtin_amdgcn_readfirstlane(
       (uint32_t)(size_t)(__attribute__((address_space(3))) unsigned char*)lds_dst);
-  asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds" ::"s"(m0v),
-               "v"(voff), "s"(rsrc), "s"(__builtin_amdgcn_readfirstlane(soff))
+  // wait states: s_nop 4 for a scalar operand fresh from v_readfirstlane read by the buffer
+  // instruction as soffset / descriptor, s_nop 0 for M0 write -> LDS-DMA (the hazard table
+  // of the MI355X asm guide, §4.1; hipcc pads nothing inside an asm string)
+  asm volatile("s_nop 4\n\ts_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
+               ::"s"(m0v), "v"(voff), "s"(rsrc), "s"(__builtin_amdgcn_readfirstlane(soff))
                : "memory", "m0");
 }
 
@@ -415,7 +420,8 @@ __global__ __launch_bounds__(512, 1) void gemm_fq6_kernel(
   // lane's group within the block (GB = 2: groups 2 kt, 2 kt + 1) goes in the per-lane
   // offset; the block's first group in the scalar one
   const int s_u = min(lane / LPG, GBn - 1);
-  const uint32_t s_off = (uint32_t)((CW * wn + (lane % LPG) * 8 + s_u * Np) * sizeof(T));
+  const uint32_t s_off0 = (uint32_t)((CW * wn + (lane % LPG) * 8) * sizeof(T));
+  const uint32_t s_off1 = s_off0 + (uint32_t)(s_u * Np * sizeof(T));
 
   auto issue = [&](int kt) {
     unsigned char* slot = lds + (kt % F5_NSLOT) * F5_SLOT;
@@ -427,8 +433,11 @@ __global__ __launch_bounds__(512, 1) void gemm_fq6_kernel(
       for (int i = 0; i < NA; ++i)
         if (PRIO != 8 || kt < 2) blds16(rA, a_off, sa + i * a_str, slot + (i * 8 + wave) * 1024);
       blds16(rB, b_off, (uint32_t)ks * 32, slot + F5_A + wave * 1024);
-      // GB = 2 blocks hold groups 2 kt and 2 kt + 1 < ngw exactly
-      const int g0 = GB == 1 ? min((kt * 64) / Gw, ngw - 1) : kt * 2;
+      // GB = 2 blocks hold groups 2 kt and 2 kt + 1; past the last group (the zero codes
+      // of the padding to Kp) the scales are clamped to group ngw - 1 -- never read past
+      // the [ngw][Np] array (a NaN there would turn 0 * s into NaN)
+      const int g0 = GB == 1 ? min((kt * 64) / Gw, ngw - 1) : min(kt * 2, ngw - 1);
+      const uint32_t s_off = g0 + 1 <= ngw - 1 ? s_off1 : s_off0;
       // GBn groups x CW columns of scales (the other lanes repeat them: same lines; one
       // wave moving all 256 columns instead measured no faster)
       blds16(rS, s_off, (uint32_t)g0 * Np * sizeof(T), slot + F5_A + F5_B + wave * 1024);

@@ -180,6 +180,8 @@ class W4A4Linear(nn.Module):
     """Mixed-precision W4A4 linear: salient input channels in D, the rest int4/int8.
 
     Forward kernels (chosen per layer, see `kernel`; "auto" = "fq" unless ops.I8_AUTO):
+      "f8"  per_token / per_tensor 4-bit activations: e4m3 act codes x e4m3 weight codes on
+            the block-scaled FP8 MFMA (exact integer block sums), per-group fp32 folds.
       "i8"  per_token / per_tensor activations: int8 act codes x int4 weight codes on the
             i8 MFMA with per-group fp32 folds (exact scale factorisation).
       "fq"  every act mode: dequantized activations x in-kernel-decoded weights on the D
@@ -414,15 +416,25 @@ class W4A4Linear(nn.Module):
         bias = None if self.bias is None else self.bias.reshape(-1)
         if bias is not None and bias.dtype != pw.dtype:
             raise RuntimeError(f"bias dtype {bias.dtype} does not match {pw.dtype}")
-        use_i8 = (self.kernel == "i8" or
-                  (self.kernel == "auto" and ops.I8_AUTO and ops.i8_eligible(pw, amode, bits)))
-        if use_i8:
+        use_f8 = (self.kernel == "f8" or
+                  (self.kernel == "auto" and ops.F8_AUTO and ops.f8_eligible(pw, amode, bits)))
+        use_i8 = not use_f8 and (
+            self.kernel == "i8" or
+            (self.kernel == "auto" and ops.I8_AUTO and ops.i8_eligible(pw, amode, bits)))
+        if use_f8:
+            a8, sa, xs = ops.quant_act_f8(xc, pw, amode, bits)
+        elif use_i8:
             a8, sa, xs = ops.quant_act_i8(xc, pw, amode, bits)
         else:
             a = ops.quant_act_fp(xc, pw, amode, bits, ag, stats_of=x)
         if mutate_input:
             ops.fake_quant_inplace(xc, amode, bits, ag, pw.amap_fq, pw.nonsal, 0)
-        y = ops.gemm_i8(a8, sa, xs, pw, bias) if use_i8 else ops.gemm_fq(a, pw, bias)
+        if use_f8:
+            y = ops.gemm_f8(a8, sa, xs, pw, bias)
+        elif use_i8:
+            y = ops.gemm_i8(a8, sa, xs, pw, bias)
+        else:
+            y = ops.gemm_fq(a, pw, bias)
         if ospec is not None:                                                # :308-316
             omode, obits, og = ospec
             if self.salient_indices is not None:

@@ -82,6 +82,8 @@ class PackedWeight:
     dense: Optional[torch.Tensor] = field(default=None)  # packed-order D operand for fine groups
     posmap: Optional[torch.Tensor] = field(default=None)  # int32 [K]: packed position of column k
     sal_key: Optional[tuple] = field(default=None)        # identity of the salient set (host)
+    w8: Optional[torch.Tensor] = field(default=None)     # uint8 [Np, Kp] e4m3 codes (f8 GEMM)
+    ws32: Optional[torch.Tensor] = field(default=None)   # fp32 [ngw, Np] scales (f8 GEMM)
 
     @property
     def gemm_operand(self):
@@ -320,9 +322,69 @@ def gemm_i8(a8: torch.Tensor, sa: torch.Tensor, xs: torch.Tensor, pw: PackedWeig
     return y
 
 
+def f8_operands(pw: PackedWeight):
+    """(w8, ws32) of the f8 GEMM, built once per packed weight."""
+    if pw.w8 is None:
+        Np = pad_n(pw.N)
+        w8 = torch.empty((Np, pw.Kp), dtype=torch.uint8, device=pw.codes.device)
+        ws32 = torch.empty((pw.ngw, Np), dtype=torch.float32, device=pw.codes.device)
+        check(load().sqmp_pack_f8(_p(pw.codes), _p(pw.wscale), _dtype_code(pw.dtype), pw.N,
+                                  pw.Kp, pw.ngw, _p(w8), _p(ws32), _stream(pw.codes)), "pack_f8")
+        pw.w8, pw.ws32 = w8, ws32
+    return pw.w8, pw.ws32
+
+
+def quant_act_f8(x2: torch.Tensor, pw: PackedWeight, act_quant: str, n_bits: int):
+    """x [M, K] -> (e4m3 codes [M, Kp] in packed order, fp32 row scales [M], exact salient
+    x [M, S_pad]) for gemm_f8 (per_token / per_tensor, n_bits <= 4)."""
+    _require_gpu(x2, "quant_act")
+    M, K = x2.shape
+    Mp = _pad_rows(M)
+    a8 = torch.empty((Mp, pw.Kp), dtype=torch.uint8, device=x2.device)[:M]
+    sa = torch.empty((M,), dtype=torch.float32, device=x2.device)
+    xs = torch.empty((Mp, max(pw.S_pad, 8)), dtype=x2.dtype, device=x2.device)[:M]
+    lib = load()
+    nb = lib.sqmp_act_workspace_bytes(M, K, pw.Kp)
+    stream = torch.cuda.current_stream(x2.device).cuda_stream
+    e = _act_ws(x2.device, stream, K, pw.Kp, nb)
+    if pw.posmap is None:
+        pw.posmap = build_posmap(pw.perm, K)
+    status = lib.sqmp_quant_act_v2(_p(x2), _dtype_code(x2.dtype), M, K, ACT_MODES[act_quant],
+                                   n_bits, 0, _p(pw.amap), pw.Kp, _p(pw.nonsal), _p(pw.salient),
+                                   pw.S, pw.S_pad, _p(pw.posmap), _lib.QA_CLEAN_WS, _lib.OUT_F8,
+                                   _p(a8), _p(sa), _p(xs), _p(e["buf"]), e["buf"].numel(),
+                                   ctypes.c_void_p(stream))
+    if status != _lib.SQMP_OK:
+        _WS.pop((x2.device.index, stream, K, pw.Kp), None)
+        check(status, "quant_act")
+    return a8, sa, xs
+
+
+def gemm_f8(a8: torch.Tensor, sa: torch.Tensor, xs: torch.Tensor, pw: PackedWeight,
+            bias: Optional[torch.Tensor]) -> torch.Tensor:
+    M = a8.shape[0]
+    w8, ws32 = f8_operands(pw)
+    y = torch.empty((M, pw.N), dtype=pw.dtype, device=a8.device)
+    check(load().sqmp_gemm_f8(_p(a8), _p(sa), _p(xs) if pw.S_pad else None, _p(w8), _p(ws32),
+                              _p(pw.wsal) if pw.S_pad else None, _p(bias), _p(y),
+                              _dtype_code(pw.dtype), M, pw.N, pw.Kp, pw.S_pad, pw.Gw, pw.ngw,
+                              _stream(a8)), "gemm_f8")
+    return y
+
+
+def f8_eligible(pw: PackedWeight, act_quant: str, act_bits: int) -> bool:
+    """Whether the block-scaled FP8 MFMA path computes this layer: one act scale per row,
+    4-bit codes on both sides (exact in e4m3), weight groups of whole 64-blocks."""
+    return (act_quant in ("per_token", "per_tensor") and pw.dtype != torch.float32
+            and pw.n_bits == 4 and pw.dense is None and pw.Gw % 64 == 0 and act_bits <= 4
+            and pw.K <= 16384)
+
+
 # Whether W4A4Linear(kernel="auto") takes the integer path for eligible layers.  Off: on
 # gfx950 the faithful fq GEMM is currently faster than gemm_i8 (DESIGN.md, perf log).
 I8_AUTO = False
+# Whether kernel="auto" takes the FP8 path for eligible layers (f8_eligible).
+F8_AUTO = False
 
 
 def i8_eligible(pw: PackedWeight, act_quant: str, act_bits: int) -> bool:

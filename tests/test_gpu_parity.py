@@ -5,8 +5,8 @@ Tolerances (stated once, used everywhere):
   * y: relative Frobenius error vs the oracle's fp64-accumulated product, which differs
     from any fp32-accumulating GEMM only by accumulation order:
         fp32 1e-5, fp16 2e-3, bf16 1e-2            (faithful "fq" kernel)
-    The integer "i8" kernel factors the scales out of the sum, so each product differs by
-    the D rounding of x_hat and W_hat (<= 2^-11 rel for fp16, 2^-8 for bf16):
+    The integer "i8" and "f8" kernels factor the scales out of the sum, so each product
+    differs by the D rounding of x_hat and W_hat (<= 2^-11 rel for fp16, 2^-8 for bf16):
         fp16 3e-3, bf16 2e-2.
 """
 import zlib
@@ -190,7 +190,8 @@ def test_oracle_parity(case):
     a = ops.quant_act_fp(xt, q.packed(), aq, bits, Gs)
     assert bits_equal(a_operand_to_original(q, a, K), D.f32(qx))
     want = O.linear(qx, w_hat, b, D)
-    kernels = ["fq"] + (["i8"] if ops.i8_eligible(q.packed(), aq, bits) else [])
+    kernels = (["fq"] + (["i8"] if ops.i8_eligible(q.packed(), aq, bits) else [])
+               + (["f8"] if ops.f8_eligible(q.packed(), aq, bits) else []))
     for kern in kernels:
         q.kernel = kern
         y = q(xt.clone())
