@@ -37,7 +37,7 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 M, K, N, G, P = 16384, 4096, 4096, 128, 0.10
-PEAK_TFLOPS = {"f16": 2516.6, "bf16": 2516.6, "i8": 5033.2}  # dense MFMA, 256 CU @ 2.4 GHz
+PEAK_TFLOPS = {"f16": 2516.6, "bf16": 2516.6, "i8": 5033.2, "f8": 5033.2}  # dense MFMA, 256 CU @ 2.4 GHz
 HBM_PEAK_GBS = 8000.0
 
 
@@ -157,7 +157,9 @@ def main():
 
     q, x, lin = make_layer(dev, args.act, seed=1234 + rank)
     pw = q.packed()
-    use_i8 = ops.I8_AUTO and ops.i8_eligible(pw, args.act, 4)  # what W4A4Linear(auto) runs
+    # what W4A4Linear(kernel="auto") runs for this layer
+    use_f8 = ops.F8_AUTO and ops.f8_eligible(pw, args.act, 4)
+    use_i8 = not use_f8 and ops.I8_AUTO and ops.i8_eligible(pw, args.act, 4)
     stream = torch.cuda.current_stream(dev)
 
     def step():
@@ -180,7 +182,12 @@ def main():
     value = world * flops * args.steps / elapsed / 1e12
 
     # ---- dominant kernel: the GEMM, timed alone on the same stream with HIP events
-    if use_i8:
+    if use_f8:
+        a8, sa, xs = ops.quant_act_f8(x, pw, args.act, 4)
+        gemm = lambda: ops.gemm_f8(a8, sa, xs, pw, lin.bias)  # noqa: E731
+        quant = lambda: ops.quant_act_f8(x, pw, args.act, 4)  # noqa: E731
+        kdt = "f8"
+    elif use_i8:
         a8, sa, xs = ops.quant_act_i8(x, pw, args.act, 4)
         gemm = lambda: ops.gemm_i8(a8, sa, xs, pw, lin.bias)  # noqa: E731
         quant = lambda: ops.quant_act_i8(x, pw, args.act, 4)  # noqa: E731
@@ -212,9 +219,9 @@ def main():
     ref_ms = time_events(lambda: ref(x), max(5, args.steps // 5), stream)
     # prepass algorithmic bytes: read x (colmax) + read x (quantize) + write operand(s)
     xbytes = M * K * 2
-    if use_i8:
+    if use_i8 or use_f8:
         wbytes = M * pw.Kp + M * 4 + M * pw.S_pad * 2
-        reads = 1
+        reads = 2 if args.act == "per_tensor" else 1
     else:
         wbytes = M * (pw.Kp + pw.S_pad) * 2
         reads = 2 if args.act in ("per_group", "per_tensor") else 1
@@ -239,14 +246,15 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "fp16",
+        "dtype": "e4m3 codes (fp32 accumulate) + fp16 salient tail" if use_f8 else "fp16",
         "data": "synthetic (random-init weights N(0,0.02^2), x N(0,1) with 1% outlier channels x30)",
         "config": {
             "workload": (f"W4A4Linear.forward: weight per_group(sorted) int4 + act {args.act} "
                          f"{'(sorted) ' if args.act == 'per_group' else ''}4-bit, "
                          f"{int(P * 100)}% salient fp16 side-GEMM"),
             "M": M, "K": K, "N": N, "group_size": G, "salient_prop": P,
-            "salient_channels": pw.S, "kernel": "gemm_i8" if use_i8 else "gemm_fq",
+            "salient_channels": pw.S,
+            "kernel": "gemm_f8" if use_f8 else "gemm_i8" if use_i8 else "gemm_fq",
             "parallelism": f"replicas x{world}",
         },
         "roofline": {
@@ -256,7 +264,8 @@ def main():
             "unit": "TFLOP/s",
             "frac": round(achieved / PEAK_TFLOPS[kdt], 4),
             "traffic": traffic,
-            "kernel": "sqmp::gemm_i8v2_kernel<F16>" if use_i8 else "sqmp::gemm_fq6_kernel<F16,1>",
+            "kernel": ("sqmp::gemm_f8_kernel<F16> (e4m3 block-scaled MFMA)" if use_f8 else
+                       "sqmp::gemm_i8v2_kernel<F16>" if use_i8 else "sqmp::gemm_fq6_kernel<F16,1>"),
             "avg_ms": round(gemm_ms, 4),
             "algorithmic_flops_per_launch": flops,
         },

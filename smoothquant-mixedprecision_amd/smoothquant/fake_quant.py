@@ -179,7 +179,8 @@ _PACKED_BUFFERS = ("w_codes", "w_scale", "w_salient", "w_perm", "w_amap", "w_ama
 class W4A4Linear(nn.Module):
     """Mixed-precision W4A4 linear: salient input channels in D, the rest int4/int8.
 
-    Forward kernels (chosen per layer, see `kernel`; "auto" = "fq" unless ops.I8_AUTO):
+    Forward kernels (chosen per layer, see `kernel`; "auto" = "f8" where ops.f8_eligible,
+    else "fq" unless ops.I8_AUTO):
       "f8"  per_token / per_tensor 4-bit activations: e4m3 act codes x e4m3 weight codes on
             the block-scaled FP8 MFMA (exact integer block sums), per-group fp32 folds.
       "i8"  per_token / per_tensor activations: int8 act codes x int4 weight codes on the

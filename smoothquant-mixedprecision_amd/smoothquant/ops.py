@@ -383,8 +383,9 @@ def f8_eligible(pw: PackedWeight, act_quant: str, act_bits: int) -> bool:
 # Whether W4A4Linear(kernel="auto") takes the integer path for eligible layers.  Off: on
 # gfx950 the faithful fq GEMM is currently faster than gemm_i8 (perf log).
 I8_AUTO = False
-# Whether kernel="auto" takes the FP8 path for eligible layers (f8_eligible).
-F8_AUTO = False
+# Whether kernel="auto" takes the FP8 path for eligible layers (f8_eligible): on gfx950
+# it is 1.4x the fq GEMM at config 2.
+F8_AUTO = True
 
 
 def i8_eligible(pw: PackedWeight, act_quant: str, act_bits: int) -> bool:

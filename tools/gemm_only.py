@@ -1,5 +1,5 @@
 """Run only the W4A4 GEMM (and optionally the prepass) of BASELINE config 2 -- a target
-for rocprofv3 counter passes.  python tools/gemm_only.py [fq|i8] [iters] [per_group|per_token] [prepass]"""
+for rocprofv3 counter passes.  python tools/gemm_only.py [fq|i8|f8] [iters] [per_group|per_token] [prepass]"""
 import os
 import sys
 
@@ -24,6 +24,12 @@ if kind == "fq":
         if prepass:
             ops.quant_act_fp(x, pw, act, 4, bench.G)
         ops.gemm_fq(a, pw, lin.bias)
+elif kind == "f8":
+    a8, sa, xs = ops.quant_act_f8(x, pw, act, 4)
+    for _ in range(iters):
+        if prepass:
+            ops.quant_act_f8(x, pw, act, 4)
+        ops.gemm_f8(a8, sa, xs, pw, lin.bias)
 else:
     a8, sa, xs = ops.quant_act_i8(x, pw, act, 4)
     for _ in range(iters):
