@@ -55,10 +55,10 @@ __device__ inline void dma16(const i32x4b& rsrc, uint32_t voff, uint32_t soff,
                              unsigned char* lds_dst) {
   const uint32_t m0v = __builtin_amdgcn_readfirstlane(
       (uint32_t)(size_t)(__attribute__((address_space(3))) unsigned char*)lds_dst);
-  // s_nop 4: scalar operand fresh from v_readfirstlane -> buffer soffset / descriptor;
-  // s_nop 0: M0 write -> LDS-DMA (hazard table, MI355X asm guide §4.1)
-  asm volatile("s_nop 4\n\ts_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
-               ::"s"(m0v), "v"(voff), "s"(rsrc), "s"(__builtin_amdgcn_readfirstlane(soff))
+  // s_nop 0: M0 write -> LDS-DMA (hazard table, MI355X asm guide §4.1); soff is SALU
+  // arithmetic ("s" rejects a VGPR value at compile time), the descriptor built long before
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
+               ::"s"(m0v), "v"(voff), "s"(rsrc), "s"(soff)
                : "memory", "m0");
 }
 

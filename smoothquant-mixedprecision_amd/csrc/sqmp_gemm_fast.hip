@@ -77,11 +77,12 @@ __device__ inline void blds16(const i32x4r& rsrc, uint32_t voff, uint32_t soff,
                               unsigned char* lds_dst) {
   const uint32_t m0v = __builtin_amdgcn_readfirstlane(
       (uint32_t)(size_t)(__attribute__((address_space(3))) unsigned char*)lds_dst);
-  // wait states: s_nop 4 for a scalar operand fresh from v_readfirstlane read by the buffer
-  // instruction as soffset / descriptor, s_nop 0 for M0 write -> LDS-DMA (the hazard table
-  // of the MI355X asm guide, §4.1; hipcc pads nothing inside an asm string)
-  asm volatile("s_nop 4\n\ts_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
-               ::"s"(m0v), "v"(voff), "s"(rsrc), "s"(__builtin_amdgcn_readfirstlane(soff))
+  // s_nop 0: M0 write -> LDS-DMA wait state (hazard table of the MI355X asm guide, §4.1;
+  // hipcc pads nothing inside an asm string).  soff is wave-uniform SALU arithmetic (the
+  // "s" constraint rejects anything else at compile time), so no v_readfirstlane ->
+  // soffset hazard arises; the descriptor is built once, long before.
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
+               ::"s"(m0v), "v"(voff), "s"(rsrc), "s"(soff)
                : "memory", "m0");
 }
 
