@@ -441,7 +441,9 @@ __global__ __launch_bounds__(512, 1) void gemm_fq6_kernel(
       const uint32_t s_off = g0 + 1 <= ngw - 1 ? s_off1 : s_off0;
       // GBn groups x CW columns of scales (the other lanes repeat them: same lines; one
       // wave moving all 256 columns instead measured no faster)
-      blds16(rS, s_off, (uint32_t)g0 * Np * sizeof(T), slot + F5_A + F5_B + wave * 1024);
+      // PRIO 15 (diagnostic): no scale pieces after the first two stages
+      if (PRIO != 15 || kt < 2)
+        blds16(rS, s_off, (uint32_t)g0 * Np * sizeof(T), slot + F5_A + F5_B + wave * 1024);
     } else if (DW == 64) {
       const int col = nkm * 64 + (kt - nkm) * 64;
       const uint32_t sa = (uint32_t)col * sizeof(T);
@@ -564,7 +566,8 @@ __global__ __launch_bounds__(512, 1) void gemm_fq6_kernel(
 
   // PRIO 4 / 5 are timing diagnostics (garbage results, in-bounds addresses): 4 keeps
   // the DMA but skips every wait on it, 5 moves no bytes after the first two stages.
-  constexpr bool DIAG_NOWAIT = PRIO == 4 || PRIO == 5 || PRIO == 8;  // 8: no A DMA in the loop
+  constexpr bool DIAG_NOWAIT = PRIO == 4 || PRIO == 5 || PRIO == 8 || PRIO == 12 || PRIO == 15;  // 8: no A DMA in the loop
+  constexpr bool DIAG_NOBAR = PRIO == 12;  // 12: no waits and no barriers in the codes loop
   issue(0);
   if (nkt > 1) issue(1);
   if (PRIO == 1 && wave >= 4) __builtin_amdgcn_s_setprio(1);
@@ -577,7 +580,7 @@ __global__ __launch_bounds__(512, 1) void gemm_fq6_kernel(
     } else {
       vm_wait<0>();
     }
-    raw_barrier();
+    if (!DIAG_NOBAR || kt < 2) raw_barrier();
     if (kt + 2 < nkt && PRIO != 5) issue(kt + 2);
     if (PRIO == 2) __builtin_amdgcn_s_setprio(1);
     compute_codes(lds + (kt % F5_NSLOT) * F5_SLOT);
@@ -600,6 +603,43 @@ __global__ __launch_bounds__(512, 1) void gemm_fq6_kernel(
   if (PRIO == 1) __builtin_amdgcn_s_setprio(0);
 
   // ---- epilogue: acc[i][j][r] = C[n = n0 + CW wn + 16 j + 4 q + r][m = m0 + MW wm + 16 i + r16]
+  {
+    // Full-width tiles: the TM x 256 output tile is staged in LDS (row m: 512 B, 16-B
+    // chunk c at c ^ (m & 15), conflict-free both ways) and stored as whole rows, one 16-B
+    // chunk per lane (two rows per wave instruction, 4 full 128-B lines each) instead of
+    // 8-B pieces of 16 rows (config-2 GEMM +2.8 %).
+    if (n0 + 256 <= N && (N & 7) == 0) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      raw_barrier();  // every wave is past its last read of the ring
+#pragma unroll
+      for (int j = 0; j < J; ++j) {
+        const int nl = wn * CW + 16 * j + 4 * q;  // first of the lane's 4 columns
+        float bv[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) bv[r] = bias ? DT::to_f(bias[n0 + nl + r]) : 0.f;
+#pragma unroll
+        for (int i = 0; i < I; ++i) {
+          const int ml = wm * MW + 16 * i + r16;
+          T v[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = DT::from_f(acc[i][j][r] + bv[r]);
+          const int c = nl >> 3;
+          *(uint2*)(lds + ml * 512 + ((c ^ (ml & 15)) << 4) + (nl & 4) * 2) = *(const uint2*)v;
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's tile writes landed
+      raw_barrier();
+      const int c = tid & 31;
+#pragma unroll
+      for (int k = 0; k < TM / 16; ++k) {
+        const int ml = 16 * k + (tid >> 5);
+        const int gm = m0 + ml;
+        const u32x4 val = *(const u32x4*)(lds + ml * 512 + ((c ^ (ml & 15)) << 4));
+        if (gm < M) *(u32x4*)(Y + (size_t)gm * N + n0 + c * 8) = val;
+      }
+      return;
+    }
+  }
   float bvs[J][4];
 #pragma unroll
   for (int j = 0; j < J; ++j)
@@ -901,6 +941,8 @@ static int fq6_launch(const void* a, const void* codes, const void* wscale, cons
   else if (pr == 5) SQMP_FQ6_L(5, 1);  // ... no DMA after the first two stages
   else if (pr == 6) SQMP_FQ6_L(6, 1);  // ... codes stages re-read stage 0 (L2 hits)
   else if (pr == 8) SQMP_FQ6_L(8, 1);  // ... codes stages move B and S only
+  else if (pr == 12) SQMP_FQ6_L(12, 1);  // ... no waits, no barriers in the codes loop
+  else if (pr == 15) SQMP_FQ6_L(15, 1);  // diagnostic: no scale pieces in the loop
   else if (pr == 3)  // A-fragment read-ahead of 5 blocks (tuning)
     gemm_fq6_kernel<DT, GB, TM, 0, 1, 5><<<dim3(tiles_m * tiles_n), dim3(512), 0, s>>>(
         (const T*)a, codes, (const T*)wscale, (const T*)wsal, (const T*)bias, (T*)y, M, N, Kp,

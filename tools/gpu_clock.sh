@@ -4,8 +4,9 @@ set -o pipefail
 R=$GRAFT_REPO_ROOT
 mkdir -p $R/gpurun_out/clk
 cd /tmp && export TMPDIR=/tmp
-for v in ${VARIANTS:-wm1}; do
-  SQMP_FQ_VARIANT=$v timeout -k 10 240 rocprofv3 --kernel-trace --pmc GRBM_GUI_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES --output-format csv -d $R/gpurun_out/clk/$v -o run -- python $R/tools/gemm_only.py fq 20 > $R/gpurun_out/clk/$v.log 2>&1 || { echo "clock $v failed"; tail -5 $R/gpurun_out/clk/$v.log; exit 1; }
+# ENVS="SQMP_FQ6_PRIO=0 SQMP_FQ6_PRIO=5": one pass per env assignment
+for v in ${ENVS:-SQMP_FQ6_PRIO=0}; do
+  env $v timeout -k 10 240 rocprofv3 --kernel-trace --pmc GRBM_GUI_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES --output-format csv -d $R/gpurun_out/clk/$v -o run -- python $R/tools/gemm_only.py fq 20 > $R/gpurun_out/clk/$v.log 2>&1 || { echo "clock $v failed"; tail -5 $R/gpurun_out/clk/$v.log; exit 1; }
 done
 python - <<'PY'
 import csv, glob, os, collections
