@@ -506,7 +506,24 @@ __global__ __launch_bounds__(256) void rank_table_kernel(
   extern __shared__ __attribute__((aligned(16))) uint32_t rt_kv[];  // roundup(L, 4 TPO)
   const int tid = threadIdx.x;
   const int L4 = (int)round_up_dev(L, 4 * TPO) >> 2;
-  for (int j = tid; j < 4 * L4; j += 256) rt_kv[j] = j < L ? key[nonsal[j]] : 0xFFFFFFFFu;
+  // gathers in batches of 16 per thread (all index loads, then all key loads): two
+  // dependent round trips per batch instead of two per element
+  for (int j0 = tid; j0 < 4 * L4; j0 += 256 * 16) {
+    int idx[16];
+    uint32_t kv[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int j = j0 + 256 * u;
+      idx[u] = j < L ? nonsal[j] : -1;
+    }
+#pragma unroll
+    for (int u = 0; u < 16; ++u) kv[u] = idx[u] >= 0 ? key[idx[u]] : 0xFFFFFFFFu;
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int j = j0 + 256 * u;
+      if (j < 4 * L4) rt_kv[j] = kv[u];
+    }
+  }
   const int nt = gridDim.x * 256;
   for (int r = L + blockIdx.x * 256 + tid; r < lc_len; r += nt) lctab[r] = lc_none;
   __syncthreads();

@@ -25,8 +25,21 @@ __global__ __launch_bounds__(256) void colmax_kernel(const typename DT::T* __res
 #pragma unroll
   for (int i = 0; i < VEC; ++i) m[i] = 0.f;
   if (c0 + VEC <= C && VEC > 1) {
-#pragma unroll 8
-    for (int r = r0 + wid; r < r1; r += 4) {
+    // explicit batches of 8 rows: 8 loads in flight per lane (an unrolled loop over a
+    // pointer chain was compiled to one load + vmcnt(0) per row)
+    int r = r0 + wid;
+    for (; r + 28 < r1; r += 32) {
+      u32x4 raw[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) raw[u] = *(const u32x4*)(x + (size_t)(r + 4 * u) * C + c0);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const T* v = (const T*)&raw[u];
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) m[i] = fmaxf(m[i], fabsf(DT::to_f(v[i])));
+      }
+    }
+    for (; r < r1; r += 4) {
       const u32x4 raw = *(const u32x4*)(x + (size_t)r * C + c0);
       const T* v = (const T*)&raw;
 #pragma unroll
@@ -58,6 +71,7 @@ static void colmax_launch(const void* x, int R, int C, uint32_t* cmax, hipStream
   // keep >= ~1024 blocks in flight when R is large, fewer row passes when R is small
   while (rows_per_block > 16 && (long)cblocks_v * cdiv(R, rows_per_block) < 1024)
     rows_per_block >>= 1;
+  if (const char* e = getenv("SQMP_COLMAX_RPB")) rows_per_block = atoi(e);
   dim3 block(256);
   if (vec_ok) {
     dim3 grid(cblocks_v, cdiv(R, rows_per_block));
