@@ -25,6 +25,8 @@
 //   q = fma(e, r, q0) is the correctly rounded quotient); code = rne(D(q)) (fp16: the
 //   1536 magic add, exact for |q| < 512); x_hat = D(code * s) (one correctly rounded D
 //   product) with the sign of x (the reference's -0.0 for small negative values).
+#include <stdlib.h>
+
 #include "sqmp_internal.h"
 
 namespace sqmp {
@@ -415,6 +417,7 @@ static int quant_lc_launch(const void* x, int M, int K, int q_max, int G, const 
   int per_cu = (int)((150 * 1024) / lds);
   const int by_waves = 32 / nw;
   per_cu = per_cu < 1 ? 1 : (per_cu > by_waves ? by_waves : per_cu);
+  if (const char* e = getenv("SQMP_LC_PERCU")) per_cu = atoi(e);  // tuning only
   int grid = 256 * per_cu;
   const int npair = (M + 1) / 2;
   if (grid > npair) grid = npair;
