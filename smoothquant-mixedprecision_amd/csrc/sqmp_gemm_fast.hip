@@ -375,7 +375,7 @@ __global__ __launch_bounds__(512, 1) void gemm_fq6_kernel(
   // handing the scale piece, or the B and scale pieces, back to their own wave: -7 / -9 %).
   // PRIO 24 = every wave issues its own pieces (the previous scheme, A/B only); LB / LS
   // (variants 22 / 23) = B / scale pieces by the owning wave.
-  constexpr bool LSPLIT = WM == 1 && (PRIO == 0 || PRIO == 19 || PRIO == 20 || PRIO == 22 || PRIO == 23);
+  constexpr bool LSPLIT = PRIO == 0 || PRIO == 19 || PRIO == 20 || PRIO == 22 || PRIO == 23;
   constexpr bool LB = LSPLIT && PRIO != 23, LS = LSPLIT && PRIO != 22 && PRIO != 23;
   constexpr int VM_LOAD = 2 * NA + (LB ? 2 : 1) + (LS ? 2 : 1);  // loader ops per codes stage
   constexpr int VM_COMP = (LB ? 0 : 1) + (LS ? 0 : 1);            // ... of waves 4-7
@@ -463,7 +463,9 @@ __global__ __launch_bounds__(512, 1) void gemm_fq6_kernel(
       if ((PRIO != 15 || kt < 2) && (!LS || wave < 4)) {
         blds16(rS, s_off, (uint32_t)g0 * Np * sizeof(T), slot + F5_A + F5_B + wave * 1024);
         if (LS)
-          blds16(rS, s_off + 4u * CW * sizeof(T), (uint32_t)g0 * Np * sizeof(T), slot + F5_A + F5_B + (wave + 4) * 1024);
+          // (WM = 2: wave + 4 has the same column block, hence the same scales)
+          blds16(rS, s_off + (WM == 1 ? 4u * CW * sizeof(T) : 0u), (uint32_t)g0 * Np * sizeof(T),
+                 slot + F5_A + F5_B + (wave + 4) * 1024);
       }
     } else if (DW == 64) {
       const int col = nkm * 64 + (kt - nkm) * 64;
@@ -588,8 +590,7 @@ __global__ __launch_bounds__(512, 1) void gemm_fq6_kernel(
   // PRIO 4 / 5 are timing diagnostics (garbage results, in-bounds addresses): 4 keeps
   // the DMA but skips every wait on it, 5 moves no bytes after the first two stages.
   constexpr bool DIAG_NOWAIT = PRIO == 4 || PRIO == 5 || PRIO == 8 || PRIO == 12 || PRIO == 15;  // 8: no A DMA in the loop
-  constexpr bool DIAG_NOBAR = PRIO == 12;
-  static_assert(!LSPLIT || WM == 1, "loader split: 1 x 8 waves");  // 12: no waits and no barriers in the codes loop
+  constexpr bool DIAG_NOBAR = PRIO == 12;  // 12: no waits and no barriers in the codes loop
   issue(0);
   if (nkt > 1) issue(1);
   if ((PRIO == 1 || PRIO == 19) && wave >= 4) __builtin_amdgcn_s_setprio(1);
