@@ -190,7 +190,9 @@ __global__ __launch_bounds__(256) void quant_act_kernel(
             if (g != G_ZERO) {
               const float s = MODE == MODE_GROUP ? sc[g] : s_row;
               const float t = DT::to_f(row[e & 0xFFFFu]);
-              r = __builtin_rintf(rd<DT>(t / s)) * s;  // x_hat, rounded to D below
+              // x_hat, rounded to D below; the sign of x is kept on zero codes (the
+              // reference's -0.0, fake_quant.py:142)
+              r = __builtin_copysignf(__builtin_rintf(rd<DT>(t / s)) * s, t);
             }
           } else if (p - P < S) {
             r = DT::to_f(row[sal[p - P]]);
@@ -213,7 +215,7 @@ __global__ __launch_bounds__(256) void quant_act_kernel(
             } else {
               const float s = MODE == MODE_GROUP ? sc[g] : s_row;
               const float t = DT::to_f(row[e & 0xFFFFu]);
-              v[e8] = DT::from_f(__builtin_rintf(rd<DT>(t / s)) * s);
+              v[e8] = DT::from_f(__builtin_copysignf(__builtin_rintf(rd<DT>(t / s)) * s, t));
             }
           }
           ((u32x4*)xr)[c] = *(const u32x4*)v;
@@ -225,7 +227,7 @@ __global__ __launch_bounds__(256) void quant_act_kernel(
           if (g == G_PASS || g == G_ZERO) continue;
           const float s = MODE == MODE_GROUP ? sc[g] : s_row;
           const float t = DT::to_f(row[e & 0xFFFFu]);
-          xr[p] = DT::from_f(__builtin_rintf(rd<DT>(t / s)) * s);
+          xr[p] = DT::from_f(__builtin_copysignf(__builtin_rintf(rd<DT>(t / s)) * s, t));
         }
       }
     }
@@ -387,7 +389,8 @@ __global__ __launch_bounds__(256) void quant_fp_kernel(
           float y = 0.f;
           if (g != G_ZERO) {
             const float2 sr = MODE == MODE_GROUP ? scr[g] : make_float2(s_row, r_row);
-            y = fast_code<DT>(DT::to_f(v[j]), sr.x, sr.y) * sr.x;
+            const float t = DT::to_f(v[j]);
+            y = __builtin_copysignf(fast_code<DT>(t, sr.x, sr.y) * sr.x, t);  // -0.0 as the reference
           }
           r[j] = DT::from_f(y);
         }
@@ -497,7 +500,7 @@ __global__ __launch_bounds__(256) void lc_table_kernel(
 // of i's own chunk below i.  Writes colsorted[r] and lctab[r] = col | posmap[col] << 16,
 // and the (zero, sink) entries of ranks [L, lc_len).  The keys are NOT cleared here (other
 // workgroups may still read them): the quantizer launched next clears them.
-constexpr int RT_MAX = 8192;
+constexpr int RT_MAX = 16384;  // 64 KiB of keys in LDS
 template <int TPO>
 __global__ __launch_bounds__(256) void rank_table_kernel(
     const uint32_t* __restrict__ key, const int32_t* __restrict__ nonsal, int L,
@@ -567,6 +570,14 @@ static int launch_rank_table(const uint32_t* key, const int32_t* nonsal, int L,
   const int tpo = tpo_env == 16 || tpo_env == 32 ? tpo_env : (L <= 2048 ? 16 : 32);
   const int grid = cdiv((long)L * tpo, 256);
   const size_t lds = sizeof(uint32_t) * (size_t)round_up(L, 4 * tpo);
+  static bool attr_set = false;  // up to 64 KiB of keys: raise the dynamic-LDS limit once
+  if (!attr_set) {
+    SQMP_HIP_CHECK(hipFuncSetAttribute((const void*)rank_table_kernel<16>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, 4 * RT_MAX));
+    SQMP_HIP_CHECK(hipFuncSetAttribute((const void*)rank_table_kernel<32>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, 4 * RT_MAX));
+    attr_set = true;
+  }
   if (tpo == 16)
     rank_table_kernel<16><<<dim3(grid), dim3(256), lds, s>>>(key, nonsal, L, posmap, colsorted,
                                                               lctab, lc_len, lc_none);
@@ -695,7 +706,8 @@ __global__ __launch_bounds__(256) void quant_fp_wave_kernel(
           float y = 0.f;
           if (g != G_ZERO) {
             const float2 sr = MODE == MODE_GROUP ? scr[g] : make_float2(s_row, r_row);
-            y = fast_code<DT>(DT::to_f(v[j]), sr.x, sr.y) * sr.x;
+            const float t = DT::to_f(v[j]);
+            y = __builtin_copysignf(fast_code<DT>(t, sr.x, sr.y) * sr.x, t);  // -0.0 as the reference
           }
           r[j] = DT::from_f(y);
         }

@@ -108,6 +108,7 @@ TIE_CASES = [
     # M, K, dtype, salient_prop  (list lengths select every sort-table block shape)
     (4, 1024, "fp16", 0.0), (3, 2048, "bf16", 0.05), (4, 4096, "fp16", 0.05),
     (2, 8192, "bf16", 0.05), (5, 11008, "fp16", 0.05), (2, 16384, "fp16", 0.02),
+    (2, 18432, "fp16", 0.02),  # list > RT_MAX: rank_count + lc_table
 ]
 
 
