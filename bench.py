@@ -54,14 +54,19 @@ def parse():
     return ap.parse_args()
 
 
-def setup_dist(n):
+def setup_dist(n, backend="nccl"):
+    """One process per GPU (torch.distributed.run env); backend "nccl" is RCCL on ROCm,
+    "gloo" is the CPU rehearsal used by tests/test_bench_dist_cpu.py."""
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     return rank, world, local
 
 
@@ -78,6 +83,12 @@ def max_over_ranks(v, world, dev):
     t = torch.tensor([v], dtype=torch.float64, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def job_tflops(world, flops_per_step, steps, elapsed_max):
+    """Whole-job throughput: every replica ran `steps` steps; the job took the slowest
+    rank's time (max over ranks)."""
+    return world * flops_per_step * steps / elapsed_max / 1e12
 
 
 def make_layer(dev, act, seed):
@@ -179,7 +190,7 @@ def main():
     elapsed = max_over_ranks(elapsed, world, dev)
     ms_per_step = elapsed / args.steps * 1e3
     flops = 2.0 * M * N * K
-    value = world * flops * args.steps / elapsed / 1e12
+    value = job_tflops(world, flops, args.steps, elapsed)
 
     # ---- dominant kernel: the GEMM, timed alone on the same stream with HIP events
     if use_f8:
