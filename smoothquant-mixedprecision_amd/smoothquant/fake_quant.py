@@ -134,7 +134,23 @@ def _bind_act(mode: str, n_bits: int, group_size: int):
     return partial(_ACT_FNS[mode], n_bits=n_bits, **kw)
 
 
+_RQ_MEMO = {}
+
+
 def resolve_quantizer(fn):
+    """Memoized _resolve_quantizer (the signature binding costs ~10 us per call; a partial's
+    func / args / keywords are read-only, so the result is fixed per callable object)."""
+    e = _RQ_MEMO.get(id(fn))
+    if e is not None and e[0] is fn:
+        return e[1]
+    r = _resolve_quantizer(fn)
+    if len(_RQ_MEMO) > 8192:
+        _RQ_MEMO.clear()
+    _RQ_MEMO[id(fn)] = (fn, r)
+    return r
+
+
+def _resolve_quantizer(fn):
     """(mode, n_bits, group_size) of an act/output quantizer callable, or None for the
     identity.  Accepts what the reference binds (fake_quant.py:246-263) and what its users
     rebind (e.g. W4A8: ``q.act_quant = partial(quantize_activation_per_group_absmax_sort,
@@ -171,6 +187,9 @@ _identity._sqmp_identity = True
 
 _PACKED_BUFFERS = ("w_codes", "w_scale", "w_salient", "w_perm", "w_amap", "w_amap_fq",
                    "w_nonsal", "salient_i32", "w_dense", "out_amap_fq", "out_nonsal")
+# buffers a PackedWeight holds (W4A4Linear.packed's reuse check)
+_PW_KEY = ("w_codes", "w_scale", "w_salient", "w_perm", "w_amap", "w_amap_fq", "w_nonsal",
+           "salient_i32", "w_dense", "w_posmap")
 
 
 # ----------------------------------------------------------------------------------------
@@ -263,6 +282,16 @@ class W4A4Linear(nn.Module):
             self.to(dev)
 
     def packed(self) -> PackedWeight:
+        # One PackedWeight per buffer set: reused while every buffer is the same object and
+        # the codes / scales were not written in place (their derived f8 operands, built
+        # once per PackedWeight, stay valid) -- a forward then costs no host rebuild.
+        # (dict lookups, not Module.__getattr__: this runs once per forward)
+        d, b = self.__dict__, self._buffers
+        c = d.get("_pw_cache")
+        if (c is not None and c[3] is d.get("_meta") and c[4] is d.get("_sal_key")
+                and c[2] == (b["w_codes"]._version, b["w_scale"]._version)
+                and all(b[n] is t for n, t in zip(_PW_KEY, c[0]))):
+            return c[1]
         if self._meta is None:
             if not self._random_init:
                 raise RuntimeError("W4A4Linear has no packed weight")
@@ -276,10 +305,15 @@ class W4A4Linear(nn.Module):
             self.w_posmap = ops.build_posmap(self.w_perm, m["K"])  # e.g. after a checkpoint load
         if self._sal_key is None:
             self._sal_key = ops.salient_key(m["K"], self.salient_i32)
-        return PackedWeight(self.w_codes, self.w_scale, self.w_salient, self.w_perm, self.w_amap,
-                            self.w_amap_fq, self.w_nonsal, self.salient_i32, m["N"], m["K"],
-                            m["S"], m["S_pad"], m["Kp"], m["Gw"], m["ngw"], m["n_bits"],
-                            m["wmode"], m["dtype"], self.w_dense, self.w_posmap, self._sal_key)
+        pw = PackedWeight(self.w_codes, self.w_scale, self.w_salient, self.w_perm, self.w_amap,
+                          self.w_amap_fq, self.w_nonsal, self.salient_i32, m["N"], m["K"],
+                          m["S"], m["S_pad"], m["Kp"], m["Gw"], m["ngw"], m["n_bits"],
+                          m["wmode"], m["dtype"], self.w_dense, self.w_posmap, self._sal_key)
+        b = self._buffers
+        self.__dict__["_pw_cache"] = (tuple(b[n] for n in _PW_KEY), pw,
+                                      (b["w_codes"]._version, b["w_scale"]._version),
+                                      m, self._sal_key)
+        return pw
 
     # ------------------------------------------------------------------ persistence
     # Packed format (the reference persists only the dequantized weight

@@ -210,6 +210,17 @@ _WS = {}
 _SORTED = ("per_group", "per_group_mean3std")
 
 
+_WSB = {}
+
+
+def _ws_bytes(M: int, K: int, Kp: int) -> int:
+    """sqmp_act_workspace_bytes, memoized per shape (saves a ctypes call per forward)."""
+    n = _WSB.get((M, K, Kp))
+    if n is None:
+        n = _WSB[(M, K, Kp)] = load().sqmp_act_workspace_bytes(M, K, Kp)
+    return n
+
+
 def _act_ws(device, stream_ptr: int, K: int, Kp: int, nbytes: int):
     key = (device.index, stream_ptr, K, Kp)
     e = _WS.get(key)
@@ -233,7 +244,7 @@ def quant_act_fp(x2: torch.Tensor, pw: PackedWeight, act_quant: str, n_bits: int
     M, K = x2.shape
     a = torch.empty((_pad_rows(M), pw.Kp + pw.S_pad), dtype=x2.dtype, device=x2.device)[:M]
     lib = load()
-    nb = lib.sqmp_act_workspace_bytes(M, K, pw.Kp)
+    nb = _ws_bytes(M, K, pw.Kp)
     stream = torch.cuda.current_stream(x2.device).cuda_stream
     e = _act_ws(x2.device, stream, K, pw.Kp, nb)
     flags = _lib.QA_CLEAN_WS
@@ -344,7 +355,7 @@ def quant_act_f8(x2: torch.Tensor, pw: PackedWeight, act_quant: str, n_bits: int
     sa = torch.empty((M,), dtype=torch.float32, device=x2.device)
     xs = torch.empty((Mp, max(pw.S_pad, 8)), dtype=x2.dtype, device=x2.device)[:M]
     lib = load()
-    nb = lib.sqmp_act_workspace_bytes(M, K, pw.Kp)
+    nb = _ws_bytes(M, K, pw.Kp)
     stream = torch.cuda.current_stream(x2.device).cuda_stream
     e = _act_ws(x2.device, stream, K, pw.Kp, nb)
     if pw.posmap is None:

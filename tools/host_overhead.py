@@ -21,8 +21,11 @@ q = W4A4Linear.from_float(lin, weight_quant="per_group", act_quant="per_group",
                           importance=x.float().abs().mean(0).cpu(), salient_prop=0.05,
                           group_size=64)
 pw = q.packed()
+a_op = ops.quant_act_fp(x, pw, "per_group", 4, 64)
 for name, fn in [("quant_act_fp", lambda: ops.quant_act_fp(x, pw, "per_group", 4, 64)),
+                 ("gemm_fq", lambda: ops.gemm_fq(a_op, pw, None)),
                  ("forward", lambda: q(x)),
+                 ("F.linear", lambda: torch.nn.functional.linear(x, lin.weight)),
                  ("packed()", lambda: q.packed())]:
     for _ in range(10):
         fn()
