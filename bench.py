@@ -8,23 +8,31 @@ x[bs*seq = 16384, 4096] fp16 -- activation quantization (column absmax over the 
 stable sort, per-(row, group) scales) + the mixed-precision MFMA GEMM with the salient
 fp16 side-GEMM.  `value` is whole-job TFLOP/s = N_gpus * 2*M*N*K / max-over-ranks time.
 
-Multi-GPU: the op is per-layer and does not shard ("replicas only"): each rank
-runs an independent replica on its own GPU; the only collectives are the timing barriers
-and the max-over-ranks of the elapsed time.
+Multi-GPU: the op is per-layer and does not shard ("replicas only"): each
+rank runs an independent replica on its own GPU; the only collectives are the timing
+barriers and the max-over-ranks of the elapsed time.  `--gpus N` without a
+torch.distributed.run environment starts one as a child process (nothing touches the
+GPU before that) and exits with its status.
 
 Also printed in the same JSON line:
   roofline      the dominant kernel (the GEMM), timed live with HIP events on the stream
-                it runs on; achieved = 2*M*N*K / average GEMM duration; peak = dense MFMA
-                peak of the dtype the kernel computes in.
-  cpu_baseline  the CPU oracle (numpy restatement of fake_quant, oracle/) on a bounded
-                sample of the same workload, rank 0, N=1 only.
-  prepass       the activation-quantization kernels' time and algorithmic GB/s.
+                it runs on; achieved = 2*M*N*K / average GEMM duration; `peak`/`frac` =
+                dense MFMA peak of the dtype the kernel computes in; `frac_contract_*` =
+                BASELINE.md §2's T_roof / time, T_roof = 2MNK'/P_i8 + 2MNS/P_f16 (120.9 us)
+  cpu_baseline  the reference's fake-quant layer restated in PyTorch ops (oracle/
+                torch_cpu.py, pinned bit-exact to the reference goldens) in fp32 on this
+                host's cores: rank 0, N=1 only, median of 3 after 1 warm-up
+  prepass       the activation-quantization kernels' time and algorithmic GB/s
+Secondary measurements (GEMM alone, prepass, vendor dense GEMM, reference fake-quant on
+the GPU) run BEFORE the W warm-up steps, so the timed region starts on a busy chip.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import statistics
+import subprocess
 import sys
 import time
 
@@ -33,33 +41,57 @@ for _p in (ROOT, os.path.join(ROOT, "smoothquant-mixedprecision_amd")):
     if _p not in sys.path:
         sys.path.insert(0, _p)
 
-import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 M, K, N, G, P = 16384, 4096, 4096, 128, 0.10
-PEAK_TFLOPS = {"f16": 2516.6, "bf16": 2516.6, "i8": 5033.2, "f8": 5033.2}  # dense MFMA, 256 CU @ 2.4 GHz
+# dense MFMA peaks (MI355X_MICROARCH.md: 256 CU @ 2.4 GHz): f16/bf16 2.5 PF, i8/fp8 5 PF,
+# fp6/fp4 10 PF
+PEAK_TFLOPS = {"f16": 2516.6, "bf16": 2516.6, "i8": 5033.2, "f8": 5033.2, "f6": 10066.3}
 HBM_PEAK_GBS = 8000.0
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    # defaults long enough for the chip to settle at the clock it holds under this load
-    # (DVFS, MI355X_MICROARCH.md): ~0.14 s of warmup and of timed steps
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=200)
     ap.add_argument("--act", default="per_group", choices=["per_group", "per_token"])
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
-    ap.add_argument("--cpu-rows", type=int, default=16384)
-    return ap.parse_args()
+    ap.add_argument("--rehearsal", action="store_true",
+                    help="CPU/gloo rehearsal of the launcher and timing path (no GPU): the "
+                         "step is the CPU fake-quant layer on a 64-row batch")
+    return ap.parse_args(argv)
+
+
+def contract_roofline_s(S: int) -> float:
+    """T_roof = 2*M*N*K'/P_i8 + 2*M*N*S/P_f16 (seconds)."""
+    return (2.0 * M * N * (K - S) / (PEAK_TFLOPS["i8"] * 1e12)
+            + 2.0 * M * N * S / (PEAK_TFLOPS["f16"] * 1e12))
+
+
+# ------------------------------------------------------------------ launcher / dist
+def launch_children(args, argv) -> int:
+    """Start `torch.distributed.run` with one rank per GPU as a child process (never an
+    exec of this process) and return its exit status."""
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr=127.0.0.1",
+           f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+    return subprocess.call(cmd)
 
 
 def setup_dist(n, backend="nccl"):
     """One process per GPU (torch.distributed.run env); backend "nccl" is RCCL on ROCm,
-    "gloo" is the CPU rehearsal used by tests/test_bench_dist_cpu.py."""
+    "gloo" the CPU rehearsal."""
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != n:
+        raise RuntimeError(f"--gpus {n} but WORLD_SIZE={world}")
     if world > 1:
         import torch.distributed as dist
         if backend == "nccl":
@@ -91,26 +123,37 @@ def job_tflops(world, flops_per_step, steps, elapsed_max):
     return world * flops_per_step * steps / elapsed_max / 1e12
 
 
-def make_layer(dev, act, seed):
-    from smoothquant.fake_quant import W4A4Linear
-    gen = torch.Generator(device=dev).manual_seed(seed)
-    lin = torch.nn.Linear(K, N, bias=True).to(dev, torch.float16)
-    with torch.no_grad():
-        lin.weight.copy_(torch.randn(N, K, generator=gen, device=dev) * 0.02)
-        lin.bias.copy_(torch.randn(N, generator=gen, device=dev) * 0.01)
+# ------------------------------------------------------------------ workload
+def synthetic_layer(gen, dev, dtype):
+    """W ~ N(0, 0.02^2), b ~ N(0, 0.01^2), x ~ N(0, 1) with 1% outlier channels x30, and
+    the importance = mean|x| of a separate 2048-row calibration batch."""
+    W = torch.randn(N, K, generator=gen, device=dev) * 0.02
+    b = torch.randn(N, generator=gen, device=dev) * 0.01
     outl = torch.randperm(K, generator=gen, device=dev)[: K // 100]
     x = torch.randn(M, K, generator=gen, device=dev)
     x[:, outl] *= 30.0
-    x = x.half()
     cal = torch.randn(2048, K, generator=gen, device=dev)
     cal[:, outl] *= 30.0
     imp = cal.abs().mean(0).cpu()
+    return W.to(dtype), b.to(dtype), x.to(dtype), imp
+
+
+def make_layer(dev, act, seed):
+    from smoothquant.fake_quant import W4A4Linear
+    gen = torch.Generator(device=dev).manual_seed(seed)
+    W, b, x, imp = synthetic_layer(gen, dev, torch.float16)
+    lin = torch.nn.Linear(K, N, bias=True).to(dev, torch.float16)
+    with torch.no_grad():
+        lin.weight.copy_(W)
+        lin.bias.copy_(b)
     q = W4A4Linear.from_float(lin, weight_quant="per_group", act_quant=act, importance=imp,
                               salient_prop=P, quant_bits=4, group_size=G)
     return q, x, lin
 
 
 def time_events(fn, iters, stream):
+    """Average ms per call, HIP events recorded on `stream` (the stream the kernels of
+    `fn` are launched on)."""
     start = torch.cuda.Event(enable_timing=True)
     end = torch.cuda.Event(enable_timing=True)
     start.record(stream)
@@ -118,50 +161,89 @@ def time_events(fn, iters, stream):
         fn()
     end.record(stream)
     end.synchronize()
-    return start.elapsed_time(end) / iters  # ms
+    return start.elapsed_time(end) / iters
 
 
-def cpu_baseline(rows, act):
-    """The oracle (numpy, fp16 emulation, fp64-accumulated product) on `rows` rows."""
-    from oracle import fake_quant_oracle as O
-    D = O.DT("fp16")
-    g = np.random.default_rng(0)
-    W = D.rnd(g.standard_normal((N, K)).astype(np.float32) * 0.02)
-    b = D.rnd(g.standard_normal(N).astype(np.float32) * 0.01)
-    x = g.standard_normal((rows, K)).astype(np.float32)
-    outl = g.permutation(K)[: K // 100]
-    x[:, outl] *= 30.0
-    x = D.rnd(x)
-    imp = np.abs(x).mean(0)
-    sal = O.select_salient(imp, P)
-    t0 = time.perf_counter()
-    w_hat = O.w4a4_from_float(W, "per_group", 4, G, sal, D)  # offline, not timed below
-    t_pack = time.perf_counter() - t0
-    t0 = time.perf_counter()
-    O.w4a4_forward(x, w_hat, b, act, 4, G, sal, False, D)
-    dt = time.perf_counter() - t0
-    threads = os.environ.get("OMP_NUM_THREADS") or str(os.cpu_count())
+def cpu_model() -> str:
     try:
-        from threadpoolctl import threadpool_info
-        info = threadpool_info()
-        if info:
-            threads = str(max(i.get("num_threads", 1) for i in info))
-    except Exception:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
         pass
+    return "unknown"
+
+
+def cpu_baseline(act, rows=M, runs=3):
+    """The reference's fake-quant layer on PyTorch-CPU (oracle/torch_cpu.py, pinned
+    bit-exact to the reference goldens), fp32 as in the reference's CPU scripts, every
+    thread torch uses on this host: 1 warm-up + median of `runs` forwards."""
+    from oracle.torch_cpu import CPUFakeQuantLinear
+    gen = torch.Generator().manual_seed(1234)
+    W, b, x, imp = synthetic_layer(gen, "cpu", torch.float32)
+    x = x[:rows].contiguous()
+    layer = CPUFakeQuantLinear(W, b, "per_group", act, 4, G, imp, P)
+    layer(x)  # warm-up
+    ts = []
+    for _ in range(runs):
+        t0 = time.perf_counter()
+        layer(x)
+        ts.append(time.perf_counter() - t0)
+    dt = statistics.median(ts)
     return {
-        "value": 2.0 * rows * N * K / dt / 1e12,
+        "value": round(2.0 * rows * N * K / dt / 1e12, 4),
         "unit": "TFLOP/s",
-        "cores": int(threads),
-        "kind": "port",
-        "sample": (f"oracle/fake_quant_oracle.py W4A4Linear forward, fp16 emulation, "
-                   f"act {act}, {rows} of {M} rows (K=N={K}, G={G}, p={P}); "
-                   f"{dt:.2f} s forward (+{t_pack:.2f} s offline weight quant, untimed)"),
+        "cores": torch.get_num_threads(),
+        "kind": "torch-cpu-fp32",
+        "cpu_model": cpu_model(),
+        "sample": (f"oracle/torch_cpu.py CPUFakeQuantLinear (the reference's fake_quant ops, "
+                   f"bit-exact to its goldens), fp32, weight per_group + act {act}, "
+                   f"{rows}x{K}->{N}, G={G}, p={P}; median of {runs} after 1 warm-up: "
+                   f"{dt:.3f} s per forward (runs {', '.join(f'{t:.3f}' for t in ts)})"),
     }
 
 
-def main():
-    args = parse()
-    rank, world, local = setup_dist(args.gpus)
+# ------------------------------------------------------------------ rehearsal (CPU)
+def rehearsal(args, rank, world):
+    """The launcher / barrier / max-over-ranks / report path on CPU with gloo: the step is
+    the CPU fake-quant layer on a 64-row batch of the config-2 layer."""
+    from oracle.torch_cpu import CPUFakeQuantLinear
+    gen = torch.Generator().manual_seed(1234 + rank)
+    W, b, x, imp = synthetic_layer(gen, "cpu", torch.float32)
+    layer = CPUFakeQuantLinear(W[:256], b[:256], "per_group", args.act, 4, G, imp, P)
+    xs = x[:64].contiguous()
+    for _ in range(args.warmup):
+        layer(xs)
+    barrier(world)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        layer(xs)
+    barrier(world)
+    elapsed = max_over_ranks(time.perf_counter() - t0, world, torch.device("cpu"))
+    flops = 2.0 * 64 * 256 * K
+    return {"metric": "rehearsal (CPU/gloo launcher check; not a measurement)",
+            "value": round(job_tflops(world, flops, args.steps, elapsed), 6),
+            "unit": "TFLOP/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4)}
+
+
+# ------------------------------------------------------------------ main
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return launch_children(args, argv)
+    rank, world, local = setup_dist(args.gpus, "gloo" if args.rehearsal else "nccl")
+    if args.rehearsal:
+        out = rehearsal(args, rank, world)
+        if rank == 0:
+            print(json.dumps(out), flush=True)
+        if world > 1:
+            import torch.distributed as dist
+            dist.destroy_process_group()
+        return 0
+
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     from smoothquant import ops
@@ -170,9 +252,44 @@ def main():
     pw = q.packed()
     # what W4A4Linear(kernel="auto") runs for this layer
     use_f8 = ops.F8_AUTO and ops.f8_eligible(pw, args.act, 4)
-    use_i8 = not use_f8 and ops.I8_AUTO and ops.i8_eligible(pw, args.act, 4)
     stream = torch.cuda.current_stream(dev)
+    flops = 2.0 * M * N * K
 
+    # ---- secondary measurements first (the chip is busy when the timed region starts)
+    # dominant kernel: the GEMM, timed alone on the stream it is launched on
+    if use_f8:
+        a8, sa, xs = ops.quant_act_f8(x, pw, args.act, 4)
+        gemm = lambda: ops.gemm_f8(a8, sa, xs, pw, lin.bias)  # noqa: E731
+        quant = lambda: ops.quant_act_f8(x, pw, args.act, 4)  # noqa: E731
+        kdt, kname = "f8", "sqmp::gemm_f8_kernel<F16> (e4m3 block-scaled MFMA)"
+    else:
+        a = ops.quant_act_fp(x, pw, args.act, 4, G)
+        gemm = lambda: ops.gemm_fq(a, pw, lin.bias)  # noqa: E731
+        quant = lambda: ops.quant_act_fp(x, pw, args.act, 4, G)  # noqa: E731
+        kdt, kname = "f16", "sqmp::gemm_fq6_kernel<F16,1,256>"
+    sec_iters = max(20, args.steps)
+    for _ in range(10):
+        gemm()
+    gemm_ms = time_events(gemm, sec_iters, stream)
+    quant_ms = time_events(quant, sec_iters, stream)
+    # vendor dense fp16 GEMM (hipBLASLt via torch) on the same shape, unquantized: what
+    # the reference's F.linear costs on this GPU, without any act-quant
+    wd = lin.weight.detach()
+    dense = lambda: torch.nn.functional.linear(x, wd, lin.bias)  # noqa: E731
+    for _ in range(10):
+        dense()
+    dense_ms = time_events(dense, sec_iters, stream)
+    # the reference's own fake-quant forward (PyTorch ops, tools/torch_fakequant.py) on
+    # this GPU, same layer and input
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from torch_fakequant import TorchFakeQuantLinear
+    ref = TorchFakeQuantLinear(q.weight, lin.bias.detach(), q.salient_indices, args.act, 4, G)
+    y_ref, y_ours = ref(x), q(x.clone())
+    ref_rel = float((y_ref.float() - y_ours.float()).norm() / y_ref.float().norm())
+    del y_ref, y_ours
+    ref_ms = time_events(lambda: ref(x), max(5, args.steps // 5), stream)
+
+    # ---- the timed region: W warm-up steps, then exactly K steps
     def step():
         return q(x)
 
@@ -189,48 +306,13 @@ def main():
     elapsed = time.perf_counter() - t0
     elapsed = max_over_ranks(elapsed, world, dev)
     ms_per_step = elapsed / args.steps * 1e3
-    flops = 2.0 * M * N * K
     value = job_tflops(world, flops, args.steps, elapsed)
 
-    # ---- dominant kernel: the GEMM, timed alone on the same stream with HIP events
-    if use_f8:
-        a8, sa, xs = ops.quant_act_f8(x, pw, args.act, 4)
-        gemm = lambda: ops.gemm_f8(a8, sa, xs, pw, lin.bias)  # noqa: E731
-        quant = lambda: ops.quant_act_f8(x, pw, args.act, 4)  # noqa: E731
-        kdt = "f8"
-    elif use_i8:
-        a8, sa, xs = ops.quant_act_i8(x, pw, args.act, 4)
-        gemm = lambda: ops.gemm_i8(a8, sa, xs, pw, lin.bias)  # noqa: E731
-        quant = lambda: ops.quant_act_i8(x, pw, args.act, 4)  # noqa: E731
-        kdt = "i8"
-    else:
-        a = ops.quant_act_fp(x, pw, args.act, 4, G)
-        gemm = lambda: ops.gemm_fq(a, pw, lin.bias)  # noqa: E731
-        quant = lambda: ops.quant_act_fp(x, pw, args.act, 4, G)  # noqa: E731
-        kdt = "f16"
-    for _ in range(max(3, args.warmup)):
-        gemm()
-    gemm_ms = time_events(gemm, max(10, args.steps), stream)
-    quant_ms = time_events(quant, max(10, args.steps), stream)
     achieved = flops / (gemm_ms * 1e-3) / 1e12
-    # reference point: the vendor dense fp16 GEMM (hipBLASLt via torch) on the same shape,
-    # unquantized -- what the reference's F.linear costs on this GPU, without any act-quant
-    wd = lin.weight.detach()
-    dense = lambda: torch.nn.functional.linear(x, wd, lin.bias)  # noqa: E731
-    for _ in range(max(3, args.warmup)):
-        dense()
-    dense_ms = time_events(dense, max(10, args.steps), stream)
-    # reference point: the reference's own fake-quant forward (restated in PyTorch ops,
-    # tools/torch_fakequant.py) on this GPU, same layer and input
-    sys.path.insert(0, os.path.join(ROOT, "tools"))
-    from torch_fakequant import TorchFakeQuantLinear
-    ref = TorchFakeQuantLinear(q.weight, lin.bias.detach(), q.salient_indices, args.act, 4, G)
-    y_ref, y_ours = ref(x), q(x.clone())
-    ref_rel = float((y_ref.float() - y_ours.float()).norm() / y_ref.float().norm())
-    ref_ms = time_events(lambda: ref(x), max(5, args.steps // 5), stream)
-    # prepass algorithmic bytes: read x (colmax) + read x (quantize) + write operand(s)
+    t_roof = contract_roofline_s(pw.S)
+    # prepass algorithmic bytes: read x (stats) + read x (quantize) + write the operand(s)
     xbytes = M * K * 2
-    if use_i8 or use_f8:
+    if use_f8:
         wbytes = M * pw.Kp + M * 4 + M * pw.S_pad * 2
         reads = 2 if args.act == "per_tensor" else 1
     else:
@@ -242,8 +324,9 @@ def main():
     prof = os.path.join(ROOT, "profiles", f"pmc_gemm_{kdt}_{args.act}.json")
     if os.path.exists(prof):
         try:
-            traffic = json.load(open(prof)).get("hbm_bytes_per_launch")
-        except Exception:
+            with open(prof) as f:
+                traffic = json.load(f).get("hbm_bytes_per_launch")
+        except (OSError, ValueError):
             traffic = None
 
     out = {
@@ -265,7 +348,7 @@ def main():
                          f"{int(P * 100)}% salient fp16 side-GEMM"),
             "M": M, "K": K, "N": N, "group_size": G, "salient_prop": P,
             "salient_channels": pw.S,
-            "kernel": "gemm_f8" if use_f8 else "gemm_i8" if use_i8 else "gemm_fq",
+            "kernel": "gemm_f8" if use_f8 else "gemm_fq",
             "parallelism": f"replicas x{world}",
         },
         "roofline": {
@@ -275,10 +358,14 @@ def main():
             "unit": "TFLOP/s",
             "frac": round(achieved / PEAK_TFLOPS[kdt], 4),
             "traffic": traffic,
-            "kernel": ("sqmp::gemm_f8_kernel<F16> (e4m3 block-scaled MFMA)" if use_f8 else
-                       "sqmp::gemm_i8v2_kernel<F16>" if use_i8 else "sqmp::gemm_fq6_kernel<F16,1>"),
+            "kernel": kname,
             "avg_ms": round(gemm_ms, 4),
             "algorithmic_flops_per_launch": flops,
+            "t_roof_contract_us": round(t_roof * 1e6, 2),
+            "frac_contract_gemm": round(t_roof / (gemm_ms * 1e-3), 4),
+            "frac_contract_step": round(t_roof / (ms_per_step * 1e-3), 4),
+            "note": ("frac = achieved / dense MFMA peak of the kernel's dtype; frac_contract_* "
+                     "= BASELINE.md §2 T_roof (2MNK'/P_i8 + 2MNS/P_f16) / GEMM time, / step time"),
         },
         "reference_points": {
             "reference_fakequant_forward_ms": round(ref_ms, 4),
@@ -298,13 +385,14 @@ def main():
         },
     }
     if rank == 0 and world == 1 and not args.no_cpu:
-        out["cpu_baseline"] = cpu_baseline(args.cpu_rows, args.act)
+        out["cpu_baseline"] = cpu_baseline(args.act)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
         import torch.distributed as dist
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -379,8 +379,15 @@ class W4A4Linear(nn.Module):
             for name in _PACKED_BUFFERS:
                 t = sd.get(prefix + name)
                 setattr(self, name, None if t is None else torch.empty_like(t))
-            if prefix + "bias" in sd and self.bias is not None:
-                self.bias = torch.empty_like(sd[prefix + "bias"])
+            t = sd.get(prefix + "bias")
+            if t is not None and self.bias is not None:
+                if isinstance(self.bias, nn.Parameter):
+                    # from_float aliased the source Linear's bias Parameter (:369-370):
+                    # give the module its own, shaped like the checkpoint's
+                    self.bias = nn.Parameter(torch.empty_like(t, device=self.bias.device),
+                                             requires_grad=False)
+                elif self.bias.shape != t.shape or self.bias.dtype != t.dtype:
+                    self.bias = torch.empty_like(t, device=self.bias.device)
         elif prefix + "weight" in sd:
             # a reference checkpoint (dequantized `weight` buffer): stored as given
             self.weight = sd[prefix + "weight"]
@@ -406,19 +413,45 @@ class W4A4Linear(nn.Module):
         super().__setattr__(name, value)
 
     def _apply(self, fn, recurse=True):
-        # A dtype cast (model.half(), .to(torch.bfloat16)) turns the reference's dequantized
-        # W_hat buffer into cast(W_hat).  Mirror that: dequantize, cast, keep it as a dense
-        # operand (casting per-group scales instead would change the values).
+        # A dtype cast (model.half(), .float(), .to(torch.bfloat16)) turns the reference's
+        # dequantized W_hat buffer into cast(W_hat) (fake_quant.py:272-277 / nn.Module).
+        # The packed form survives the cast when cast(code * s) == code * cast(s) for every
+        # weight (e.g. fp16 / bf16 -> fp32 always): the codes stay, the scales and the
+        # salient slice are cast.  Otherwise the layer keeps the reference's values as a
+        # dense operand and says so (a dense GEMM moves 4x the weight bytes).
         if self._meta is not None and self.w_scale is not None:
-            probe = fn(torch.empty(0, dtype=self._meta["dtype"], device=self.w_scale.device))
-            if probe.dtype != self._meta["dtype"]:
-                w_new = fn(self.weight)
-                out = super()._apply(fn, recurse)
-                name = self.weight_quant_name
-                self._pack_from(w_new, "None")
-                self.weight_quant_name = name
-                return out
+            old = self._meta["dtype"]
+            probe = fn(torch.empty(0, dtype=old, device=self.w_scale.device))
+            if probe.dtype != old:
+                return self._apply_cast(fn, recurse, probe.dtype)
         return super()._apply(fn, recurse)
+
+    def _apply_cast(self, fn, recurse, new_dtype):
+        w_new = fn(self.weight)
+        pw = self.packed()
+        keep_packed = pw.n_bits == 0
+        if not keep_packed:
+            cand = ops.PackedWeight(pw.codes, fn(pw.wscale), fn(pw.wsal), pw.perm, pw.amap,
+                                    pw.amap_fq, pw.nonsal, pw.salient, pw.N, pw.K, pw.S,
+                                    pw.S_pad, pw.Kp, pw.Gw, pw.ngw, pw.n_bits, pw.wmode,
+                                    new_dtype)
+            keep_packed = bool(torch.equal(ops.dequant_weight(cand), w_new.to(pw.codes.device)))
+        if keep_packed:
+            out = super()._apply(fn, recurse)
+            self._meta = dict(self._meta, dtype=new_dtype)
+            self.__dict__.pop("_pw_cache", None)
+            return out
+        import warnings
+        warnings.warn(
+            f"W4A4Linear({self.in_features}, {self.out_features}): casting {pw.dtype} -> "
+            f"{new_dtype} changes the dequantized weight values (cast(code*s) != code*cast(s)); "
+            "the layer keeps the reference's cast(W_hat) as a DENSE operand -- quantize the "
+            "model in the target dtype to keep the int4 packing", RuntimeWarning, stacklevel=3)
+        out = super()._apply(fn, recurse)
+        name = self.weight_quant_name
+        self._pack_from(w_new, "None")
+        self.weight_quant_name = name
+        return out
 
     def to(self, *args, **kwargs):
         super().to(*args, **kwargs)
@@ -452,7 +485,8 @@ class W4A4Linear(nn.Module):
         if bias is not None and bias.dtype != pw.dtype:
             raise RuntimeError(f"bias dtype {bias.dtype} does not match {pw.dtype}")
         use_f8 = (self.kernel == "f8" or
-                  (self.kernel == "auto" and ops.F8_AUTO and ops.f8_eligible(pw, amode, bits)))
+                  (self.kernel == "auto" and ops.F8_AUTO and ops.f8_eligible(pw, amode, bits)
+                   and ops.f8_input_ok(xc)))
         use_i8 = not use_f8 and (
             self.kernel == "i8" or
             (self.kernel == "auto" and ops.I8_AUTO and ops.i8_eligible(pw, amode, bits)))
@@ -501,6 +535,12 @@ class W4A4Linear(nn.Module):
         if weight_quant not in _WEIGHT_EXT:
             raise ValueError(f"Invalid weight_quant: {weight_quant}")         # :361
         new_module._pack_from(module.weight.data, weight_quant)
+        if weight_quant in ("per_channel", "per_tensor"):
+            # the reference quantizes module.weight IN PLACE for these modes and then
+            # restores the salient columns through the alias (:349-355, :363-365): the
+            # source Linear (and any weight tied to it) ends up holding W_hat
+            with torch.no_grad():
+                module.weight.data.copy_(new_module.weight.to(module.weight.device))
         if module.bias is not None:
             new_module.bias = module.bias                                     # :369-370
         return new_module

@@ -309,6 +309,9 @@ def fake_quant_inplace(t2: torch.Tensor, act_quant: str, n_bits: int, group_size
         _WS.pop((t2.device.index, stream, C, C), None)
         check(status, "fake_quant")
     e["stats"] = None  # the sorted-column list now describes t2, not a layer input
+    # the kernel wrote t2 through a raw pointer: bump its version counter so statistics
+    # another workspace recorded for this (now quantized) tensor are not reused
+    torch.autograd.graph.increment_version(t2)
     return t2
 
 
@@ -385,10 +388,18 @@ def gemm_f8(a8: torch.Tensor, sa: torch.Tensor, xs: torch.Tensor, pw: PackedWeig
 
 def f8_eligible(pw: PackedWeight, act_quant: str, act_bits: int) -> bool:
     """Whether the block-scaled FP8 MFMA path computes this layer: one act scale per row,
-    4-bit codes on both sides (exact in e4m3), weight groups of whole 64-blocks."""
+    4-bit codes on both sides (exact in e4m3), weight groups of whole 64-blocks, and the
+    lane-contiguous quantizer's shape limits (K % 8 == 0, K <= 16384; quant_lc_supported in
+    sqmp_actquant.hip).  The input pointer's 16-B alignment is checked per call
+    (f8_input_ok)."""
     return (act_quant in ("per_token", "per_tensor") and pw.dtype != torch.float32
             and pw.n_bits == 4 and pw.dense is None and pw.Gw % 64 == 0 and act_bits <= 4
-            and pw.K <= 16384)
+            and pw.K <= 16384 and pw.K % 8 == 0)
+
+
+def f8_input_ok(x2: torch.Tensor) -> bool:
+    """The e4m3 quantizer reads x with 16-B loads: x must be contiguous and 16-B aligned."""
+    return x2.is_contiguous() and x2.data_ptr() % 16 == 0
 
 
 # Whether W4A4Linear(kernel="auto") takes the integer path for eligible layers.  Off: on

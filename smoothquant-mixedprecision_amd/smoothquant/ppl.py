@@ -1,59 +1,75 @@
-"""Perplexity harness: the reference's Evaluator.
+"""Perplexity harness with the reference's Evaluator interface.
 
     Evaluator(dataset, tokenizer, device, n_samples=10, batch_size=2048)
-        run_experiments/run_experiments.py:86-123 (smoothquant/ppl_eval.py:32-61 is the same
-        with n_samples=40 and batch_size fixed at 2048)
+        behaviour of run_experiments/run_experiments.py:86-123 (smoothquant/ppl_eval.py:32-61
+        is the same with n_samples=40)
 
-The whole split is joined with "\\n\\n" and tokenized once; window i is tokens
-[i*B, (i+1)*B); the loss is the mean cross-entropy over the B-1 shifted labels, scaled by
-B, and PPL = exp(sum(nll) / (n * B)).  n_samples=None (or 0) evaluates every full window.
-`dataset` is anything with a "text" column (a `datasets.Dataset`, or {"text": [...]}) --
-pass local data when the hub is not reachable; `input_ids` may also be given directly.
+The split is joined with "\\n\\n" and tokenized once into a [1, T] id stream.  Window i is
+ids[:, i*B:(i+1)*B]; its negative log-likelihood is B x the mean cross-entropy of the
+B-1 next-token predictions (fp32 logits), and PPL = exp(sum of window NLLs / (n*B)).
+n_samples=None/0 means every full window.  Without hub access pass a dataset with a
+"text" column, or the token ids directly (`input_ids=`).  `last_tokens_per_s` is the
+throughput of the last evaluate() (windows x B tokens over its wall time).
 """
+from __future__ import annotations
+
 import time
 
 import torch
-import torch.nn as nn
+import torch.nn.functional as F
 
 try:
-    from tqdm import tqdm as _tqdm
+    from tqdm import tqdm as _progress
 except ImportError:  # pragma: no cover
-    def _tqdm(it, **_kw):
+    def _progress(it, **_kw):
         return it
+
+
+def window_nll(model, window: torch.Tensor) -> torch.Tensor:
+    """B x mean next-token cross-entropy of one [1, B] window (fp32 scalar tensor)."""
+    logits = model(window).logits
+    pred = logits[:, :-1, :].float()
+    target = window[:, 1:].to(pred.device)
+    ce = F.cross_entropy(pred.reshape(-1, pred.shape[-1]), target.reshape(-1))
+    return ce.float() * window.shape[1]
+
+
+def _model_device(model, fallback):
+    for p in model.parameters():
+        return p.device
+    return fallback
 
 
 class Evaluator:
     def __init__(self, dataset, tokenizer, device, n_samples=10, batch_size=2048, input_ids=None):
-        self.dataset = dataset
         self.tokenizer = tokenizer
         self.device = device
-        if input_ids is None:
-            input_ids = tokenizer("\n\n".join(dataset["text"]), return_tensors="pt").input_ids
-        self.dataset = input_ids.to(device)
+        ids = input_ids
+        if ids is None:
+            ids = tokenizer("\n\n".join(dataset["text"]), return_tensors="pt").input_ids
+        self.dataset = ids.to(device)
         self.n_samples = n_samples
         self.batch_size = batch_size
         self.last_tokens_per_s = None
 
+    def windows(self):
+        B = self.batch_size
+        n = self.n_samples or self.dataset.shape[1] // B
+        return [self.dataset[:, i * B:(i + 1) * B] for i in range(n)]
+
     @torch.no_grad()
     def evaluate(self, model):
         model.eval()
-        nlls = []
-        B = self.batch_size
-        n_samples = self.n_samples if self.n_samples else self.dataset.size(1) // B
-        dev = next(model.parameters()).device if any(True for _ in model.parameters()) else self.device
-        t0 = time.perf_counter()
-        for i in _tqdm(range(n_samples), desc="Evaluating"):
-            batch = self.dataset[:, i * B:(i + 1) * B].to(dev)
-            lm_logits = model(batch).logits
-            shift_logits = lm_logits[:, :-1, :].contiguous().float()
-            shift_labels = self.dataset[:, i * B:(i + 1) * B][:, 1:].to(shift_logits.device)
-            loss = nn.CrossEntropyLoss()(shift_logits.view(-1, shift_logits.size(-1)),
-                                         shift_labels.reshape(-1))
-            nlls.append(loss.float() * B)
+        dev = _model_device(model, self.device)
+        wins = self.windows()
+        start = time.perf_counter()
+        total = torch.stack([window_nll(model, w.to(dev))
+                             for w in _progress(wins, desc="Evaluating")]).sum()
         if torch.cuda.is_available():
             torch.cuda.synchronize()
-        self.last_tokens_per_s = n_samples * B / (time.perf_counter() - t0)
-        return torch.exp(torch.stack(nlls).sum() / (n_samples * B))
+        tokens = len(wins) * self.batch_size
+        self.last_tokens_per_s = tokens / (time.perf_counter() - start)
+        return torch.exp(total / tokens)
 
 
-__all__ = ["Evaluator"]
+__all__ = ["Evaluator", "window_nll"]

@@ -1,0 +1,113 @@
+"""Golden fixtures for BASELINE configs 1, 3 and 4 at their real layer dimensions, from the
+REFERENCE (run on this container's CPU; tests/config_cases.py defines the cases).
+
+For every case: build the seeded random-init model (config_cases.build), collect the
+mean|x| calibration features with the reference's hook formula (run_experiments.py:55-84)
+and sum them into each Linear's importance (fake_quant.py:396 / :486), quantize with the
+reference's own `quantize_opt` / `quantize_llama_like` (argsort pinned stable, as in
+gen_golden.py) and run the eval sequence.  Stored (small; no model tensors):
+  <key>__imp__<linear>    fp32 importance the quantizer consumed (fed back as [imp])
+  <key>__sal__<linear>    the reference's salient_indices (int32)
+  meta: per linear the sha256 of W_hat (-0.0 folded to +0.0) and its fp64 sum, shapes and
+        modes; per case the eval loss (mean next-token CE, fp64) and the logits norm
+  <key>__logits, __lse    fp32 logits[:, :VOCAB_SLICE] and the fp64 logsumexp over the
+                          vocabulary at config_cases.positions(case)
+
+Usage:  python tests/golden/gen_config_golden.py     (needs /root/reference)
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+sys.path.insert(0, os.path.dirname(HERE))
+from gen_golden import load_reference  # noqa: E402
+import config_cases as C  # noqa: E402
+
+
+@torch.no_grad()
+def importance_of(model, blocks):
+    """{linear name: sum over blocks of mean_m |x| (model dtype), cast to fp32}."""
+    feat = {}
+
+    def hook(name, m, inp, out):
+        x = inp[0] if isinstance(inp, tuple) else inp
+        feat.setdefault(name, []).append(x.view(-1, x.shape[-1]).abs().mean(dim=0).cpu())
+
+    hs = [m.register_forward_hook(lambda m, i, o, n=n: hook(n, m, i, o))
+          for n, m in model.named_modules() if isinstance(m, nn.Linear)]
+    for b in blocks:
+        model(b)
+    for h in hs:
+        h.remove()
+    return {n: sum(v).float() for n, v in feat.items()}
+
+
+@torch.no_grad()
+def eval_loss(logits, ids):
+    pred = logits[:, :-1].double()
+    return float(nn.functional.cross_entropy(pred.reshape(-1, pred.shape[-1]),
+                                             ids[:, 1:].reshape(-1)))
+
+
+def main():
+    ref = load_reference()
+    torch.set_num_threads(os.cpu_count() or 8)
+    arrays, cases = {}, {}
+    for case in C.CASES:
+        t0 = time.time()
+        key = case["key"]
+        model = C.build(case)
+        imp = importance_of(model, C.tokens(case, "cal"))
+        for n, v in imp.items():
+            arrays[f"{key}__imp__{n}"] = v.numpy()
+        # input_feat as the quantizers index it ("model." + module path); one-element lists
+        # so sum(...) returns the stored fp32 importance unchanged
+        feat = {n: [v] for n, v in imp.items()}
+        q = getattr(ref, case["quantizer"])(model, input_feat=feat, **case["kwargs"])
+        linears = {}
+        for n, m in q.named_modules():
+            if type(m).__name__ != "W4A4Linear":
+                continue
+            sal = m.salient_indices
+            if sal is not None:
+                arrays[f"{key}__sal__{n}"] = sal.numpy().astype(np.int32)
+            w = m.weight
+            linears[n] = dict(N=int(w.shape[0]), K=int(w.shape[1]),
+                              weight_quant=m.weight_quant_name, act_quant=m.act_quant_name,
+                              output_quant=m.output_quant_name,
+                              n_salient=0 if sal is None else int(sal.numel()),
+                              what_sha256=C.what_digest(w),
+                              what_sum=float(w.double().sum()))
+        ids = C.tokens(case, "eval")
+        with torch.no_grad():
+            logits = q(ids).logits.float()
+        pos = C.positions(case)
+        # a vocabulary slice of the logits at the stored positions + the full-vocabulary
+        # logsumexp there (keeps the fixture small for the 50272-entry OPT-125M head)
+        arrays[f"{key}__logits"] = logits[0, pos, :C.VOCAB_SLICE].numpy()
+        arrays[f"{key}__lse"] = torch.logsumexp(logits[0, pos].double(), dim=-1).numpy()
+        cases[key] = dict(n_linears=len(linears), linears=linears,
+                          loss=eval_loss(logits, ids),
+                          logits_norm=float(logits.double().norm()),
+                          positions=pos.tolist())
+        print(f"{key}: {len(linears)} W4A4Linear, loss {cases[key]['loss']:.5f}, "
+              f"{time.time() - t0:.1f} s", flush=True)
+        del model, q, logits
+    meta = dict(source="adithyab100/smoothquant-mixedprecision reference fake_quant.py on CPU "
+                       "(argsort pinned stable=True)", torch=torch.__version__, cases=cases)
+    arrays["meta_json"] = np.frombuffer(json.dumps(meta).encode(), dtype=np.uint8)
+    np.savez_compressed(C.GOLDEN, **arrays)
+    print(f"wrote {C.GOLDEN}: {os.path.getsize(C.GOLDEN) / 1e6:.2f} MB")
+
+
+if __name__ == "__main__":
+    main()

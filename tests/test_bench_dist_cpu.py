@@ -49,3 +49,22 @@ def test_bench_replicas_gloo_world2():
         assert w == world
         assert e == 1.5  # max over ranks
         assert abs(v - world * flops * 10 / 1.5 / 1e12) < 1e-9 * v
+
+
+def test_bench_cli_spawns_world2():
+    """`python bench.py --gpus 2` without a torch.distributed.run environment starts one
+    (child process, one rank per device) and reports n_gpus 2; the CPU rehearsal runs the
+    same launcher, barriers and max-over-ranks over gloo."""
+    import json
+    import subprocess
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env["OMP_NUM_THREADS"] = "1"
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2",
+                          "--rehearsal", "--steps", "3", "--warmup", "1"],
+                         env=env, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 2 and rec["steps"] == 3 and rec["value"] > 0

@@ -92,3 +92,62 @@ def test_f8_gemm_vs_oracle(case):
     q.kernel = "f8"
     y = to_np(q(to_t(x, dt, dev)))
     assert rel(y, want) < TOL_I8[dt], rel(y, want)
+
+
+def test_f8_full_size_config2_per_token():
+    """BASELINE config 2 with per_token activations on the FP8 path (the default for this
+    layer): y against an fp64 product of the faithful operands (the per_token q_x, which
+    test_gpu_parity pins bit-exact, and W_hat) at M = 16384, K = N = 4096; and the e4m3
+    codes of sampled rows decode to that q_x exactly."""
+    dev = _dev()
+    from smoothquant import ops
+    from smoothquant.fake_quant import W4A4Linear
+    M, K, N, Gs, p = 16384, 4096, 4096, 128, 0.10
+    gen = torch.Generator(device=dev).manual_seed(5)
+    lin = torch.nn.Linear(K, N, bias=True).to(dev, torch.float16)
+    with torch.no_grad():
+        lin.weight.copy_((torch.randn(N, K, generator=gen, device=dev) * 0.02).half())
+        lin.bias.copy_((torch.randn(N, generator=gen, device=dev) * 0.01).half())
+    x = torch.randn(M, K, generator=gen, device=dev)
+    x[:, torch.randperm(K, generator=gen, device=dev)[:41]] *= 30
+    x = x.half()
+    imp = x[:2048].float().abs().mean(0).cpu()
+    q = W4A4Linear.from_float(lin, weight_quant="per_group", act_quant="per_token",
+                              importance=imp, salient_prop=p, group_size=Gs)
+    pw = q.packed()
+    assert ops.f8_eligible(pw, "per_token", 4)
+    y = q(x)  # kernel "auto" -> FP8
+    a = ops.quant_act_fp(x, pw, "per_token", 4, Gs)
+    b_full = torch.cat([ops.dequant_weight_packed(pw), pw.wsal], dim=1)
+    ref = torch.addmm(lin.bias.double(), a.double(), b_full.double().t())
+    r = float((y.double() - ref).norm() / ref.norm())
+    assert r < TOL_I8["fp16"], r
+    a8, sa, _ = ops.quant_act_f8(x, pw, "per_token", 4)
+    rows = torch.arange(0, M, 509, device=dev)
+    codes = torch.from_numpy(e4m3_to_float(a8[rows].cpu().numpy()))
+    dec = (codes * sa[rows].cpu().double()[:, None]).half()  # D(c * sa): one rounding
+    assert torch.equal(dec.float()[:, :pw.Kp], a[rows, :pw.Kp].float().cpu())
+
+
+def test_per_token_k_not_multiple_of_8_falls_back():
+    """per_channel weights + per_token acts (the reference's from_float defaults) with
+    K % 8 != 0: kernel "auto" must take the faithful path (the e4m3 quantizer needs K % 8
+    == 0) and match the oracle."""
+    dev = _dev()
+    from smoothquant import ops
+    D = O.DT("fp16")
+    g = np.random.default_rng(21)
+    K, N, M = 100, 64, 33
+    W = D.rnd(g.standard_normal((N, K)) * 0.02)
+    b = D.rnd(g.standard_normal(N) * 0.01)
+    imp = np.abs(g.standard_normal(K)).astype(np.float32)
+    for p in (0.0, 0.05):
+        q = make_layer(W, b, "fp16", dev, weight_quant="per_channel", act_quant="per_token",
+                       importance=torch.from_numpy(imp), salient_prop=p)
+        assert not ops.f8_eligible(q.packed(), "per_token", 4)
+        x = D.rnd(g.standard_normal((M, K)))
+        sal = O.select_salient(imp, p)
+        w_hat = O.w4a4_from_float(W, "per_channel", 4, 128, sal, D)
+        want = D.f32(O.w4a4_forward(x, w_hat, b, "per_token", 4, 128, sal, False, D))
+        y = to_np(q(to_t(x, "fp16", dev)))
+        assert rel(y, want) < 2e-3

@@ -391,3 +391,69 @@ def test_packed_checkpoint_roundtrip(tmp_path):
     y1 = fresh(x.clone())
     assert bits_equal(to_np(y1), to_np(y0))
     assert bits_equal(to_np(fresh[0].weight), to_np(model[0].weight))
+
+
+# ------------------------------------------------------------------ casts (.to / _apply)
+def test_dtype_cast_keeps_packing_when_exact():
+    """model.float() on an fp16 W4A4Linear: cast(code * s) == code * cast(s) exactly, so
+    the layer stays int4-packed (no dense fallback) and equals the reference's cast(W_hat)
+    layer; a cast that changes the values (fp32 -> fp16 here) keeps the reference's values
+    as a dense operand and warns."""
+    dev = _dev()
+    import warnings
+    D16, D32 = O.DT("fp16"), O.DT("fp32")
+    g = np.random.default_rng(17)
+    K, N, M = 512, 256, 64
+    W = D16.rnd(g.standard_normal((N, K)) * 0.02)
+    b = D16.rnd(g.standard_normal(N) * 0.01)
+    imp = np.abs(g.standard_normal(K)).astype(np.float32)
+    q = make_layer(W, b, "fp16", dev, weight_quant="per_group", act_quant="per_group",
+                   importance=torch.from_numpy(imp), salient_prop=0.05, group_size=64)
+    w16 = to_np(q.weight)
+    with warnings.catch_warnings():
+        warnings.simplefilter("error")
+        q.float()
+    pw = q.packed()
+    assert pw.n_bits == 4 and pw.dtype == torch.float32 and q.w_codes.dtype == torch.uint8
+    assert bits_equal(to_np(q.weight), w16)  # cast(W_hat) fp16 -> fp32 is exact
+    x = D32.rnd(g.standard_normal((M, K)))
+    sal = O.select_salient(imp, 0.05)
+    want = D32.f32(O.w4a4_forward(x, w16, D32.rnd(b), "per_group", 4, 64, sal, False, D32))
+    assert rel(to_np(q(to_t(x, "fp32", dev))), want) < TOL_FQ["fp32"]
+    # fp32-quantized layer cast to fp16: the values change -> dense + warning
+    W32 = D32.rnd(g.standard_normal((N, K)) * 0.02)
+    q2 = make_layer(W32, None, "fp32", dev, weight_quant="per_group", act_quant="per_group",
+                    importance=torch.from_numpy(imp), salient_prop=0.05, group_size=64)
+    w_cast = to_np(q2.weight.half())
+    with pytest.warns(RuntimeWarning):
+        q2.half()
+    assert q2.packed().n_bits == 0 and bits_equal(to_np(q2.weight), w_cast)
+
+
+def test_packed_checkpoint_loads_into_from_float_module(tmp_path):
+    """A checkpoint loads into a model whose layers are already W4A4Linear.from_float
+    modules (their bias is the aliased nn.Parameter of the source Linear,
+    fake_quant.py:369-370) and reproduces the saved model's output exactly."""
+    dev = _dev()
+    import os
+    from smoothquant.checkpoint import load_quantized, save_quantized
+    g = np.random.default_rng(23)
+    K, N = 256, 256
+    imp = torch.from_numpy(np.abs(g.standard_normal(K)).astype(np.float32))
+
+    def model_from(seed):
+        gg = np.random.default_rng(seed)
+        W = gg.standard_normal((N, K)).astype(np.float32) * 0.02
+        b = gg.standard_normal(N).astype(np.float32) * 0.01
+        return torch.nn.Sequential(
+            make_layer(W, b, "fp16", dev, weight_quant="per_group", act_quant="per_group",
+                       importance=imp, salient_prop=0.05, group_size=64))
+
+    src, dst = model_from(1), model_from(2)
+    assert isinstance(dst[0].bias, torch.nn.Parameter)
+    x = to_t(g.standard_normal((32, K)), "fp16", dev)
+    y0 = src(x.clone())
+    p = os.path.join(tmp_path, "q.pt")
+    save_quantized(src, p)
+    load_quantized(dst, p)
+    assert bits_equal(to_np(dst(x.clone())), to_np(y0))
