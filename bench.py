@@ -267,7 +267,9 @@ def main(argv=None):
         gemm = lambda: ops.gemm_fq(a, pw, lin.bias)  # noqa: E731
         quant = lambda: ops.quant_act_fp(x, pw, args.act, 4, G)  # noqa: E731
         kdt, kname = "f16", "sqmp::gemm_fq6_kernel<F16,1,256>"
-    sec_iters = max(20, args.steps)
+    # ~0.1 s of back-to-back GEMMs per measurement: long enough for the chip to settle at
+    # the clock it holds under this load (DVFS, MI355X_MICROARCH.md), whatever --steps is
+    sec_iters = max(200, args.steps)
     for _ in range(10):
         gemm()
     gemm_ms = time_events(gemm, sec_iters, stream)
@@ -287,7 +289,7 @@ def main(argv=None):
     y_ref, y_ours = ref(x), q(x.clone())
     ref_rel = float((y_ref.float() - y_ours.float()).norm() / y_ref.float().norm())
     del y_ref, y_ours
-    ref_ms = time_events(lambda: ref(x), max(5, args.steps // 5), stream)
+    ref_ms = time_events(lambda: ref(x), max(20, args.steps // 5), stream)
 
     # ---- the timed region: W warm-up steps, then exactly K steps
     def step():

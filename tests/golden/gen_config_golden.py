@@ -10,6 +10,8 @@ gen_golden.py) and run the eval sequence.  Stored (small; no model tensors):
   <key>__sal__<linear>    the reference's salient_indices (int32)
   meta: per linear the sha256 of W_hat (-0.0 folded to +0.0) and its fp64 sum, shapes and
         modes; per case the eval loss (mean next-token CE, fp64) and the logits norm
+  meta noise_*: the reference's own spread when its F.linear accumulates in fp64 instead
+        (logits / logsumexp relative, |loss difference|): the model-level noise floor
   <key>__logits, __lse    fp32 logits[:, :VOCAB_SLICE] and the fp64 logsumexp over the
                           vocabulary at config_cases.positions(case)
 
@@ -29,7 +31,7 @@ import torch.nn as nn
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 sys.path.insert(0, os.path.dirname(HERE))
-from gen_golden import load_reference  # noqa: E402
+from gen_golden import _StableTorch, load_reference  # noqa: E402
 import config_cases as C  # noqa: E402
 
 
@@ -56,6 +58,24 @@ def eval_loss(logits, ids):
     pred = logits[:, :-1].double()
     return float(nn.functional.cross_entropy(pred.reshape(-1, pred.shape[-1]),
                                              ids[:, 1:].reshape(-1)))
+
+
+class _F64LinearTorch(_StableTorch):
+    """The reference's `torch` with F.linear accumulated in fp64 (rounded once to the
+    model dtype): the same fake-quant model under another GEMM accumulation order."""
+
+    class _Functional:
+        class F:
+            @staticmethod
+            def linear(x, w, b=None):
+                y = nn.functional.linear(x.double(), w.double(), None if b is None else b.double())
+                return y.to(x.dtype)
+
+    functional = _Functional
+
+
+def _rel(a, b):
+    return float((a.double() - b.double()).norm() / b.double().norm())
 
 
 def main():
@@ -90,6 +110,13 @@ def main():
         ids = C.tokens(case, "eval")
         with torch.no_grad():
             logits = q(ids).logits.float()
+        # the reference's own accumulation-order noise on this model: the same quantized
+        # model with every F.linear (fake_quant.py:306) accumulated in fp64
+        real_torch = ref.torch
+        ref.torch = _F64LinearTorch(torch)
+        with torch.no_grad():
+            logits64 = q(ids).logits.float()
+        ref.torch = real_torch
         pos = C.positions(case)
         # a vocabulary slice of the logits at the stored positions + the full-vocabulary
         # logsumexp there (keeps the fixture small for the 50272-entry OPT-125M head)
@@ -98,8 +125,14 @@ def main():
         cases[key] = dict(n_linears=len(linears), linears=linears,
                           loss=eval_loss(logits, ids),
                           logits_norm=float(logits.double().norm()),
+                          noise_logits_rel=_rel(logits64[0, pos, :C.VOCAB_SLICE],
+                                                logits[0, pos, :C.VOCAB_SLICE]),
+                          noise_lse_rel=_rel(torch.logsumexp(logits64[0, pos].double(), -1),
+                                             torch.logsumexp(logits[0, pos].double(), -1)),
+                          noise_loss=abs(eval_loss(logits64, ids) - eval_loss(logits, ids)),
                           positions=pos.tolist())
-        print(f"{key}: {len(linears)} W4A4Linear, loss {cases[key]['loss']:.5f}, "
+        print(f"{key}: {len(linears)} W4A4Linear, loss {cases[key]['loss']:.5f}, noise "
+              f"logits {cases[key]['noise_logits_rel']:.3e} loss {cases[key]['noise_loss']:.3e}, "
               f"{time.time() - t0:.1f} s", flush=True)
         del model, q, logits
     meta = dict(source="adithyab100/smoothquant-mixedprecision reference fake_quant.py on CPU "

@@ -7,14 +7,18 @@ tests/config_cases.py):
     is BIT-EXACT with the reference's (sha256 of the bytes, -0.0 folded to +0.0);
   * every W4A4Linear, teacher-forced on the input it actually received in the GPU
     forward: q_x BIT-EXACT with the PyTorch-CPU restatement of the reference
-    (oracle/torch_cpu.py, itself pinned bit-exact to the reference goldens), and y within
-    the accumulation-order tolerance of an fp64 product of those exact operands
-    (+ the output quantizer for OPT q/k/v): fp32 1e-5, fp16 2e-3; x10 with output quant;
+    (oracle/torch_cpu.py, itself pinned bit-exact to the reference goldens); the GEMM
+    output within the accumulation-order tolerance of an fp64 product of those exact
+    operands (fp32 1e-5, fp16 2e-3); and for OPT q/k/v (bmm-input quant) the forward's y
+    BIT-EXACT with the reference output quantizer applied to that GEMM output;
   * model level: logits (vocabulary slice at 8 positions), the full-vocabulary logsumexp
-    there, and the eval loss against the reference's CPU run.  Non-quantized ops
-    (attention, norms) run on the GPU here and on the CPU there, so hidden states differ
-    by rounding and an activation code may flip at a rounding boundary in a later layer:
-    logits relative Frobenius <= 2e-2, loss within 1e-2 relative.
+    there, and the eval loss against the reference's CPU run.  Here 4-bit activations of
+    a random-init model are chaotic: the reference itself, re-run with its F.linear
+    accumulated in fp64, moves its logits by noise_logits_rel (0.08-0.25 on these cases,
+    stored by the generator) -- any last-bit difference flips an activation code at a
+    rounding boundary and the flip propagates.  The bound is 3x that noise floor + 2e-2
+    (logits, logsumexp) and 3x the loss noise + 1e-3 relative.  The per-layer checks above
+    are the binding parity evidence.
 """
 import numpy as np
 import pytest
@@ -26,7 +30,7 @@ from oracle import torch_cpu as T
 pytestmark = pytest.mark.gpu
 
 TOL_Y = {"fp32": 1e-5, "fp16": 2e-3}
-TOL_LOGITS, TOL_LOSS = 2e-2, 1e-2
+TOL_LOGITS, TOL_LOSS = 2e-2, 1e-3
 
 
 def _golden():
@@ -52,6 +56,7 @@ def _rel(a, b):
 
 
 @pytest.mark.parametrize("case", C.CASES, ids=[c["key"] for c in C.CASES])
+@torch.no_grad()
 def test_config_workload_matches_reference(case):
     if not torch.cuda.is_available():
         pytest.skip("no ROCm device")
@@ -121,21 +126,28 @@ def test_config_workload_matches_reference(case):
         if bool(keep.any()):
             qx_ref[:, keep] = T.act_quant(xc[:, keep], amode, bits, ag)
         assert np.array_equal(got_qx, qx_ref.float().numpy()), f"{n}: q_x differs"
-        # y vs an fp64 product of the exact operands (+ output quant)
-        w_hat = m.weight.double()
-        yr = qx_ref.cuda().double() @ w_hat.t()
-        if m.bias is not None:
-            yr = yr + m.bias.reshape(-1).double()
-        yr = yr.to(x.dtype).cpu()
-        ospec = resolve_quantizer(m.output_quant)
-        tol = TOL_Y[dt]
-        if ospec is not None:
-            okeep = keep if m.salient_indices is not None else torch.ones(yr.shape[1], dtype=torch.bool)
-            yr[:, okeep] = T.act_quant(yr[:, okeep], *ospec)
-            tol *= 10
-        r = _rel(y.reshape(yr.shape).float().cpu().numpy(), yr.float().numpy())
+        # the GEMM: our y before any output quantization vs an fp64 product of the exact
+        # operands (accumulation-order tolerance)
+        bias = None if m.bias is None else m.bias.reshape(-1)
+        y_pre = ops.gemm_fq(a, pw, bias)
+        yr = qx_ref.cuda().double() @ m.weight.double().t()
+        if bias is not None:
+            yr = yr + bias.double()
+        r = _rel(y_pre.float().cpu().numpy(), yr.cpu().numpy())
         worst = max(worst, r)
-        assert r < tol, (n, r)
+        assert r < TOL_Y[dt], (n, r)
+        ospec = resolve_quantizer(m.output_quant)
+        if ospec is None:
+            assert torch.equal(y.reshape(y_pre.shape), y_pre), n  # forward = this GEMM
+        else:
+            # output quantization (fake_quant.py:308-316) is discontinuous in the GEMM
+            # output, so it is checked on OUR pre-quant output: the forward's y must be
+            # the reference quantizer (CPU restatement) applied to it, bit for bit
+            okeep = keep if m.salient_indices is not None else torch.ones(y_pre.shape[1], dtype=torch.bool)
+            want = y_pre.cpu().clone()
+            want[:, okeep] = T.act_quant(want[:, okeep], *ospec)
+            assert np.array_equal(y.reshape(want.shape).float().cpu().numpy(),
+                                  want.float().numpy()), f"{n}: output quant differs"
 
     # ---- model level
     pos = np.array(meta["positions"])
@@ -146,8 +158,9 @@ def test_config_workload_matches_reference(case):
     pred = logits[:, :-1].double()
     loss = float(torch.nn.functional.cross_entropy(pred.reshape(-1, pred.shape[-1]),
                                                    ids[:, 1:].reshape(-1)))
-    print(f"{key}: {len(layers)} layers, worst per-layer y rel {worst:.2e}; logits rel "
-          f"{r_logits:.2e}; loss {loss:.5f} vs {meta['loss']:.5f}")
-    assert r_logits <= TOL_LOGITS
-    assert _rel(lse, CG.arr(key, "lse")) <= TOL_LOGITS
-    assert abs(loss - meta["loss"]) <= TOL_LOSS * abs(meta["loss"])
+    print(f"{key}: {len(layers)} layers, worst per-layer GEMM rel {worst:.2e}; logits rel "
+          f"{r_logits:.2e} (reference noise {meta['noise_logits_rel']:.2e}); loss {loss:.5f} "
+          f"vs {meta['loss']:.5f} (noise {meta['noise_loss']:.2e})")
+    assert r_logits <= 3 * meta["noise_logits_rel"] + TOL_LOGITS
+    assert _rel(lse, CG.arr(key, "lse")) <= 3 * meta["noise_lse_rel"] + TOL_LOGITS
+    assert abs(loss - meta["loss"]) <= 3 * meta["noise_loss"] + TOL_LOSS * abs(meta["loss"])

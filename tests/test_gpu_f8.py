@@ -94,6 +94,7 @@ def test_f8_gemm_vs_oracle(case):
     assert rel(y, want) < TOL_I8[dt], rel(y, want)
 
 
+@torch.no_grad()
 def test_f8_full_size_config2_per_token():
     """BASELINE config 2 with per_token activations on the FP8 path (the default for this
     layer): y against an fp64 product of the faithful operands (the per_token q_x, which

@@ -395,39 +395,37 @@ def test_packed_checkpoint_roundtrip(tmp_path):
 
 # ------------------------------------------------------------------ casts (.to / _apply)
 def test_dtype_cast_keeps_packing_when_exact():
-    """model.float() on an fp16 W4A4Linear: cast(code * s) == code * cast(s) exactly, so
-    the layer stays int4-packed (no dense fallback) and equals the reference's cast(W_hat)
-    layer; a cast that changes the values (fp32 -> fp16 here) keeps the reference's values
-    as a dense operand and warns."""
+    """model.float() on an fp16 W4A4Linear turns the reference's W_hat buffer into
+    cast(W_hat) = fp32(fp16(code * s)).  When that equals code * fp32(s) for every weight
+    (here: power-of-two group scales) the layer stays int4-packed with fp32 scales; when it
+    does not (random weights: fp16 rounded the products) it keeps the reference's values as
+    a dense operand and warns.  Either way the values are the reference's."""
     dev = _dev()
     import warnings
     D16, D32 = O.DT("fp16"), O.DT("fp32")
     g = np.random.default_rng(17)
     K, N, M = 512, 256, 64
-    W = D16.rnd(g.standard_normal((N, K)) * 0.02)
-    b = D16.rnd(g.standard_normal(N) * 0.01)
     imp = np.abs(g.standard_normal(K)).astype(np.float32)
-    q = make_layer(W, b, "fp16", dev, weight_quant="per_group", act_quant="per_group",
-                   importance=torch.from_numpy(imp), salient_prop=0.05, group_size=64)
-    w16 = to_np(q.weight)
-    with warnings.catch_warnings():
-        warnings.simplefilter("error")
-        q.float()
-    pw = q.packed()
-    assert pw.n_bits == 4 and pw.dtype == torch.float32 and q.w_codes.dtype == torch.uint8
-    assert bits_equal(to_np(q.weight), w16)  # cast(W_hat) fp16 -> fp32 is exact
-    x = D32.rnd(g.standard_normal((M, K)))
     sal = O.select_salient(imp, 0.05)
-    want = D32.f32(O.w4a4_forward(x, w16, D32.rnd(b), "per_group", 4, 64, sal, False, D32))
-    assert rel(to_np(q(to_t(x, "fp32", dev))), want) < TOL_FQ["fp32"]
-    # fp32-quantized layer cast to fp16: the values change -> dense + warning
-    W32 = D32.rnd(g.standard_normal((N, K)) * 0.02)
-    q2 = make_layer(W32, None, "fp32", dev, weight_quant="per_group", act_quant="per_group",
-                    importance=torch.from_numpy(imp), salient_prop=0.05, group_size=64)
-    w_cast = to_np(q2.weight.half())
-    with pytest.warns(RuntimeWarning):
-        q2.half()
-    assert q2.packed().n_bits == 0 and bits_equal(to_np(q2.weight), w_cast)
+    x = D32.rnd(g.standard_normal((M, K)))
+    codes = g.integers(-7, 8, (N, K)).astype(np.float32)
+    codes[g.integers(0, N, K), np.arange(K)] = 7  # every column absmax 7 -> s = 2^-6
+    cases = [(codes * 2.0 ** -6, False), (D16.rnd(g.standard_normal((N, K)) * 0.02), True)]
+    for W, expect_warn in cases:
+        b = D16.rnd(g.standard_normal(N) * 0.01)
+        q = make_layer(W, b, "fp16", dev, weight_quant="per_group", act_quant="per_group",
+                       importance=torch.from_numpy(imp), salient_prop=0.05, group_size=64)
+        w_cast = to_np(q.weight.float())
+        with warnings.catch_warnings(record=True) as rec:
+            warnings.simplefilter("always")
+            q.float()
+        warned = any(issubclass(w.category, RuntimeWarning) for w in rec)
+        assert warned == expect_warn
+        pw = q.packed()
+        assert pw.dtype == torch.float32 and pw.n_bits == (0 if expect_warn else 4)
+        assert bits_equal(to_np(q.weight), w_cast)
+        want = D32.f32(O.w4a4_forward(x, w_cast, D32.rnd(b), "per_group", 4, 64, sal, False, D32))
+        assert rel(to_np(q(to_t(x, "fp32", dev))), want) < TOL_FQ["fp32"]
 
 
 def test_packed_checkpoint_loads_into_from_float_module(tmp_path):
