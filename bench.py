@@ -255,7 +255,29 @@ def main(argv=None):
     stream = torch.cuda.current_stream(dev)
     flops = 2.0 * M * N * K
 
-    # ---- secondary measurements first (the chip is busy when the timed region starts)
+    # ---- secondary measurements first, slowest-to-settle last: the reference fake-quant
+    # forward (PyTorch ops), the vendor dense GEMM, then ~0.1 s of back-to-back W4A4
+    # GEMMs right before the warm-up, so the timed region starts at the clock the chip
+    # holds under this load (DVFS, MI355X_MICROARCH.md; a kernel trace of a 20-step run
+    # shows the GEMM at 510-680 us in its first milliseconds, 480 us once settled)
+    sec_iters = max(200, args.steps)  # ~0.1 s of back-to-back GEMMs, whatever --steps is
+    # the reference's own fake-quant forward (PyTorch ops, tools/torch_fakequant.py) on
+    # this GPU, same layer and input
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from torch_fakequant import TorchFakeQuantLinear
+    ref = TorchFakeQuantLinear(q.weight, lin.bias.detach(), q.salient_indices, args.act, 4, G)
+    y_ref, y_ours = ref(x), q(x.clone())
+    ref_rel = float((y_ref.float() - y_ours.float()).norm() / y_ref.float().norm())
+    del y_ref, y_ours
+    ref_ms = time_events(lambda: ref(x), max(20, args.steps // 5), stream)
+
+    # vendor dense fp16 GEMM (hipBLASLt via torch) on the same shape, unquantized: what
+    # the reference's F.linear costs on this GPU, without any act-quant
+    wd = lin.weight.detach()
+    dense = lambda: torch.nn.functional.linear(x, wd, lin.bias)  # noqa: E731
+    for _ in range(10):
+        dense()
+    dense_ms = time_events(dense, sec_iters, stream)
     # dominant kernel: the GEMM, timed alone on the stream it is launched on
     if use_f8:
         a8, sa, xs = ops.quant_act_f8(x, pw, args.act, 4)
@@ -267,30 +289,10 @@ def main(argv=None):
         gemm = lambda: ops.gemm_fq(a, pw, lin.bias)  # noqa: E731
         quant = lambda: ops.quant_act_fp(x, pw, args.act, 4, G)  # noqa: E731
         kdt, kname = "f16", "sqmp::gemm_fq6_kernel<F16,1,256>"
-    # ~0.1 s of back-to-back GEMMs per measurement: long enough for the chip to settle at
-    # the clock it holds under this load (DVFS, MI355X_MICROARCH.md), whatever --steps is
-    sec_iters = max(200, args.steps)
+    quant_ms = time_events(quant, sec_iters, stream)
     for _ in range(10):
         gemm()
     gemm_ms = time_events(gemm, sec_iters, stream)
-    quant_ms = time_events(quant, sec_iters, stream)
-    # vendor dense fp16 GEMM (hipBLASLt via torch) on the same shape, unquantized: what
-    # the reference's F.linear costs on this GPU, without any act-quant
-    wd = lin.weight.detach()
-    dense = lambda: torch.nn.functional.linear(x, wd, lin.bias)  # noqa: E731
-    for _ in range(10):
-        dense()
-    dense_ms = time_events(dense, sec_iters, stream)
-    # the reference's own fake-quant forward (PyTorch ops, tools/torch_fakequant.py) on
-    # this GPU, same layer and input
-    sys.path.insert(0, os.path.join(ROOT, "tools"))
-    from torch_fakequant import TorchFakeQuantLinear
-    ref = TorchFakeQuantLinear(q.weight, lin.bias.detach(), q.salient_indices, args.act, 4, G)
-    y_ref, y_ours = ref(x), q(x.clone())
-    ref_rel = float((y_ref.float() - y_ours.float()).norm() / y_ref.float().norm())
-    del y_ref, y_ours
-    ref_ms = time_events(lambda: ref(x), max(20, args.steps // 5), stream)
-
     # ---- the timed region: W warm-up steps, then exactly K steps
     def step():
         return q(x)

@@ -5,8 +5,9 @@
     python bench_e2e.py --model opt-1.3b   (config 3: G=128, 5 % salient, quantize_opt with
                                             its default bmm-input output quantization)
 
-The architecture of the named model with random-init fp16 weights built directly on the
-GPU (there are no checkpoints offline), random token windows.  Importance: the reference's
+The architecture of the named model with random-init weights built directly on the GPU
+(there are no checkpoints offline), random token windows, in the reference's dtype for that
+model (run_experiments.py:146-154: Llama fp16, OPT the default fp32; --dtype overrides).  Importance: the reference's
 mean|x| calibration features (smoothquant.calibration.get_calib_feat) on synthetic
 512-token blocks; quantization: the reference's entry point (quantize_llama_like /
 quantize_opt, fake_quant.py:377-561) with every nn.Linear of the decoder becoming a HIP
@@ -17,6 +18,12 @@ clock around the whole window loop after one warm-up window, for (1) the fp16 mo
 (4) the same with an fp32 GEMM -- (3) vs (4) is the reference's own sensitivity to GEMM
 accumulation order, the noise floor against which the W4A4 kernel's PPL delta reads.
 Perplexities are of a random model: only differences are meaningful.
+
+CPU baseline (north star: e2e tokens/s "next to the CPU baseline"): the same architecture
+with the reference's fake-quant layers (oracle/torch_cpu.py, bit-exact to the reference's
+goldens) on PyTorch-CPU in fp32, every host thread; 1 and 2 decoder layers are timed on
+one window (median of 2 after a warm-up) and the whole model's time is extrapolated as
+t(1) + (L - 1) * (t(2) - t(1)) -- a bounded sample, stated in the output.
 """
 from __future__ import annotations
 
@@ -39,11 +46,11 @@ MODELS = {
     "llama2-7b": ("llama", dict(vocab_size=32000, hidden_size=4096, intermediate_size=11008,
                                 num_hidden_layers=32, num_attention_heads=32,
                                 num_key_value_heads=32, max_position_embeddings=4096,
-                                rms_norm_eps=1e-5), 64),
+                                rms_norm_eps=1e-5), 64, "fp16"),
     "opt-1.3b": ("opt", dict(vocab_size=50272, hidden_size=2048, ffn_dim=8192,
-                             num_hidden_layers=24, num_attention_heads=16,
+                             num_hidden_layers=24, num_attention_heads=32,
                              max_position_embeddings=2048, word_embed_proj_dim=2048,
-                             do_layer_norm_before=True), 128),
+                             do_layer_norm_before=True), 128, "fp32"),
 }
 
 
@@ -60,6 +67,9 @@ def parse(argv=None):
     ap.add_argument("--act-bits", type=int, default=4, help="8 = W4A8 (act_quant rebound)")
     ap.add_argument("--cal-blocks", type=int, default=4)
     ap.add_argument("--no-ref", action="store_true", help="skip the reference fake-quant legs")
+    ap.add_argument("--dtype", default=None, choices=["fp16", "bf16", "fp32"],
+                    help="model dtype (default: the reference's for this model)")
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     return ap.parse_args(argv)
 
 
@@ -81,8 +91,11 @@ def run_windows(model, ids, seq, n):
     return float(torch.exp(torch.stack(nlls).sum() / (n * seq))), dt
 
 
-def build(name, layers):
-    family, cfg_kw, _ = MODELS[name]
+TDT = {"fp16": torch.float16, "bf16": torch.bfloat16, "fp32": torch.float32}
+
+
+def build(name, layers, dtype=torch.float16, device="cuda"):
+    family, cfg_kw, _, _ = MODELS[name]
     cfg_kw = dict(cfg_kw)
     if layers:
         cfg_kw["num_hidden_layers"] = layers
@@ -93,11 +106,62 @@ def build(name, layers):
         from transformers import OPTConfig, OPTForCausalLM
         cfg, cls = OPTConfig(attn_implementation="sdpa", **cfg_kw), OPTForCausalLM
     prev = torch.get_default_dtype()
-    torch.set_default_dtype(torch.float16)
-    with torch.device("cuda"):
+    torch.set_default_dtype(dtype)
+    with torch.device(device):
         model = cls(cfg).eval()
     torch.set_default_dtype(prev)
     return family, cfg, model
+
+
+class CPURefLinear(nn.Module):
+    """nn.Linear -> the reference's fake-quant layer on the host (oracle/torch_cpu.py)."""
+
+    def __init__(self, lin, weight_quant, act, G, p, output_quant):
+        super().__init__()
+        from oracle.torch_cpu import CPUFakeQuantLinear
+        imp = torch.rand(lin.in_features, generator=torch.Generator().manual_seed(7))
+        self.f = CPUFakeQuantLinear(lin.weight.detach(), None if lin.bias is None else lin.bias.detach(),
+                                    weight_quant, act, 4, G, imp, p, output_quant)
+
+    def forward(self, x):
+        return self.f(x)
+
+
+@torch.no_grad()
+def cpu_baseline(args, G):
+    """Reference fake-quant model on PyTorch-CPU, fp32: t(1 layer), t(2 layers) on one
+    window -> extrapolated whole-model tokens/s (see the module docstring)."""
+    family, cfg_kw, _, _ = MODELS[args.model]
+    L = args.layers or cfg_kw["num_hidden_layers"]
+    seq = args.seq
+    times = {}
+    for nl in (1, 2):
+        _, _, m = build(args.model, nl, torch.float32, "cpu")
+        for name, mod in list(m.named_modules()):
+            for attr, child in list(mod.named_children()):
+                if isinstance(child, nn.Linear) and "lm_head" not in f"{name}.{attr}":
+                    outq = family == "opt" and attr in ("q_proj", "k_proj", "v_proj")
+                    setattr(mod, attr, CPURefLinear(child, args.weight, args.act, G,
+                                                    args.salient, outq))
+        ids = torch.randint(0, m.config.vocab_size, (1, seq),
+                            generator=torch.Generator().manual_seed(3))
+        m(ids[:, :128])  # warm-up
+        ts = []
+        for _ in range(2):
+            t0 = time.perf_counter()
+            m(ids)
+            ts.append(time.perf_counter() - t0)
+        times[nl] = sorted(ts)[0] if len(ts) == 1 else sum(ts) / len(ts)
+        del m
+    per_layer = max(times[2] - times[1], 1e-9)
+    total = times[1] + (L - 1) * per_layer
+    return {
+        "tokens_per_s": round(seq / total, 2),
+        "cores": torch.get_num_threads(),
+        "kind": "torch-cpu-fp32 (reference fake_quant ops, oracle/torch_cpu.py)",
+        "sample": (f"1 window of {seq} tokens through 1 and 2 decoder layers: {times[1]:.2f} s, "
+                   f"{times[2]:.2f} s -> {L} layers extrapolated {total:.1f} s per window"),
+    }
 
 
 def linear_flops_per_token(model):
@@ -140,7 +204,8 @@ def main(argv=None):
 
     from smoothquant import fake_quant as FQ
     from smoothquant.calibration import get_calib_feat
-    family, cfg, model = build(args.model, args.layers)
+    dtn = args.dtype or MODELS[args.model][3]
+    family, cfg, model = build(args.model, args.layers, TDT[dtn])
     G = args.group or MODELS[args.model][2]
     dev = torch.device("cuda")
     torch.manual_seed(0)
@@ -176,9 +241,10 @@ def main(argv=None):
         "unit": "tokens/s",
         "higher_is_better": True,
         "n_gpus": 1,
-        "fp16_tokens_per_s": round(tokens / dt16, 1),
-        "w4a4_over_fp16": round(dt16 / dt4, 4),
-        "ppl_fp16": round(ppl16, 4),
+        "dtype": dtn,
+        "unquantized_tokens_per_s": round(tokens / dt16, 1),
+        "w4a4_over_unquantized": round(dt16 / dt4, 4),
+        "ppl_unquantized": round(ppl16, 4),
         "ppl_w4a4": round(ppl4, 4),
         "linear_TFLOP_per_s_w4a4": round(flops_tok * tokens / dt4 / 1e12, 1),
     }
@@ -196,7 +262,7 @@ def main(argv=None):
             "reference_gemm_order_noise": round(pplr32 - pplr, 4),
         })
     out.update({
-        "data": "synthetic: random-init fp16 weights of the named architecture, random tokens; "
+        "data": f"synthetic: random-init {dtn} weights of the named architecture, random tokens; "
                 "PPL values are of a random model -- only differences are meaningful",
         "config": {"workload": f"{args.model} prefill, batch 1", "layers": cfg.num_hidden_layers,
                    "seq_len": args.seq, "windows": args.windows, "group_size": G,
@@ -206,6 +272,12 @@ def main(argv=None):
                    "calibration": f"{args.cal_blocks} x 512 random tokens"},
         "setup_s": {"calibrate_and_quantize": round(t_q, 1)},
     })
+    if not args.no_cpu:
+        del model
+        torch.cuda.empty_cache()
+        cpu = cpu_baseline(args, G)
+        cpu["w4a4_gpu_over_cpu"] = round(out["value"] / cpu["tokens_per_s"], 1)
+        out["cpu_baseline"] = cpu
     print(json.dumps(out), flush=True)
     return out
 

@@ -6,7 +6,7 @@ cd /tmp && export TMPDIR=/tmp
 rocprofv3 -L > $R/gpurun_out/pmc/counters_list.txt 2>&1 || true
 run() {  # name, counters...
   local name=$1; shift
-  timeout -k 10 240 rocprofv3 --pmc "$@" --output-format csv -d $R/gpurun_out/pmc/$name -o run -- python $R/tools/gemm_only.py ${KIND:-fq} 5 > $R/gpurun_out/pmc/$name.log 2>&1 || { echo "pmc $name failed"; tail -5 $R/gpurun_out/pmc/$name.log; return 1; }
+  timeout -k 10 240 rocprofv3 --pmc "$@" --output-format csv -d $R/gpurun_out/pmc/$name -o run -- python $R/tools/gemm_only.py ${KIND:-fq} 20 > $R/gpurun_out/pmc/$name.log 2>&1 || { echo "pmc $name failed"; tail -5 $R/gpurun_out/pmc/$name.log; return 1; }
 }
 P=${PASSES:-fq_a fq_b fq_c fq_d i8_a i8_b i8_c}
 for name in $P; do

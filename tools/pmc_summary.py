@@ -1,0 +1,62 @@
+"""Summarise rocprofv3 --pmc passes (tools/gpu_pmc.sh layout: <dir>/<kind>_<pass>/
+run_counter_collection.csv) into one JSON per GEMM kind with the derived figures DESIGN.md
+quotes, so every fraction can be recomputed from profiles/ alone.
+
+    python tools/pmc_summary.py <pmc dir> <kind> <avg kernel us> <algorithmic bytes> <mfma cycles per inst> [out.json]
+
+Derivations (MI355X_MICROARCH.md: HBM / rocprofv3 sections):
+  hbm_bytes      = 2 * FETCH_SIZE * 1024 + WRITE_SIZE * 1024   (gfx950 FETCH_SIZE reads 1/2
+                   of a wide coalesced stream; sizes are in KiB)
+  clock_GHz      = GRBM_GUI_ACTIVE / 8 XCDs / kernel time       (profiled pass; reads low
+                   against an unprofiled run)
+  mfma_busy      = SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs * GRBM_GUI_ACTIVE / 8)
+  mfma_busy_chk  = SQ_INSTS_MFMA * cycles per MFMA (cross-check of the busy counter)
+"""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+
+def load(d):
+    vals = defaultdict(list)
+    for f in glob.glob(os.path.join(d, "*counter_collection.csv")):
+        for r in csv.DictReader(open(f)):
+            if "gemm" in r.get("Kernel_Name", ""):
+                vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in vals.items()}
+
+
+def main():
+    root, kind, us, alg_bytes, cyc = sys.argv[1], sys.argv[2], float(sys.argv[3]), float(sys.argv[4]), float(sys.argv[5])
+    c = {}
+    for d in sorted(glob.glob(os.path.join(root, f"{kind}_*"))):
+        if os.path.isdir(d):
+            c.update(load(d))
+    t = us * 1e-6
+    xcd_cycles = c["GRBM_GUI_ACTIVE"] / 8
+    out = {
+        "kind": kind, "avg_kernel_us": us, "counters_per_dispatch": c,
+        "hbm_bytes_per_launch": 2 * c["FETCH_SIZE"] * 1024 + c["WRITE_SIZE"] * 1024,
+        "hbm_read_bytes": 2 * c["FETCH_SIZE"] * 1024, "hbm_write_bytes": c["WRITE_SIZE"] * 1024,
+        "algorithmic_bytes": alg_bytes,
+        "clock_GHz_profiled": xcd_cycles / t / 1e9,
+        "mfma_busy": c["SQ_VALU_MFMA_BUSY_CYCLES"] / (1024 * xcd_cycles),
+        "mfma_busy_from_inst_count": c["SQ_INSTS_MFMA"] * cyc / (1024 * xcd_cycles),
+        "valu_insts_per_mfma": c["SQ_INSTS_VALU"] / c["SQ_INSTS_MFMA"],
+        "lds_bank_conflict_frac_of_lds_insts": c.get("SQ_LDS_BANK_CONFLICT", 0) / max(c.get("SQ_INSTS_LDS", 1), 1),
+        "l2_hit_rate": c["TCC_HIT_sum"] / (c["TCC_HIT_sum"] + c["TCC_MISS_sum"]),
+        "wave_cycles_wait_any_frac": c["SQ_WAIT_ANY"] / c["SQ_WAVE_CYCLES"],
+        "wave_cycles_wait_inst_any_frac": c["SQ_WAIT_INST_ANY"] / c["SQ_WAVE_CYCLES"],
+    }
+    out["traffic_over_algorithmic"] = out["hbm_bytes_per_launch"] / alg_bytes
+    s = json.dumps(out, indent=1)
+    if len(sys.argv) > 6:
+        open(sys.argv[6], "w").write(s + "\n")
+    print(s)
+
+
+if __name__ == "__main__":
+    main()
