@@ -256,6 +256,237 @@ __global__ __launch_bounds__(512, 1) void gemm_f8_kernel(
     }
 }
 
+// ================================================================= gemm_f8v2
+// Weight groups of whole 128-position blocks (Gw % 128 == 0): the same contraction on
+// v_mfma_scale_f32_16x16x128_f8f6f4.  One MFMA covers a whole 128-position block, which
+// lies in one weight group, so each 16 x 16 tile folds its exact integer block sum once per
+// 128 positions: 4 fp32 FMAs per lane per MFMA, against 16 per 64 positions on the 32x32x64
+// kernel above (whose fold kept the VALU, not the matrix pipe, busy: DESIGN.md §4).
+//
+// Tile 256 (m) x 256 (n) per 512-thread workgroup, 8 waves as 2 (m) x 4 (n), each wave
+// 128 rows x 64 weight columns = 8 x 4 tiles of 16 x 16 (128 fp32 accumulators).  The
+// weight fragment goes in the MFMA's A slot (D row = weight column), so a lane holds 4
+// consecutive output columns of one activation row: one float4 of weight scales per tile
+// column for the fold, one activation-row scale per tile row, 8-byte output stores.
+// K-stages: 128-position code blocks (A and B images 256 rows x 128 B of e4m3 + the
+// block's 256 fp32 weight scales), then the exact salient tail as 64-column D stages (the
+// same 256 x 128 B images; 16x16x32 D MFMA into the same accumulators after the row
+// scales are applied).  Two ring slots of 65 KiB; the DMA of stage k+1 (8 1-KiB pieces per
+// wave through buffer resources, +1 scale piece on wave 0) runs under the compute of
+// stage k.  LDS rows are 128 B with 16-B chunk c of row r at c ^ v2_sw(r), conflict-free
+// for the ds_read_b128 lane groups of both the e4m3 fragment reads (chunks 2q, 2q + 1)
+// and the D tail reads (chunk 4u + q).
+namespace {
+constexpr int V2_A = 0, V2_B = 32768, V2_S = 65536;
+constexpr int V2_SLOT = 66560;  // A 32 KiB + B 32 KiB + S 1 KiB
+constexpr int V2_NSLOT = 2;     // 133120 B
+
+__device__ inline int v2_sw(int r) {
+  return ((r >> 1) & 1) ^ (((r >> 2) & 1) << 2) ^ (((r >> 3) & 1) * 6);
+}
+__device__ inline int v2_off(int r, int c) { return (r << 7) + ((c ^ v2_sw(r)) << 4); }
+__device__ inline i32x8b cat8(const u32x4& a, const u32x4& b) {
+  return i32x8b{(int)a[0], (int)a[1], (int)a[2], (int)a[3], (int)b[0], (int)b[1], (int)b[2], (int)b[3]};
+}
+}  // namespace
+
+template <class DT>
+__global__ __launch_bounds__(512, 1) void gemm_f8v2_kernel(
+    const unsigned char* __restrict__ A8, const float* __restrict__ ascale,
+    const typename DT::T* __restrict__ XS, const unsigned char* __restrict__ W8,
+    const float* __restrict__ ws32, const typename DT::T* __restrict__ wsal,
+    const typename DT::T* __restrict__ bias, typename DT::T* __restrict__ Y, int M, int N,
+    int Kp, int S_pad, int Gw, int ngw, int tiles_m, int tiles_n) {
+  typedef typename DT::T T;
+  __shared__ __attribute__((aligned(16))) unsigned char lds[V2_NSLOT * V2_SLOT];
+
+  int tm, tn;
+  tile_coords(tiles_m, tiles_n, 4, tm, tn);
+  const int m0 = tm * 256, n0 = tn * 256;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  const int r16 = lane & 15, q = lane >> 4;
+  const int nk8 = Kp / 128, nkt = nk8 + S_pad / 64;
+  const int Np = pad_n(N);
+
+  // ---- DMA geometry: piece p = 4 wave + j moves rows 8p .. 8p + 7 of a 256 x 128 B image;
+  // lane L writes row 8p + (L >> 3), physical chunk L & 7 = logical chunk (L & 7) ^ v2_sw
+  // (offsets recomputed per stage: a few VALU ops instead of 12 live VGPRs)
+  const int drow0 = 32 * wave + (lane >> 3);
+  auto drow = [&](int j) { return drow0 + 8 * j; };
+  auto dchunk16 = [&](int j) { return (uint32_t)(((lane & 7) ^ v2_sw(drow(j))) << 4); };
+  const i32x4b rA = rsrc_of(A8 + (size_t)m0 * Kp, 0xFFFFFFFFu);
+  const i32x4b rW = rsrc_of(W8 + (size_t)n0 * Kp, 0xFFFFFFFFu);
+  const i32x4b rX = rsrc_of(XS + (size_t)m0 * S_pad, 0xFFFFFFFFu);
+  const i32x4b rL = rsrc_of(wsal, 0xFFFFFFFFu);
+  const i32x4b rS = rsrc_of(ws32 + n0, 0xFFFFFFFFu);
+  const i32x4b rR = rsrc_of(ascale + m0, (uint32_t)(M - m0) * 4u);  // rows >= M read 0
+
+  auto issue = [&](int kt) {
+    unsigned char* slot = lds + (kt & 1) * V2_SLOT;
+    if (kt < nk8) {
+      const uint32_t so = (uint32_t)kt * 128;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t v = (uint32_t)drow(j) * Kp + dchunk16(j);
+        dma16(rA, v, so, slot + V2_A + (4 * wave + j) * 1024);
+        dma16(rW, v, so, slot + V2_B + (4 * wave + j) * 1024);
+      }
+      if (wave == 0) {
+        const int g = min((kt * 128) / Gw, ngw - 1);
+        dma16(rS, (uint32_t)lane * 16, (uint32_t)g * Np * 4, slot + V2_S);
+      }
+    } else {
+      const uint32_t so = (uint32_t)(kt - nk8) * 64 * sizeof(T);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t c = dchunk16(j);
+        dma16(rX, (uint32_t)drow(j) * S_pad * sizeof(T) + c, so, slot + V2_A + (4 * wave + j) * 1024);
+        dma16(rL, (uint32_t)min(n0 + drow(j), N - 1) * S_pad * sizeof(T) + c, so,
+              slot + V2_B + (4 * wave + j) * 1024);
+      }
+      if (wave == 0 && kt == nk8) dma16(rR, (uint32_t)lane * 16, 0u, slot + V2_S);
+    }
+  };
+
+  f32x4 tot[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) tot[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int wcol0 = wn * 64 + r16;   // + 16 j: the lane's weight row in the B image
+  const int xrow0 = wm * 128 + r16;  // + 16 i: the lane's activation row in the A image
+  auto compute_f8 = [&](const unsigned char* __restrict__ slot) {
+    i32x8b bw[4];
+    f32x4 sv[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c = wcol0 + 16 * j;
+      bw[j] = cat8(*(const u32x4*)(slot + V2_B + v2_off(c, 2 * q)),
+                   *(const u32x4*)(slot + V2_B + v2_off(c, 2 * q + 1)));
+      sv[j] = *(const f32x4*)(slot + V2_S + (wn * 64 + 16 * j + 4 * q) * 4);
+    }
+    auto ald = [&](int i) {
+      const int r = xrow0 + 16 * i;
+      return cat8(*(const u32x4*)(slot + V2_A + v2_off(r, 2 * q)),
+                  *(const u32x4*)(slot + V2_A + v2_off(r, 2 * q + 1)));
+    };
+    const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
+    // per activation tile i: 4 MFMAs, the fold of MFMA j - 1 issued behind MFMA j (its
+    // result latency), the next tile's fragment read under them; one sched barrier per
+    // tile keeps the compiler from hoisting every fragment read (register pressure)
+    i32x8b ax = ald(0);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const i32x8b cur = ax;
+      if (i + 1 < 8) ax = ald(i + 1);
+      f32x4 t0 = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(bw[0], cur, zero, 0, 0, 0, 127, 0, 127);
+      f32x4 t1 = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(bw[1], cur, zero, 0, 0, 0, 127, 0, 127);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) tot[i][0][r] = __builtin_fmaf(t0[r], sv[0][r], tot[i][0][r]);
+      t0 = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(bw[2], cur, zero, 0, 0, 0, 127, 0, 127);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) tot[i][1][r] = __builtin_fmaf(t1[r], sv[1][r], tot[i][1][r]);
+      t1 = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(bw[3], cur, zero, 0, 0, 0, 127, 0, 127);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) tot[i][2][r] = __builtin_fmaf(t0[r], sv[2][r], tot[i][2][r]);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) tot[i][3][r] = __builtin_fmaf(t1[r], sv[3][r], tot[i][3][r]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  // first tail stage (or the end, without a tail): scale row 16 i + r16 by its act scale
+  auto apply_row_scales = [&](const float* rs) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float s = rs[wm * 128 + 16 * i + r16];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) tot[i][j] *= s;
+    }
+  };
+  auto compute_tail = [&](const unsigned char* __restrict__ slot) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      u32x4 bf[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bf[j] = *(const u32x4*)(slot + V2_B + v2_off(wcol0 + 16 * j, 4 * u + q));
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const u32x4 af = *(const u32x4*)(slot + V2_A + v2_off(xrow0 + 16 * i, 4 * u + q));
+#pragma unroll
+        for (int j = 0; j < 4; ++j) Mfma<DT>::run(tot[i][j], bf[j], af);
+      }
+    }
+  };
+
+  // ---- two-slot ring: stage k's DMA is the only one in flight when stage k starts.  One
+  // loop per compute body (no branch between bodies inside a loop: the accumulators keep
+  // their registers); the last code stage issues the first tail stage.
+  auto top = [&](int kt) {
+    vmw<0>();
+    __builtin_amdgcn_s_barrier();  // every wave's pieces of stage kt have landed; every
+    asm volatile("" ::: "memory");  // wave is past its reads of slot (kt + 1) & 1
+    __builtin_amdgcn_sched_barrier(0);
+    return (const unsigned char*)(lds + (kt & 1) * V2_SLOT);
+  };
+  issue(0);
+  int kt = 0;
+  for (; kt + 1 < nk8; ++kt) {
+    const unsigned char* slot = top(kt);
+    issue(kt + 1);
+    compute_f8(slot);
+  }
+  if (kt < nk8) {  // last code stage
+    const unsigned char* slot = top(kt);
+    if (kt + 1 < nkt) issue(kt + 1);
+    compute_f8(slot);
+    ++kt;
+  }
+  for (; kt < nkt; ++kt) {
+    const unsigned char* slot = top(kt);
+    if (kt + 1 < nkt) issue(kt + 1);
+    if (kt == nk8) apply_row_scales((const float*)(slot + V2_S));
+    compute_tail(slot);
+  }
+  if (nkt == nk8) {  // no salient tail: row scales straight from global memory
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int gm = m0 + wm * 128 + 16 * i + r16;
+      const float s = gm < M ? ascale[gm] : 0.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) tot[i][j] *= s;
+    }
+  }
+
+  // ---- epilogue: lane = row m0 + xrow0 + 16 i, columns n0 + wn 64 + 16 j + 4 q + r
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int nb = n0 + wn * 64 + 16 * j + 4 * q;
+    if (nb >= N) continue;
+    float bv[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bv[r] = (bias && nb + r < N) ? DT::to_f(bias[nb + r]) : 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int gm = m0 + xrow0 + 16 * i;
+      if (gm >= M) continue;
+      T v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = DT::from_f(tot[i][j][r] + bv[r]);
+      T* dst = Y + (size_t)gm * N + nb;
+      if (nb + 4 <= N && (N & 3) == 0) {
+        *(uint2*)dst = *(const uint2*)v;
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (nb + r < N) dst[r] = v[r];
+      }
+    }
+  }
+}
+
 // bpack int4 codes -> e4m3 bytes [Np][Kp] (natural packed order), D scales -> fp32.
 template <class DT>
 __global__ __launch_bounds__(256) void pack_f8_kernel(const uint32_t* __restrict__ codes,
@@ -321,13 +552,26 @@ extern "C" int sqmp_gemm_f8(const void* a8, const float* ascale, const void* xs,
   hipStream_t s = (hipStream_t)stream;
   const int tiles_m = cdiv(M, 256), tiles_n = cdiv(N, 256);
   const dim3 grid(tiles_m * tiles_n), block(512);
+  // Gw % 128 == 0 runs the 16x16x128 kernel (SQMP_F8_V1=1 keeps the 32x32x64 one, A/B)
+  static const bool v1_only = [] {
+    const char* e = getenv("SQMP_F8_V1");
+    return e && atoi(e) != 0;
+  }();
+  const bool v2 = Gw % 128 == 0 && !v1_only;
 #define SQMP_F8L(DTT)                                                                        \
-  gemm_f8_kernel<DTT><<<grid, block, 0, s>>>(                                                \
+  if (v2) gemm_f8v2_kernel<DTT><<<grid, block, 0, s>>>(                                      \
+      (const unsigned char*)a8, ascale, (const DTT::T*)xs, (const unsigned char*)w8, ws32,   \
+      (const DTT::T*)wsal, (const DTT::T*)bias, (DTT::T*)y, M, N, Kp, S_pad, Gw, ngw, tiles_m, \
+      tiles_n);                                                                              \
+  else gemm_f8_kernel<DTT><<<grid, block, 0, s>>>(                                           \
       (const unsigned char*)a8, ascale, (const DTT::T*)xs, (const unsigned char*)w8, ws32,   \
       (const DTT::T*)wsal, (const DTT::T*)bias, (DTT::T*)y, M, N, Kp, S_pad, Gw, ngw, tiles_m, \
       tiles_n)
-  if (dtype == SQMP_F16) SQMP_F8L(F16);
-  else SQMP_F8L(BF16);
+  if (dtype == SQMP_F16) {
+    SQMP_F8L(F16);
+  } else {
+    SQMP_F8L(BF16);
+  }
 #undef SQMP_F8L
   SQMP_LAUNCH_CHECK();
   return SQMP_OK;
