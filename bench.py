@@ -283,7 +283,10 @@ def main(argv=None):
         a8, sa, xs = ops.quant_act_f8(x, pw, args.act, 4)
         gemm = lambda: ops.gemm_f8(a8, sa, xs, pw, lin.bias)  # noqa: E731
         quant = lambda: ops.quant_act_f8(x, pw, args.act, 4)  # noqa: E731
-        kdt, kname = "f8", "sqmp::gemm_f8_kernel<F16> (e4m3 block-scaled MFMA)"
+        kdt = "f8"
+        kname = ("sqmp::gemm_f8v2_kernel<F16> (e4m3 on v_mfma_scale_f32_16x16x128_f8f6f4)"
+                 if pw.Gw % 128 == 0 else
+                 "sqmp::gemm_f8_kernel<F16> (e4m3 on v_mfma_scale_f32_32x32x64_f8f6f4)")
     else:
         a = ops.quant_act_fp(x, pw, args.act, 4, G)
         gemm = lambda: ops.gemm_fq(a, pw, lin.bias)  # noqa: E731
@@ -325,7 +328,8 @@ def main(argv=None):
     prepass_bytes = reads * xbytes + wbytes
 
     traffic = None
-    prof = os.path.join(ROOT, "profiles", f"pmc_gemm_{kdt}_{args.act}.json")
+    prof = os.path.join(ROOT, "profiles", "r02_pmc_gemm_f8v2_per_token.json" if kdt == "f8"
+                        else f"r02_pmc_gemm_fq6_{args.act}.json")
     if os.path.exists(prof):
         try:
             with open(prof) as f:

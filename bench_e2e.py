@@ -12,8 +12,8 @@ mean|x| calibration features (smoothquant.calibration.get_calib_feat) on synthet
 512-token blocks; quantization: the reference's entry point (quantize_llama_like /
 quantize_opt, fake_quant.py:377-561) with every nn.Linear of the decoder becoming a HIP
 W4A4Linear.  Timing: Evaluator-style prefill (run_experiments.py:86-123), batch 1, wall
-clock around the whole window loop after one warm-up window, for (1) the fp16 model,
-(2) the W4A4 model, (3) the reference's fake-quant forward restated in PyTorch ops
+clock around the whole window loop after one warm-up window, for (1) the unquantized model,
+(2) the W4A4 model (1 and 2 in interleaved rounds, best of each), (3) the reference's fake-quant forward restated in PyTorch ops
 (tools/torch_fakequant.py) on the same W_hat and salient sets, with the fp16 GEMM, and
 (4) the same with an fp32 GEMM -- (3) vs (4) is the reference's own sensitivity to GEMM
 accumulation order, the noise floor against which the W4A4 kernel's PPL delta reads.
@@ -28,6 +28,7 @@ t(1) + (L - 1) * (t(2) - t(1)) -- a bounded sample, stated in the output.
 from __future__ import annotations
 
 import argparse
+import copy
 import json
 import os
 import sys
@@ -70,6 +71,8 @@ def parse(argv=None):
     ap.add_argument("--dtype", default=None, choices=["fp16", "bf16", "fp32"],
                     help="model dtype (default: the reference's for this model)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--rounds", type=int, default=2,
+                    help="interleaved (unquantized, W4A4) timing rounds; the best of each")
     return ap.parse_args(argv)
 
 
@@ -215,24 +218,31 @@ def main(argv=None):
            for _ in range(args.cal_blocks)]
     flops_tok = linear_flops_per_token(model)
 
-    ppl16, dt16 = run_windows(model, ids, args.seq, args.windows)
-
     t_q = time.perf_counter()
     feat = get_calib_feat(model, None, samples=cal, device=dev)
     qfn = FQ.quantize_llama_like if family == "llama" else FQ.quantize_opt
-    model = qfn(model, weight_quant=args.weight, act_quant=args.act, input_feat=feat,
-                salient_prop=args.salient, quant_bits=4, group_size=G)
+    # the unquantized model stays alive beside its quantized copy, so the two are timed in
+    # interleaved rounds on the same warmed-up chip (separate runs drifted by up to 25 %)
+    qmodel = qfn(copy.deepcopy(model), weight_quant=args.weight, act_quant=args.act,
+                 input_feat=feat, salient_prop=args.salient, quant_bits=4, group_size=G)
     if args.act_bits != 4:
         # W4A8 (config 5): rebind the bound activation quantizer, as a reference user would
         fn = FQ._ACT_FNS[args.act]
         kw = {"group_size": G} if args.act.startswith("per_group") else {}
-        for m in model.modules():
+        for m in qmodel.modules():
             if isinstance(m, FQ.W4A4Linear):
                 m.act_quant = partial(fn, n_bits=args.act_bits, **kw)
     torch.cuda.synchronize()
     t_q = time.perf_counter() - t_q
-    n_w4 = sum(isinstance(m, FQ.W4A4Linear) for m in model.modules())
-    ppl4, dt4 = run_windows(model, ids, args.seq, args.windows)
+    n_w4 = sum(isinstance(m, FQ.W4A4Linear) for m in qmodel.modules())
+    runs16, runs4 = [], []
+    for _ in range(args.rounds):
+        runs16.append(run_windows(model, ids, args.seq, args.windows))
+        runs4.append(run_windows(qmodel, ids, args.seq, args.windows))
+    ppl16, dt16 = min(runs16, key=lambda r: r[1])
+    ppl4, dt4 = min(runs4, key=lambda r: r[1])
+    del model
+    model = qmodel
 
     tokens = args.windows * args.seq
     out = {
@@ -247,6 +257,8 @@ def main(argv=None):
         "ppl_unquantized": round(ppl16, 4),
         "ppl_w4a4": round(ppl4, 4),
         "linear_TFLOP_per_s_w4a4": round(flops_tok * tokens / dt4 / 1e12, 1),
+        "rounds_s": {"unquantized": [round(r[1], 4) for r in runs16],
+                     "w4a4": [round(r[1], 4) for r in runs4]},
     }
     if not args.no_ref:
         swap_reference(model, accum32=False)

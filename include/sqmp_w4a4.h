@@ -155,6 +155,12 @@ int sqmp_quant_act(void* x, int dtype, int M, int K, int amode, int n_bits,
                                  batch x and non-salient list (a previous call on the same
                                  input, e.g. q/k/v or gate/up sharing x): skip the column
                                  statistics and the rank (sorted per_group modes only) */
+#define SQMP_QA_STATS_GIVEN 4 /* SQMP_OUT_INPLACE, act per_group (sorted) or per_tensor:
+                                 the workspace's column-maximum region (its first K words:
+                                 fp32 bits of max_m |x[m][k]|) was filled by the producer of
+                                 x -- sqmp_gemm_fq_colmax's epilogue -- so the column
+                                 statistics pass is skipped (output quantization fused into
+                                 the GEMM epilogue, fake_quant.py:308-316) */
 
 /* sqmp_quant_act with the per-weight map posmap (int32 [K]: packed position of column k,
  * the inverse of perm; NULL = derive it per call) and flags.  With posmap, OUT_FP on
@@ -178,6 +184,16 @@ int sqmp_quant_act_v2(void* x, int dtype, int M, int K, int amode, int n_bits,
 int sqmp_gemm_fq(const void* a, const void* codes, const void* wscale, const void* wsal,
                  const void* bias, void* y, int dtype, int M, int N, int Kp, int S_pad,
                  int Gw, int ngw, int n_bits, void* stream);
+
+/* sqmp_gemm_fq whose epilogue also folds the column maxima of the stored output into
+ * colmax[N]: colmax[n] = max(colmax[n], bits(fp32 max_m |y[m][n]|)) by atomic max (the
+ * values are those of y after the rounding to D).  colmax = NULL is sqmp_gemm_fq.  Feeds
+ * the in-place output quantizer (sqmp_quant_act_v2 + SQMP_QA_STATS_GIVEN): the reference's
+ * output quantization (fake_quant.py:308-316) without a statistics pass over y. */
+int sqmp_gemm_fq_colmax(const void* a, const void* codes, const void* wscale,
+                        const void* wsal, const void* bias, void* y, int dtype, int M, int N,
+                        int Kp, int S_pad, int Gw, int ngw, int n_bits, uint32_t* colmax,
+                        void* stream);
 
 /* Integer GEMM (per_token / per_tensor activations): int8 act codes x int4 weight codes
  * on the i8 MFMA, per-weight-group fp32 fold, per-row act scale, salient tail on the D

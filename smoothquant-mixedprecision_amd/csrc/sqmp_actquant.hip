@@ -891,7 +891,12 @@ extern "C" int sqmp_quant_act_v2(void* x, int dtype, int M, int K, int amode, in
   if (amode < SQMP_ACT_PER_TOKEN || amode > SQMP_ACT_PER_GROUP_MEAN3STD) return SQMP_EINVAL;
   if (n_bits < 2 || n_bits > 8) return SQMP_EUNSUPPORTED;
   if (S < 0 || S > K || !x || !amap || (K - S > 0 && !nonsal)) return SQMP_EINVAL;
-  if (flags & ~(SQMP_QA_CLEAN_WS | SQMP_QA_REUSE_STATS)) return SQMP_EINVAL;
+  if (flags & ~(SQMP_QA_CLEAN_WS | SQMP_QA_REUSE_STATS | SQMP_QA_STATS_GIVEN)) return SQMP_EINVAL;
+  // column maxima already in the workspace (written by sqmp_gemm_fq_colmax's epilogue)
+  const bool stats_given = (flags & SQMP_QA_STATS_GIVEN) != 0;
+  if (stats_given && (out_kind != SQMP_OUT_INPLACE ||
+                      (amode != SQMP_ACT_PER_GROUP && amode != SQMP_ACT_PER_TENSOR)))
+    return SQMP_EINVAL;
   if (out_kind == SQMP_OUT_INPLACE) {
     if (Kp != K) return SQMP_EINVAL;
   } else if (out_kind == SQMP_OUT_FP || out_kind == SQMP_OUT_I8 || out_kind == SQMP_OUT_F8) {
@@ -953,8 +958,12 @@ extern "C" int sqmp_quant_act_v2(void* x, int dtype, int M, int K, int amode, in
         tmode = TAB_COUNTS;
         int st2;
         if (amode == SQMP_ACT_PER_GROUP) {
-          if (!clean) SQMP_HIP_CHECK(hipMemsetAsync(cmax, 0, sizeof(uint32_t) * k64, s));
-          st2 = launch_colmax(x, dtype, M, K, cmax, s, false);
+          if (stats_given) {
+            st2 = SQMP_OK;
+          } else {
+            if (!clean) SQMP_HIP_CHECK(hipMemsetAsync(cmax, 0, sizeof(uint32_t) * k64, s));
+            st2 = launch_colmax(x, dtype, M, K, cmax, s, false);
+          }
         } else {
           st2 = launch_colkey_mean3std(x, dtype, M, K, sums, cmax, s, clean);
         }
@@ -1022,7 +1031,7 @@ extern "C" int sqmp_quant_act_v2(void* x, int dtype, int M, int K, int amode, in
   }
 
   // ---- general path (fp32, 8-bit int output, large rows, other group sizes)
-  if (amode == SQMP_ACT_PER_TENSOR || amode == SQMP_ACT_PER_GROUP) {
+  if ((amode == SQMP_ACT_PER_TENSOR || amode == SQMP_ACT_PER_GROUP) && !stats_given) {
     SQMP_HIP_CHECK(hipMemsetAsync(cmax, 0, sizeof(uint32_t) * k64, s));
     st = launch_colmax(x, dtype, M, K, cmax, s, false);
     if (st) return st;

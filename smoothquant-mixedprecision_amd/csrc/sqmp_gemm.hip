@@ -66,7 +66,7 @@ __global__ __launch_bounds__(256, 2) void gemm_generic_kernel(
     const typename DT::T* __restrict__ A, const uint8_t* __restrict__ codes,
     const typename DT::T* __restrict__ wscale, const typename DT::T* __restrict__ wsal,
     const typename DT::T* __restrict__ bias, typename DT::T* __restrict__ Y, int M, int N,
-    int Kp, int S_pad, int Gw, int ngw, int tiles_m, int tiles_n) {
+    int Kp, int S_pad, int Gw, int ngw, int tiles_m, int tiles_n, uint32_t* __restrict__ colmax) {
   typedef typename DT::T T;
   typedef BDecode<DT, WBITS> Dec;
   constexpr int BKE = ROWB / sizeof(T);
@@ -172,27 +172,36 @@ __global__ __launch_bounds__(256, 2) void gemm_generic_kernel(
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int gn = n0 + wn * 64 + j * 16 + (lane & 15);
-    if (gn >= N) continue;
-    const float bv = bias ? DT::to_f(bias[gn]) : 0.f;
+    const float bv = bias && gn < N ? DT::to_f(bias[gn]) : 0.f;
+    float cm = 0.f;  // max |y| of this lane's rows in column gn (the stored D values)
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int gm = m0 + wm * 64 + i * 16 + (lane >> 4) * 4 + r;
-        if (gm < M) Y[(size_t)gm * N + gn] = DT::from_f(acc[i][j][r] + bv);
+        const T v = DT::from_f(acc[i][j][r] + bv);
+        if (gm < M && gn < N) {
+          Y[(size_t)gm * N + gn] = v;
+          cm = fmaxf(cm, fabsf(DT::to_f(v)));
+        }
       }
+    if (colmax) {  // lanes l, l + 16, l + 32, l + 48 hold the same column
+      cm = fmaxf(cm, __shfl_xor(cm, 16, 64));
+      cm = fmaxf(cm, __shfl_xor(cm, 32, 64));
+      if (lane < 16 && gn < N) atomicMax(colmax + gn, __float_as_uint(cm));
+    }
   }
 }
 
 template <class DT, int WBITS>
 static int generic_launch(const void* a, const void* codes, const void* wscale,
                           const void* wsal, const void* bias, void* y, int M, int N, int Kp,
-                          int S_pad, int Gw, int ngw, hipStream_t s) {
+                          int S_pad, int Gw, int ngw, uint32_t* colmax, hipStream_t s) {
   typedef typename DT::T T;
   const int tiles_m = cdiv(M, BM), tiles_n = cdiv(N, BN);
   gemm_generic_kernel<DT, WBITS><<<dim3(tiles_m * tiles_n), dim3(256), 0, s>>>(
       (const T*)a, (const uint8_t*)codes, (const T*)wscale, (const T*)wsal, (const T*)bias,
-      (T*)y, M, N, Kp, S_pad, Gw, ngw, tiles_m, tiles_n);
+      (T*)y, M, N, Kp, S_pad, Gw, ngw, tiles_m, tiles_n, colmax);
   SQMP_LAUNCH_CHECK();
   return SQMP_OK;
 }
@@ -218,6 +227,14 @@ extern "C" int sqmp_gemm_fq(const void* a, const void* codes, const void* wscale
                             const void* wsal, const void* bias, void* y, int dtype, int M,
                             int N, int Kp, int S_pad, int Gw, int ngw, int n_bits,
                             void* stream) {
+  return sqmp_gemm_fq_colmax(a, codes, wscale, wsal, bias, y, dtype, M, N, Kp, S_pad, Gw, ngw,
+                             n_bits, nullptr, stream);
+}
+
+extern "C" int sqmp_gemm_fq_colmax(const void* a, const void* codes, const void* wscale,
+                                   const void* wsal, const void* bias, void* y, int dtype,
+                                   int M, int N, int Kp, int S_pad, int Gw, int ngw,
+                                   int n_bits, uint32_t* colmax, void* stream) {
   int st = check_gemm_geometry(dtype, M, N, Kp, S_pad, Gw, ngw, n_bits);
   if (st) return st;
   if (!a || !codes || (n_bits && !wscale) || !y || (S_pad > 0 && !wsal)) return SQMP_EINVAL;
@@ -225,8 +242,10 @@ extern "C" int sqmp_gemm_fq(const void* a, const void* codes, const void* wscale
   if (n_bits == 0) { Gw = Kp; ngw = 1; }
   hipStream_t s = (hipStream_t)stream;
   const bool fast = dtype != SQMP_F32 && (n_bits == 0 || (n_bits == 4 && (Gw % 64 == 0 || Gw == 32)));
-  if (fast) return launch_gemm_fq_fast(dtype, a, codes, wscale, wsal, bias, y, M, N, Kp, S_pad, Gw, ngw, n_bits, s);
-#define SQMP_G(DTT, WB) generic_launch<DTT, WB>(a, codes, wscale, wsal, bias, y, M, N, Kp, S_pad, Gw, ngw, s)
+  if (fast)
+    return launch_gemm_fq_fast(dtype, a, codes, wscale, wsal, bias, y, M, N, Kp, S_pad, Gw, ngw,
+                               n_bits, colmax, s);
+#define SQMP_G(DTT, WB) generic_launch<DTT, WB>(a, codes, wscale, wsal, bias, y, M, N, Kp, S_pad, Gw, ngw, colmax, s)
   switch (dtype) {
     case SQMP_F32: return n_bits == 4 ? SQMP_G(F32, 4) : n_bits == 8 ? SQMP_G(F32, 8) : SQMP_G(F32, 0);
     case SQMP_F16: return n_bits == 4 ? SQMP_G(F16, 4) : n_bits == 8 ? SQMP_G(F16, 8) : SQMP_G(F16, 0);

@@ -296,12 +296,12 @@ __global__ __launch_bounds__(512, 1) void gemm_f8v2_kernel(
     const typename DT::T* __restrict__ XS, const unsigned char* __restrict__ W8,
     const float* __restrict__ ws32, const typename DT::T* __restrict__ wsal,
     const typename DT::T* __restrict__ bias, typename DT::T* __restrict__ Y, int M, int N,
-    int Kp, int S_pad, int Gw, int ngw, int tiles_m, int tiles_n) {
+    int Kp, int S_pad, int Gw, int ngw, int tiles_m, int tiles_n, int group_m) {
   typedef typename DT::T T;
   __shared__ __attribute__((aligned(16))) unsigned char lds[V2_NSLOT * V2_SLOT];
 
   int tm, tn;
-  tile_coords(tiles_m, tiles_n, 4, tm, tn);
+  tile_coords(tiles_m, tiles_n, group_m, tm, tn);
   const int m0 = tm * 256, n0 = tn * 256;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -558,11 +558,15 @@ extern "C" int sqmp_gemm_f8(const void* a8, const float* ascale, const void* xs,
     return e && atoi(e) != 0;
   }();
   const bool v2 = Gw % 128 == 0 && !v1_only;
+  static const int group_m = [] {  // M-tiles per raster group (SQMP_GROUP_M: A/B knob)
+    const char* e = getenv("SQMP_GROUP_M");
+    return e && atoi(e) > 0 ? atoi(e) : 4;
+  }();
 #define SQMP_F8L(DTT)                                                                        \
   if (v2) gemm_f8v2_kernel<DTT><<<grid, block, 0, s>>>(                                      \
       (const unsigned char*)a8, ascale, (const DTT::T*)xs, (const unsigned char*)w8, ws32,   \
       (const DTT::T*)wsal, (const DTT::T*)bias, (DTT::T*)y, M, N, Kp, S_pad, Gw, ngw, tiles_m, \
-      tiles_n);                                                                              \
+      tiles_n, group_m);                                                                     \
   else gemm_f8_kernel<DTT><<<grid, block, 0, s>>>(                                           \
       (const unsigned char*)a8, ascale, (const DTT::T*)xs, (const unsigned char*)w8, ws32,   \
       (const DTT::T*)wsal, (const DTT::T*)bias, (DTT::T*)y, M, N, Kp, S_pad, Gw, ngw, tiles_m, \

@@ -48,9 +48,11 @@ int launch_quant_lc(int dtype, int mode, const void* x, int M, int K, int q_max,
 // e4m3 code output (token / tensor modes): out = codes [M][P], out_xs = D [M][S_pad].
 
 // Fast GEMMs (sqmp_gemm_fast.hip); SQMP_EUNSUPPORTED when the shape has no fast kernel.
+// colmax != NULL: the epilogue also atomic-maxes bits(max |y|) per output column into it
 int launch_gemm_fq_fast(int dtype, const void* a, const void* codes, const void* wscale,
                         const void* wsal, const void* bias, void* y, int M, int N, int Kp,
-                        int S_pad, int Gw, int ngw, int n_bits, hipStream_t s);
+                        int S_pad, int Gw, int ngw, int n_bits, uint32_t* colmax,
+                        hipStream_t s);
 int launch_gemm_i8_fast(int dtype, const int8_t* a8, const float* ascale, const void* xs,
                         const void* codes, const void* wscale, const void* wsal,
                         const void* bias, void* y, int M, int N, int Kp, int S_pad, int Gw,

@@ -20,7 +20,7 @@ ACT_PER_GROUP_MEAN3STD = 4
 W_PER_CHANNEL, W_PER_TENSOR, W_PER_GROUP, W_PER_GROUP_UNSORTED, W_NONE = 0, 1, 2, 3, 4
 W_PER_GROUP_MEAN3STD = 5
 OUT_FP, OUT_I8, OUT_INPLACE, OUT_F8 = 0, 1, 2, 3
-QA_CLEAN_WS, QA_REUSE_STATS = 1, 2
+QA_CLEAN_WS, QA_REUSE_STATS, QA_STATS_GIVEN = 1, 2, 4
 
 _vp, _i, _sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t
 _ip = ctypes.POINTER(ctypes.c_int)
@@ -43,6 +43,8 @@ SIGNATURES = {
     "sqmp_quant_act_v2": (_i, [_vp, _i, _i, _i, _i, _i, _i, _vp, _i, _vp, _vp, _i, _i, _vp, _i,
                                _i, _vp, _vp, _vp, _vp, _sz, _vp]),
     "sqmp_gemm_fq": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _vp]),
+    "sqmp_gemm_fq_colmax": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i,
+                                 _vp, _vp]),
     "sqmp_gemm_i8": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i,
                           _i, _vp]),
     "sqmp_pack_f8": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _vp, _vp]),

@@ -184,6 +184,9 @@ def _spec_list(spec):
 
 
 _identity._sqmp_identity = True
+# output-quant statistics fused into the GEMM epilogue (SQMP_OQ_FUSE=0: separate
+# statistics pass; A/B timing only -- the numerics are identical)
+_OQ_FUSE = __import__("os").environ.get("SQMP_OQ_FUSE", "1") != "0"
 
 _PACKED_BUFFERS = ("w_codes", "w_scale", "w_salient", "w_perm", "w_amap", "w_amap_fq",
                    "w_nonsal", "salient_i32", "w_dense", "out_amap_fq", "out_nonsal")
@@ -498,25 +501,36 @@ class W4A4Linear(nn.Module):
             a = ops.quant_act_fp(xc, pw, amode, bits, ag, stats_of=x)
         if mutate_input:
             ops.fake_quant_inplace(xc, amode, bits, ag, pw.amap_fq, pw.nonsal, 0)
+        if ospec is not None and self.salient_indices is not None and pw.N != pw.K:
+            raise IndexError(                                                # :311-314
+                f"The shape of the mask [{pw.K}] at index 0 does not match the shape "
+                f"of the indexed tensor [{x2.shape[0]}, {pw.N}] at index 1")
+        # output quantization fused into the GEMM epilogue (fake_quant.py:308-316): for
+        # per_group (sorted) / per_tensor the faithful GEMM also writes the column maxima of
+        # y into the output quantizer's workspace, which then skips its statistics pass
+        fuse = (ospec is not None and ospec[0] in ("per_group", "per_tensor") and _OQ_FUSE
+                and not use_f8
+                and not use_i8 and (self.salient_indices is None or pw.K - pw.S > 0))
         if use_f8:
             y = ops.gemm_f8(a8, sa, xs, pw, bias)
         elif use_i8:
             y = ops.gemm_i8(a8, sa, xs, pw, bias)
+        elif fuse:
+            ws = ops.out_quant_workspace(x2.shape[0], pw.N, x2.device)
+            y = ops.gemm_fq(a, pw, bias, colmax=ws["buf"])
         else:
             y = ops.gemm_fq(a, pw, bias)
         if ospec is not None:                                                # :308-316
             omode, obits, og = ospec
             if self.salient_indices is not None:
-                if pw.N != pw.K:
-                    raise IndexError(
-                        f"The shape of the mask [{pw.K}] at index 0 does not match the shape "
-                        f"of the indexed tensor [{y.shape[0]}, {pw.N}] at index 1")
                 if pw.K - pw.S > 0:
-                    ops.fake_quant_inplace(y, omode, obits, og, pw.amap_fq, pw.nonsal, pw.S)
+                    ops.fake_quant_inplace(y, omode, obits, og, pw.amap_fq, pw.nonsal, pw.S,
+                                           stats_given=fuse)
             else:
                 if self.out_amap_fq is None:
                     _, _, self.out_amap_fq, self.out_nonsal = ops.build_maps(pw.N, None, y.device)
-                ops.fake_quant_inplace(y, omode, obits, og, self.out_amap_fq, self.out_nonsal, 0)
+                ops.fake_quant_inplace(y, omode, obits, og, self.out_amap_fq, self.out_nonsal, 0,
+                                       stats_given=fuse)
         if len(x_shape) == 3:
             return y.view(x_shape[0], x_shape[1], -1)
         return y

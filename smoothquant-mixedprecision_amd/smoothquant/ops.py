@@ -292,18 +292,30 @@ def quant_act_i8(x2: torch.Tensor, pw: PackedWeight, act_quant: str, n_bits: int
     return a8, sa, xs
 
 
+def out_quant_workspace(M: int, C: int, device):
+    """The persistent workspace fake_quant_inplace uses for an [M, C] tensor on the current
+    stream (its first C words: the column-maximum region sqmp_gemm_fq_colmax fills)."""
+    nb = _ws_bytes(M, C, C)
+    stream = torch.cuda.current_stream(device).cuda_stream
+    return _act_ws(device, stream, C, C, nb)
+
+
 def fake_quant_inplace(t2: torch.Tensor, act_quant: str, n_bits: int, group_size: int,
-                       amap_fq: torch.Tensor, nonsal: torch.Tensor, S: int):
-    """Fake-quantize t [M, C] in place; columns marked -2 in amap_fq pass through."""
+                       amap_fq: torch.Tensor, nonsal: torch.Tensor, S: int,
+                       stats_given: bool = False):
+    """Fake-quantize t [M, C] in place; columns marked -2 in amap_fq pass through.
+    stats_given: the workspace's column maxima were produced by the GEMM that wrote t
+    (sqmp_gemm_fq_colmax; act modes per_group / per_tensor)."""
     _require_gpu(t2, "fake_quant")
     M, C = t2.shape
     lib = load()
     nb = lib.sqmp_act_workspace_bytes(M, C, C)
     stream = torch.cuda.current_stream(t2.device).cuda_stream
     e = _act_ws(t2.device, stream, C, C, nb)
+    flags = _lib.QA_CLEAN_WS | (_lib.QA_STATS_GIVEN if stats_given else 0)
     status = lib.sqmp_quant_act_v2(_p(t2), _dtype_code(t2.dtype), M, C, ACT_MODES[act_quant],
                                    n_bits, group_size, _p(amap_fq), C, _p(nonsal), None, S, 0,
-                                   None, _lib.QA_CLEAN_WS, _lib.OUT_INPLACE, None, None, None,
+                                   None, flags, _lib.OUT_INPLACE, None, None, None,
                                    _p(e["buf"]), e["buf"].numel(), ctypes.c_void_p(stream))
     if status != _lib.SQMP_OK:
         _WS.pop((t2.device.index, stream, C, C), None)
@@ -315,13 +327,19 @@ def fake_quant_inplace(t2: torch.Tensor, act_quant: str, n_bits: int, group_size
     return t2
 
 
-def gemm_fq(a: torch.Tensor, pw: PackedWeight, bias: Optional[torch.Tensor]) -> torch.Tensor:
+def gemm_fq(a: torch.Tensor, pw: PackedWeight, bias: Optional[torch.Tensor],
+            colmax: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """y = D(A . W_hat^T + bias).  colmax: a zeroed uint32 buffer of >= N words that the
+    epilogue max-reduces bits(|y|) per column into (fused output-quant statistics)."""
     M = a.shape[0]
     y = torch.empty((M, pw.N), dtype=pw.dtype, device=a.device)
     b_op, nb = pw.gemm_operand
-    check(load().sqmp_gemm_fq(_p(a), _p(b_op), _p(pw.wscale), _p(pw.wsal) if pw.S_pad else None,
-                              _p(bias), _p(y), _dtype_code(pw.dtype), M, pw.N, pw.Kp, pw.S_pad,
-                              pw.Gw, pw.ngw, nb, _stream(a)), "gemm_fq")
+    args = (_p(a), _p(b_op), _p(pw.wscale), _p(pw.wsal) if pw.S_pad else None, _p(bias), _p(y),
+            _dtype_code(pw.dtype), M, pw.N, pw.Kp, pw.S_pad, pw.Gw, pw.ngw, nb)
+    if colmax is None:
+        check(load().sqmp_gemm_fq(*args, _stream(a)), "gemm_fq")
+    else:
+        check(load().sqmp_gemm_fq_colmax(*args, _p(colmax), _stream(a)), "gemm_fq")
     return y
 
 
