@@ -384,13 +384,15 @@ class W4A4Linear(nn.Module):
                 setattr(self, name, None if t is None else torch.empty_like(t))
             t = sd.get(prefix + "bias")
             if t is not None and self.bias is not None:
+                # the bias lives with the packed buffers (the checkpoint's device), never
+                # on the fresh module's construction device: the GEMM reads it by pointer
                 if isinstance(self.bias, nn.Parameter):
                     # from_float aliased the source Linear's bias Parameter (:369-370):
                     # give the module its own, shaped like the checkpoint's
-                    self.bias = nn.Parameter(torch.empty_like(t, device=self.bias.device),
-                                             requires_grad=False)
-                elif self.bias.shape != t.shape or self.bias.dtype != t.dtype:
-                    self.bias = torch.empty_like(t, device=self.bias.device)
+                    self.bias = nn.Parameter(torch.empty_like(t), requires_grad=False)
+                elif (self.bias.shape != t.shape or self.bias.dtype != t.dtype
+                      or self.bias.device != t.device):
+                    self.bias = torch.empty_like(t)
         elif prefix + "weight" in sd:
             # a reference checkpoint (dequantized `weight` buffer): stored as given
             self.weight = sd[prefix + "weight"]
@@ -487,6 +489,9 @@ class W4A4Linear(nn.Module):
         bias = None if self.bias is None else self.bias.reshape(-1)
         if bias is not None and bias.dtype != pw.dtype:
             raise RuntimeError(f"bias dtype {bias.dtype} does not match {pw.dtype}")
+        if bias is not None and bias.device != x.device:
+            raise RuntimeError(f"bias on {bias.device}, input on {x.device}: move the module "
+                               "to the input's device")
         use_f8 = (self.kernel == "f8" or
                   (self.kernel == "auto" and ops.F8_AUTO and ops.f8_eligible(pw, amode, bits)
                    and ops.f8_input_ok(xc)))

@@ -25,7 +25,13 @@ WEIGHT_MODES = {"per_channel": _lib.W_PER_CHANNEL, "per_tensor": _lib.W_PER_TENS
 
 
 def _p(t: Optional[torch.Tensor]):
-    return None if t is None else ctypes.c_void_p(t.data_ptr())
+    """Device pointer of t for the C-ABI (every kernel operand lives in HBM: a host tensor
+    here would be dereferenced by the GPU, so it is refused)."""
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise RuntimeError(f"kernel operand on {t.device}: every operand must be on the GPU")
+    return ctypes.c_void_p(t.data_ptr())
 
 
 def _stream(t: torch.Tensor):

@@ -83,3 +83,22 @@ def test_checkpoint_rejects_foreign_files(tmp_path):
     with pytest.raises(RuntimeError):
         load_quantized(nn.Linear(2, 2), p)
     assert FORMAT.startswith("sqmp-")
+
+
+def test_loaded_bias_follows_the_checkpoint_device():
+    """The packed buffers take the checkpoint's device; the bias must follow them, not the
+    fresh module's construction device (a host bias pointer handed to the GEMM is a GPU
+    memory fault).  The meta device stands in for the GPU here."""
+    sd = {k: (v.to("meta") if isinstance(v, torch.Tensor) else v)
+          for k, v in _fake_packed().state_dict().items()}
+    fresh = W4A4Linear(64, 32, bias=True)
+    assert fresh.bias.device.type == "cpu"
+    fresh.load_state_dict(sd, strict=True)
+    assert fresh.bias.device.type == "meta" and fresh.w_codes.device.type == "meta"
+
+
+def test_host_operands_are_refused():
+    from smoothquant import ops
+    with pytest.raises(RuntimeError, match="on the GPU"):
+        ops._p(torch.zeros(4))
+    assert ops._p(None) is None
