@@ -460,6 +460,41 @@ __global__ __launch_bounds__(512, 1) void gemm_f8v2_kernel(
     }
   }
 
+  // ---- epilogue, full-width tiles: the 256 x 256 output tile is staged in LDS (row m:
+  // 512 B, 16-B chunk c at physical chunk c ^ (m & 31)), then each row leaves as one
+  // 512-B run (32 lanes x 16 B) instead of 16 rows x 32 B per store instruction
+  if (n0 + 256 <= N && (N & 7) == 0) {
+    __builtin_amdgcn_s_barrier();  // every wave is past its last fragment read
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int nl = wn * 64 + 16 * j + 4 * q;
+      float bv[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) bv[r] = bias ? DT::to_f(bias[n0 + nl + r]) : 0.f;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int ml = xrow0 + 16 * i;
+        T v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = DT::from_f(tot[i][j][r] + bv[r]);
+        *(uint2*)(lds + ml * 512 + (((nl >> 3) ^ (ml & 31)) << 4) + (nl & 4) * 2) =
+            *(const uint2*)v;
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's tile writes landed
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    const int c = tid & 31;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int ml = 16 * k + (tid >> 5);
+      const u32x4 val = *(const u32x4*)(lds + ml * 512 + ((c ^ (ml & 31)) << 4));
+      if (m0 + ml < M) *(u32x4*)(Y + (size_t)(m0 + ml) * N + n0 + c * 8) = val;
+    }
+    return;
+  }
+
   // ---- epilogue: lane = row m0 + xrow0 + 16 i, columns n0 + wn 64 + 16 j + 4 q + r
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
