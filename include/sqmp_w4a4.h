@@ -91,11 +91,15 @@ enum sqmp_act_out {
                            out_xs: D [M][S_pad] exact salient x (operand of sqmp_gemm_i8) */
   SQMP_OUT_INPLACE = 2, /* fake-quantize `x` in place through amap_fq (output quant,
                            fake_quant.py:308-316) */
-  SQMP_OUT_F8 = 3       /* per_token / per_tensor, n_bits <= 4, sqmp_quant_act_v2 with
+  SQMP_OUT_F8 = 3,      /* per_token / per_tensor, n_bits <= 4, sqmp_quant_act_v2 with
                            posmap only: out = OCP e4m3 integer codes [M][Kp] (bytes) in
                            packed order (0 at salient / padding positions); out_scale: fp32
                            [M] (the D scale); out_xs: D [M][S_pad] exact salient x
                            (operands of sqmp_gemm_f8) */
+  SQMP_OUT_F6 = 4       /* as SQMP_OUT_F8 with the codes as OCP FP6 e2m3 in the "f6
+                           packed" format: per row, every 32 consecutive packed positions
+                           one 24-byte block, value e at bits [6e, 6e+6); out [M][Kp*3/4]
+                           bytes (operand of sqmp_gemm_f6) */
 };
 
 /* Library identity. */
@@ -205,7 +209,8 @@ int sqmp_gemm_i8(const int8_t* a8, const float* ascale, const void* xs,
 
 /* e4m3 operands of sqmp_gemm_f8 from a packed 4-bit weight: w8 = the int4 codes as OCP
  * e4m3 bytes [Np][Kp] in packed order, ws32 = the D group scales as fp32 [ngw][Np]
- * (Np = roundup(N, 256)).  Once per layer. */
+ * (Np = roundup(N, 256)).  Once per layer.  w8 = NULL builds the scales only (the f6
+ * GEMM's ws32). */
 int sqmp_pack_f8(const void* codes, const void* wscale, int dtype, int N, int Kp, int ngw,
                  void* w8, float* ws32, void* stream);
 
@@ -215,6 +220,19 @@ int sqmp_pack_f8(const void* codes, const void* wscale, int dtype, int N, int Kp
  * salient tail on the D MFMA, bias, one rounding to D.  Gw % 64 == 0, fp16/bf16.
  * a8 and xs: roundup(M, 256) rows allocated (operand allocation rule above). */
 int sqmp_gemm_f8(const void* a8, const float* ascale, const void* xs, const void* w8,
+                 const float* ws32, const void* wsal, const void* bias, void* y, int dtype,
+                 int M, int N, int Kp, int S_pad, int Gw, int ngw, void* stream);
+
+/* FP6 weight operand of sqmp_gemm_f6: the int4 codes as OCP FP6 e2m3 [Np][Kp*3/4] bytes
+ * in the f6-packed format of SQMP_OUT_F6 (Np = roundup(N, 256)); the scales are
+ * sqmp_pack_f8's ws32.  Once per layer. */
+int sqmp_pack_f6(const void* codes, int N, int Kp, void* w6, void* stream);
+
+/* sqmp_gemm_f8 on FP6 e2m3 operands (SQMP_OUT_F6 codes x sqmp_pack_f6 codes) through the
+ * same block-scaled MFMA at twice the e4m3 rate: the same exact integer block sums and
+ * fp32 fold order, so y is bit-identical to sqmp_gemm_f8's.  Gw % 128 == 0, fp16/bf16;
+ * a6 and xs: roundup(M, 256) rows allocated. */
+int sqmp_gemm_f6(const void* a6, const float* ascale, const void* xs, const void* w6,
                  const float* ws32, const void* wsal, const void* bias, void* y, int dtype,
                  int M, int N, int Kp, int S_pad, int Gw, int ngw, void* stream);
 

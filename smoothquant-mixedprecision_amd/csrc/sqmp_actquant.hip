@@ -899,11 +899,12 @@ extern "C" int sqmp_quant_act_v2(void* x, int dtype, int M, int K, int amode, in
     return SQMP_EINVAL;
   if (out_kind == SQMP_OUT_INPLACE) {
     if (Kp != K) return SQMP_EINVAL;
-  } else if (out_kind == SQMP_OUT_FP || out_kind == SQMP_OUT_I8 || out_kind == SQMP_OUT_F8) {
+  } else if (out_kind == SQMP_OUT_FP || out_kind == SQMP_OUT_I8 || out_kind == SQMP_OUT_F8 ||
+             out_kind == SQMP_OUT_F6) {
     if (Kp < K || Kp % 128 != 0 || S_pad < S || S_pad % 64 != 0 || !out) return SQMP_EINVAL;
-    if (out_kind == SQMP_OUT_F8) {
+    if (out_kind == SQMP_OUT_F8 || out_kind == SQMP_OUT_F6) {
       if (!out_scale || (S_pad > 0 && !out_xs)) return SQMP_EINVAL;
-      // e4m3 holds every integer code up to 16 exactly; one scale per row
+      // e4m3 holds every integer code up to 16 exactly, e2m3 up to 7; one scale per row
       if (n_bits > 4 || (amode != SQMP_ACT_PER_TOKEN && amode != SQMP_ACT_PER_TENSOR))
         return SQMP_EUNSUPPORTED;
     }
@@ -985,8 +986,9 @@ extern "C" int sqmp_quant_act_v2(void* x, int dtype, int M, int K, int amode, in
     return SQMP_OK;
   };
 
-  // e4m3 codes for the f8 GEMM (token / tensor scales): list-order table, lc quantizer
-  if (out_kind == SQMP_OUT_F8) {
+  // e4m3 / e2m3 codes for the f8 / f6 GEMM (token / tensor scales): list-order table, lc
+  // quantizer
+  if (out_kind == SQMP_OUT_F8 || out_kind == SQMP_OUT_F6) {
     if (!posmap || lc_off || !quant_lc_supported(dtype, M, K, false, 0, Kn, Kp, S_pad, x, out) ||
         ((uintptr_t)out_xs) % 16 != 0)
       return SQMP_EUNSUPPORTED;
@@ -1001,7 +1003,7 @@ extern "C" int sqmp_quant_act_v2(void* x, int dtype, int M, int K, int amode, in
     SQMP_LAUNCH_CHECK();
     st = launch_quant_lc(dtype, amode == SQMP_ACT_PER_TENSOR ? 1 : 0, x, M, K, q_max, 1, lctab,
                          Kn, amap, Kp, salient, S, S_pad, cmax, nonsal, out, nullptr, 0, s,
-                         (float*)out_scale, out_xs);
+                         (float*)out_scale, out_xs, out_kind == SQMP_OUT_F6);
     if (st) return st;
     // the per-tensor maximum was read by every workgroup: clear it after the launch
     if (clean && amode == SQMP_ACT_PER_TENSOR)

@@ -201,8 +201,10 @@ _PW_KEY = ("w_codes", "w_scale", "w_salient", "w_perm", "w_amap", "w_amap_fq", "
 class W4A4Linear(nn.Module):
     """Mixed-precision W4A4 linear: salient input channels in D, the rest int4/int8.
 
-    Forward kernels (chosen per layer, see `kernel`; "auto" = "f8" where ops.f8_eligible,
-    else "fq" unless ops.I8_AUTO):
+    Forward kernels (chosen per layer, see `kernel`; "auto" = "f6" where ops.f6_eligible,
+    else "f8" where ops.f8_eligible, else "fq" unless ops.I8_AUTO):
+      "f6"  as "f8" with both code operands in FP6 e2m3 (weight groups of whole 128-blocks):
+            twice the MFMA rate, 0.75-byte operands, the same y bit for bit.
       "f8"  per_token / per_tensor 4-bit activations: e4m3 act codes x e4m3 weight codes on
             the block-scaled FP8 MFMA (exact integer block sums), per-group fp32 folds.
       "i8"  per_token / per_tensor activations: int8 act codes x int4 weight codes on the
@@ -492,13 +494,18 @@ class W4A4Linear(nn.Module):
         if bias is not None and bias.device != x.device:
             raise RuntimeError(f"bias on {bias.device}, input on {x.device}: move the module "
                                "to the input's device")
-        use_f8 = (self.kernel == "f8" or
-                  (self.kernel == "auto" and ops.F8_AUTO and ops.f8_eligible(pw, amode, bits)
+        use_f6 = (self.kernel == "f6" or
+                  (self.kernel == "auto" and ops.F6_AUTO and ops.f6_eligible(pw, amode, bits)
                    and ops.f8_input_ok(xc)))
+        use_f8 = use_f6 or self.kernel == "f8" or (
+            self.kernel == "auto" and ops.F8_AUTO and ops.f8_eligible(pw, amode, bits)
+            and ops.f8_input_ok(xc))
         use_i8 = not use_f8 and (
             self.kernel == "i8" or
             (self.kernel == "auto" and ops.I8_AUTO and ops.i8_eligible(pw, amode, bits)))
-        if use_f8:
+        if use_f6:
+            a8, sa, xs = ops.quant_act_f6(xc, pw, amode, bits)
+        elif use_f8:
             a8, sa, xs = ops.quant_act_f8(xc, pw, amode, bits)
         elif use_i8:
             a8, sa, xs = ops.quant_act_i8(xc, pw, amode, bits)
@@ -516,7 +523,9 @@ class W4A4Linear(nn.Module):
         fuse = (ospec is not None and ospec[0] in ("per_group", "per_tensor") and _OQ_FUSE
                 and not use_f8
                 and not use_i8 and (self.salient_indices is None or pw.K - pw.S > 0))
-        if use_f8:
+        if use_f6:
+            y = ops.gemm_f6(a8, sa, xs, pw, bias)
+        elif use_f8:
             y = ops.gemm_f8(a8, sa, xs, pw, bias)
         elif use_i8:
             y = ops.gemm_i8(a8, sa, xs, pw, bias)

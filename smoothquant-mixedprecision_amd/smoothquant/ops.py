@@ -89,7 +89,8 @@ class PackedWeight:
     posmap: Optional[torch.Tensor] = field(default=None)  # int32 [K]: packed position of column k
     sal_key: Optional[tuple] = field(default=None)        # identity of the salient set (host)
     w8: Optional[torch.Tensor] = field(default=None)     # uint8 [Np, Kp] e4m3 codes (f8 GEMM)
-    ws32: Optional[torch.Tensor] = field(default=None)   # fp32 [ngw, Np] scales (f8 GEMM)
+    ws32: Optional[torch.Tensor] = field(default=None)   # fp32 [ngw, Np] scales (f8/f6 GEMM)
+    w6: Optional[torch.Tensor] = field(default=None)     # uint8 [Np, Kp*3/4] e2m3 (f6 GEMM)
 
     @property
     def gemm_operand(self):
@@ -360,25 +361,48 @@ def gemm_i8(a8: torch.Tensor, sa: torch.Tensor, xs: torch.Tensor, pw: PackedWeig
     return y
 
 
+def _ws32(pw: PackedWeight) -> torch.Tensor:
+    """fp32 [ngw, Np] weight scales of the f8 / f6 GEMMs, built once per packed weight."""
+    if pw.ws32 is None:
+        ws32 = torch.empty((pw.ngw, pad_n(pw.N)), dtype=torch.float32, device=pw.codes.device)
+        check(load().sqmp_pack_f8(_p(pw.codes), _p(pw.wscale), _dtype_code(pw.dtype), pw.N,
+                                  pw.Kp, pw.ngw, None, _p(ws32), _stream(pw.codes)), "pack_f8")
+        pw.ws32 = ws32
+    return pw.ws32
+
+
 def f8_operands(pw: PackedWeight):
     """(w8, ws32) of the f8 GEMM, built once per packed weight."""
     if pw.w8 is None:
-        Np = pad_n(pw.N)
-        w8 = torch.empty((Np, pw.Kp), dtype=torch.uint8, device=pw.codes.device)
-        ws32 = torch.empty((pw.ngw, Np), dtype=torch.float32, device=pw.codes.device)
+        w8 = torch.empty((pad_n(pw.N), pw.Kp), dtype=torch.uint8, device=pw.codes.device)
         check(load().sqmp_pack_f8(_p(pw.codes), _p(pw.wscale), _dtype_code(pw.dtype), pw.N,
-                                  pw.Kp, pw.ngw, _p(w8), _p(ws32), _stream(pw.codes)), "pack_f8")
-        pw.w8, pw.ws32 = w8, ws32
-    return pw.w8, pw.ws32
+                                  pw.Kp, pw.ngw, _p(w8), _p(_ws32(pw)), _stream(pw.codes)),
+              "pack_f8")
+        pw.w8 = w8
+    return pw.w8, _ws32(pw)
 
 
-def quant_act_f8(x2: torch.Tensor, pw: PackedWeight, act_quant: str, n_bits: int):
+def f6_operands(pw: PackedWeight):
+    """(w6, ws32) of the f6 GEMM, built once per packed weight."""
+    if pw.w6 is None:
+        w6 = torch.empty((pad_n(pw.N), pw.Kp // 32 * 24), dtype=torch.uint8,
+                         device=pw.codes.device)
+        check(load().sqmp_pack_f6(_p(pw.codes), pw.N, pw.Kp, _p(w6), _stream(pw.codes)),
+              "pack_f6")
+        pw.w6 = w6
+    return pw.w6, _ws32(pw)
+
+
+def quant_act_f8(x2: torch.Tensor, pw: PackedWeight, act_quant: str, n_bits: int,
+                 out_kind: int = _lib.OUT_F8):
     """x [M, K] -> (e4m3 codes [M, Kp] in packed order, fp32 row scales [M], exact salient
-    x [M, S_pad]) for gemm_f8 (per_token / per_tensor, n_bits <= 4)."""
+    x [M, S_pad]) for gemm_f8 (per_token / per_tensor, n_bits <= 4).  out_kind OUT_F6: the
+    codes as f6-packed e2m3 [M, Kp * 3 / 4] bytes for gemm_f6."""
     _require_gpu(x2, "quant_act")
     M, K = x2.shape
     Mp = _pad_rows(M)
-    a8 = torch.empty((Mp, pw.Kp), dtype=torch.uint8, device=x2.device)[:M]
+    width = pw.Kp // 32 * 24 if out_kind == _lib.OUT_F6 else pw.Kp
+    a8 = torch.empty((Mp, width), dtype=torch.uint8, device=x2.device)[:M]
     sa = torch.empty((M,), dtype=torch.float32, device=x2.device)
     xs = torch.empty((Mp, max(pw.S_pad, 8)), dtype=x2.dtype, device=x2.device)[:M]
     lib = load()
@@ -389,7 +413,7 @@ def quant_act_f8(x2: torch.Tensor, pw: PackedWeight, act_quant: str, n_bits: int
         pw.posmap = build_posmap(pw.perm, K)
     status = lib.sqmp_quant_act_v2(_p(x2), _dtype_code(x2.dtype), M, K, ACT_MODES[act_quant],
                                    n_bits, 0, _p(pw.amap), pw.Kp, _p(pw.nonsal), _p(pw.salient),
-                                   pw.S, pw.S_pad, _p(pw.posmap), _lib.QA_CLEAN_WS, _lib.OUT_F8,
+                                   pw.S, pw.S_pad, _p(pw.posmap), _lib.QA_CLEAN_WS, out_kind,
                                    _p(a8), _p(sa), _p(xs), _p(e["buf"]), e["buf"].numel(),
                                    ctypes.c_void_p(stream))
     if status != _lib.SQMP_OK:
@@ -408,6 +432,30 @@ def gemm_f8(a8: torch.Tensor, sa: torch.Tensor, xs: torch.Tensor, pw: PackedWeig
                               _dtype_code(pw.dtype), M, pw.N, pw.Kp, pw.S_pad, pw.Gw, pw.ngw,
                               _stream(a8)), "gemm_f8")
     return y
+
+
+def quant_act_f6(x2: torch.Tensor, pw: PackedWeight, act_quant: str, n_bits: int):
+    """quant_act_f8 with the codes as f6-packed e2m3 (operands of gemm_f6)."""
+    return quant_act_f8(x2, pw, act_quant, n_bits, _lib.OUT_F6)
+
+
+def gemm_f6(a6: torch.Tensor, sa: torch.Tensor, xs: torch.Tensor, pw: PackedWeight,
+            bias: Optional[torch.Tensor]) -> torch.Tensor:
+    """gemm_f8 on FP6 e2m3 operands (twice the MFMA rate; the same y bit for bit)."""
+    M = a6.shape[0]
+    w6, ws32 = f6_operands(pw)
+    y = torch.empty((M, pw.N), dtype=pw.dtype, device=a6.device)
+    check(load().sqmp_gemm_f6(_p(a6), _p(sa), _p(xs) if pw.S_pad else None, _p(w6), _p(ws32),
+                              _p(pw.wsal) if pw.S_pad else None, _p(bias), _p(y),
+                              _dtype_code(pw.dtype), M, pw.N, pw.Kp, pw.S_pad, pw.Gw, pw.ngw,
+                              _stream(a6)), "gemm_f6")
+    return y
+
+
+def f6_eligible(pw: PackedWeight, act_quant: str, act_bits: int) -> bool:
+    """f8_eligible with weight groups of whole 128-position blocks (one 16x16x128 MFMA per
+    group block)."""
+    return f8_eligible(pw, act_quant, act_bits) and pw.Gw % 128 == 0
 
 
 def f8_eligible(pw: PackedWeight, act_quant: str, act_bits: int) -> bool:
@@ -432,6 +480,8 @@ I8_AUTO = False
 # Whether kernel="auto" takes the FP8 path for eligible layers (f8_eligible): on gfx950
 # it is 1.4x the fq GEMM at config 2.
 F8_AUTO = True
+# Whether kernel="auto" takes the FP6 path where f6_eligible (bit-identical to "f8").
+F6_AUTO = True
 
 
 def i8_eligible(pw: PackedWeight, act_quant: str, act_bits: int) -> bool:
