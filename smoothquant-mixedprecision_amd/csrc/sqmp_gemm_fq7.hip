@@ -1,0 +1,534 @@
+// gemm_fq7 -- the faithful W4A4 GEMM (fake_quant.py:306 F.linear on q_x and W_hat) with
+// the int4 weight operand held in registers.
+//
+//   y[M][N] = D( A[M][Kp + S_pad] . W_hat^T + bias ),  A = x_hat in packed K order + the
+//   exact salient columns (sqmp_quant_act_v2 OUT_FP), W_hat = D(code * scale) decoded in
+//   registers (bit-exact with the reference's W_hat), then the exact salient weights.
+//
+// Why a second faithful kernel (gemm_fq6 stages A, the codes and the scales by LDS-DMA,
+// 48 one-KiB pieces per 256 x 256 x 64 stage, and an LDS-DMA piece holds its wave's
+// instruction stream for 60-185 cycles, MI355X_MICROARCH.md cycle table):
+//   * TM x 512 output tile (TM = 128 or 64) per 512-thread workgroup, 8 waves as 1 x 8,
+//     each TM x 64 on v_mfma_f32_16x16x32 -- half the A bytes per FLOP of a 256 x 256 tile;
+//   * only A moves through LDS (16 pieces per stage at TM = 128, 4-slot ring, 3 stages in
+//     flight).  Each wave's weight rows are private to it, so their codes, scales and
+//     salient slice are loaded straight into VGPRs from a tile-major copy of the packed
+//     weight (sqmp_pack_fq7): per stage a lane loads exactly its fragment bytes, 32 B of
+//     codes + 8 B of scales (codes stages) or 128 B of salient weights (tail stages), one
+//     stage ahead, with buffer loads whose per-stage offset is a scalar;
+//   * every vector-memory op of the loop (the DMA and the register loads) is issued from
+//     inline asm and waited for by hand-counted s_waitcnt vmcnt(N) (see gemm_fq6 for why
+//     the compiler must not see the LDS-DMA), with an empty asm "fence" that ties each
+//     loaded register to the wait before its first use.
+// Fragment geometry (as gemm_fq6): lane (r16, q) of sub-step s (32 of a 64-position stage)
+// takes bpack dword 2q + s of its weight row and A chunk c = 4 (q & 1) + 2 s + (q >> 1) --
+// the positions 8c .. 8c + 7 of that dword.  The weight fragment goes in the MFMA's A
+// slot, so acc[i][j][r] = C[n = n0 + 64 wave + 16 j + 4 q + r][m = m0 + 16 i + r16].
+#include <stdlib.h>
+
+#include <type_traits>
+
+#include "sqmp_mfma.h"
+
+namespace sqmp {
+namespace fq7 {
+
+typedef int rsrc_t __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+// raw buffer resource, no range check (every offset stays inside its operand)
+__device__ inline rsrc_t make_rsrc(const void* base) {
+  const uint64_t a = (uint64_t)(size_t)base;
+  rsrc_t r;
+  r[0] = (int)__builtin_amdgcn_readfirstlane((uint32_t)a);
+  r[1] = (int)__builtin_amdgcn_readfirstlane((uint32_t)(a >> 32) & 0xFFFFu);
+  r[2] = -1;
+  r[3] = 0x00020000;
+  return r;
+}
+
+template <int N>
+__device__ inline void vmwait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+// wave-uniform count -> immediate (waiting for more than needed is always safe)
+__device__ inline void vmwait_dyn(int n) {
+  switch (n) {
+    case 1: vmwait<1>(); break;
+    case 2: vmwait<2>(); break;
+    case 3: vmwait<3>(); break;
+    case 4: vmwait<4>(); break;
+    case 5: vmwait<5>(); break;
+    case 6: vmwait<6>(); break;
+    default: vmwait<0>(); break;
+  }
+}
+__device__ inline void barrier() {
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");  // no LDS read moves above the barrier
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+// LDS-DMA of 16 B per lane to the wave-uniform LDS base + 16 * lane.  s_nop 0: the M0
+// write -> LDS-DMA wait state (hipcc pads nothing inside an asm string).
+__device__ inline void dma16(const rsrc_t& r, uint32_t voff, uint32_t soff, unsigned char* lds_dst) {
+  const uint32_t m0v = __builtin_amdgcn_readfirstlane(
+      (uint32_t)(size_t)(__attribute__((address_space(3))) unsigned char*)lds_dst);
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds" ::"s"(m0v),
+               "v"(voff), "s"(r), "s"(soff)
+               : "memory", "m0");
+}
+// register loads, counted in vmcnt together with the DMA
+template <int OFF>
+__device__ inline void ld16(u32x4& d, const rsrc_t& r, uint32_t voff, uint32_t soff) {
+  asm volatile("buffer_load_dwordx4 %0, %1, %2, %3 offen offset:%4"
+               : "=v"(d)
+               : "v"(voff), "s"(r), "s"(soff), "n"(OFF));
+}
+__device__ inline void ld8(u32x2& d, const rsrc_t& r, uint32_t voff, uint32_t soff) {
+  asm volatile("buffer_load_dwordx2 %0, %1, %2, %3 offen" : "=v"(d) : "v"(voff), "s"(r), "s"(soff));
+}
+template <class V>
+__device__ inline void fence(V& v) {
+  asm volatile("" : "+v"(v));
+}
+
+__host__ __device__ inline int brev3(int c) { return ((c & 1) << 2) | (c & 2) | ((c >> 2) & 1); }
+
+// DIAG (timing diagnostics, wrong results by design; 0 = the product kernel): 1 no weight
+// register loads after the prologue, 2 no A DMA after the prologue, 3 no int4 decode, 4 no
+// per-stage barrier
+template <class DT, int GB, int TM, int DIAG = 0>
+__global__ __launch_bounds__(512, 1) void gemm_fq7_kernel(
+    const typename DT::T* __restrict__ A, const uint32_t* __restrict__ Bt,
+    const typename DT::T* __restrict__ St, const typename DT::T* __restrict__ Salt,
+    const typename DT::T* __restrict__ bias, typename DT::T* __restrict__ Y, int M, int N,
+    int Kp, int S_pad, int Gw, int ngw, int tiles_m, int tiles_n, int group_m,
+    uint32_t* __restrict__ colmax) {
+  typedef typename DT::T T;
+  constexpr int I = TM / 16, J = 4;     // 16 x 16 tiles per wave: TM rows x 64 weight rows
+  constexpr int PA = 3, NS = PA + 1;    // A stages in flight, ring slots
+  constexpr int SLOT = TM * 128;        // TM rows x 64 positions x 2 B
+  constexpr int NA = TM / 64;           // A pieces per wave per stage
+  constexpr int PF = 3;                 // A fragment read-ahead (blocks)
+  constexpr int LDS_BYTES = NS * SLOT > TM * 1024 ? NS * SLOT : TM * 1024;
+  static_assert(J <= I, "sub-step 1 decode must finish before block I");
+  __shared__ __attribute__((aligned(16))) unsigned char lds[LDS_BYTES];
+
+  int tm, tn;
+  tile_coords(tiles_m, tiles_n, group_m, tm, tn);
+  const int m0 = tm * TM, n0 = tn * 512;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r16 = lane & 15, q = lane >> 4;
+  const int lda = Kp + S_pad;
+  const int nkm = Kp / 64, nks = S_pad / 64, nkt = nkm + nks;
+  const int nb = tn * 8 + wave;  // this wave's 64-row weight block
+
+  // ---- A (x_hat) by LDS-DMA: piece i of wave w = rows 64 i + 8 w + (lane >> 3), the lane
+  // moving logical chunk brev3(p ^ ((row >> 1) & 7)) into physical chunk p = lane & 7
+  const int arow = 8 * wave + (lane >> 3);
+  const rsrc_t rA = make_rsrc(A + (size_t)m0 * lda);
+  uint32_t a_off[NA];
+#pragma unroll
+  for (int i = 0; i < NA; ++i)
+    a_off[i] = (uint32_t)((size_t)(arow + 64 * i) * lda * sizeof(T)) +
+               (uint32_t)(brev3((lane & 7) ^ ((arow >> 1) & 7)) << 4);
+  auto issue_a = [&](int kt) {
+    if (kt < nkt && (DIAG != 2 || kt < PA)) {
+      unsigned char* slot = lds + (kt % NS) * SLOT;
+      const uint32_t so = (uint32_t)kt * 64 * sizeof(T);
+#pragma unroll
+      for (int i = 0; i < NA; ++i) dma16(rA, a_off[i], so, slot + (i * 8 + wave) * 1024);
+    }
+  };
+
+  // ---- weight operand straight to registers (tile-major copies, sqmp_pack_fq7)
+  const rsrc_t rB = make_rsrc(Bt + (size_t)nb * nkm * 512);           // 2 KiB per stage
+  const rsrc_t rS = make_rsrc(St + (size_t)nb * ngw * 64);            // 128 B per group
+  const rsrc_t rD = make_rsrc(Salt + (size_t)nb * (nks > 0 ? nks : 1) * 4096);  // 8 KiB per stage
+  const uint32_t vB = (uint32_t)lane * 32u, vD = (uint32_t)lane * 128u;
+  const uint32_t vS = (uint32_t)r16 * 8u;
+  // one stage ahead: stage kt computes on register set kt & 1 (codes) / kd & 1 (salient
+  // tail) while the next stage's loads land in the other set.  No value in flight is ever
+  // copied (a copy the compiler placed before the wait would read the registers before
+  // the load lands), so the loops are unrolled by two with compile-time set indices: Kp %
+  // 128 == 0 makes the codes stage count even and the last codes stage odd.
+  struct Codes {
+    u32x4 w[2];  // dwords [j][s] of rows 16 j + r16
+    u32x2 s;     // scales of rows 16 j + r16 (4 x D)
+  };
+  struct Dense {
+    u32x4 w[8];  // chunk c(q, s) of rows 16 j + r16, [j][s]
+  };
+
+  auto issue_codes = [&](int kt, Codes& d) {
+    if (DIAG == 1 && kt > 1) return;
+    ld16<0>(d.w[0], rB, vB, (uint32_t)kt * 2048u);
+    ld16<16>(d.w[1], rB, vB, (uint32_t)kt * 2048u);
+    if (GB == 1) {
+      const int g = min((kt * 64) / Gw, ngw - 1);
+      ld8(d.s, rS, vS, (uint32_t)g * 128u);
+    } else {  // Gw = 32: the lane's dwords lie in group 2 kt + (q & 1) (clamped: padding)
+      const int g = min(2 * kt + (q & 1), ngw - 1);
+      ld8(d.s, rS, (uint32_t)g * 128u + vS, 0u);
+    }
+  };
+  // salient stage kd, sub-step s: the fragments [j][s] (4 x 16 B per lane)
+  auto issue_dense = [&](int kd, Dense& d, auto sc) {
+    constexpr int S = decltype(sc)::value;
+    const uint32_t so = (uint32_t)kd * 8192u;
+    ld16<16 * S>(d.w[S], rD, vD, so);
+    ld16<32 + 16 * S>(d.w[2 + S], rD, vD, so);
+    ld16<64 + 16 * S>(d.w[4 + S], rD, vD, so);
+    ld16<96 + 16 * S>(d.w[6 + S], rD, vD, so);
+  };
+  auto fence_codes = [&](Codes& d) {
+    fence(d.w[0]);
+    fence(d.w[1]);
+    fence(d.s);
+  };
+
+  f32x4 acc[I][J];
+#pragma unroll
+  for (int i = 0; i < I; ++i)
+#pragma unroll
+    for (int j = 0; j < J; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const DecK dk = make_deck();
+  const int a_sw = (r16 >> 1) & 7;
+  // A fragment of block t (sub-step s = t / I, row tile i = t % I)
+  auto ald = [&](const unsigned char* __restrict__ slot, int t) {
+    const int c = 4 * (q & 1) + 2 * (t / I) + (q >> 1);
+    return *(const u32x4*)(slot + (16 * (t % I) + r16) * 128 + ((brev3(c) ^ a_sw) << 4));
+  };
+#define SQMP_FQ7_BLOCKS(BF, ...)                                               \
+  {                                                                            \
+    u32x4 a[PF + 1];                                                           \
+    _Pragma("unroll") for (int t = 0; t < PF; ++t) a[t] = ald(slot, t);        \
+    _Pragma("unroll") for (int t = 0; t < 2 * I; ++t) {                        \
+      if (t + PF < 2 * I) a[(t + PF) % (PF + 1)] = ald(slot, t + PF);          \
+      _Pragma("unroll") for (int j = 0; j < J; ++j)                            \
+          Mfma<DT>::run(acc[t % I][j], BF(t / I, j), a[t % (PF + 1)]);         \
+      __VA_ARGS__;                                                             \
+      __builtin_amdgcn_sched_barrier(0);                                       \
+    }                                                                          \
+  }
+
+  auto compute_codes = [&](const unsigned char* __restrict__ slot, const Codes& cd) {
+    const uint32_t sb[4] = {cd.s.x & 0xFFFFu, cd.s.x >> 16, cd.s.y & 0xFFFFu, cd.s.y >> 16};
+    uint32_t sp[J];
+#pragma unroll
+    for (int j = 0; j < J; ++j) sp[j] = Dec<DT>::prep(sb[j]);
+    u32x4 bf[2][J];
+#pragma unroll
+    for (int j = 0; j < J; ++j)
+      bf[0][j] = DIAG == 3 ? u32x4{cd.w[j >> 1][(j & 1) * 2], sp[j], sp[j], sp[j]}
+                           : Dec<DT>::run(cd.w[j >> 1][(j & 1) * 2], sp[j], dk);
+#define SQMP_BF7(s, j) bf[s][j]
+    SQMP_FQ7_BLOCKS(SQMP_BF7,
+                    if (t < J) bf[1][t] = DIAG == 3 ? u32x4{cd.w[t >> 1][(t & 1) * 2 + 1], sp[t], sp[t], sp[t]}
+                                                    : Dec<DT>::run(cd.w[t >> 1][(t & 1) * 2 + 1], sp[t], dk));
+#undef SQMP_BF7
+  };
+  // hook(t) runs after the MFMAs of block t (the mid-stage wait / issue at t = I - 1)
+  auto compute_dense = [&](const unsigned char* __restrict__ slot, Dense& dd, auto hook) {
+#define SQMP_BD7(s, j) dd.w[2 * (j) + (s)]
+    SQMP_FQ7_BLOCKS(SQMP_BD7, hook(t));
+#undef SQMP_BD7
+  };
+#undef SQMP_FQ7_BLOCKS
+
+  // ops issued after B(kt) when stage kt starts: A(kt - 1 + PA) (or, at kt = 0, the
+  // prologue's A(1 .. PA-1)); A(kt) is older than B(kt) and so covered by the same wait
+  auto wait_stage = [&](int kt) {
+    const int n = kt == 0 ? NA * min(PA - 1, nkt - 1) : (kt - 1 + PA < nkt ? NA : 0);
+    vmwait_dyn(n);
+  };
+
+  using Z = std::integral_constant<int, 0>;
+  using O = std::integral_constant<int, 1>;
+  Codes cs[2];
+  Dense dd;  // one set: sub-step 0 of stage kd + 1 lands while sub-step 1 of kd computes
+
+  // prologue: A(0), B(0), A(1 .. PA-1)
+  issue_a(0);
+  issue_codes(0, cs[0]);
+#pragma unroll
+  for (int p = 1; p < PA; ++p) issue_a(p);
+
+  // codes stage kt on set P; the next codes stage's loads go to the other set, and after
+  // the last codes stage the first salient stage's two sub-steps
+  auto codes_step = [&](int kt, auto pc, bool last) {
+    constexpr int P = decltype(pc)::value;
+    wait_stage(kt);
+    fence_codes(cs[P]);
+    if (DIAG != 4) barrier();
+    if (!last) issue_codes(kt + 1, cs[P ^ 1]);
+    issue_a(kt + PA);
+    compute_codes(lds + (kt % NS) * SLOT, cs[P]);
+    if (last && nks > 0) {
+      issue_dense(0, dd, Z());
+      issue_dense(0, dd, O());
+    }
+  };
+  int kt = 0;
+  for (; kt + 2 < nkm; kt += 2) {
+    codes_step(kt, Z(), false);
+    codes_step(kt + 1, O(), false);
+  }
+  codes_step(kt, Z(), false);
+  codes_step(kt + 1, O(), true);
+  kt += 2;
+  // salient tail.  Issue order per stage kd: A(k + PA) at the top, sub-step 0 of kd + 1
+  // after block I - 1, sub-step 1 of kd + 1 at the end; so at the top of stage kd the ops
+  // younger than its sub-step 0 are its sub-step 1 (4), and at block I those younger
+  // than its sub-step 1 are A(k + PA).
+  for (int kd = 0; kd < nks; ++kd) {
+    const int k = nkm + kd;
+    vmwait<4>();
+#pragma unroll
+    for (int j = 0; j < J; ++j) fence(dd.w[2 * j]);
+    barrier();
+    issue_a(k + PA);
+    const bool more = kd + 1 < nks;
+    compute_dense(lds + (k % NS) * SLOT, dd, [&](int t) {
+      if (t == I - 1) {
+        if (k + PA < nkt)
+          vmwait<NA>();
+        else
+          vmwait<0>();
+#pragma unroll
+        for (int j = 0; j < J; ++j) fence(dd.w[2 * j + 1]);
+        if (more) issue_dense(kd + 1, dd, Z());
+      }
+    });
+    if (more) issue_dense(kd + 1, dd, O());
+  }
+
+  // ---- epilogue: the TM x 512 tile staged in LDS (row m: 1 KiB, 16-B chunk c at
+  // c ^ (m & 15)), stored as whole rows, one 16-B chunk per lane
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  barrier();  // every wave is past its last read of the ring
+  float cmx[J][4] = {};
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    const int nl = 64 * wave + 16 * j + 4 * q;  // first of the lane's 4 columns
+    float bv[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      bv[r] = bias && n0 + nl + r < N ? DT::to_f(bias[n0 + nl + r]) : 0.f;
+#pragma unroll
+    for (int i = 0; i < I; ++i) {
+      const int ml = 16 * i + r16;
+      T v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = DT::from_f(acc[i][j][r] + bv[r]);
+      if (colmax && m0 + ml < M) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) cmx[j][r] = fmaxf(cmx[j][r], fabsf(DT::to_f(v[r])));
+      }
+      const int c = nl >> 3;
+      *(u32x2*)(lds + ml * 1024 + ((c ^ (ml & 15)) << 4) + (nl & 4) * 2) = *(const u32x2*)v;
+    }
+  }
+  if (colmax) {
+#pragma unroll
+    for (int j = 0; j < J; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float v = cmx[j][r];
+        v = fmaxf(v, __shfl_xor(v, 1, 64));
+        v = fmaxf(v, __shfl_xor(v, 2, 64));
+        v = fmaxf(v, __shfl_xor(v, 4, 64));
+        v = fmaxf(v, __shfl_xor(v, 8, 64));
+        const int n = n0 + 64 * wave + 16 * j + 4 * q + r;
+        if (r16 == 0 && n < N) atomicMax(colmax + n, __float_as_uint(v));
+      }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  barrier();
+  const int c = lane;  // 64 chunks per row, one wave per row
+  const bool cok = n0 + c * 8 < N;  // N % 8 == 0 (launcher)
+#pragma unroll
+  for (int k = 0; k < TM / 8; ++k) {
+    const int ml = 8 * k + wave;
+    const int gm = m0 + ml;
+    const u32x4 val = *(const u32x4*)(lds + ml * 1024 + ((c ^ (ml & 15)) << 4));
+    if (gm < M && cok) *(u32x4*)(Y + (size_t)gm * N + n0 + c * 8) = val;
+  }
+}
+
+// ---- tile-major copies of the packed weight (once per layer)
+// Bt[nb][kb][lane][j][s] (dwords) = bpack dword 2q + s of block kb of row 64 nb + 16 j + r16
+__global__ void pack_codes_kernel(const uint32_t* __restrict__ codes, uint32_t* __restrict__ Bt,
+                                  int Np, int KB, long total) {
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= total) return;
+  const int d = (int)(idx & 7), lane = (int)((idx >> 3) & 63);
+  const long rest = idx >> 9;
+  const int kb = (int)(rest % KB);
+  const long nbk = rest / KB;
+  const int j = d >> 1, s = d & 1, q = lane >> 4, r16 = lane & 15;
+  const long n = nbk * 64 + 16 * j + r16;
+  Bt[idx] = n < Np ? codes[n * (KB * 8) + kb * 8 + 2 * q + s] : 0u;
+}
+// St[nb][g][r16][j] = wscale[g][64 nb + 16 j + r16]
+template <class T>
+__global__ void pack_scales_kernel(const T* __restrict__ wscale, T* __restrict__ St, int Np,
+                                   int ngw, long total) {
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= total) return;
+  const int j = (int)(idx & 3), r16 = (int)((idx >> 2) & 15);
+  const long rest = idx >> 6;
+  const int g = (int)(rest % ngw);
+  const long nbk = rest / ngw;
+  const long n = nbk * 64 + 16 * j + r16;
+  St[idx] = n < Np ? wscale[(long)g * Np + n] : (T)0.f;
+}
+// Salt[nb][kd][lane][j][s][e] = wsal[64 nb + 16 j + r16][64 kd + 8 c(q, s) + e]
+template <class T>
+__global__ void pack_sal_kernel(const T* __restrict__ wsal, T* __restrict__ Salt, int N,
+                                int S_pad, long total) {
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= total) return;
+  const int e = (int)(idx & 7), s = (int)((idx >> 3) & 1), j = (int)((idx >> 4) & 3);
+  const int lane = (int)((idx >> 6) & 63);
+  const int KS = S_pad / 64;
+  const long rest = idx >> 12;
+  const int kd = (int)(rest % KS);
+  const long nbk = rest / KS;
+  const int q = lane >> 4, r16 = lane & 15;
+  const int c = 4 * (q & 1) + 2 * s + (q >> 1);
+  const long n = nbk * 64 + 16 * j + r16;
+  Salt[idx] = n < N ? wsal[n * S_pad + kd * 64 + 8 * c + e] : (T)0.f;
+}
+
+static int group_m_env() {
+  static int v = [] {
+    const char* e = getenv("SQMP_FQ7_GROUP_M");
+    return e && atoi(e) > 0 ? atoi(e) : 8;
+  }();
+  return v;
+}
+
+static int diag_env() {
+  static int v = [] {
+    const char* e = getenv("SQMP_FQ7_DIAG");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+
+template <class DT, int GB, int TM, int DIAG = 0>
+static int launch_k(const void* a, const void* bt, const void* st, const void* salt,
+                  const void* bias, void* y, int M, int N, int Kp, int S_pad, int Gw, int ngw,
+                  uint32_t* colmax, hipStream_t s) {
+  typedef typename DT::T T;
+  const int tiles_m = cdiv(M, TM), tiles_n = cdiv(N, 512);
+  gemm_fq7_kernel<DT, GB, TM, DIAG><<<dim3(tiles_m * tiles_n), dim3(512), 0, s>>>(
+      (const T*)a, (const uint32_t*)bt, (const T*)st, (const T*)salt, (const T*)bias, (T*)y, M,
+      N, Kp, S_pad, Gw, ngw, tiles_m, tiles_n, group_m_env(), colmax);
+  SQMP_LAUNCH_CHECK();
+  return SQMP_OK;
+}
+
+template <class DT, int GB, int TM>
+static int launch(const void* a, const void* bt, const void* st, const void* salt,
+                  const void* bias, void* y, int M, int N, int Kp, int S_pad, int Gw, int ngw,
+                  uint32_t* colmax, hipStream_t s) {
+#define SQMP_L(D) launch_k<DT, GB, TM, D>(a, bt, st, salt, bias, y, M, N, Kp, S_pad, Gw, ngw, colmax, s)
+  if (std::is_same<DT, F16>::value && GB == 1 && TM == 128) {
+    switch (diag_env()) {
+      case 1: return SQMP_L(1);
+      case 2: return SQMP_L(2);
+      case 3: return SQMP_L(3);
+      case 4: return SQMP_L(4);
+      default: break;
+    }
+  }
+  return SQMP_L(0);
+#undef SQMP_L
+}
+
+template <class DT>
+static int dispatch(const void* a, const void* bt, const void* st, const void* salt,
+                    const void* bias, void* y, int M, int N, int Kp, int S_pad, int Gw,
+                    int ngw, uint32_t* colmax, hipStream_t s) {
+  // 64-row tiles when 128-row tiles leave CUs idle
+  const int tm = (long)cdiv(M, 128) * cdiv(N, 512) >= 256 ? 128 : 64;
+#define SQMP_FQ7(GB)                                                                          \
+  (tm == 128 ? launch<DT, GB, 128>(a, bt, st, salt, bias, y, M, N, Kp, S_pad, Gw, ngw, colmax, s) \
+             : launch<DT, GB, 64>(a, bt, st, salt, bias, y, M, N, Kp, S_pad, Gw, ngw, colmax, s))
+  if (Gw % 64 == 0) return SQMP_FQ7(1);
+  if (Gw == 32) return SQMP_FQ7(2);
+  return SQMP_EUNSUPPORTED;
+#undef SQMP_FQ7
+}
+
+}  // namespace fq7
+
+// rows of the tile-major copies: N rounded up to the 512-row tile
+static inline long fq7_rows(int N) { return (N + 511) / 512 * 512L; }
+
+extern "C" int sqmp_fq7_sizes(int N, int Kp, int S_pad, int ngw, size_t* codes_bytes,
+                              size_t* scale_elems, size_t* sal_elems) {
+  if (N <= 0 || Kp <= 0 || Kp % 64 || S_pad < 0 || S_pad % 64 || ngw <= 0) return SQMP_EINVAL;
+  const long R = fq7_rows(N);
+  if (codes_bytes) *codes_bytes = (size_t)R * Kp / 2;
+  if (scale_elems) *scale_elems = (size_t)R * ngw;
+  if (sal_elems) *sal_elems = (size_t)R * (S_pad > 0 ? S_pad : 64);
+  return SQMP_OK;
+}
+
+extern "C" int sqmp_pack_fq7(const void* codes, const void* wscale, const void* wsal, int dtype,
+                             int N, int Kp, int S_pad, int ngw, void* codes_t, void* scale_t,
+                             void* sal_t, void* stream) {
+  if (!codes || !wscale || !codes_t || !scale_t || !sal_t || (S_pad > 0 && !wsal))
+    return SQMP_EINVAL;
+  if (dtype != SQMP_F16 && dtype != SQMP_BF16) return SQMP_EUNSUPPORTED;
+  if (N <= 0 || Kp <= 0 || Kp % 64 || S_pad < 0 || S_pad % 64 || ngw <= 0) return SQMP_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  const long R = fq7_rows(N);
+  const int Np = pad_n(N), KB = Kp / 64;
+  const long tc = R * Kp / 8, ts = R * ngw;
+  fq7::pack_codes_kernel<<<dim3((unsigned)cdiv(tc, 256)), dim3(256), 0, s>>>(
+      (const uint32_t*)codes, (uint32_t*)codes_t, Np, KB, tc);
+  SQMP_LAUNCH_CHECK();
+  if (dtype == SQMP_F16)
+    fq7::pack_scales_kernel<_Float16><<<dim3((unsigned)cdiv(ts, 256)), dim3(256), 0, s>>>(
+        (const _Float16*)wscale, (_Float16*)scale_t, Np, ngw, ts);
+  else
+    fq7::pack_scales_kernel<__bf16><<<dim3((unsigned)cdiv(ts, 256)), dim3(256), 0, s>>>(
+        (const __bf16*)wscale, (__bf16*)scale_t, Np, ngw, ts);
+  SQMP_LAUNCH_CHECK();
+  if (S_pad > 0) {
+    const long tsl = R * S_pad;
+    if (dtype == SQMP_F16)
+      fq7::pack_sal_kernel<_Float16><<<dim3((unsigned)cdiv(tsl, 256)), dim3(256), 0, s>>>(
+          (const _Float16*)wsal, (_Float16*)sal_t, N, S_pad, tsl);
+    else
+      fq7::pack_sal_kernel<__bf16><<<dim3((unsigned)cdiv(tsl, 256)), dim3(256), 0, s>>>(
+          (const __bf16*)wsal, (__bf16*)sal_t, N, S_pad, tsl);
+    SQMP_LAUNCH_CHECK();
+  }
+  return SQMP_OK;
+}
+
+extern "C" int sqmp_gemm_fq7(const void* a, const void* codes_t, const void* scale_t,
+                             const void* sal_t, const void* bias, void* y, int dtype, int M,
+                             int N, int Kp, int S_pad, int Gw, int ngw, uint32_t* colmax,
+                             void* stream) {
+  if (!a || !codes_t || !scale_t || !sal_t || !y) return SQMP_EINVAL;
+  if (M < 0 || N <= 0 || Kp <= 0 || Kp % 128 || S_pad < 0 || S_pad % 64 || Gw <= 0 || ngw <= 0)
+    return SQMP_EINVAL;
+  if (dtype != SQMP_F16 && dtype != SQMP_BF16) return SQMP_EUNSUPPORTED;
+  if (N % 8) return SQMP_EUNSUPPORTED;  // whole 16-B output chunks
+  if (M == 0) return SQMP_OK;
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == SQMP_F16)
+    return fq7::dispatch<F16>(a, codes_t, scale_t, sal_t, bias, y, M, N, Kp, S_pad, Gw, ngw, colmax, s);
+  return fq7::dispatch<BF16>(a, codes_t, scale_t, sal_t, bias, y, M, N, Kp, S_pad, Gw, ngw, colmax, s);
+}
+
+}  // namespace sqmp

@@ -53,6 +53,11 @@ SIGNATURES = {
     "sqmp_pack_f6": (_i, [_vp, _i, _i, _vp, _vp]),
     "sqmp_gemm_f6": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i,
                           _vp]),
+    "sqmp_fq7_sizes": (_i, [_i, _i, _i, _i, ctypes.POINTER(_sz), ctypes.POINTER(_sz),
+                            ctypes.POINTER(_sz)]),
+    "sqmp_pack_fq7": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp]),
+    "sqmp_gemm_fq7": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _vp,
+                           _vp]),
 }
 
 _lock = threading.Lock()

@@ -6,6 +6,7 @@ raises if a tensor is not on a ROCm device: the W4A4 operator has no CPU path.
 from __future__ import annotations
 
 import ctypes
+import os
 import weakref
 from dataclasses import dataclass, field
 from typing import Optional
@@ -91,6 +92,7 @@ class PackedWeight:
     w8: Optional[torch.Tensor] = field(default=None)     # uint8 [Np, Kp] e4m3 codes (f8 GEMM)
     ws32: Optional[torch.Tensor] = field(default=None)   # fp32 [ngw, Np] scales (f8/f6 GEMM)
     w6: Optional[torch.Tensor] = field(default=None)     # uint8 [Np, Kp*3/4] e2m3 (f6 GEMM)
+    fq7: Optional[tuple] = field(default=None)           # (codes_t, scale_t, sal_t) of gemm_fq7
 
     @property
     def gemm_operand(self):
@@ -334,10 +336,54 @@ def fake_quant_inplace(t2: torch.Tensor, act_quant: str, n_bits: int, group_size
     return t2
 
 
+# Whether gemm_fq runs the register-operand kernel (sqmp_gemm_fq7) where fq7_eligible.
+FQ7_AUTO = os.environ.get("SQMP_FQ7", "0") == "1"
+
+
+def fq7_eligible(pw: PackedWeight) -> bool:
+    """4-bit codes in whole-64-block or 32-wide groups, fp16/bf16, whole 16-B output chunks
+    (sqmp_gemm_fq7)."""
+    return (pw.n_bits == 4 and pw.dense is None and pw.dtype != torch.float32
+            and (pw.Gw % 64 == 0 or pw.Gw == 32) and pw.N % 8 == 0)
+
+
+def fq7_operands(pw: PackedWeight):
+    """(codes_t, scale_t, sal_t) of gemm_fq7: tile-major copies of the packed weight, built
+    once per packed weight."""
+    if pw.fq7 is None:
+        sizes = [ctypes.c_size_t() for _ in range(3)]
+        check(load().sqmp_fq7_sizes(pw.N, pw.Kp, pw.S_pad, pw.ngw,
+                                    *[ctypes.byref(v) for v in sizes]), "fq7_sizes")
+        dev = pw.codes.device
+        bt = torch.empty(sizes[0].value, dtype=torch.uint8, device=dev)
+        st = torch.empty(sizes[1].value, dtype=pw.dtype, device=dev)
+        salt = torch.empty(sizes[2].value, dtype=pw.dtype, device=dev)
+        check(load().sqmp_pack_fq7(_p(pw.codes), _p(pw.wscale), _p(pw.wsal) if pw.S_pad else None,
+                                   _dtype_code(pw.dtype), pw.N, pw.Kp, pw.S_pad, pw.ngw, _p(bt),
+                                   _p(st), _p(salt), _stream(pw.codes)), "pack_fq7")
+        pw.fq7 = (bt, st, salt)
+    return pw.fq7
+
+
+def gemm_fq7(a: torch.Tensor, pw: PackedWeight, bias: Optional[torch.Tensor],
+             colmax: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """gemm_fq on the register-operand kernel (same operands and numerics)."""
+    M = a.shape[0]
+    y = torch.empty((M, pw.N), dtype=pw.dtype, device=a.device)
+    bt, st, salt = fq7_operands(pw)
+    check(load().sqmp_gemm_fq7(_p(a), _p(bt), _p(st), _p(salt), _p(bias), _p(y),
+                               _dtype_code(pw.dtype), M, pw.N, pw.Kp, pw.S_pad, pw.Gw, pw.ngw,
+                               _p(colmax) if colmax is not None else None, _stream(a)),
+          "gemm_fq7")
+    return y
+
+
 def gemm_fq(a: torch.Tensor, pw: PackedWeight, bias: Optional[torch.Tensor],
             colmax: Optional[torch.Tensor] = None) -> torch.Tensor:
     """y = D(A . W_hat^T + bias).  colmax: a zeroed uint32 buffer of >= N words that the
     epilogue max-reduces bits(|y|) per column into (fused output-quant statistics)."""
+    if FQ7_AUTO and fq7_eligible(pw):
+        return gemm_fq7(a, pw, bias, colmax)
     M = a.shape[0]
     y = torch.empty((M, pw.N), dtype=pw.dtype, device=a.device)
     b_op, nb = pw.gemm_operand

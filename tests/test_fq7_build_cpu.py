@@ -1,0 +1,40 @@
+"""Build-time guard for sqmp_gemm_fq7 (CPU, no GPU needed).
+
+The kernel keeps its weight loads in flight in VGPRs across hand-counted s_waitcnt; the
+compiler does not know those registers are still being written, so a spill (or any copy
+of them before the wait) would read them early.  Every fq7 kernel variant must therefore
+compile with zero VGPR spills (the timing-diagnostic DIAG variants are exempt) and no scratch (the ISA was also checked for copies of the
+in-flight registers when the loop structure was written)."""
+import os
+import re
+import shutil
+import subprocess
+
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+SRC = os.path.join(ROOT, "smoothquant-mixedprecision_amd", "csrc", "sqmp_gemm_fq7.hip")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC) and shutil.which("hipcc") is None,
+                    reason="hipcc not available")
+def test_fq7_kernels_do_not_spill(tmp_path):
+    r = subprocess.run([HIPCC, "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-I",
+                        os.path.join(ROOT, "include"), "-c", SRC, "-o", str(tmp_path / "fq7.o"),
+                        "-Rpass-analysis=kernel-resource-usage"],
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    blocks = re.split(r"remark: Function Name: ", r.stderr)
+    seen = 0
+    for b in blocks[1:]:
+        name = b.split()[0]
+        m = re.search(r"gemm_fq7_kernelI.*?ELi(\d+)ELi(\d+)ELi(\d+)E", name)
+        if not m or m.group(3) != "0":  # product kernels only (DIAG = 0)
+            continue
+        seen += 1
+        spill = int(re.search(r"VGPRs Spill: (\d+)", b).group(1))
+        scratch = int(re.search(r"ScratchSize \[bytes/lane\]: (\d+)", b).group(1))
+        assert spill == 0 and scratch == 0, f"{name}: {spill} VGPR spills, {scratch} B scratch"
+    assert seen >= 8
