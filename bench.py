@@ -252,6 +252,7 @@ def main(argv=None):
     pw = q.packed()
     # what W4A4Linear(kernel="auto") runs for this layer
     use_f8 = ops.F8_AUTO and ops.f8_eligible(pw, args.act, 4)
+    use_fqt = not use_f8 and ops.fqt_eligible(pw, args.act, 4, G, M)
     stream = torch.cuda.current_stream(dev)
     flops = 2.0 * M * N * K
 
@@ -287,6 +288,11 @@ def main(argv=None):
         kname = ("sqmp::gemm_f8v2_kernel<F16> (e4m3 on v_mfma_scale_f32_16x16x128_f8f6f4)"
                  if pw.Gw % 128 == 0 else
                  "sqmp::gemm_f8_kernel<F16> (e4m3 on v_mfma_scale_f32_32x32x64_f8f6f4)")
+    elif use_fqt:
+        c4 = ops.quant_act_c4(x, pw, args.act, 4, G)
+        gemm = lambda: ops.gemm_fqt(*c4, pw, lin.bias, G)  # noqa: E731
+        quant = lambda: ops.quant_act_c4(x, pw, args.act, 4, G)  # noqa: E731
+        kdt, kname = "f16", "sqmp::gemm_fq6_kernel<F16,1,256,true> (activation order, sqmp_gemm_fqt)"
     else:
         a = ops.quant_act_fp(x, pw, args.act, 4, G)
         gemm = lambda: ops.gemm_fq(a, pw, lin.bias)  # noqa: E731
@@ -322,6 +328,13 @@ def main(argv=None):
     if use_f8:
         wbytes = M * pw.Kp + M * 4 + M * pw.S_pad * 2
         reads = 2 if args.act == "per_tensor" else 1
+    elif use_fqt:
+        Kq = (K - pw.S + 63) // 64 * 64
+        # act codes + group scales + exact salient x, then the permuted weight (write) from
+        # the packed codes (read)
+        wbytes = (M * Kq // 2 + M * (Kq // G) * 2 + M * pw.S_pad * 2
+                  + N * (Kq + pw.S_pad) * 2 + N * pw.Kp // 2)
+        reads = 2
     else:
         wbytes = M * (pw.Kp + pw.S_pad) * 2
         reads = 2 if args.act in ("per_group", "per_tensor") else 1
@@ -329,6 +342,7 @@ def main(argv=None):
 
     traffic = None
     prof = os.path.join(ROOT, "profiles", "r02_pmc_gemm_f8v2_per_token.json" if kdt == "f8"
+                        else "r02_pmc_gemm_fqt_per_group.json" if use_fqt
                         else f"r02_pmc_gemm_fq6_{args.act}.json")
     if os.path.exists(prof):
         try:
@@ -356,7 +370,7 @@ def main(argv=None):
                          f"{int(P * 100)}% salient fp16 side-GEMM"),
             "M": M, "K": K, "N": N, "group_size": G, "salient_prop": P,
             "salient_channels": pw.S,
-            "kernel": "gemm_f8" if use_f8 else "gemm_fq",
+            "kernel": "gemm_f8" if use_f8 else "gemm_fqt" if use_fqt else "gemm_fq",
             "parallelism": f"replicas x{world}",
         },
         "roofline": {

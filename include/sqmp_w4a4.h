@@ -96,10 +96,17 @@ enum sqmp_act_out {
                            packed order (0 at salient / padding positions); out_scale: fp32
                            [M] (the D scale); out_xs: D [M][S_pad] exact salient x
                            (operands of sqmp_gemm_f8) */
-  SQMP_OUT_F6 = 4       /* as SQMP_OUT_F8 with the codes as OCP FP6 e2m3 in the "f6
+  SQMP_OUT_F6 = 4,      /* as SQMP_OUT_F8 with the codes as OCP FP6 e2m3 in the "f6
                            packed" format: per row, every 32 consecutive packed positions
                            one 24-byte block, value e at bits [6e, 6e+6); out [M][Kp*3/4]
                            bytes (operand of sqmp_gemm_f6) */
+  SQMP_OUT_C4 = 5       /* per_group activations in ACTIVATION order (operands of
+                           sqmp_gemm_fqt): out = int4 codes [roundup(M, 256)][Kq / 2] bytes,
+                           Kq = roundup(K - S, 64), bpack rows whose position j is the
+                           column of activation rank j (zeros past K - S); out_scale = the D
+                           group scales [Kq / group_size][roundup(M, 256)]; out_xs = the
+                           exact salient columns [M][S_pad].  4-bit, group_size % 64 == 0,
+                           fp16/bf16, posmap required. */
 };
 
 /* Library identity. */
@@ -259,6 +266,35 @@ int sqmp_pack_fq7(const void* codes, const void* wscale, const void* wsal, int d
 int sqmp_gemm_fq7(const void* a, const void* codes_t, const void* scale_t, const void* sal_t,
                   const void* bias, void* y, int dtype, int M, int N, int Kp, int S_pad,
                   int Gw, int ngw, uint32_t* colmax, void* stream);
+
+/* The weight operand of sqmp_gemm_fqt for the activation order of the LAST
+ * sqmp_quant_act_v2(SQMP_OUT_C4) call on `workspace` (same K, Kp, S, S_pad): wp
+ * [roundup(N, 256)][Kq + S_pad] in D, wp[n][j] = W_hat[n][column of activation rank j]
+ * (= D(code * scale), bit-exact with the reference's W_hat) for j < K - S, 0 for
+ * K - S <= j < Kq, then the exact salient weights wsal[n][:]; rows >= N are 0.
+ * codes / wscale / wsal: a packed 4-bit weight (sqmp_pack_weight). */
+int sqmp_perm_weight_c4(const void* workspace, int K, int Kp, int S, int S_pad,
+                        const void* codes, const void* wscale, const void* wsal, int dtype,
+                        int N, int Gw, int ngw, void* wp, void* stream);
+
+/* sqmp_quant_act_v2(SQMP_OUT_C4) + sqmp_perm_weight_c4 in one call: the quantizer and the
+ * weight permutation run in the same launch (independent given the rank table).  The
+ * whole per-forward prepass of sqmp_gemm_fqt. */
+int sqmp_quant_act_c4(void* x, int dtype, int M, int K, int amode, int n_bits, int group_size,
+                      const int32_t* amap, int Kp, const int32_t* nonsal,
+                      const int32_t* salient, int S, int S_pad, const int32_t* posmap,
+                      int flags, void* acodes, void* ascale, void* xs, const void* codes,
+                      const void* wscale, const void* wsal, int N, int Gw, int ngw, void* wp,
+                      void* workspace, size_t ws_bytes, void* stream);
+
+/* The faithful GEMM in activation order: y[M][N] = D(x_hat . W_hat^T + bias) computed as
+ * y^T = wp . codes^T with the act codes decoded in registers to D(code * scale) (= the
+ * reference's x_hat bit for bit) and the exact salient tail (xs x wsal): the same products
+ * as sqmp_gemm_fq minus the zero salient positions of the packed-order stream.  Operands
+ * of SQMP_OUT_C4 + sqmp_perm_weight_c4; G % 64 == 0, N % 8 == 0, fp16/bf16. */
+int sqmp_gemm_fqt(const void* acodes, const void* ascale, const void* xs, const void* wp,
+                  const void* bias, void* y, int dtype, int M, int N, int Kq, int S_pad,
+                  int G, int ngq, void* stream);
 
 #ifdef __cplusplus
 }

@@ -880,12 +880,28 @@ extern "C" size_t sqmp_act_workspace_bytes(int M, int K, int Kp) {
   return sizeof(uint32_t) * ws_u32_words(K, Kp) + 2 * sizeof(double) * ws_k64(K);
 }
 
+static int quant_act_impl(void* x, int dtype, int M, int K, int amode, int n_bits,
+                          int group_size, const int32_t* amap, int Kp, const int32_t* nonsal,
+                          const int32_t* salient, int S, int S_pad, const int32_t* posmap,
+                          int flags, int out_kind, void* out, void* out_scale, void* out_xs,
+                          void* workspace, size_t ws_bytes, void* stream, const C4Weight* cw);
+
 extern "C" int sqmp_quant_act_v2(void* x, int dtype, int M, int K, int amode, int n_bits,
                                  int group_size, const int32_t* amap, int Kp,
                                  const int32_t* nonsal, const int32_t* salient, int S,
                                  int S_pad, const int32_t* posmap, int flags, int out_kind,
                                  void* out, void* out_scale, void* out_xs, void* workspace,
                                  size_t ws_bytes, void* stream) {
+  return quant_act_impl(x, dtype, M, K, amode, n_bits, group_size, amap, Kp, nonsal, salient, S,
+                        S_pad, posmap, flags, out_kind, out, out_scale, out_xs, workspace,
+                        ws_bytes, stream, nullptr);
+}
+
+static int quant_act_impl(void* x, int dtype, int M, int K, int amode, int n_bits,
+                          int group_size, const int32_t* amap, int Kp, const int32_t* nonsal,
+                          const int32_t* salient, int S, int S_pad, const int32_t* posmap,
+                          int flags, int out_kind, void* out, void* out_scale, void* out_xs,
+                          void* workspace, size_t ws_bytes, void* stream, const C4Weight* cw) {
   hipStream_t s = (hipStream_t)stream;
   if (dtype < SQMP_F32 || dtype > SQMP_BF16 || M < 0 || K <= 0 || K > 65000) return SQMP_EINVAL;
   if (amode < SQMP_ACT_PER_TOKEN || amode > SQMP_ACT_PER_GROUP_MEAN3STD) return SQMP_EINVAL;
@@ -899,6 +915,13 @@ extern "C" int sqmp_quant_act_v2(void* x, int dtype, int M, int K, int amode, in
     return SQMP_EINVAL;
   if (out_kind == SQMP_OUT_INPLACE) {
     if (Kp != K) return SQMP_EINVAL;
+  } else if (out_kind == SQMP_OUT_C4) {
+    if (Kp < K || Kp % 128 != 0 || S_pad < S || S_pad % 64 != 0 || !out || !out_scale) return SQMP_EINVAL;
+    if ((S > 0 && (!salient || !out_xs)) || !posmap) return SQMP_EINVAL;
+    if (n_bits > 4 || (amode != SQMP_ACT_PER_GROUP && amode != SQMP_ACT_PER_GROUP_UNSORTED &&
+                       amode != SQMP_ACT_PER_GROUP_MEAN3STD) ||
+        group_size % 64 != 0)
+      return SQMP_EUNSUPPORTED;
   } else if (out_kind == SQMP_OUT_FP || out_kind == SQMP_OUT_I8 || out_kind == SQMP_OUT_F8 ||
              out_kind == SQMP_OUT_F6) {
     if (Kp < K || Kp % 128 != 0 || S_pad < S || S_pad % 64 != 0 || !out) return SQMP_EINVAL;
@@ -1011,6 +1034,20 @@ extern "C" int sqmp_quant_act_v2(void* x, int dtype, int M, int K, int amode, in
     return SQMP_OK;
   }
 
+  // act-order int4 codes (the sqmp_gemm_fqt operand): the OUT_FP fast path's table, codes
+  // written straight from the quantizing lanes
+  if (out_kind == SQMP_OUT_C4) {
+    if (Kn == 0 || lc_off || !quant_lc_supported(dtype, M, K, true, group_size, Kn, Kp, S_pad, x, out) ||
+        ((uintptr_t)out_xs) % 16 != 0)
+      return SQMP_EUNSUPPORTED;
+    uint32_t* kc;
+    st = lc_prepare(posmap, lc_none, (flags & SQMP_QA_REUSE_STATS) != 0, kc);
+    if (st) return st;
+    return launch_quant_lc_c4(dtype, x, M, K, q_max, group_size, lctab, Kn, Kp, salient, S,
+                              S_pad, cmax, nonsal, out, out_scale, (int)round_up(M, 256),
+                              out_xs, kc, (int)k64, s, cw);
+  }
+
   // fast path: the table maps ranks straight to packed positions (per-weight posmap)
   if (use_lc && posmap && amode != SQMP_ACT_PER_TENSOR) {
     uint32_t* kc;
@@ -1095,4 +1132,40 @@ extern "C" int sqmp_quant_act(void* x, int dtype, int M, int K, int amode, int n
   return sqmp_quant_act_v2(x, dtype, M, K, amode, n_bits, group_size, amap, Kp, nonsal,
                            salient, S, S_pad, nullptr, 0, out_kind, out, out_scale, out_xs,
                            workspace, ws_bytes, stream);
+}
+
+// ---------------------------------------------------------------- act-order weight (C4)
+static const uint32_t* ws_lctab(const void* workspace, int K, int Kp) {
+  const size_t k64 = ws_k64(K);
+  return (const uint32_t*)workspace + k64 * (2 + (size_t)rank_tiles(K)) +
+         (size_t)round_up(Kp > K ? Kp : K, 64);
+}
+
+extern "C" int sqmp_perm_weight_c4(const void* workspace, int K, int Kp, int S, int S_pad,
+                                   const void* codes, const void* wscale, const void* wsal,
+                                   int dtype, int N, int Gw, int ngw, void* wp, void* stream) {
+  if (!workspace || !codes || !wscale || !wp || (S > 0 && !wsal)) return SQMP_EINVAL;
+  if (K <= 0 || S < 0 || S >= K || Kp < K || Kp % 128 || S_pad < S || S_pad % 64 || N <= 0 ||
+      Gw <= 0 || ngw <= 0)
+    return SQMP_EINVAL;
+  if (dtype != SQMP_F16 && dtype != SQMP_BF16) return SQMP_EUNSUPPORTED;
+  if (Gw % 8 || Kp > 32768) return SQMP_EUNSUPPORTED;
+  return launch_perm_weight_c4(dtype, ws_lctab(workspace, K, Kp), codes, wscale, wsal, N, Kp,
+                               Gw, ngw, K - S, S_pad, wp, (hipStream_t)stream);
+}
+
+extern "C" int sqmp_quant_act_c4(void* x, int dtype, int M, int K, int amode, int n_bits,
+                                 int group_size, const int32_t* amap, int Kp,
+                                 const int32_t* nonsal, const int32_t* salient, int S,
+                                 int S_pad, const int32_t* posmap, int flags, void* acodes,
+                                 void* ascale, void* xs, const void* codes, const void* wscale,
+                                 const void* wsal, int N, int Gw, int ngw, void* wp,
+                                 void* workspace, size_t ws_bytes, void* stream) {
+  if (!codes || !wscale || !wp || (S > 0 && !wsal) || N <= 0 || Gw <= 0 || ngw <= 0)
+    return SQMP_EINVAL;
+  if (Gw % 8 || Kp > 32768) return SQMP_EUNSUPPORTED;
+  const C4Weight cw{codes, wscale, wsal, wp, N, Kp, Gw, ngw};
+  return quant_act_impl(x, dtype, M, K, amode, n_bits, group_size, amap, Kp, nonsal, salient, S,
+                        S_pad, posmap, flags, SQMP_OUT_C4, acodes, ascale, xs, workspace,
+                        ws_bytes, stream, &cw);
 }

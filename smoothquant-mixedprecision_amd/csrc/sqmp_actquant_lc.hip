@@ -169,14 +169,20 @@ __device__ inline uint32_t f6_pair(uint32_t v, const PairScale& c) {
 // RPL = ranks per thread; GS = the group size when it is below RPL (RPL / GS groups per
 // thread), else 0.  blockDim = 64 * NW.  F8 = 1 (token / tensor modes): out is e4m3 codes
 // [M][P] (bytes), out_scale the fp32 row scales, out_xs the exact salient columns [M][S_pad].
+// F8 = 3 (SQMP_OUT_C4, group mode, G >= RPL): out is the int4 codes in ACTIVATION-RANK
+// order as bpack rows of Kq positions (Kq / 2 bytes per row; the act-order GEMM operand),
+// out_scale (as D) the group scales [Kq / G][ldsc], out_xs the exact salient columns.
+// (the body of quant_lc_kernel: workgroup `bid` of `nblk` quantizer workgroups)
 template <class DT, int MODE, int RPL, int GS, int F8 = 0>
-__global__ __launch_bounds__(1024) void quant_lc_kernel(
+__device__ __forceinline__ void quant_lc_body(
     const typename DT::T* x, int M, int K, int q_max, int G,
     const uint32_t* __restrict__ lctab, int Kn, const int32_t* __restrict__ amap, int P,
     const int32_t* __restrict__ sal, int S, int S_pad, const uint32_t* __restrict__ cmax,
     const int32_t* __restrict__ nonsal, typename DT::T* out, uint32_t* __restrict__ key_clear,
-    int clear_words, float* __restrict__ out_scale, typename DT::T* __restrict__ out_xs) {
-  static_assert(!F8 || MODE != LC_MODE_GROUP, "F8 codes need one scale per row");
+    int clear_words, float* __restrict__ out_scale, typename DT::T* __restrict__ out_xs,
+    int Kq, int ldsc, const int bid, const int nblk) {
+  static_assert(!F8 || F8 == 3 || MODE != LC_MODE_GROUP, "F8 codes need one scale per row");
+  static_assert(F8 != 3 || (MODE == LC_MODE_GROUP && GS == 0), "C4: groups of >= RPL ranks");
   // x and out alias for in-place output quantization (every row is read before it is
   // written: a workgroup stores a pair only after loading it)
   typedef typename DT::T T;
@@ -208,7 +214,7 @@ __global__ __launch_bounds__(1024) void quant_lc_kernel(
       }
     }
   };
-  int rp = blockIdx.x;
+  int rp = bid;
   if (rp < npair) load_pair(rp);
 
   // ---- once per workgroup: salient-position mask, zeroed buffer (+ two spare words: W =
@@ -234,7 +240,7 @@ __global__ __launch_bounds__(1024) void quant_lc_kernel(
   // the column statistics of this call, read by the (completed) table kernel: restore the
   // clean-workspace zeros
   if (key_clear)
-    for (int c = blockIdx.x * nthr + tid; c < (clear_words >> 2); c += gridDim.x * nthr)
+    for (int c = bid * nthr + tid; c < (clear_words >> 2); c += nblk * nthr)
       ((u32x4*)key_clear)[c] = u32x4{0u, 0u, 0u, 0u};
   PairScale tens;
   if (MODE == LC_MODE_TENSOR) {
@@ -250,7 +256,7 @@ __global__ __launch_bounds__(1024) void quant_lc_kernel(
   }
   __syncthreads();
 
-  for (; rp < npair; rp += gridDim.x) {
+  for (; rp < npair; rp += nblk) {
     const int m0 = 2 * rp;
     const bool has1 = m0 + 1 < M;
     // ---- this thread's RPL table entries (L1/L2-resident, padded to whole rounds with
@@ -329,7 +335,34 @@ __global__ __launch_bounds__(1024) void quant_lc_kernel(
       } else {
         __syncthreads();
       }
-      if (F8) {
+      if (F8 == 3) {
+        // ranks rb .. rb + 15 = positions 16 u .. 16 u + 15 of bpack block rb / 64: dwords u
+        // (elements 0-7) and 4 + u (8-15); element e at nibble e / 2 (even e) or 4 + e / 2
+        if (rb < Kq) {
+          uint32_t d0[2] = {0u, 0u}, d1[2] = {0u, 0u};
+#pragma unroll
+          for (int i = 0; i < RPL; ++i) {
+            const f32x2 code = code_pair<DT>(v[i], c);
+            const int e = i & 7, sh = (e & 1) ? 16 + 4 * (e >> 1) : 4 * (e >> 1);
+            d0[i >> 3] |= (uint32_t)((int)code[0] + 8) << sh;
+            d1[i >> 3] |= (uint32_t)((int)code[1] + 8) << sh;
+          }
+          const int u = (rb >> 4) & 3;
+          uint32_t* r0 = (uint32_t*)((unsigned char*)out + (size_t)m0 * (Kq / 2)) + (rb >> 6) * 8;
+          uint32_t* r1 = (uint32_t*)((unsigned char*)out + (size_t)(m0 + 1) * (Kq / 2)) + (rb >> 6) * 8;
+          r0[u] = d0[0];
+          r0[4 + u] = d0[1];
+          if (has1) {
+            r1[u] = d1[0];
+            r1[4 + u] = d1[1];
+          }
+          if (rb % G == 0) {
+            uint16_t* sc = (uint16_t*)out_scale + (size_t)(rb / G) * ldsc + m0;
+            sc[0] = (uint16_t)(c.sd & 0xFFFFu);
+            if (has1) sc[1] = (uint16_t)(c.sd >> 16);
+          }
+        }
+      } else if (F8) {
 #pragma unroll
         for (int i = 0; i < RPL; ++i)
           lc_buf[tab[i] >> 16] = F8 == 2 ? f6_pair<DT>(v[i], c) : f8_pair<DT>(v[i], c);
@@ -343,8 +376,9 @@ __global__ __launch_bounds__(1024) void quant_lc_kernel(
       }
     }
     // salient columns' own packed positions hold 0 (their weight codes are 0 too)
-    for (uint64_t zm = zmask; zm; zm &= zm - 1) lc_buf[zp0 + __builtin_ctzll(zm)] = 0u;
-    if (rp + (int)gridDim.x < npair) load_pair(rp + gridDim.x);  // prefetch the next pair
+    if (F8 != 3)
+      for (uint64_t zm = zmask; zm; zm &= zm - 1) lc_buf[zp0 + __builtin_ctzll(zm)] = 0u;
+    if (rp + nblk < npair) load_pair(rp + nblk);  // prefetch the next pair
     __syncthreads();
 
     if (F8 == 2) {
@@ -441,6 +475,111 @@ __global__ __launch_bounds__(1024) void quant_lc_kernel(
   }
 }
 
+
+template <class DT, int MODE, int RPL, int GS, int F8 = 0>
+__global__ __launch_bounds__(1024) void quant_lc_kernel(
+    const typename DT::T* x, int M, int K, int q_max, int G,
+    const uint32_t* __restrict__ lctab, int Kn, const int32_t* __restrict__ amap, int P,
+    const int32_t* __restrict__ sal, int S, int S_pad, const uint32_t* __restrict__ cmax,
+    const int32_t* __restrict__ nonsal, typename DT::T* out, uint32_t* __restrict__ key_clear,
+    int clear_words, float* __restrict__ out_scale, typename DT::T* __restrict__ out_xs,
+    int Kq, int ldsc) {
+  quant_lc_body<DT, MODE, RPL, GS, F8>(x, M, K, q_max, G, lctab, Kn, amap, P, sal, S, S_pad,
+                                       cmax, nonsal, out, key_clear, clear_words, out_scale,
+                                       out_xs, Kq, ldsc, blockIdx.x, gridDim.x);
+}
+
+// ---- the activation-order weight operand (sqmp_gemm_fqt): wp[n][j] = W_hat[n][pos_j],
+// pos_j = lctab[j] >> 16 (the weight-packed position of the column of activation rank j),
+// 0 past Kn, then wsal[n][:].  Workgroup `bid` dequantizes its RB codes rows into LDS in
+// packed order (one bpack dword -> 8 D values D(code * scale), one 16-B LDS write), then
+// gathers them in rank order (an output chunk's table entries are read once for all RB
+// rows) and stores 16-B chunks.  Latency-bound rather than byte-bound, so it runs in the
+// same launch as the C4 quantizer (quant_c4_fused_kernel), on workgroups of its own.
+struct PermArgs {
+  const uint32_t* codes;  // bpack [Np][Kp/2]
+  const void* wscale;     // D [ngw][Np]
+  const void* wsal;       // D [N][S_pad]
+  void* wp;               // D [Np][Kq + S_pad]
+  int N, Np, Kp, Gw, ngw, Kn, Kq, S_pad, RB;
+};
+
+template <class DT>
+__device__ __forceinline__ void perm_weight_body(const PermArgs& a, const uint32_t* __restrict__ lctab,
+                                                 const int bid) {
+  typedef typename DT::T T;
+  extern __shared__ __attribute__((aligned(16))) uint32_t pw_lds[];  // [RB][Kp] D values
+  T* wl = (T*)pw_lds;
+  const T* wscale = (const T*)a.wscale;
+  const T* wsal = (const T*)a.wsal;
+  T* wp = (T*)a.wp;
+  const int RB = a.RB, Kp = a.Kp, n0 = bid * RB, tid = threadIdx.x;
+  const int dw = Kp / 8;  // bpack dwords per codes row
+#pragma unroll 4
+  for (int i = tid; i < RB * dw; i += blockDim.x) {
+    const int r = i / dw, d = i - r * dw, n = n0 + r;
+    const int p0 = bpack_pos(d, 0);  // its 8 positions p0 .. p0 + 7 (one group: Gw % 8 == 0)
+    T v[8];
+    if (n < a.N) {
+      const uint32_t w = a.codes[(size_t)n * dw + d];
+      const float sc = DT::to_f(wscale[(size_t)min(p0 / a.Gw, a.ngw - 1) * a.Np + n]);
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        v[e] = DT::from_f((float)((int)((w >> bpack_shift(e)) & 0xFu) - 8) * sc);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = DT::from_f(0.f);
+    }
+    *(u32x4*)(wl + (size_t)r * Kp + p0) = *(const u32x4*)v;
+  }
+  __syncthreads();
+  const int W = a.Kq + a.S_pad, nch = W / 8;
+  for (int c = tid; c < nch; c += blockDim.x) {
+    const int j0 = 8 * c;
+    if (j0 < a.Kq) {
+      int pos[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) pos[e] = j0 + e < a.Kn ? (int)(lctab[j0 + e] >> 16) : -1;
+      for (int r = 0; r < RB; ++r) {
+        T v[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = pos[e] >= 0 ? wl[(size_t)r * Kp + pos[e]] : DT::from_f(0.f);
+        *(u32x4*)(wp + (size_t)(n0 + r) * W + j0) = *(const u32x4*)v;
+      }
+    } else {
+      for (int r = 0; r < RB; ++r) {
+        const int n = n0 + r;
+        u32x4 v = u32x4{0u, 0u, 0u, 0u};
+        if (n < a.N) v = *(const u32x4*)(wsal + (size_t)n * a.S_pad + (j0 - a.Kq));
+        *(u32x4*)(wp + (size_t)n * W + j0) = v;
+      }
+    }
+  }
+}
+
+template <class DT>
+__global__ __launch_bounds__(1024) void perm_weight_kernel(PermArgs a, const uint32_t* __restrict__ lctab) {
+  perm_weight_body<DT>(a, lctab, blockIdx.x);
+}
+
+// The C4 quantizer (workgroups 0 .. nq-1) and the weight permutation (the rest) in one
+// launch: the two are independent given the table and overlap on the chip.
+template <class DT>
+__global__ __launch_bounds__(1024) void quant_c4_fused_kernel(
+    const typename DT::T* x, int M, int K, int q_max, int G, const uint32_t* __restrict__ lctab,
+    int Kn, int P, const int32_t* __restrict__ sal, int S, int S_pad,
+    const uint32_t* __restrict__ cmax, const int32_t* __restrict__ nonsal, void* codes,
+    uint32_t* __restrict__ key_clear, int clear_words, void* scales, typename DT::T* xs,
+    int Kq, int ldsc, int nq, PermArgs pa) {
+  if ((int)blockIdx.x < nq)
+    quant_lc_body<DT, LC_MODE_GROUP, 16, 0, 3>(x, M, K, q_max, G, lctab, Kn, nullptr, P, sal, S,
+                                               S_pad, cmax, nonsal, (typename DT::T*)codes,
+                                               key_clear, clear_words, (float*)scales, xs, Kq,
+                                               ldsc, blockIdx.x, nq);
+  else
+    perm_weight_body<DT>(pa, lctab, blockIdx.x - nq);
+}
+
 constexpr int LC_RPL = 16;
 
 static int lc_waves(int K, int Kn) {
@@ -454,7 +593,7 @@ static int quant_lc_launch(const void* x, int M, int K, int q_max, int G, const 
                            int Kn, const int32_t* amap, int P, const int32_t* sal, int S,
                            int S_pad, const uint32_t* cmax, const int32_t* nonsal, void* out,
                            uint32_t* key_clear, int clear_words, float* out_scale,
-                           void* out_xs, hipStream_t s) {
+                           void* out_xs, hipStream_t s, int Kq = 0, int ldsc = 0) {
   typedef typename DT::T T;
   const int nw = lc_waves(K, Kn);
   const size_t lds = sizeof(uint32_t) * (size_t)(P + S_pad + 8);
@@ -469,7 +608,7 @@ static int quant_lc_launch(const void* x, int M, int K, int q_max, int G, const 
   if (grid > npair) grid = npair;
   quant_lc_kernel<DT, MODE, LC_RPL, GS, F8><<<dim3(grid), dim3(64 * nw), lds, s>>>(
       (const T*)x, M, K, q_max, G, lctab, Kn, amap, P, sal, S, S_pad, cmax, nonsal, (T*)out,
-      key_clear, clear_words, out_scale, (T*)out_xs);
+      key_clear, clear_words, out_scale, (T*)out_xs, Kq, ldsc);
   SQMP_LAUNCH_CHECK();
   return SQMP_OK;
 }
@@ -512,6 +651,98 @@ int launch_quant_lc(int dtype, int mode, const void* x, int M, int K, int q_max,
   return SQMP_EUNSUPPORTED;
 #undef SQMP_LC_MODE
 #undef SQMP_LC
+}
+
+static int pw_rows(int Kp) {
+  // rows per permutation workgroup: 16 KiB of dequantized rows; Np % 256 == 0, so RB | Np
+  static const int env = [] {
+    const char* e = getenv("SQMP_PW_RB");
+    return e ? atoi(e) : 0;
+  }();
+  int rb = env > 0 ? env : 16384 / (Kp * 2);
+  return rb >= 8 ? 8 : rb >= 4 ? 4 : rb >= 2 ? 2 : 1;
+}
+
+int launch_perm_weight_c4(int dtype, const uint32_t* lctab, const void* codes,
+                          const void* wscale, const void* wsal, int N, int Kp, int Gw, int ngw,
+                          int Kn, int S_pad, void* wp, hipStream_t s) {
+  const int Np = pad_n(N), RB = pw_rows(Kp);
+  PermArgs pa{(const uint32_t*)codes, wscale, wsal, wp, N, Np, Kp, Gw, ngw, Kn,
+              (int)round_up(Kn, 64), S_pad, RB};
+  const size_t lds = (size_t)RB * Kp * 2;
+  if (dtype == SQMP_F16) {
+    SQMP_HIP_CHECK(hipFuncSetAttribute((const void*)perm_weight_kernel<F16>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    perm_weight_kernel<F16><<<dim3(Np / RB), dim3(256), lds, s>>>(pa, lctab);
+  } else if (dtype == SQMP_BF16) {
+    SQMP_HIP_CHECK(hipFuncSetAttribute((const void*)perm_weight_kernel<BF16>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    perm_weight_kernel<BF16><<<dim3(Np / RB), dim3(256), lds, s>>>(pa, lctab);
+  } else {
+    return SQMP_EUNSUPPORTED;
+  }
+  SQMP_LAUNCH_CHECK();
+  return SQMP_OK;
+}
+
+int launch_quant_lc_c4(int dtype, const void* x, int M, int K, int q_max, int G,
+                       const uint32_t* lctab, int Kn, int P, const int32_t* sal, int S,
+                       int S_pad, const uint32_t* cmax, const int32_t* nonsal, void* codes,
+                       void* scales, int ldsc, void* xs, uint32_t* key_clear, int clear_words,
+                       hipStream_t s, const C4Weight* cw) {
+  const int Kq = (int)round_up(Kn, 64);
+  if (G < LC_RPL) return SQMP_EUNSUPPORTED;
+  if (!cw) {
+    if (dtype == SQMP_F16)
+      return quant_lc_launch<F16, LC_MODE_GROUP, 0, 3>(x, M, K, q_max, G, lctab, Kn, nullptr, P,
+                                                       sal, S, S_pad, cmax, nonsal, codes,
+                                                       key_clear, clear_words, (float*)scales, xs,
+                                                       s, Kq, ldsc);
+    if (dtype == SQMP_BF16)
+      return quant_lc_launch<BF16, LC_MODE_GROUP, 0, 3>(x, M, K, q_max, G, lctab, Kn, nullptr, P,
+                                                        sal, S, S_pad, cmax, nonsal, codes,
+                                                        key_clear, clear_words, (float*)scales,
+                                                        xs, s, Kq, ldsc);
+    return SQMP_EUNSUPPORTED;
+  }
+  // fused: the quantizer's grid (as quant_lc_launch) + Np / RB permutation workgroups
+  const int nw = lc_waves(K, Kn);
+  const int Np = pad_n(cw->N), RB = pw_rows(cw->Kp);
+  PermArgs pa{(const uint32_t*)cw->codes, cw->wscale, cw->wsal, cw->wp, cw->N, Np, cw->Kp,
+              cw->Gw, cw->ngw, Kn, Kq, S_pad, RB};
+  const size_t lq = sizeof(uint32_t) * (size_t)(P + S_pad + 8), lp = (size_t)RB * cw->Kp * 2;
+  const size_t lds = lq > lp ? lq : lp;
+  int per_cu = (int)((150 * 1024) / lds);
+  const int by_waves = 32 / nw;
+  per_cu = per_cu < 1 ? 1 : (per_cu > by_waves ? by_waves : per_cu);
+  // quantizer workgroups per CU: leave two slots of every CU to the permutation
+  // workgroups (issued after them), so the two run side by side
+  static const int q_env = [] {
+    const char* e = getenv("SQMP_C4_QPERCU");
+    return e ? atoi(e) : 0;
+  }();
+  const int qpc = q_env > 0 ? q_env : (per_cu > 2 ? per_cu - 2 : 1);
+  int nq = 256 * (qpc < per_cu ? qpc : per_cu);
+  const int npair = (M + 1) / 2;
+  if (nq > npair) nq = npair;
+  const dim3 grid(nq + Np / RB), block(64 * nw);
+  if (dtype == SQMP_F16) {
+    SQMP_HIP_CHECK(hipFuncSetAttribute((const void*)quant_c4_fused_kernel<F16>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    quant_c4_fused_kernel<F16><<<grid, block, lds, s>>>(
+        (const _Float16*)x, M, K, q_max, G, lctab, Kn, P, sal, S, S_pad, cmax, nonsal, codes,
+        key_clear, clear_words, scales, (_Float16*)xs, Kq, ldsc, nq, pa);
+  } else if (dtype == SQMP_BF16) {
+    SQMP_HIP_CHECK(hipFuncSetAttribute((const void*)quant_c4_fused_kernel<BF16>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    quant_c4_fused_kernel<BF16><<<grid, block, lds, s>>>(
+        (const __bf16*)x, M, K, q_max, G, lctab, Kn, P, sal, S, S_pad, cmax, nonsal, codes,
+        key_clear, clear_words, scales, (__bf16*)xs, Kq, ldsc, nq, pa);
+  } else {
+    return SQMP_EUNSUPPORTED;
+  }
+  SQMP_LAUNCH_CHECK();
+  return SQMP_OK;
 }
 
 }  // namespace sqmp

@@ -267,3 +267,17 @@ extern "C" int sqmp_gemm_i8(const int8_t* a8, const float* ascale, const void* x
   return launch_gemm_i8_fast(dtype, a8, ascale, xs, codes, wscale, wsal, bias, y, M, N, Kp,
                              S_pad, Gw, ngw, (hipStream_t)stream);
 }
+
+extern "C" int sqmp_gemm_fqt(const void* acodes, const void* ascale, const void* xs,
+                             const void* wp, const void* bias, void* y, int dtype, int M, int N,
+                             int Kq, int S_pad, int G, int ngq, void* stream) {
+  using namespace sqmp;
+  if (!acodes || !ascale || !wp || !y || (S_pad > 0 && !xs)) return SQMP_EINVAL;
+  if (M < 0 || N <= 0 || Kq <= 0 || Kq % 64 || S_pad < 0 || S_pad % 64 || G <= 0 || ngq <= 0)
+    return SQMP_EINVAL;
+  if (dtype != SQMP_F16 && dtype != SQMP_BF16) return SQMP_EUNSUPPORTED;
+  if (G % 64 || N % 8) return SQMP_EUNSUPPORTED;
+  if (M == 0) return SQMP_OK;
+  return launch_gemm_fqt(dtype, acodes, ascale, xs, wp, bias, y, M, N, Kq, S_pad, G, ngq,
+                         (hipStream_t)stream);
+}

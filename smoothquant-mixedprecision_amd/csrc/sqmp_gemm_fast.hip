@@ -106,7 +106,10 @@ __device__ inline int d_f(int g) { return (-g) & 3; }
 // 5-block A read-ahead, the scale / B pieces issued by their own waves -- none faster.)
 // colmax != NULL: the epilogue also atomic-maxes bits(max |y|) of each output column into
 // colmax (the statistics of the fused output quantizer, SQMP_QA_STATS_GIVEN).
-template <class DT, int GB, int TM>
+// TR (sqmp_gemm_fqt, activation order): A = the permuted weight wp, Bw / wscale / wsal = the
+// act codes / group scales / exact salient x, so the tile is y^T: the epilogue adds bias[m]
+// per A row and stores Y[n][m] (ld = M); colmax must be NULL.
+template <class DT, int GB, int TM, bool TR = false>
 __global__ __launch_bounds__(512, 1) void gemm_fq6_kernel(
     const typename DT::T* __restrict__ A, const void* __restrict__ Bw,
     const typename DT::T* __restrict__ wscale, const typename DT::T* __restrict__ wsal,
@@ -374,6 +377,35 @@ __global__ __launch_bounds__(512, 1) void gemm_fq6_kernel(
       compute_dense(slot, std::integral_constant<int, 0>());
     else
       compute_dense32(slot);
+  }
+
+  if constexpr (TR) {
+    // y^T tile staged [nl 256][ml TM] at a row stride of 2 TM + 16 bytes (the four q-groups
+    // of a write land 16 banks apart), then stored as TM-wide row pieces of Y[n][m]
+    constexpr int RS = 2 * TM + 16;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    raw_barrier();  // every wave is past its last read of the ring
+#pragma unroll
+    for (int i = 0; i < I; ++i) {
+      const int ml = wm * MW + 16 * i + r16;
+      const float bv = bias && m0 + ml < M ? DT::to_f(bias[m0 + ml]) : 0.f;
+#pragma unroll
+      for (int j = 0; j < J; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          *(T*)(lds + (wn * CW + 16 * j + 4 * q + r) * RS + ml * 2) = DT::from_f(acc[i][j][r] + bv);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    raw_barrier();
+    constexpr int CPR = TM / 8;  // 16-B chunks per staged row
+#pragma unroll 4
+    for (int k = tid; k < 256 * CPR; k += 512) {
+      const int nl = k / CPR, c = k % CPR;
+      const int gn = n0 + nl, gm = m0 + c * 8;
+      if (gn < N && gm < M)  // M % 8 == 0 (launcher)
+        *(u32x4*)(Y + (size_t)gn * M + gm) = *(const u32x4*)(lds + nl * RS + c * 16);
+    }
+    return;
   }
 
   // ---- epilogue: acc[i][j][r] = C[n = n0 + CW wn + 16 j + 4 q + r][m = m0 + MW wm + 16 i + r16]
@@ -697,13 +729,13 @@ static int fq6_group_m() {
   return v;
 }
 
-template <class DT, int GB, int TM>
+template <class DT, int GB, int TM, bool TR = false>
 static int fq6_launch(const void* a, const void* codes, const void* wscale, const void* wsal,
                       const void* bias, void* y, int M, int N, int Kp, int S_pad, int Gw,
                       int ngw, uint32_t* colmax, hipStream_t s) {
   typedef typename DT::T T;
   const int tiles_m = cdiv(M, TM), tiles_n = cdiv(N, 256);
-  gemm_fq6_kernel<DT, GB, TM><<<dim3(tiles_m * tiles_n), dim3(512), 0, s>>>(
+  gemm_fq6_kernel<DT, GB, TM, TR><<<dim3(tiles_m * tiles_n), dim3(512), 0, s>>>(
       (const T*)a, codes, (const T*)wscale, (const T*)wsal, (const T*)bias, (T*)y, M, N, Kp,
       S_pad, Gw, ngw, tiles_m, tiles_n, fq6_group_m(), colmax);
   SQMP_LAUNCH_CHECK();
@@ -739,6 +771,30 @@ int launch_gemm_fq_fast(int dtype, const void* a, const void* codes, const void*
     return fq6_dispatch<F16>(a, codes, wscale, wsal, bias, y, M, N, Kp, S_pad, Gw, ngw, n_bits, colmax, s);
   if (dtype == SQMP_BF16)
     return fq6_dispatch<BF16>(a, codes, wscale, wsal, bias, y, M, N, Kp, S_pad, Gw, ngw, n_bits, colmax, s);
+  return SQMP_EUNSUPPORTED;
+}
+
+// sqmp_gemm_fqt: the activation-order GEMM on gemm_fq6<TR> (kernel M = weight rows N, kernel
+// N = activation rows M)
+template <class DT>
+static int fqt_dispatch(const void* acodes, const void* ascale, const void* xs, const void* wp,
+                        const void* bias, void* y, int M, int N, int Kq, int S_pad, int G,
+                        int ngq, hipStream_t s) {
+  const long t256 = (long)cdiv(N, 256) * cdiv(M, 256);
+  if (t256 >= 2L * 256)
+    return fq6_launch<DT, 1, 256, true>(wp, acodes, ascale, xs, bias, y, N, M, Kq, S_pad, G, ngq,
+                                        nullptr, s);
+  return fq6_launch<DT, 1, 128, true>(wp, acodes, ascale, xs, bias, y, N, M, Kq, S_pad, G, ngq,
+                                      nullptr, s);
+}
+
+int launch_gemm_fqt(int dtype, const void* acodes, const void* ascale, const void* xs,
+                    const void* wp, const void* bias, void* y, int M, int N, int Kq, int S_pad,
+                    int G, int ngq, hipStream_t s) {
+  if (dtype == SQMP_F16)
+    return fqt_dispatch<F16>(acodes, ascale, xs, wp, bias, y, M, N, Kq, S_pad, G, ngq, s);
+  if (dtype == SQMP_BF16)
+    return fqt_dispatch<BF16>(acodes, ascale, xs, wp, bias, y, M, N, Kq, S_pad, G, ngq, s);
   return SQMP_EUNSUPPORTED;
 }
 

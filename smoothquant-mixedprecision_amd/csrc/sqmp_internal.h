@@ -48,12 +48,35 @@ int launch_quant_lc(int dtype, int mode, const void* x, int M, int K, int q_max,
 // key_clear: zeroed (clear_words % 4 == 0), may be NULL.  out_scale != NULL selects the
 // e4m3 code output (token / tensor modes): out = codes [M][P], out_xs = D [M][S_pad].
 
+// SQMP_OUT_C4 lane-contiguous quantizer (act-order int4 codes, group scales [Kq/G][ldsc],
+// exact salient columns); P = the table's packed length (Kp).  cw != NULL: the same launch
+// also builds the activation-order weight operand (sqmp_quant_act_c4).
+struct C4Weight {
+  const void* codes;   // bpack [pad_n(N)][Kp/2]
+  const void* wscale;  // D [ngw][pad_n(N)]
+  const void* wsal;    // D [N][S_pad]
+  void* wp;            // D [pad_n(N)][Kq + S_pad]
+  int N, Kp, Gw, ngw;
+};
+int launch_quant_lc_c4(int dtype, const void* x, int M, int K, int q_max, int G,
+                       const uint32_t* lctab, int Kn, int P, const int32_t* sal, int S,
+                       int S_pad, const uint32_t* cmax, const int32_t* nonsal, void* codes,
+                       void* scales, int ldsc, void* xs, uint32_t* key_clear, int clear_words,
+                       hipStream_t s, const C4Weight* cw = nullptr);
+int launch_perm_weight_c4(int dtype, const uint32_t* lctab, const void* codes,
+                          const void* wscale, const void* wsal, int N, int Kp, int Gw, int ngw,
+                          int Kn, int S_pad, void* wp, hipStream_t s);
+
 // Fast GEMMs (sqmp_gemm_fast.hip); SQMP_EUNSUPPORTED when the shape has no fast kernel.
 // colmax != NULL: the epilogue also atomic-maxes bits(max |y|) per output column into it
 int launch_gemm_fq_fast(int dtype, const void* a, const void* codes, const void* wscale,
                         const void* wsal, const void* bias, void* y, int M, int N, int Kp,
                         int S_pad, int Gw, int ngw, int n_bits, uint32_t* colmax,
                         hipStream_t s);
+// activation-order GEMM (sqmp_gemm_fqt): y^T = wp . codes^T on gemm_fq6<TR>
+int launch_gemm_fqt(int dtype, const void* acodes, const void* ascale, const void* xs,
+                    const void* wp, const void* bias, void* y, int M, int N, int Kq, int S_pad,
+                    int G, int ngq, hipStream_t s);
 int launch_gemm_i8_fast(int dtype, const int8_t* a8, const float* ascale, const void* xs,
                         const void* codes, const void* wscale, const void* wsal,
                         const void* bias, void* y, int M, int N, int Kp, int S_pad, int Gw,

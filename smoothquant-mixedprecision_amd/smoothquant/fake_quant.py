@@ -211,6 +211,10 @@ class W4A4Linear(nn.Module):
             i8 MFMA with per-group fp32 folds (exact scale factorisation).
       "fq"  every act mode: dequantized activations x in-kernel-decoded weights on the D
             MFMA (bit-exact operands; the reference's numerics up to accumulation order).
+      "fqt" per_group activations (auto from ops.FQT_MIN_ROWS rows, ops.fqt_eligible): "fq"
+            in ACTIVATION order -- 4-bit act codes decoded in the GEMM, the weight W_hat
+            permuted per forward, no salient zero positions in the K loop; the same
+            operands bit for bit, so "fq"'s numerics.
     """
 
     def __init__(self, in_features, out_features, bias=True, act_quant="per_token",
@@ -503,12 +507,18 @@ class W4A4Linear(nn.Module):
         use_i8 = not use_f8 and (
             self.kernel == "i8" or
             (self.kernel == "auto" and ops.I8_AUTO and ops.i8_eligible(pw, amode, bits)))
+        use_fqt = (not use_f8 and not use_i8 and self.kernel in ("auto", "fqt")
+                   and ops.fqt_eligible(pw, amode, bits, ag, x2.shape[0],
+                                        force=self.kernel == "fqt")
+                   and ops.f8_input_ok(xc))
         if use_f6:
             a8, sa, xs = ops.quant_act_f6(xc, pw, amode, bits)
         elif use_f8:
             a8, sa, xs = ops.quant_act_f8(xc, pw, amode, bits)
         elif use_i8:
             a8, sa, xs = ops.quant_act_i8(xc, pw, amode, bits)
+        elif use_fqt:
+            c4 = ops.quant_act_c4(xc, pw, amode, bits, ag, stats_of=x)
         else:
             a = ops.quant_act_fp(xc, pw, amode, bits, ag, stats_of=x)
         if mutate_input:
@@ -522,13 +532,16 @@ class W4A4Linear(nn.Module):
         # y into the output quantizer's workspace, which then skips its statistics pass
         fuse = (ospec is not None and ospec[0] in ("per_group", "per_tensor") and _OQ_FUSE
                 and not use_f8
-                and not use_i8 and (self.salient_indices is None or pw.K - pw.S > 0))
+                and not use_i8 and not use_fqt
+                and (self.salient_indices is None or pw.K - pw.S > 0))
         if use_f6:
             y = ops.gemm_f6(a8, sa, xs, pw, bias)
         elif use_f8:
             y = ops.gemm_f8(a8, sa, xs, pw, bias)
         elif use_i8:
             y = ops.gemm_i8(a8, sa, xs, pw, bias)
+        elif use_fqt:
+            y = ops.gemm_fqt(*c4, pw, bias, ag)
         elif fuse:
             ws = ops.out_quant_workspace(x2.shape[0], pw.N, x2.device)
             y = ops.gemm_fq(a, pw, bias, colmax=ws["buf"])

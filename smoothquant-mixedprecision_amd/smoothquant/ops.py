@@ -284,6 +284,85 @@ def quant_act_fp(x2: torch.Tensor, pw: PackedWeight, act_quant: str, n_bits: int
     return a
 
 
+# Activation-order path (SQMP_OUT_C4 + sqmp_perm_weight_c4 + sqmp_gemm_fqt) for sorted
+# per_group activations: the GEMM runs over the K - S non-salient positions in activation
+# order instead of the Kp packed positions (which carry S zero salient positions), and the
+# quantizer writes 4-bit codes instead of D values.  It rebuilds the permuted weight per
+# forward (N x (Kq + S_pad) D values), so it pays from FQT_MIN_ROWS rows on.
+FQT_MODE = os.environ.get("SQMP_FQT", "auto")   # "auto" | "1" (whenever eligible) | "0"
+FQT_MIN_ROWS = int(os.environ.get("SQMP_FQT_MIN_ROWS", "8192"))
+
+
+def fqt_eligible(pw: PackedWeight, act_quant: str, act_bits: int, group_size: int,
+                 M: int, force: bool = False) -> bool:
+    """Whether the activation-order path computes this layer (force: kernel="fqt", no row
+    threshold)."""
+    if not force and (FQT_MODE == "0" or (FQT_MODE == "auto" and M < FQT_MIN_ROWS)):
+        return False
+    return (act_quant in _SORTED or act_quant == "per_group_unsorted") and act_bits <= 4 \
+        and pw.n_bits == 4 and pw.dense is None and pw.dtype != torch.float32 \
+        and group_size % 64 == 0 and pw.N % 8 == 0 and pw.K % 8 == 0 and pw.K <= 16384 \
+        and pw.K - pw.S > 0
+
+
+def quant_act_c4(x2: torch.Tensor, pw: PackedWeight, act_quant: str, n_bits: int,
+                 group_size: int, stats_of: Optional[torch.Tensor] = None):
+    """x [M, K] -> the activation-order operands of gemm_fqt: (int4 codes [M, Kq/2] bytes,
+    D group scales [Kq/G, Mp], exact salient x [M, S_pad], permuted weight [Np, Kq + S_pad])
+    with Kq = roundup(K - S, 64).  Statistics reuse as quant_act_fp."""
+    _require_gpu(x2, "quant_act")
+    M, K = x2.shape
+    Mp = _pad_rows(M)
+    Kn = K - pw.S
+    Kq = (Kn + 63) // 64 * 64
+    ngq = (Kn + group_size - 1) // group_size
+    dev = x2.device
+    codes = torch.empty((Mp, Kq // 2), dtype=torch.uint8, device=dev)[:M]
+    scales = torch.empty((ngq, Mp), dtype=x2.dtype, device=dev)
+    xs = torch.empty((Mp, max(pw.S_pad, 8)), dtype=x2.dtype, device=dev)[:M]
+    lib = load()
+    nb = _ws_bytes(M, K, pw.Kp)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    e = _act_ws(dev, stream, K, pw.Kp, nb)
+    flags = _lib.QA_CLEAN_WS
+    src = x2 if stats_of is None else stats_of
+    skey = (src.data_ptr(), tuple(src.shape), src.dtype, src._version, pw.sal_key, act_quant,
+            M, K)
+    st = e["stats"]
+    if (act_quant in _SORTED and st is not None and st[0]() is src and st[1] == skey
+            and st[2] != pw.codes.data_ptr()):
+        flags |= _lib.QA_REUSE_STATS
+    if pw.posmap is None:
+        pw.posmap = build_posmap(pw.perm, K)
+    wp = torch.empty((pad_n(pw.N), Kq + pw.S_pad), dtype=pw.dtype, device=dev)
+    # one call: quantizer + weight permutation in the same launch
+    status = lib.sqmp_quant_act_c4(_p(x2), _dtype_code(x2.dtype), M, K, ACT_MODES[act_quant],
+                                   n_bits, group_size, _p(pw.amap), pw.Kp, _p(pw.nonsal),
+                                   _p(pw.salient), pw.S, pw.S_pad, _p(pw.posmap), flags,
+                                   _p(codes), _p(scales), _p(xs) if pw.S_pad else None,
+                                   _p(pw.codes), _p(pw.wscale), _p(pw.wsal) if pw.S_pad else None,
+                                   pw.N, pw.Gw, pw.ngw, _p(wp), _p(e["buf"]), e["buf"].numel(),
+                                   ctypes.c_void_p(stream))
+    if status != _lib.SQMP_OK:
+        _WS.pop((dev.index, stream, K, pw.Kp), None)
+        check(status, "quant_act_c4")
+    if act_quant in _SORTED:
+        e["stats"] = (weakref.ref(src), skey, pw.codes.data_ptr())
+    return codes, scales, xs, wp
+
+
+def gemm_fqt(codes: torch.Tensor, scales: torch.Tensor, xs: torch.Tensor, wp: torch.Tensor,
+             pw: PackedWeight, bias: Optional[torch.Tensor], group_size: int) -> torch.Tensor:
+    """y = D(x_hat . W_hat^T + bias) on the activation-order operands of quant_act_c4."""
+    M = codes.shape[0]
+    y = torch.empty((M, pw.N), dtype=pw.dtype, device=codes.device)
+    Kq = codes.shape[1] * 2
+    check(load().sqmp_gemm_fqt(_p(codes), _p(scales), _p(xs) if pw.S_pad else None, _p(wp),
+                               _p(bias), _p(y), _dtype_code(pw.dtype), M, pw.N, Kq, pw.S_pad,
+                               group_size, scales.shape[0], _stream(codes)), "gemm_fqt")
+    return y
+
+
 def quant_act_i8(x2: torch.Tensor, pw: PackedWeight, act_quant: str, n_bits: int):
     """x [M, K] -> (int8 codes [M, roundup(Kp, 256)] in the i8 GEMM's K order, fp32
     scales [M], exact salient x [M, S_pad])."""

@@ -1,5 +1,5 @@
 """Time the W4A4 GEMM alone on BASELINE config 2 (HIP events, GEMM on torch's current
-stream).  python tools/gemm_time.py [fq|fq7|i8|f8|f6] [iters]  -> one line: kind, avg ms, TFLOP/s."""
+stream).  python tools/gemm_time.py [fq|fq7|fqt|i8|f8|f6] [iters]  -> one line: kind, avg ms, TFLOP/s."""
 import os
 import sys
 
@@ -13,13 +13,16 @@ from smoothquant import ops  # noqa: E402
 kind = sys.argv[1] if len(sys.argv) > 1 else "fq"
 iters = int(sys.argv[2]) if len(sys.argv) > 2 else 50
 dev = torch.device("cuda")
-act = "per_group" if kind in ("fq", "fq7") else "per_token"
+act = "per_group" if kind in ("fq", "fq7", "fqt") else "per_token"
 q, x, lin = bench.make_layer(dev, act, seed=1)
 pw = q.packed()
 if kind == "fq":
     a = ops.quant_act_fp(x, pw, act, 4, bench.G)
     ops.FQ7_AUTO = False
     run = lambda: ops.gemm_fq(a, pw, lin.bias)  # noqa: E731
+elif kind == "fqt":
+    c4 = ops.quant_act_c4(x, pw, act, 4, bench.G)
+    run = lambda: ops.gemm_fqt(*c4, pw, lin.bias, bench.G)  # noqa: E731
 elif kind == "fq7":
     a = ops.quant_act_fp(x, pw, act, 4, bench.G)
     run = lambda: ops.gemm_fq7(a, pw, lin.bias)  # noqa: E731
