@@ -5,6 +5,10 @@
 //                   gemm_generic below for everything else (fp32, 8-bit codes, groups
 //                   of 8 / 16 elements): the round-1 register-staged 128 x 128 kernel.
 //   sqmp_gemm_i8 -> gemm_i8v2 (sqmp_gemm_fast.hip).
+#include <stdlib.h>
+
+#include <type_traits>
+
 #include "sqmp_mfma.h"
 
 namespace sqmp {
@@ -61,8 +65,11 @@ struct BDecode {
   }
 };
 
-template <class DT, int WBITS>
-__global__ __launch_bounds__(256, 2) void gemm_generic_kernel(
+// WN = waves along N (2: 4 waves of 64 x 64, the 16-bit default; 4: 8 waves of 64 x 32, the
+// fp32 build -- two waves per SIMD at one 128 x 128 tile per CU, so one wave's MFMAs cover
+// the other's barrier and staging; f32 MFMAs leave VALU and LDS idle otherwise)
+template <class DT, int WBITS, int WN = 2>
+__global__ __launch_bounds__(128 * WN, 2) void gemm_generic_kernel(
     const typename DT::T* __restrict__ A, const uint8_t* __restrict__ codes,
     const typename DT::T* __restrict__ wscale, const typename DT::T* __restrict__ wsal,
     const typename DT::T* __restrict__ bias, typename DT::T* __restrict__ Y, int M, int N,
@@ -72,35 +79,41 @@ __global__ __launch_bounds__(256, 2) void gemm_generic_kernel(
   constexpr int BKE = ROWB / sizeof(T);
   __shared__ __attribute__((aligned(16))) unsigned char lds[2 * 2 * TILE_BYTES];
 
+  constexpr int NT = 128 * WN;          // threads
+  constexpr int LI = 1024 / NT;          // 16-B A / dense-B chunks per thread per stage
+  constexpr int CW = BN / WN, J = CW / 16;  // columns per wave, 16-wide tiles
   int tm, tn;
   tile_coords(tiles_m, tiles_n, 8, tm, tn);
   const int m0 = tm * BM, n0 = tn * BN;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wm = wid >> 1, wn = wid & 1;
+  const int wm = wid / WN, wn = wid % WN;
   const int Ktot = Kp + S_pad;
   const int nkt_main = Kp / BKE, nkt = Ktot / BKE;
   const int Np = pad_n(N);
 
-  f32x4 acc[4][4];
+  f32x4 acc[4][J];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < J; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  u32x4 ra[4], rb[4];
+  u32x4 ra[LI], rb[LI];
   uint32_t rc[Dec::RAWW];
   float rs[4];
-  const int bn = tid >> 1, bh = tid & 1;
+  // weight decode: thread (bn, bh) decodes half bh of weight row bn (256 threads)
+  const bool dec_thr = tid < 256;
+  const int bn = (tid & 255) >> 1, bh = tid & 1;
   const int gbn = n0 + bn;
 
   auto load = [&](int kt) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int q = tid + 256 * i, row = q >> 3, c = q & 7;
+    for (int i = 0; i < LI; ++i) {
+      const int q = tid + NT * i, row = q >> 3, c = q & 7;
       const int gm = min(m0 + row, M - 1);
       ra[i] = *(const u32x4*)(A + (size_t)gm * Ktot + (size_t)kt * BKE + c * (16 / sizeof(T)));
     }
     if (kt < nkt_main) {
+      if (!dec_thr) return;
       const int p0 = kt * BKE + bh * (BKE / 2);
       const int n = min(gbn, N - 1);
       Dec::load(codes, n, Kp, p0, rc);
@@ -112,8 +125,8 @@ __global__ __launch_bounds__(256, 2) void gemm_generic_kernel(
     } else {
       const int ks = (kt - nkt_main) * BKE;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int q = tid + 256 * i, row = q >> 3, c = q & 7;
+      for (int i = 0; i < LI; ++i) {
+        const int q = tid + NT * i, row = q >> 3, c = q & 7;
         const int gn = min(n0 + row, N - 1);
         rb[i] = *(const u32x4*)(wsal + (size_t)gn * S_pad + ks + c * (16 / sizeof(T)));
       }
@@ -123,19 +136,20 @@ __global__ __launch_bounds__(256, 2) void gemm_generic_kernel(
     unsigned char* la = lds + buf * 2 * TILE_BYTES;
     unsigned char* lb = la + TILE_BYTES;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int q = tid + 256 * i, row = q >> 3, c = q & 7;
+    for (int i = 0; i < LI; ++i) {
+      const int q = tid + NT * i, row = q >> 3, c = q & 7;
       *(u32x4*)(la + lds_off(row, c)) = ra[i];
     }
     if (kt < nkt_main) {
+      if (!dec_thr) return;
       u32x4 dec[4];
       Dec::run(rc, rs, dec);
 #pragma unroll
       for (int c = 0; c < 4; ++c) *(u32x4*)(lb + lds_off(bn, bh * 4 + c)) = dec[c];
     } else {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int q = tid + 256 * i, row = q >> 3, c = q & 7;
+      for (int i = 0; i < LI; ++i) {
+        const int q = tid + NT * i, row = q >> 3, c = q & 7;
         *(u32x4*)(lb + lds_off(row, c)) = rb[i];
       }
     }
@@ -145,16 +159,16 @@ __global__ __launch_bounds__(256, 2) void gemm_generic_kernel(
     const unsigned char* lb = la + TILE_BYTES;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
-      u32x4 af[4], bf[4];
+      u32x4 af[4], bf[J];
       const int ch = kk * 4 + (lane >> 4);
 #pragma unroll
       for (int i = 0; i < 4; ++i) af[i] = *(const u32x4*)(la + lds_off(wm * 64 + i * 16 + (lane & 15), ch));
 #pragma unroll
-      for (int j = 0; j < 4; ++j) bf[j] = *(const u32x4*)(lb + lds_off(wn * 64 + j * 16 + (lane & 15), ch));
+      for (int j = 0; j < J; ++j) bf[j] = *(const u32x4*)(lb + lds_off(wn * CW + j * 16 + (lane & 15), ch));
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) Mfma<DT>::run(acc[i][j], af[i], bf[j]);
+        for (int j = 0; j < J; ++j) Mfma<DT>::run(acc[i][j], af[i], bf[j]);
     }
   };
 
@@ -170,8 +184,8 @@ __global__ __launch_bounds__(256, 2) void gemm_generic_kernel(
   }
 
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int gn = n0 + wn * 64 + j * 16 + (lane & 15);
+  for (int j = 0; j < J; ++j) {
+    const int gn = n0 + wn * CW + j * 16 + (lane & 15);
     const float bv = bias && gn < N ? DT::to_f(bias[gn]) : 0.f;
     float cm = 0.f;  // max |y| of this lane's rows in column gn (the stored D values)
 #pragma unroll
@@ -199,6 +213,17 @@ static int generic_launch(const void* a, const void* codes, const void* wscale,
                           int S_pad, int Gw, int ngw, uint32_t* colmax, hipStream_t s) {
   typedef typename DT::T T;
   const int tiles_m = cdiv(M, BM), tiles_n = cdiv(N, BN);
+  static const bool f32_4w = [] {  // A/B knob: the 4-wave build for fp32 too
+    const char* e = getenv("SQMP_F32_WN2");
+    return e && atoi(e) == 1;
+  }();
+  if constexpr (std::is_same<DT, F32>::value) if (!f32_4w) {
+    gemm_generic_kernel<DT, WBITS, 4><<<dim3(tiles_m * tiles_n), dim3(512), 0, s>>>(
+        (const T*)a, (const uint8_t*)codes, (const T*)wscale, (const T*)wsal, (const T*)bias,
+        (T*)y, M, N, Kp, S_pad, Gw, ngw, tiles_m, tiles_n, colmax);
+    SQMP_LAUNCH_CHECK();
+    return SQMP_OK;
+  }
   gemm_generic_kernel<DT, WBITS><<<dim3(tiles_m * tiles_n), dim3(256), 0, s>>>(
       (const T*)a, (const uint8_t*)codes, (const T*)wscale, (const T*)wsal, (const T*)bias,
       (T*)y, M, N, Kp, S_pad, Gw, ngw, tiles_m, tiles_n, colmax);

@@ -1,6 +1,6 @@
 """Per-linear timing at a model's prefill shapes (M = 2048 tokens): prepass, GEMM, output
 quantization (OPT q/k/v with quantize_bmm_input), the whole W4A4Linear.forward, and the
-fp16 F.linear (hipBLASLt).  python tools/model_shapes.py [llama2-7b|opt-1.3b] [M]"""
+fp16 F.linear (hipBLASLt).  python tools/model_shapes.py [llama2-7b|opt-1.3b] [M] [fp16|fp32]"""
 import os
 import sys
 
@@ -13,6 +13,7 @@ from smoothquant.fake_quant import W4A4Linear  # noqa: E402
 
 model = sys.argv[1] if len(sys.argv) > 1 else "llama2-7b"
 M = int(sys.argv[2]) if len(sys.argv) > 2 else 2048
+DT = {"fp16": torch.float16, "fp32": torch.float32, "bf16": torch.bfloat16}[sys.argv[3] if len(sys.argv) > 3 else "fp16"]
 if model == "llama2-7b":
     G, LIN = 64, [("qkvo", 4096, 4096, 4, False), ("gate_up", 4096, 11008, 2, False),
                   ("down", 11008, 4096, 1, False)]
@@ -38,10 +39,10 @@ def t_ms(fn, it=30):
 tot = {"pre": 0.0, "gemm": 0.0, "oq": 0.0, "fwd": 0.0, "fp16": 0.0}
 for name, K, N, count, oq in LIN:
     g = torch.Generator(device=dev).manual_seed(0)
-    lin = torch.nn.Linear(K, N, bias=True).to(dev, torch.float16)
+    lin = torch.nn.Linear(K, N, bias=True).to(dev, DT)
     with torch.no_grad():
         lin.weight.copy_(torch.randn(N, K, generator=g, device=dev) * 0.02)
-    x = torch.randn(M, K, generator=g, device=dev).half()
+    x = torch.randn(M, K, generator=g, device=dev).to(DT)
     q = W4A4Linear.from_float(lin, weight_quant="per_group", act_quant="per_group",
                               quantize_output=oq, importance=x.float().abs().mean(0).cpu(),
                               salient_prop=0.05, group_size=G)
