@@ -244,28 +244,30 @@ int sqmp_gemm_f6(const void* a6, const float* ascale, const void* xs, const void
                  int M, int N, int Kp, int S_pad, int Gw, int ngw, void* stream);
 
 /* Register-operand copy of a packed 4-bit weight for sqmp_gemm_fq7 (same values, tile-major
- * order; once per layer).  Sizes from sqmp_fq7_sizes: codes_t bytes = R * Kp / 2, scale_t
- * elements (D) = R * ngw, sal_t elements (D) = R * max(S_pad, 64), R = roundup(N, 512).
- *   codes_t[n/64][Kp/64][lane][j][s] dwords = bpack dword 2q + s (q = lane >> 4) of the
- *     64-position block of row 64 (n/64) + 16 j + (lane & 15);
- *   scale_t[n/64][g][r][j] = wscale[g][64 (n/64) + 16 j + r];
- *   sal_t[n/64][S_pad/64][lane][j][s][e] = wsal[64 (n/64) + 16 j + (lane & 15)]
+ * order; once per layer), for J (2 or 4) 16-row weight tiles per wave (WR = 16 J rows per
+ * block).  Sizes from sqmp_fq7_sizes: codes_t bytes = R * Kp / 2, scale_t elements (D) =
+ * R * ngw, sal_t elements (D) = R * max(S_pad, 64), R = roundup(N, 128 J).
+ *   codes_t[n/WR][Kp/64][lane][j][s] dwords = bpack dword 2q + s (q = lane >> 4) of the
+ *     64-position block of row WR (n/WR) + 16 j + (lane & 15);
+ *   scale_t[n/WR][g][r][j] = wscale[g][WR (n/WR) + 16 j + r];
+ *   sal_t[n/WR][S_pad/64][lane][j][s][e] = wsal[WR (n/WR) + 16 j + (lane & 15)]
  *     [64 kd + 8 (4 (q & 1) + 2 s + (q >> 1)) + e]  (the GEMM's fragment chunk order).
  * Rows >= N are zero. */
-int sqmp_fq7_sizes(int N, int Kp, int S_pad, int ngw, size_t* codes_bytes,
+int sqmp_fq7_sizes(int N, int Kp, int S_pad, int ngw, int J, size_t* codes_bytes,
                    size_t* scale_elems, size_t* sal_elems);
 int sqmp_pack_fq7(const void* codes, const void* wscale, const void* wsal, int dtype, int N,
-                  int Kp, int S_pad, int ngw, void* codes_t, void* scale_t, void* sal_t,
+                  int Kp, int S_pad, int ngw, int J, void* codes_t, void* scale_t, void* sal_t,
                   void* stream);
 
 /* sqmp_gemm_fq_colmax (4-bit codes, Gw % 64 == 0 or Gw == 32, fp16/bf16, N % 8 == 0) on
  * the sqmp_pack_fq7 operands: the same operands and numerics (x_hat . W_hat with W_hat =
  * D(code * scale) decoded in registers, fp32 accumulation, bias, one rounding to D), the
- * codes, scales and salient weights loaded straight into registers; 128 x 512 tiles.
+ * codes, scales and salient weights loaded straight into registers; 128 x 512 tiles (J = 4)
+ * or 256 x 256 (J = 2), the operands packed with the same J.
  * a: roundup(M, 256) rows allocated.  colmax may be NULL. */
 int sqmp_gemm_fq7(const void* a, const void* codes_t, const void* scale_t, const void* sal_t,
                   const void* bias, void* y, int dtype, int M, int N, int Kp, int S_pad,
-                  int Gw, int ngw, uint32_t* colmax, void* stream);
+                  int Gw, int ngw, int J, uint32_t* colmax, void* stream);
 
 /* The weight operand of sqmp_gemm_fqt for the activation order of the LAST
  * sqmp_quant_act_v2(SQMP_OUT_C4) call on `workspace` (same K, Kp, S, S_pad): wp

@@ -88,6 +88,11 @@ __device__ inline void ld16(u32x4& d, const rsrc_t& r, uint32_t voff, uint32_t s
 __device__ inline void ld8(u32x2& d, const rsrc_t& r, uint32_t voff, uint32_t soff) {
   asm volatile("buffer_load_dwordx2 %0, %1, %2, %3 offen" : "=v"(d) : "v"(voff), "s"(r), "s"(soff));
 }
+__device__ inline void ld4(uint32_t& d, const rsrc_t& r, uint32_t voff, uint32_t soff) {
+  asm volatile("buffer_load_dword %0, %1, %2, %3 offen" : "=v"(d) : "v"(voff), "s"(r), "s"(soff));
+}
+__device__ inline void ld_s(u32x2& d, const rsrc_t& r, uint32_t voff, uint32_t soff) { ld8(d, r, voff, soff); }
+__device__ inline void ld_s(uint32_t& d, const rsrc_t& r, uint32_t voff, uint32_t soff) { ld4(d, r, voff, soff); }
 template <class V>
 __device__ inline void fence(V& v) {
   asm volatile("" : "+v"(v));
@@ -98,7 +103,9 @@ __host__ __device__ inline int brev3(int c) { return ((c & 1) << 2) | (c & 2) | 
 // DIAG (timing diagnostics, wrong results by design; 0 = the product kernel): 1 no weight
 // register loads after the prologue, 2 no A DMA after the prologue, 3 no int4 decode, 4 no
 // per-stage barrier
-template <class DT, int GB, int TM, int DIAG = 0>
+// J = 16-row weight tiles per wave: tile TM x TN with TN = 8 * 16 J (J = 4: 128 x 512;
+// J = 2: 256 x 256, fq6's decode-optimal shape -- a decoded fragment feeds TM / 16 MFMAs)
+template <class DT, int GB, int TM, int J, int DIAG = 0>
 __global__ __launch_bounds__(512, 1) void gemm_fq7_kernel(
     const typename DT::T* __restrict__ A, const uint32_t* __restrict__ Bt,
     const typename DT::T* __restrict__ St, const typename DT::T* __restrict__ Salt,
@@ -106,24 +113,25 @@ __global__ __launch_bounds__(512, 1) void gemm_fq7_kernel(
     int Kp, int S_pad, int Gw, int ngw, int tiles_m, int tiles_n, int group_m,
     uint32_t* __restrict__ colmax) {
   typedef typename DT::T T;
-  constexpr int I = TM / 16, J = 4;     // 16 x 16 tiles per wave: TM rows x 64 weight rows
+  constexpr int I = TM / 16;            // 16 x 16 tiles per wave: TM rows x 16 J weight rows
+  constexpr int TN = 128 * J, WR = 16 * J;  // tile width, weight rows per wave
   constexpr int PA = 3, NS = PA + 1;    // A stages in flight, ring slots
   constexpr int SLOT = TM * 128;        // TM rows x 64 positions x 2 B
   constexpr int NA = TM / 64;           // A pieces per wave per stage
-  constexpr int PF = 3;                 // A fragment read-ahead (blocks)
-  constexpr int LDS_BYTES = NS * SLOT > TM * 1024 ? NS * SLOT : TM * 1024;
+  constexpr int PF = TM == 256 ? 2 : 3;  // A fragment read-ahead (blocks; 2 keeps TM = 256 spill-free)
+  constexpr int LDS_BYTES = NS * SLOT > TM * TN * 2 ? NS * SLOT : TM * TN * 2;
   static_assert(J <= I, "sub-step 1 decode must finish before block I");
   __shared__ __attribute__((aligned(16))) unsigned char lds[LDS_BYTES];
 
   int tm, tn;
   tile_coords(tiles_m, tiles_n, group_m, tm, tn);
-  const int m0 = tm * TM, n0 = tn * 512;
+  const int m0 = tm * TM, n0 = tn * TN;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r16 = lane & 15, q = lane >> 4;
   const int lda = Kp + S_pad;
   const int nkm = Kp / 64, nks = S_pad / 64, nkt = nkm + nks;
-  const int nb = tn * 8 + wave;  // this wave's 64-row weight block
+  const int nb = tn * 8 + wave;  // this wave's WR-row weight block
 
   // ---- A (x_hat) by LDS-DMA: piece i of wave w = rows 64 i + 8 w + (lane >> 3), the lane
   // moving logical chunk brev3(p ^ ((row >> 1) & 7)) into physical chunk p = lane & 7
@@ -144,48 +152,50 @@ __global__ __launch_bounds__(512, 1) void gemm_fq7_kernel(
   };
 
   // ---- weight operand straight to registers (tile-major copies, sqmp_pack_fq7)
-  const rsrc_t rB = make_rsrc(Bt + (size_t)nb * nkm * 512);           // 2 KiB per stage
-  const rsrc_t rS = make_rsrc(St + (size_t)nb * ngw * 64);            // 128 B per group
-  const rsrc_t rD = make_rsrc(Salt + (size_t)nb * (nks > 0 ? nks : 1) * 4096);  // 8 KiB per stage
-  const uint32_t vB = (uint32_t)lane * 32u, vD = (uint32_t)lane * 128u;
-  const uint32_t vS = (uint32_t)r16 * 8u;
+  // per wave block and stage: codes 512 J B, scales (per group) 32 J B, salient 2048 J B
+  const rsrc_t rB = make_rsrc(Bt + (size_t)nb * nkm * (128 * J));
+  const rsrc_t rS = make_rsrc(St + (size_t)nb * ngw * (16 * J));
+  const rsrc_t rD = make_rsrc(Salt + (size_t)nb * (nks > 0 ? nks : 1) * (1024 * J));
+  const uint32_t vB = (uint32_t)lane * (8u * J), vD = (uint32_t)lane * (32u * J);
+  const uint32_t vS = (uint32_t)r16 * (2u * J);
   // one stage ahead: stage kt computes on register set kt & 1 (codes) / kd & 1 (salient
   // tail) while the next stage's loads land in the other set.  No value in flight is ever
   // copied (a copy the compiler placed before the wait would read the registers before
   // the load lands), so the loops are unrolled by two with compile-time set indices: Kp %
   // 128 == 0 makes the codes stage count even and the last codes stage odd.
+  typedef typename std::conditional<J == 4, u32x2, uint32_t>::type SRegs;
   struct Codes {
-    u32x4 w[2];  // dwords [j][s] of rows 16 j + r16
-    u32x2 s;     // scales of rows 16 j + r16 (4 x D)
+    u32x4 w[J / 2];  // dwords [j][s] of rows 16 j + r16
+    SRegs s;         // scales of rows 16 j + r16 (J x D)
   };
   struct Dense {
-    u32x4 w[8];  // chunk c(q, s) of rows 16 j + r16, [j][s]
+    u32x4 w[2 * J];  // chunk c(q, s) of rows 16 j + r16, [j][s]
   };
 
   auto issue_codes = [&](int kt, Codes& d) {
     if (DIAG == 1 && kt > 1) return;
-    ld16<0>(d.w[0], rB, vB, (uint32_t)kt * 2048u);
-    ld16<16>(d.w[1], rB, vB, (uint32_t)kt * 2048u);
-    if (GB == 1) {
-      const int g = min((kt * 64) / Gw, ngw - 1);
-      ld8(d.s, rS, vS, (uint32_t)g * 128u);
-    } else {  // Gw = 32: the lane's dwords lie in group 2 kt + (q & 1) (clamped: padding)
-      const int g = min(2 * kt + (q & 1), ngw - 1);
-      ld8(d.s, rS, (uint32_t)g * 128u + vS, 0u);
-    }
+    ld16<0>(d.w[0], rB, vB, (uint32_t)kt * (512u * J));
+    if (J == 4) ld16<16>(d.w[J / 2 - 1], rB, vB, (uint32_t)kt * (512u * J));
+    // Gw = 32: the lane's dwords lie in group 2 kt + (q & 1) (clamped: padding)
+    const int g = GB == 1 ? min((kt * 64) / Gw, ngw - 1) : min(2 * kt + (q & 1), ngw - 1);
+    const uint32_t vo = GB == 1 ? vS : (uint32_t)g * (32u * J) + vS;
+    const uint32_t so = GB == 1 ? (uint32_t)g * (32u * J) : 0u;
+    ld_s(d.s, rS, vo, so);
   };
   // salient stage kd, sub-step s: the fragments [j][s] (4 x 16 B per lane)
   auto issue_dense = [&](int kd, Dense& d, auto sc) {
     constexpr int S = decltype(sc)::value;
-    const uint32_t so = (uint32_t)kd * 8192u;
+    const uint32_t so = (uint32_t)kd * (2048u * J);
     ld16<16 * S>(d.w[S], rD, vD, so);
     ld16<32 + 16 * S>(d.w[2 + S], rD, vD, so);
-    ld16<64 + 16 * S>(d.w[4 + S], rD, vD, so);
-    ld16<96 + 16 * S>(d.w[6 + S], rD, vD, so);
+    if (J == 4) {
+      ld16<64 + 16 * S>(d.w[(4 + S) % (2 * J)], rD, vD, so);
+      ld16<96 + 16 * S>(d.w[(6 + S) % (2 * J)], rD, vD, so);
+    }
   };
   auto fence_codes = [&](Codes& d) {
-    fence(d.w[0]);
-    fence(d.w[1]);
+#pragma unroll
+    for (int u = 0; u < J / 2; ++u) fence(d.w[u]);
     fence(d.s);
   };
 
@@ -216,7 +226,12 @@ __global__ __launch_bounds__(512, 1) void gemm_fq7_kernel(
   }
 
   auto compute_codes = [&](const unsigned char* __restrict__ slot, const Codes& cd) {
-    const uint32_t sb[4] = {cd.s.x & 0xFFFFu, cd.s.x >> 16, cd.s.y & 0xFFFFu, cd.s.y >> 16};
+    uint32_t sb[4];
+    if constexpr (J == 4) {
+      sb[0] = cd.s.x & 0xFFFFu, sb[1] = cd.s.x >> 16, sb[2] = cd.s.y & 0xFFFFu, sb[3] = cd.s.y >> 16;
+    } else {
+      sb[0] = cd.s & 0xFFFFu, sb[1] = cd.s >> 16, sb[2] = 0u, sb[3] = 0u;
+    }
     uint32_t sp[J];
 #pragma unroll
     for (int j = 0; j < J; ++j) sp[j] = Dec<DT>::prep(sb[j]);
@@ -286,7 +301,7 @@ __global__ __launch_bounds__(512, 1) void gemm_fq7_kernel(
   // than its sub-step 1 are A(k + PA).
   for (int kd = 0; kd < nks; ++kd) {
     const int k = nkm + kd;
-    vmwait<4>();
+    vmwait<J>();
 #pragma unroll
     for (int j = 0; j < J; ++j) fence(dd.w[2 * j]);
     barrier();
@@ -306,14 +321,14 @@ __global__ __launch_bounds__(512, 1) void gemm_fq7_kernel(
     if (more) issue_dense(kd + 1, dd, O());
   }
 
-  // ---- epilogue: the TM x 512 tile staged in LDS (row m: 1 KiB, 16-B chunk c at
+  // ---- epilogue: the TM x TN tile staged in LDS (row m: 2 TN bytes, 16-B chunk c at
   // c ^ (m & 15)), stored as whole rows, one 16-B chunk per lane
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   barrier();  // every wave is past its last read of the ring
   float cmx[J][4] = {};
 #pragma unroll
   for (int j = 0; j < J; ++j) {
-    const int nl = 64 * wave + 16 * j + 4 * q;  // first of the lane's 4 columns
+    const int nl = WR * wave + 16 * j + 4 * q;  // first of the lane's 4 columns
     float bv[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r)
@@ -329,7 +344,7 @@ __global__ __launch_bounds__(512, 1) void gemm_fq7_kernel(
         for (int r = 0; r < 4; ++r) cmx[j][r] = fmaxf(cmx[j][r], fabsf(DT::to_f(v[r])));
       }
       const int c = nl >> 3;
-      *(u32x2*)(lds + ml * 1024 + ((c ^ (ml & 15)) << 4) + (nl & 4) * 2) = *(const u32x2*)v;
+      *(u32x2*)(lds + ml * (TN * 2) + ((c ^ (ml & 15)) << 4) + (nl & 4) * 2) = *(const u32x2*)v;
     }
   }
   if (colmax) {
@@ -342,65 +357,66 @@ __global__ __launch_bounds__(512, 1) void gemm_fq7_kernel(
         v = fmaxf(v, __shfl_xor(v, 2, 64));
         v = fmaxf(v, __shfl_xor(v, 4, 64));
         v = fmaxf(v, __shfl_xor(v, 8, 64));
-        const int n = n0 + 64 * wave + 16 * j + 4 * q + r;
+        const int n = n0 + WR * wave + 16 * j + 4 * q + r;
         if (r16 == 0 && n < N) atomicMax(colmax + n, __float_as_uint(v));
       }
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   barrier();
-  const int c = lane;  // 64 chunks per row, one wave per row
+  constexpr int CPR = TN / 8, RPP = 512 / CPR;  // 16-B chunks per row, rows per pass
+  const int c = tid % CPR;
   const bool cok = n0 + c * 8 < N;  // N % 8 == 0 (launcher)
 #pragma unroll
-  for (int k = 0; k < TM / 8; ++k) {
-    const int ml = 8 * k + wave;
+  for (int k = 0; k < TM / RPP; ++k) {
+    const int ml = RPP * k + tid / CPR;
     const int gm = m0 + ml;
-    const u32x4 val = *(const u32x4*)(lds + ml * 1024 + ((c ^ (ml & 15)) << 4));
+    const u32x4 val = *(const u32x4*)(lds + ml * (TN * 2) + ((c ^ (ml & 15)) << 4));
     if (gm < M && cok) *(u32x4*)(Y + (size_t)gm * N + n0 + c * 8) = val;
   }
 }
 
-// ---- tile-major copies of the packed weight (once per layer)
-// Bt[nb][kb][lane][j][s] (dwords) = bpack dword 2q + s of block kb of row 64 nb + 16 j + r16
+// ---- tile-major copies of the packed weight (once per layer), blocks of WR = 16 J rows
+// Bt[nb][kb][lane][j][s] (dwords) = bpack dword 2q + s of block kb of row WR nb + 16 j + r16
 __global__ void pack_codes_kernel(const uint32_t* __restrict__ codes, uint32_t* __restrict__ Bt,
-                                  int Np, int KB, long total) {
+                                  int Np, int KB, int J, long total) {
   const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= total) return;
-  const int d = (int)(idx & 7), lane = (int)((idx >> 3) & 63);
-  const long rest = idx >> 9;
+  const int d = (int)(idx % (2 * J)), lane = (int)((idx / (2 * J)) & 63);
+  const long rest = idx / (128 * J);
   const int kb = (int)(rest % KB);
   const long nbk = rest / KB;
   const int j = d >> 1, s = d & 1, q = lane >> 4, r16 = lane & 15;
-  const long n = nbk * 64 + 16 * j + r16;
+  const long n = nbk * 16 * J + 16 * j + r16;
   Bt[idx] = n < Np ? codes[n * (KB * 8) + kb * 8 + 2 * q + s] : 0u;
 }
-// St[nb][g][r16][j] = wscale[g][64 nb + 16 j + r16]
+// St[nb][g][r16][j] = wscale[g][WR nb + 16 j + r16]
 template <class T>
 __global__ void pack_scales_kernel(const T* __restrict__ wscale, T* __restrict__ St, int Np,
-                                   int ngw, long total) {
+                                   int ngw, int J, long total) {
   const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= total) return;
-  const int j = (int)(idx & 3), r16 = (int)((idx >> 2) & 15);
-  const long rest = idx >> 6;
+  const int j = (int)(idx % J), r16 = (int)((idx / J) & 15);
+  const long rest = idx / (16 * J);
   const int g = (int)(rest % ngw);
   const long nbk = rest / ngw;
-  const long n = nbk * 64 + 16 * j + r16;
+  const long n = nbk * 16 * J + 16 * j + r16;
   St[idx] = n < Np ? wscale[(long)g * Np + n] : (T)0.f;
 }
-// Salt[nb][kd][lane][j][s][e] = wsal[64 nb + 16 j + r16][64 kd + 8 c(q, s) + e]
+// Salt[nb][kd][lane][j][s][e] = wsal[WR nb + 16 j + r16][64 kd + 8 c(q, s) + e]
 template <class T>
 __global__ void pack_sal_kernel(const T* __restrict__ wsal, T* __restrict__ Salt, int N,
-                                int S_pad, long total) {
+                                int S_pad, int J, long total) {
   const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= total) return;
-  const int e = (int)(idx & 7), s = (int)((idx >> 3) & 1), j = (int)((idx >> 4) & 3);
-  const int lane = (int)((idx >> 6) & 63);
+  const int e = (int)(idx & 7), s = (int)((idx >> 3) & 1), j = (int)((idx >> 4) % J);
+  const int lane = (int)((idx / (16 * J)) & 63);
   const int KS = S_pad / 64;
-  const long rest = idx >> 12;
+  const long rest = idx / (1024 * J);
   const int kd = (int)(rest % KS);
   const long nbk = rest / KS;
   const int q = lane >> 4, r16 = lane & 15;
   const int c = 4 * (q & 1) + 2 * s + (q >> 1);
-  const long n = nbk * 64 + 16 * j + r16;
+  const long n = nbk * 16 * J + 16 * j + r16;
   Salt[idx] = n < N ? wsal[n * S_pad + kd * 64 + 8 * c + e] : (T)0.f;
 }
 
@@ -420,25 +436,25 @@ static int diag_env() {
   return v;
 }
 
-template <class DT, int GB, int TM, int DIAG = 0>
+template <class DT, int GB, int TM, int J, int DIAG = 0>
 static int launch_k(const void* a, const void* bt, const void* st, const void* salt,
                   const void* bias, void* y, int M, int N, int Kp, int S_pad, int Gw, int ngw,
                   uint32_t* colmax, hipStream_t s) {
   typedef typename DT::T T;
-  const int tiles_m = cdiv(M, TM), tiles_n = cdiv(N, 512);
-  gemm_fq7_kernel<DT, GB, TM, DIAG><<<dim3(tiles_m * tiles_n), dim3(512), 0, s>>>(
+  const int tiles_m = cdiv(M, TM), tiles_n = cdiv(N, 128 * J);
+  gemm_fq7_kernel<DT, GB, TM, J, DIAG><<<dim3(tiles_m * tiles_n), dim3(512), 0, s>>>(
       (const T*)a, (const uint32_t*)bt, (const T*)st, (const T*)salt, (const T*)bias, (T*)y, M,
       N, Kp, S_pad, Gw, ngw, tiles_m, tiles_n, group_m_env(), colmax);
   SQMP_LAUNCH_CHECK();
   return SQMP_OK;
 }
 
-template <class DT, int GB, int TM>
+template <class DT, int GB, int TM, int J>
 static int launch(const void* a, const void* bt, const void* st, const void* salt,
                   const void* bias, void* y, int M, int N, int Kp, int S_pad, int Gw, int ngw,
                   uint32_t* colmax, hipStream_t s) {
-#define SQMP_L(D) launch_k<DT, GB, TM, D>(a, bt, st, salt, bias, y, M, N, Kp, S_pad, Gw, ngw, colmax, s)
-  if (std::is_same<DT, F16>::value && GB == 1 && TM == 128) {
+#define SQMP_L(D) launch_k<DT, GB, TM, J, D>(a, bt, st, salt, bias, y, M, N, Kp, S_pad, Gw, ngw, colmax, s)
+  if (std::is_same<DT, F16>::value && GB == 1 && TM == 128 * 4 / J) {
     switch (diag_env()) {
       case 1: return SQMP_L(1);
       case 2: return SQMP_L(2);
@@ -454,12 +470,16 @@ static int launch(const void* a, const void* bt, const void* st, const void* sal
 template <class DT>
 static int dispatch(const void* a, const void* bt, const void* st, const void* salt,
                     const void* bias, void* y, int M, int N, int Kp, int S_pad, int Gw,
-                    int ngw, uint32_t* colmax, hipStream_t s) {
-  // 64-row tiles when 128-row tiles leave CUs idle
-  const int tm = (long)cdiv(M, 128) * cdiv(N, 512) >= 256 ? 128 : 64;
-#define SQMP_FQ7(GB)                                                                          \
-  (tm == 128 ? launch<DT, GB, 128>(a, bt, st, salt, bias, y, M, N, Kp, S_pad, Gw, ngw, colmax, s) \
-             : launch<DT, GB, 64>(a, bt, st, salt, bias, y, M, N, Kp, S_pad, Gw, ngw, colmax, s))
+                    int ngw, int J, uint32_t* colmax, hipStream_t s) {
+  // J = 4: 128 x 512 tiles (64-row tiles when those leave CUs idle); J = 2: 256 x 256
+  // (128 x 256 when those leave CUs idle)
+  const int tm = J == 4 ? ((long)cdiv(M, 128) * cdiv(N, 512) >= 256 ? 128 : 64)
+                        : ((long)cdiv(M, 256) * cdiv(N, 256) >= 512 ? 256 : 128);
+#define SQMP_FQ7(GB)                                                                              \
+  (J == 4 ? (tm == 128 ? launch<DT, GB, 128, 4>(a, bt, st, salt, bias, y, M, N, Kp, S_pad, Gw, ngw, colmax, s) \
+                       : launch<DT, GB, 64, 4>(a, bt, st, salt, bias, y, M, N, Kp, S_pad, Gw, ngw, colmax, s))  \
+          : (tm == 256 ? launch<DT, GB, 256, 2>(a, bt, st, salt, bias, y, M, N, Kp, S_pad, Gw, ngw, colmax, s) \
+                       : launch<DT, GB, 128, 2>(a, bt, st, salt, bias, y, M, N, Kp, S_pad, Gw, ngw, colmax, s)))
   if (Gw % 64 == 0) return SQMP_FQ7(1);
   if (Gw == 32) return SQMP_FQ7(2);
   return SQMP_EUNSUPPORTED;
@@ -468,13 +488,14 @@ static int dispatch(const void* a, const void* bt, const void* st, const void* s
 
 }  // namespace fq7
 
-// rows of the tile-major copies: N rounded up to the 512-row tile
-static inline long fq7_rows(int N) { return (N + 511) / 512 * 512L; }
+// rows of the tile-major copies: N rounded up to the 128 J-row tile
+static inline long fq7_rows(int N, int J) { return (N + 128L * J - 1) / (128L * J) * (128L * J); }
 
-extern "C" int sqmp_fq7_sizes(int N, int Kp, int S_pad, int ngw, size_t* codes_bytes,
+extern "C" int sqmp_fq7_sizes(int N, int Kp, int S_pad, int ngw, int J, size_t* codes_bytes,
                               size_t* scale_elems, size_t* sal_elems) {
   if (N <= 0 || Kp <= 0 || Kp % 64 || S_pad < 0 || S_pad % 64 || ngw <= 0) return SQMP_EINVAL;
-  const long R = fq7_rows(N);
+  if (J != 2 && J != 4) return SQMP_EINVAL;
+  const long R = fq7_rows(N, J);
   if (codes_bytes) *codes_bytes = (size_t)R * Kp / 2;
   if (scale_elems) *scale_elems = (size_t)R * ngw;
   if (sal_elems) *sal_elems = (size_t)R * (S_pad > 0 ? S_pad : 64);
@@ -482,34 +503,35 @@ extern "C" int sqmp_fq7_sizes(int N, int Kp, int S_pad, int ngw, size_t* codes_b
 }
 
 extern "C" int sqmp_pack_fq7(const void* codes, const void* wscale, const void* wsal, int dtype,
-                             int N, int Kp, int S_pad, int ngw, void* codes_t, void* scale_t,
-                             void* sal_t, void* stream) {
+                             int N, int Kp, int S_pad, int ngw, int J, void* codes_t,
+                             void* scale_t, void* sal_t, void* stream) {
   if (!codes || !wscale || !codes_t || !scale_t || !sal_t || (S_pad > 0 && !wsal))
     return SQMP_EINVAL;
   if (dtype != SQMP_F16 && dtype != SQMP_BF16) return SQMP_EUNSUPPORTED;
   if (N <= 0 || Kp <= 0 || Kp % 64 || S_pad < 0 || S_pad % 64 || ngw <= 0) return SQMP_EINVAL;
+  if (J != 2 && J != 4) return SQMP_EINVAL;
   hipStream_t s = (hipStream_t)stream;
-  const long R = fq7_rows(N);
+  const long R = fq7_rows(N, J);
   const int Np = pad_n(N), KB = Kp / 64;
   const long tc = R * Kp / 8, ts = R * ngw;
   fq7::pack_codes_kernel<<<dim3((unsigned)cdiv(tc, 256)), dim3(256), 0, s>>>(
-      (const uint32_t*)codes, (uint32_t*)codes_t, Np, KB, tc);
+      (const uint32_t*)codes, (uint32_t*)codes_t, Np, KB, J, tc);
   SQMP_LAUNCH_CHECK();
   if (dtype == SQMP_F16)
     fq7::pack_scales_kernel<_Float16><<<dim3((unsigned)cdiv(ts, 256)), dim3(256), 0, s>>>(
-        (const _Float16*)wscale, (_Float16*)scale_t, Np, ngw, ts);
+        (const _Float16*)wscale, (_Float16*)scale_t, Np, ngw, J, ts);
   else
     fq7::pack_scales_kernel<__bf16><<<dim3((unsigned)cdiv(ts, 256)), dim3(256), 0, s>>>(
-        (const __bf16*)wscale, (__bf16*)scale_t, Np, ngw, ts);
+        (const __bf16*)wscale, (__bf16*)scale_t, Np, ngw, J, ts);
   SQMP_LAUNCH_CHECK();
   if (S_pad > 0) {
     const long tsl = R * S_pad;
     if (dtype == SQMP_F16)
       fq7::pack_sal_kernel<_Float16><<<dim3((unsigned)cdiv(tsl, 256)), dim3(256), 0, s>>>(
-          (const _Float16*)wsal, (_Float16*)sal_t, N, S_pad, tsl);
+          (const _Float16*)wsal, (_Float16*)sal_t, N, S_pad, J, tsl);
     else
       fq7::pack_sal_kernel<__bf16><<<dim3((unsigned)cdiv(tsl, 256)), dim3(256), 0, s>>>(
-          (const __bf16*)wsal, (__bf16*)sal_t, N, S_pad, tsl);
+          (const __bf16*)wsal, (__bf16*)sal_t, N, S_pad, J, tsl);
     SQMP_LAUNCH_CHECK();
   }
   return SQMP_OK;
@@ -517,18 +539,19 @@ extern "C" int sqmp_pack_fq7(const void* codes, const void* wscale, const void* 
 
 extern "C" int sqmp_gemm_fq7(const void* a, const void* codes_t, const void* scale_t,
                              const void* sal_t, const void* bias, void* y, int dtype, int M,
-                             int N, int Kp, int S_pad, int Gw, int ngw, uint32_t* colmax,
+                             int N, int Kp, int S_pad, int Gw, int ngw, int J, uint32_t* colmax,
                              void* stream) {
   if (!a || !codes_t || !scale_t || !sal_t || !y) return SQMP_EINVAL;
   if (M < 0 || N <= 0 || Kp <= 0 || Kp % 128 || S_pad < 0 || S_pad % 64 || Gw <= 0 || ngw <= 0)
     return SQMP_EINVAL;
+  if (J != 2 && J != 4) return SQMP_EINVAL;
   if (dtype != SQMP_F16 && dtype != SQMP_BF16) return SQMP_EUNSUPPORTED;
   if (N % 8) return SQMP_EUNSUPPORTED;  // whole 16-B output chunks
   if (M == 0) return SQMP_OK;
   hipStream_t s = (hipStream_t)stream;
   if (dtype == SQMP_F16)
-    return fq7::dispatch<F16>(a, codes_t, scale_t, sal_t, bias, y, M, N, Kp, S_pad, Gw, ngw, colmax, s);
-  return fq7::dispatch<BF16>(a, codes_t, scale_t, sal_t, bias, y, M, N, Kp, S_pad, Gw, ngw, colmax, s);
+    return fq7::dispatch<F16>(a, codes_t, scale_t, sal_t, bias, y, M, N, Kp, S_pad, Gw, ngw, J, colmax, s);
+  return fq7::dispatch<BF16>(a, codes_t, scale_t, sal_t, bias, y, M, N, Kp, S_pad, Gw, ngw, J, colmax, s);
 }
 
 }  // namespace sqmp

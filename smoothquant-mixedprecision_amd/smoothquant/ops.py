@@ -92,7 +92,7 @@ class PackedWeight:
     w8: Optional[torch.Tensor] = field(default=None)     # uint8 [Np, Kp] e4m3 codes (f8 GEMM)
     ws32: Optional[torch.Tensor] = field(default=None)   # fp32 [ngw, Np] scales (f8/f6 GEMM)
     w6: Optional[torch.Tensor] = field(default=None)     # uint8 [Np, Kp*3/4] e2m3 (f6 GEMM)
-    fq7: Optional[tuple] = field(default=None)           # (codes_t, scale_t, sal_t) of gemm_fq7
+    fq7: Optional[tuple] = field(default=None)           # (codes_t, scale_t, sal_t, J) of gemm_fq7
 
     @property
     def gemm_operand(self):
@@ -417,6 +417,8 @@ def fake_quant_inplace(t2: torch.Tensor, act_quant: str, n_bits: int, group_size
 
 # Whether gemm_fq runs the register-operand kernel (sqmp_gemm_fq7) where fq7_eligible.
 FQ7_AUTO = os.environ.get("SQMP_FQ7", "0") == "1"
+# weight rows per wave / 16: 4 -> 128 x 512 tiles, 2 -> 256 x 256 tiles
+FQ7_J = int(os.environ.get("SQMP_FQ7_J", "2"))
 
 
 def fq7_eligible(pw: PackedWeight) -> bool:
@@ -429,18 +431,18 @@ def fq7_eligible(pw: PackedWeight) -> bool:
 def fq7_operands(pw: PackedWeight):
     """(codes_t, scale_t, sal_t) of gemm_fq7: tile-major copies of the packed weight, built
     once per packed weight."""
-    if pw.fq7 is None:
+    if pw.fq7 is None or pw.fq7[3] != FQ7_J:
         sizes = [ctypes.c_size_t() for _ in range(3)]
-        check(load().sqmp_fq7_sizes(pw.N, pw.Kp, pw.S_pad, pw.ngw,
+        check(load().sqmp_fq7_sizes(pw.N, pw.Kp, pw.S_pad, pw.ngw, FQ7_J,
                                     *[ctypes.byref(v) for v in sizes]), "fq7_sizes")
         dev = pw.codes.device
         bt = torch.empty(sizes[0].value, dtype=torch.uint8, device=dev)
         st = torch.empty(sizes[1].value, dtype=pw.dtype, device=dev)
         salt = torch.empty(sizes[2].value, dtype=pw.dtype, device=dev)
         check(load().sqmp_pack_fq7(_p(pw.codes), _p(pw.wscale), _p(pw.wsal) if pw.S_pad else None,
-                                   _dtype_code(pw.dtype), pw.N, pw.Kp, pw.S_pad, pw.ngw, _p(bt),
-                                   _p(st), _p(salt), _stream(pw.codes)), "pack_fq7")
-        pw.fq7 = (bt, st, salt)
+                                   _dtype_code(pw.dtype), pw.N, pw.Kp, pw.S_pad, pw.ngw, FQ7_J,
+                                   _p(bt), _p(st), _p(salt), _stream(pw.codes)), "pack_fq7")
+        pw.fq7 = (bt, st, salt, FQ7_J)
     return pw.fq7
 
 
@@ -449,9 +451,9 @@ def gemm_fq7(a: torch.Tensor, pw: PackedWeight, bias: Optional[torch.Tensor],
     """gemm_fq on the register-operand kernel (same operands and numerics)."""
     M = a.shape[0]
     y = torch.empty((M, pw.N), dtype=pw.dtype, device=a.device)
-    bt, st, salt = fq7_operands(pw)
+    bt, st, salt, J = fq7_operands(pw)
     check(load().sqmp_gemm_fq7(_p(a), _p(bt), _p(st), _p(salt), _p(bias), _p(y),
-                               _dtype_code(pw.dtype), M, pw.N, pw.Kp, pw.S_pad, pw.Gw, pw.ngw,
+                               _dtype_code(pw.dtype), M, pw.N, pw.Kp, pw.S_pad, pw.Gw, pw.ngw, J,
                                _p(colmax) if colmax is not None else None, _stream(a)),
           "gemm_fq7")
     return y
