@@ -30,11 +30,12 @@ def test_fq7_kernels_do_not_spill(tmp_path):
     seen = 0
     for b in blocks[1:]:
         name = b.split()[0]
-        m = re.search(r"gemm_fq7_kernelI.*?ELi(\d+)ELi(\d+)ELi(\d+)E", name)
-        if not m or m.group(3) != "0":  # product kernels only (DIAG = 0)
+        # template <DT, GB, TM, J, DIAG>: product kernels only (DIAG = 0)
+        m = re.search(r"gemm_fq7_kernelI.*?ELi(\d+)ELi(\d+)ELi(\d+)ELi(\d+)E", name)
+        if not m or m.group(4) != "0":
             continue
         seen += 1
         spill = int(re.search(r"VGPRs Spill: (\d+)", b).group(1))
         scratch = int(re.search(r"ScratchSize \[bytes/lane\]: (\d+)", b).group(1))
         assert spill == 0 and scratch == 0, f"{name}: {spill} VGPR spills, {scratch} B scratch"
-    assert seen >= 8
+    assert seen >= 16
