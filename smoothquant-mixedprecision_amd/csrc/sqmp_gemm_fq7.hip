@@ -475,10 +475,12 @@ static int dispatch(const void* a, const void* bt, const void* st, const void* s
   // (128 x 256 when those leave CUs idle)
   const int tm = J == 4 ? ((long)cdiv(M, 128) * cdiv(N, 512) >= 256 ? 128 : 64)
                         : ((long)cdiv(M, 256) * cdiv(N, 256) >= 512 ? 256 : 128);
+  // (bf16 at 256 x 256 puts an array in scratch: 128-row tiles there)
+  constexpr int TM2 = std::is_same<DT, BF16>::value ? 128 : 256;
 #define SQMP_FQ7(GB)                                                                              \
   (J == 4 ? (tm == 128 ? launch<DT, GB, 128, 4>(a, bt, st, salt, bias, y, M, N, Kp, S_pad, Gw, ngw, colmax, s) \
                        : launch<DT, GB, 64, 4>(a, bt, st, salt, bias, y, M, N, Kp, S_pad, Gw, ngw, colmax, s))  \
-          : (tm == 256 ? launch<DT, GB, 256, 2>(a, bt, st, salt, bias, y, M, N, Kp, S_pad, Gw, ngw, colmax, s) \
+          : (tm == 256 ? launch<DT, GB, TM2, 2>(a, bt, st, salt, bias, y, M, N, Kp, S_pad, Gw, ngw, colmax, s) \
                        : launch<DT, GB, 128, 2>(a, bt, st, salt, bias, y, M, N, Kp, S_pad, Gw, ngw, colmax, s)))
   if (Gw % 64 == 0) return SQMP_FQ7(1);
   if (Gw == 32) return SQMP_FQ7(2);
