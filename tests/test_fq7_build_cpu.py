@@ -38,4 +38,4 @@ def test_fq7_kernels_do_not_spill(tmp_path):
         spill = int(re.search(r"VGPRs Spill: (\d+)", b).group(1))
         scratch = int(re.search(r"ScratchSize \[bytes/lane\]: (\d+)", b).group(1))
         assert spill == 0 and scratch == 0, f"{name}: {spill} VGPR spills, {scratch} B scratch"
-    assert seen >= 16
+    assert seen >= 14
