@@ -298,6 +298,20 @@ int sqmp_gemm_fqt(const void* acodes, const void* ascale, const void* xs, const 
                   const void* bias, void* y, int dtype, int M, int N, int Kq, int S_pad,
                   int G, int ngq, void* stream);
 
+/* fp32 models (the reference runs OPT in fp32): the faithful GEMM on the bf16 MFMA.
+ * sqmp_split3_bf16: src fp32 [R][L] -> three bf16 planes dst [3][ldr][L] with
+ * src == h + m + l exactly (h = bf16(v), m = bf16(v - h), l = v - h - m); rows R..ldr-1
+ * are zero.  Once per layer, on the packed-order W_hat + salient slice (ldr = Np).
+ * sqmp_gemm_x3: y[M][N] = A[M][L] . W^T + bias in fp32, A = the packed-order x_hat +
+ * exact salient columns (SQMP_OUT_FP output, fp32, roundup(M, 256) rows allocated), W
+ * given as the planes b3 [3][roundup(N, 256)][L]; every product a.w is summed as the six
+ * largest of its nine exact piece products (ah.wh + ah.wm + am.wh + ah.wl + al.wh + am.wm,
+ * fp32 accumulation): a relative error per product of a few 2^-24, the rounding of an
+ * fp32 FMA.  L % 32 == 0.  colmax (may be NULL): as sqmp_gemm_fq_colmax. */
+int sqmp_split3_bf16(const float* src, int R, int L, int ldr, void* dst, void* stream);
+int sqmp_gemm_x3(const float* a, const void* b3, const float* bias, float* y, int M, int N,
+                 int L, uint32_t* colmax, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

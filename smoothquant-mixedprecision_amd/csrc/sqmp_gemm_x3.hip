@@ -1,0 +1,237 @@
+// fp32 W4A4 GEMM on the bf16 MFMA (sqmp_gemm_x3): the F.linear of fake_quant.py:306 for
+// fp32 models (OPT runs in fp32 in the reference, run_experiments.py:146-156).
+//
+// Every fp32 value v is split exactly into three bf16 pieces v = h + m + l (h = bf16(v),
+// m = bf16(v - h), l = v - h - m; bf16 has the exponent range of fp32 and 8-bit
+// significands, so the third residual is representable).  A product a.b is then the sum
+// of the nine piece products, each exact in fp32; the three of order 2^-24 and below
+// (m.l, l.m, l.l) are dropped, so
+//     acc += ah.bh + ah.bm + am.bh + ah.bl + al.bh + am.bm
+// on v_mfma_f32_16x16x32_bf16 (fp32 accumulation): a relative error per product of a few
+// units of 2^-24 -- the rounding an fp32 FMA makes -- at 6/16 of the f32-MFMA cost (the
+// f32 MFMA runs at 1/16 of the bf16 rate on gfx950, MI355X_MICROARCH.md).
+//
+// A: x_hat in packed K order + the exact salient columns, fp32 [>= 128-row pad][L], split
+//    in registers while it is staged into LDS (one HBM/L2 read of 4 B per element).
+// B: the packed-order W_hat + salient slice, split once per layer (sqmp_split3_bf16) into
+//    three bf16 planes [3][Np][L].
+// Tile 128 x 128, K stage 32, 4 waves (2 x 2, 64 x 64 each, 16 x 16 output tiles),
+// 96 MFMAs per wave per stage; single-buffered LDS (48 KiB) with the next stage's global
+// loads in flight over the MFMAs, two workgroups per CU.
+#include "sqmp_mfma.h"
+
+namespace sqmp {
+
+namespace {
+
+constexpr int X3_BM = 128, X3_BN = 128, X3_BK = 32;
+constexpr int X3_PLANE = X3_BM * X3_BK * 2;  // one bf16 plane of a 128-row tile: 8 KiB
+constexpr int X3_LDS = 6 * X3_PLANE;         // A planes h, m, l then B planes h, m, l
+
+// 64-B rows (four 16-B chunks).  ds_read_b128 serves lanes in groups
+// {0-3,12-15,20-27}, {4-11,16-19,28-31} (+32): lane (r16, q) reads chunk q of row r16; the
+// physical chunk q ^ H[(row >> 2) & 3] with H = {0, 2, 3, 1} puts the 16 lanes of every
+// group on 16 distinct (row & 3, chunk) bank quarters -- conflict-free.
+__device__ inline int x3_off(int row, int chunk) {
+  const int h = (0x1320 >> (4 * ((row >> 2) & 3))) & 3;  // H = {0, 2, 3, 1}
+  return row * 64 + ((chunk ^ h) << 4);
+}
+
+__device__ inline uint32_t bf16_bits(float v) {
+  const __bf16 b = (__bf16)v;  // RNE
+  return (uint32_t)(*(const uint16_t*)&b);
+}
+__device__ inline float bf16_val(uint32_t bits) { return __uint_as_float(bits << 16); }
+
+// v -> (h, m, l) bf16 bit patterns with v == h + m + l exactly
+__device__ inline void split3(float v, uint32_t& h, uint32_t& m, uint32_t& l) {
+  h = bf16_bits(v);
+  const float r = v - bf16_val(h);  // exact
+  m = bf16_bits(r);
+  l = bf16_bits(r - bf16_val(m));   // exact, and exact in bf16
+}
+
+template <bool COLMAX>
+__global__ __launch_bounds__(256, 2) void gemm_x3_kernel(
+    const float* __restrict__ A, const uint16_t* __restrict__ B3, const float* __restrict__ bias,
+    float* __restrict__ Y, int M, int N, int L, int Np, int tiles_m, int tiles_n,
+    uint32_t* __restrict__ colmax) {
+  __shared__ __attribute__((aligned(16))) unsigned char lds[X3_LDS];
+  int tm, tn;
+  tile_coords(tiles_m, tiles_n, 8, tm, tn);
+  const int m0 = tm * X3_BM, n0 = tn * X3_BN;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int r16 = lane & 15, q = lane >> 4;
+  const int nkt = L / X3_BK;
+  const size_t plane = (size_t)Np * L;
+
+  // staging: A 128 rows x 8 chunks of 4 fp32 (4 per thread); B 3 planes x 128 rows x 4
+  // chunks of 8 bf16 (6 per thread)
+  u32x4 ra[4], rb[6];
+  auto load = [&](int kt) {
+    const int k0 = kt * X3_BK;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int idx = tid + 256 * i, row = idx >> 3, c = idx & 7;
+      ra[i] = *(const u32x4*)(A + (size_t)(m0 + row) * L + k0 + 4 * c);
+    }
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      const int idx = tid + 256 * i, p = idx >> 9, row = (idx >> 2) & 127, c = idx & 3;
+      rb[i] = *(const u32x4*)(B3 + p * plane + (size_t)(n0 + row) * L + k0 + 8 * c);
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int idx = tid + 256 * i, row = idx >> 3, c = idx & 7;
+      uint32_t h[4], m[4], l[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) split3(__uint_as_float(ra[i][e]), h[e], m[e], l[e]);
+      const int off = x3_off(row, c >> 1) + (c & 1) * 8;
+      *(uint2*)(lds + off) = uint2{h[0] | (h[1] << 16), h[2] | (h[3] << 16)};
+      *(uint2*)(lds + X3_PLANE + off) = uint2{m[0] | (m[1] << 16), m[2] | (m[3] << 16)};
+      *(uint2*)(lds + 2 * X3_PLANE + off) = uint2{l[0] | (l[1] << 16), l[2] | (l[3] << 16)};
+    }
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      const int idx = tid + 256 * i, p = idx >> 9, row = (idx >> 2) & 127, c = idx & 3;
+      *(u32x4*)(lds + (3 + p) * X3_PLANE + x3_off(row, c)) = rb[i];
+    }
+  };
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto compute = [&]() {
+    // B fragments (output columns) in the MFMA's A slot: the lane's 4 results are 4
+    // consecutive columns of one row (16-B stores)
+    u32x4 bf[3][4];
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        bf[p][j] = *(const u32x4*)(lds + (3 + p) * X3_PLANE + x3_off(wn * 64 + 16 * j + r16, q));
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      u32x4 af[3];
+#pragma unroll
+      for (int p = 0; p < 3; ++p)
+        af[p] = *(const u32x4*)(lds + p * X3_PLANE + x3_off(wm * 64 + 16 * i + r16, q));
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        // smallest terms first
+        Mfma<BF16>::run(acc[i][j], bf[1][j], af[1]);
+        Mfma<BF16>::run(acc[i][j], bf[2][j], af[0]);
+        Mfma<BF16>::run(acc[i][j], bf[0][j], af[2]);
+        Mfma<BF16>::run(acc[i][j], bf[1][j], af[0]);
+        Mfma<BF16>::run(acc[i][j], bf[0][j], af[1]);
+        Mfma<BF16>::run(acc[i][j], bf[0][j], af[0]);
+      }
+    }
+  };
+
+  load(0);
+  for (int kt = 0; kt < nkt; ++kt) {
+    store();
+    __syncthreads();
+    if (kt + 1 < nkt) load(kt + 1);
+    compute();
+    __syncthreads();
+  }
+
+  // epilogue: acc[i][j][r] = C[m = m0 + 64 wm + 16 i + r16][n = n0 + 64 wn + 16 j + 4 q + r]
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int nb = n0 + wn * 64 + 16 * j + 4 * q;
+    float bv[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bv[r] = bias && nb + r < N ? bias[nb + r] : 0.f;
+    float cm[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int gm = m0 + wm * 64 + 16 * i + r16;
+      f32x4 v;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r] + bv[r];
+      if (gm < M) {
+        if (nb + 4 <= N && (N & 3) == 0) {
+          *(f32x4*)(Y + (size_t)gm * N + nb) = v;
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (nb + r < N) Y[(size_t)gm * N + nb + r] = v[r];
+        }
+        if (COLMAX) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) cm[r] = fmaxf(cm[r], fabsf(v[r]));
+        }
+      }
+    }
+    if (COLMAX) {  // the 16 lanes of a q group hold the tile's 16 rows of these columns
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float c = cm[r];
+        c = fmaxf(c, __shfl_xor(c, 1, 64));
+        c = fmaxf(c, __shfl_xor(c, 2, 64));
+        c = fmaxf(c, __shfl_xor(c, 4, 64));
+        c = fmaxf(c, __shfl_xor(c, 8, 64));
+        if (r16 == 0 && nb + r < N) atomicMax(colmax + nb + r, __float_as_uint(c));
+      }
+    }
+  }
+}
+
+// [R][L] fp32 (row stride L) -> three bf16 planes [3][ldr rows][L]; rows >= R zero-filled
+__global__ void split3_kernel(const float* __restrict__ src, int R, int L, int ldr,
+                              uint16_t* __restrict__ dst) {
+  const size_t n = (size_t)ldr * L;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (size_t)gridDim.x * blockDim.x) {
+    const size_t row = i / L;
+    const float v = row < (size_t)R ? src[i] : 0.f;
+    uint32_t h, m, l;
+    split3(v, h, m, l);
+    dst[i] = (uint16_t)h;
+    dst[n + i] = (uint16_t)m;
+    dst[2 * n + i] = (uint16_t)l;
+  }
+}
+
+}  // namespace
+
+}  // namespace sqmp
+
+using namespace sqmp;
+
+extern "C" int sqmp_split3_bf16(const float* src, int R, int L, int ldr, void* dst,
+                                void* stream) {
+  if (!src || !dst || R <= 0 || L <= 0 || ldr < R) return SQMP_EINVAL;
+  const size_t n = (size_t)ldr * L;
+  const size_t nb = (n + 255) / 256;
+  const int blocks = (int)(nb < 8192 ? nb : 8192);
+  split3_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(src, R, L, ldr, (uint16_t*)dst);
+  SQMP_LAUNCH_CHECK();
+  return SQMP_OK;
+}
+
+extern "C" int sqmp_gemm_x3(const float* a, const void* b3, const float* bias, float* y, int M,
+                            int N, int L, uint32_t* colmax, void* stream) {
+  if (!a || !b3 || !y || M < 0 || N <= 0 || L <= 0) return SQMP_EINVAL;
+  if (L % X3_BK != 0) return SQMP_EINVAL;
+  if (M == 0) return SQMP_OK;
+  const int Np = pad_n(N);
+  const int tiles_m = cdiv(M, X3_BM), tiles_n = cdiv(N, X3_BN);
+  if (colmax)
+    gemm_x3_kernel<true><<<tiles_m * tiles_n, 256, 0, (hipStream_t)stream>>>(
+        a, (const uint16_t*)b3, bias, y, M, N, L, Np, tiles_m, tiles_n, colmax);
+  else
+    gemm_x3_kernel<false><<<tiles_m * tiles_n, 256, 0, (hipStream_t)stream>>>(
+        a, (const uint16_t*)b3, bias, y, M, N, L, Np, tiles_m, tiles_n, nullptr);
+  SQMP_LAUNCH_CHECK();
+  return SQMP_OK;
+}

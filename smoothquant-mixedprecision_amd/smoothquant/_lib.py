@@ -62,6 +62,8 @@ SIGNATURES = {
     "sqmp_pack_fq7": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp]),
     "sqmp_gemm_fq7": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _vp,
                            _vp]),
+    "sqmp_split3_bf16": (_i, [_vp, _i, _i, _i, _vp, _vp]),
+    "sqmp_gemm_x3": (_i, [_vp, _vp, _vp, _vp, _i, _i, _i, _vp, _vp]),
 }
 
 _lock = threading.Lock()

@@ -93,6 +93,7 @@ class PackedWeight:
     ws32: Optional[torch.Tensor] = field(default=None)   # fp32 [ngw, Np] scales (f8/f6 GEMM)
     w6: Optional[torch.Tensor] = field(default=None)     # uint8 [Np, Kp*3/4] e2m3 (f6 GEMM)
     fq7: Optional[tuple] = field(default=None)           # (codes_t, scale_t, sal_t, J) of gemm_fq7
+    x3: Optional[torch.Tensor] = field(default=None)     # bf16 [3, Np, Kp + S_pad] (gemm_x3)
 
     @property
     def gemm_operand(self):
@@ -459,12 +460,50 @@ def gemm_fq7(a: torch.Tensor, pw: PackedWeight, bias: Optional[torch.Tensor],
     return y
 
 
+# Whether fp32 layers run the faithful GEMM on the bf16 MFMA (sqmp_gemm_x3: exact
+# three-way bf16 splits, six piece products) instead of the f32 MFMA (1/16 of the rate).
+X3_AUTO = os.environ.get("SQMP_X3", "1") == "1"
+
+
+def x3_operand(pw: PackedWeight) -> torch.Tensor:
+    """bf16 planes [3, Np, Kp + S_pad] of the packed-order W_hat + exact salient slice
+    (sqmp_split3_bf16), built once per packed fp32 weight."""
+    if pw.x3 is None:
+        w = pw.codes[:pw.N] if pw.n_bits == 0 and pw.dense is None else (
+            pw.dense if pw.dense is not None else dequant_weight_packed(pw))
+        full = torch.cat([w, pw.wsal], dim=1) if pw.S_pad else w
+        full = full.contiguous()
+        Np, L = pad_n(pw.N), pw.Kp + pw.S_pad
+        planes = torch.empty((3, Np, L), dtype=torch.bfloat16, device=full.device)
+        check(load().sqmp_split3_bf16(_p(full), pw.N, L, Np, _p(planes), _stream(full)),
+              "split3_bf16")
+        pw.x3 = planes
+    return pw.x3
+
+
+def gemm_x3(a: torch.Tensor, pw: PackedWeight, bias: Optional[torch.Tensor],
+            colmax: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """gemm_fq for fp32 layers on the bf16 MFMA (fp32-accurate products, see
+    include/sqmp_w4a4.h sqmp_gemm_x3)."""
+    M = a.shape[0]
+    L = pw.Kp + pw.S_pad
+    if a.dtype != torch.float32 or a.shape[1] != L or a.stride(0) != L:
+        raise ValueError("gemm_x3: A must be fp32 [M, Kp + S_pad] with row stride Kp + S_pad")
+    y = torch.empty((M, pw.N), dtype=torch.float32, device=a.device)
+    check(load().sqmp_gemm_x3(_p(a), _p(x3_operand(pw)), _p(bias), _p(y), M, pw.N, L,
+                              _p(colmax) if colmax is not None else None, _stream(a)),
+          "gemm_x3")
+    return y
+
+
 def gemm_fq(a: torch.Tensor, pw: PackedWeight, bias: Optional[torch.Tensor],
             colmax: Optional[torch.Tensor] = None) -> torch.Tensor:
     """y = D(A . W_hat^T + bias).  colmax: a zeroed uint32 buffer of >= N words that the
     epilogue max-reduces bits(|y|) per column into (fused output-quant statistics)."""
     if FQ7_AUTO and fq7_eligible(pw):
         return gemm_fq7(a, pw, bias, colmax)
+    if X3_AUTO and pw.dtype == torch.float32:
+        return gemm_x3(a, pw, bias, colmax)
     M = a.shape[0]
     y = torch.empty((M, pw.N), dtype=pw.dtype, device=a.device)
     b_op, nb = pw.gemm_operand

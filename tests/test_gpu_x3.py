@@ -1,0 +1,122 @@
+"""GPU: the fp32 faithful GEMM on the bf16 MFMA (sqmp_gemm_x3, three-way exact bf16 splits,
+six piece products) -- the F.linear of fake_quant.py:306 for fp32 models (OPT runs in fp32 in
+the reference, run_experiments.py:146-156).
+
+* the split: h + m + l == v exactly for every fp32 value (random, huge, tiny, zero, signs);
+* the GEMM against an fp64 product of the SAME operands (the packed A operand and the
+  packed-order W_hat + salient slice): relative Frobenius error <= 2e-6 -- the rounding level
+  of an fp32 GEMM (the fp32 faithful tolerance of the parity tests is 1e-5); ragged M, N
+  (N % 4 != 0, N < 128), with and without bias and salient tail;
+* the fused output-quant column maxima (colmax) equal max |y| per column;
+* the f32-MFMA kernel (SQMP_X3=0 path) and x3 agree to fp32 rounding level.
+The layer-level fp32 cases of test_gpu_parity / test_gpu_configs (oracle, reference
+goldens, config 1 and 3 layers) run through this kernel by default (ops.X3_AUTO)."""
+import numpy as np
+import pytest
+import torch
+
+from test_gpu_parity import _dev, make_layer, rel
+
+pytestmark = pytest.mark.gpu
+
+
+def test_split3_exact():
+    from smoothquant import ops
+    from smoothquant._lib import load
+    dev = _dev()
+    g = torch.Generator().manual_seed(3)
+    R, L = 37, 96
+    v = torch.randn(R, L, generator=g, dtype=torch.float64)
+    v *= torch.exp2(torch.randint(-60, 60, (R, L), generator=g).double())
+    v[0, :8] = torch.tensor([0.0, -0.0, 1.0, -1.0, 1e38, -1.5e-30, 1e-30, 65504.0])
+    v = v.float().to(dev)
+    ldr = 64
+    out = torch.empty((3, ldr, L), dtype=torch.bfloat16, device=dev)
+    ops.check(load().sqmp_split3_bf16(ops._p(v), R, L, ldr, ops._p(out), ops._stream(v)), "split3")
+    torch.cuda.synchronize()
+    o = out.double()
+    # h + m + l in fp64 is exact (each piece has <= 8 significant bits, |m| <= 2^-8 |h|...)
+    s = o[0, :R] + o[1, :R] + o[2, :R]
+    assert torch.equal(s, v.double()), (s - v.double()).abs().max()
+    assert torch.equal(o[:, R:], torch.zeros_like(o[:, R:]))
+    # the pieces are ordered by magnitude
+    assert bool(((o[1, :R].abs() <= o[0, :R].abs() * 2.0 ** -8)).all())
+
+
+CASES = [
+    # weight_quant, act, p, G, M, K, N, bias, quantize_output
+    ("per_group", "per_group", 0.10, 128, 512, 1024, 512, True, False),
+    ("per_group", "per_group", 0.05, 128, 300, 2048, 200, False, False),
+    ("per_channel", "per_token", 0.0, 128, 129, 768, 77, True, False),       # N % 4 != 0
+    ("per_group", "per_group", 0.05, 128, 64, 2048, 2048, True, True),      # colmax fused
+    ("per_tensor", "per_tensor", 0.10, 128, 1, 1024, 256, True, False),      # one row
+]
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_x3_matches_fp64_product(case):
+    from smoothquant import ops
+    wq, act, p, G, M, K, N, has_bias, oq = case
+    dev = _dev()
+    rng = np.random.default_rng(11)
+    W = (rng.standard_normal((N, K)) * 0.02).astype(np.float32)
+    b = (rng.standard_normal(N) * 0.1).astype(np.float32) if has_bias else None
+    x = rng.standard_normal((M, K)).astype(np.float32)
+    x[:, rng.choice(K, max(1, K // 100), replace=False)] *= 30.0
+    q = make_layer(W, b, "fp32", dev, weight_quant=wq, act_quant=act, quantize_output=oq,
+                   importance=torch.from_numpy(np.abs(x).mean(0)), salient_prop=p, group_size=G)
+    pw = q.packed()
+    xt = torch.from_numpy(x).to(dev)
+    a = ops.quant_act_fp(xt.clone(), pw, act, 4, G)
+    bias = None if q.bias is None else q.bias.detach().reshape(-1)
+    y = ops.gemm_x3(a, pw, bias)
+    planes = ops.x3_operand(pw)
+    Wfull = (planes[0].double() + planes[1].double() + planes[2].double())[:N]
+    ref = a.double() @ Wfull.t()
+    if bias is not None:
+        ref += bias.double()
+    e = rel(y.double().cpu().numpy(), ref.cpu().numpy())
+    assert e <= 2e-6, e
+    # the f32-MFMA kernel on the same operands
+    old = ops.X3_AUTO
+    try:
+        ops.X3_AUTO = False
+        y32 = ops.gemm_fq(a, pw, bias)
+    finally:
+        ops.X3_AUTO = old
+    assert rel(y.double().cpu().numpy(), y32.double().cpu().numpy()) <= 2e-6
+    # fused column maxima
+    colmax = torch.zeros(N + 5, dtype=torch.int32, device=dev)
+    y2 = ops.gemm_x3(a, pw, bias, colmax=colmax)
+    assert torch.equal(y2, y)
+    cm = colmax[:N].view(torch.float32)
+    assert torch.equal(cm, y.abs().amax(0))
+    assert bool((colmax[N:] == 0).all())
+
+
+def test_x3_layer_forward_uses_x3_and_matches_f32_kernel():
+    """W4A4Linear.forward on an fp32 layer takes gemm_x3 (ops.X3_AUTO) and agrees with the
+    f32-MFMA kernel to fp32 rounding level, output quantization included."""
+    from smoothquant import ops
+    dev = _dev()
+    rng = np.random.default_rng(5)
+    K, N, M = 2048, 2048, 256
+    W = (rng.standard_normal((N, K)) * 0.02).astype(np.float32)
+    x = torch.from_numpy(rng.standard_normal((2, M // 2, K)).astype(np.float32)).to(dev)
+    q = make_layer(W, np.zeros(N, np.float32), "fp32", dev, weight_quant="per_group",
+                   act_quant="per_group", quantize_output=True,
+                   importance=x.abs().mean((0, 1)).cpu(), salient_prop=0.05, group_size=128)
+    assert ops.X3_AUTO
+    y = q(x.clone())
+    assert q.packed().x3 is not None
+    old = ops.X3_AUTO
+    try:
+        ops.X3_AUTO = False
+        y32 = q(x.clone())
+    finally:
+        ops.X3_AUTO = old
+    # the group scales of the output quantizer follow last-bit differences of max |y| (every
+    # value of a group moves by a few ulps), and a 4-bit code flips where y sits on a
+    # rounding boundary: count the flips (differences far above fp32 rounding)
+    flips = ((y - y32).abs() > 1e-4 * y32.abs().max()).float().mean().item()
+    assert flips < 0.01, flips
