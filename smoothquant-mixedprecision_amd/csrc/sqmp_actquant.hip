@@ -242,7 +242,13 @@ __global__ __launch_bounds__(256) void quant_act_kernel(
 // division decides.  |q| < 0.25 always yields a (signed) zero code.
 template <class DT>
 __device__ inline float fast_code(float t, float s, float r) {
-  if (DT::id == SQMP_F32) return __builtin_rintf(t / s);
+  if (DT::id == SQMP_F32) {
+    // RN(t / s) from r = RN(1 / s): q0 = t r, e = t - q0 s exactly (fma), RN(q0 + e r) is
+    // the correctly rounded quotient (Markstein); the code is its rint
+    const float q0 = t * r;
+    const float e = __builtin_fmaf(-q0, s, t);
+    return __builtin_rintf(__builtin_fmaf(e, r, q0));
+  }
   const float q = t * r;
   const uint32_t b = __float_as_uint(q);
   constexpr int DROP = DT::id == SQMP_F16 ? 13 : 16;
@@ -357,7 +363,7 @@ __global__ __launch_bounds__(256) void quant_fp_kernel(
           }
         }
 #pragma unroll
-        for (int w = 0; w < 4; ++w) vals[i][w] = ((const uint32_t*)v)[w];
+        for (int j = 0; j < 8; ++j) vals[i][j] = v[j];
       }
     }
     float s_row = s_all, r_row = r_all;
@@ -627,7 +633,8 @@ __global__ __launch_bounds__(256) void quant_fp_wave_kernel(
   }
   __syncthreads();  // tables complete; row buffers are the waves' own
 
-  const int nch = K / 8;
+  constexpr int EPC = 16 / (int)sizeof(T);  // elements per 16-B row chunk
+  const int nch = K / EPC;
   const int wstride = gridDim.x * 4;
   u32x4 nxt[RCH];
   auto load_row = [&](int mm) {
@@ -652,7 +659,7 @@ __global__ __launch_bounds__(256) void quant_fp_wave_kernel(
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     // ---- gather pass
-    uint32_t vals[VCH][4];
+    T vals[VCH][8];
     float lmax = 0.f;
 #pragma unroll
     for (int i = 0; i < VCH; ++i) {
@@ -673,7 +680,7 @@ __global__ __launch_bounds__(256) void quant_fp_wave_kernel(
           }
         }
 #pragma unroll
-        for (int w = 0; w < 4; ++w) vals[i][w] = ((const uint32_t*)v)[w];
+        for (int j = 0; j < 8; ++j) vals[i][j] = v[j];
       }
     }
     float s_row = s_all, r_row = r_all;
@@ -698,7 +705,7 @@ __global__ __launch_bounds__(256) void quant_fp_wave_kernel(
       if (c < NCH) {
         const u32x4 e0 = ent[c], e1 = ent[NCH + c];
         const uint32_t e[8] = {e0[0], e0[1], e0[2], e0[3], e1[0], e1[1], e1[2], e1[3]};
-        const T* v = (const T*)vals[i];
+        const T* v = vals[i];
         T r[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
@@ -711,7 +718,8 @@ __global__ __launch_bounds__(256) void quant_fp_wave_kernel(
           }
           r[j] = DT::from_f(y);
         }
-        ((u32x4*)o)[c] = *(const u32x4*)r;
+#pragma unroll
+        for (int h = 0; h < 8 / EPC; ++h) ((u32x4*)o)[(8 / EPC) * c + h] = ((const u32x4*)r)[h];
       }
     }
     for (int c = NCH + lane; c < WCH; c += 64) {
@@ -721,11 +729,137 @@ __global__ __launch_bounds__(256) void quant_fp_wave_kernel(
         const uint32_t k = salc[(c - NCH) * 8 + j];
         r[j] = k != 0xFFFFu ? row[k] : DT::from_f(0.f);
       }
-      ((u32x4*)o)[c] = *(const u32x4*)r;
+#pragma unroll
+      for (int h = 0; h < 8 / EPC; ++h) ((u32x4*)o)[(8 / EPC) * c + h] = ((const u32x4*)r)[h];
     }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");  // row / gmax reuse
   }
+}
+
+
+// ---------------------------------------------------------------- fp32 rows, any length
+// One wave per row, the row staged in LDS (K * 4 bytes per wave), the call's entry table
+// read from global memory (chunk-major planes of build_ent_kernel, L2-resident), two
+// gathers from LDS (statistics, then quantize) instead of values held in registers, so
+// rows of any length that fits LDS run at full occupancy of what fits.  OUT_FP writes the
+// packed-order x_hat + exact salient tail; INPLACE (the output quantizer, P == K) writes
+// the row back over itself, G_ZERO positions (salient columns) passing through.
+template <int MODE, bool INPLACE>
+__global__ __launch_bounds__(256) void quant_f32w_kernel(
+    float* __restrict__ x, int M, int K, int q_max, int nga, const u32x4* __restrict__ ent,
+    int P, const int32_t* __restrict__ nonsal, int Kn, const int32_t* __restrict__ sal,
+    int S, int S_pad, const uint32_t* __restrict__ cmax, float* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_f32w[];
+  const int NCH = P / 8;
+  const int W = INPLACE ? K : P + S_pad, WCH = W / 8;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nwave = blockDim.x >> 6;
+  const int wbytes = (int)round_up_dev(4 * K, 16) + (int)round_up_dev(12 * nga, 16);
+  float* row = (float*)(smem_f32w + wave * wbytes);
+  float2* scr = (float2*)(row + round_up_dev(K, 4));
+  uint32_t* gmax = (uint32_t*)(scr + nga);
+  float s_all = 0.f, r_all = 0.f;
+  if (MODE == MODE_TENSOR) {
+    float m = 0.f;
+    for (int i = lane; i < Kn; i += 64) m = fmaxf(m, __uint_as_float(cmax[nonsal[i]]));
+    m = wave_max(m);
+    s_all = group_scale<F32>(m, q_max);
+    r_all = 1.0f / s_all;
+  }
+  const int nch4 = K / 4;
+  for (int m = blockIdx.x * nwave + wave; m < M; m += gridDim.x * nwave) {
+    const u32x4* src = (const u32x4*)(x + (size_t)m * K);
+#pragma unroll 8
+    for (int c = lane; c < nch4; c += 64) ((u32x4*)row)[c] = src[c];
+    if (MODE == MODE_GROUP)
+      for (int g = lane; g < nga; g += 64) gmax[g] = 0u;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    float lmax = 0.f;
+    for (int c = lane; c < NCH; c += 64) {
+      const u32x4 e0 = ent[c], e1 = ent[NCH + c];
+      const uint32_t e[8] = {e0[0], e0[1], e0[2], e0[3], e1[0], e1[1], e1[2], e1[3]};
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const uint32_t g = e[j] >> 16;
+        if (g == G_ZERO) continue;
+        const float a = fabsf(row[e[j] & 0xFFFFu]);
+        if (MODE == MODE_GROUP) {
+          if (a > 0.f) atomicMax(&gmax[g], __float_as_uint(a));
+        } else {
+          lmax = fmaxf(lmax, a);
+        }
+      }
+    }
+    float s_row = s_all, r_row = r_all;
+    if (MODE == MODE_TOKEN) {
+      s_row = group_scale<F32>(wave_max(lmax), q_max);
+      r_row = 1.0f / s_row;
+    } else if (MODE == MODE_GROUP) {
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      for (int g = lane; g < nga; g += 64) {
+        const float sg = group_scale<F32>(__uint_as_float(gmax[g]), q_max);
+        scr[g] = make_float2(sg, 1.0f / sg);
+      }
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    }
+    float* o = (INPLACE ? x : out) + (size_t)m * W;
+    for (int c = lane; c < NCH; c += 64) {
+      const u32x4 e0 = ent[c], e1 = ent[NCH + c];
+      const uint32_t e[8] = {e0[0], e0[1], e0[2], e0[3], e1[0], e1[1], e1[2], e1[3]};
+      float r[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const uint32_t g = e[j] >> 16;
+        if (g == G_ZERO) {
+          r[j] = INPLACE ? row[8 * c + j] : 0.f;
+        } else {
+          const float2 sr = MODE == MODE_GROUP ? scr[g] : make_float2(s_row, r_row);
+          const float t = row[e[j] & 0xFFFFu];
+          r[j] = __builtin_copysignf(fast_code<F32>(t, sr.x, sr.y) * sr.x, t);
+        }
+      }
+      ((u32x4*)o)[2 * c] = ((const u32x4*)r)[0];
+      ((u32x4*)o)[2 * c + 1] = ((const u32x4*)r)[1];
+    }
+    if (!INPLACE) {
+      for (int c = NCH + lane; c < WCH; c += 64) {
+        float r[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int i = (c - NCH) * 8 + j;
+          r[j] = i < S ? row[sal[i]] : 0.f;
+        }
+        ((u32x4*)o)[2 * c] = ((const u32x4*)r)[0];
+        ((u32x4*)o)[2 * c + 1] = ((const u32x4*)r)[1];
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");  // row / gmax reuse
+  }
+}
+
+template <int MODE, bool INPLACE>
+static int quant_f32w_launch(void* x, int M, int K, int q_max, int nga, const uint32_t* ent,
+                             int P, const int32_t* nonsal, int Kn, const int32_t* sal, int S,
+                             int S_pad, const uint32_t* cmax, void* out, hipStream_t s) {
+  const size_t wb = (size_t)round_up(4L * K, 16) + (size_t)round_up(12L * nga, 16);
+  int nw = (int)((160 * 1024) / wb);
+  if (nw < 1) return SQMP_EUNSUPPORTED;
+  nw = nw > 4 ? 4 : nw;
+  const size_t lds = nw * wb;
+  SQMP_HIP_CHECK(hipFuncSetAttribute((const void*)quant_f32w_kernel<MODE, INPLACE>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  const int per_cu = (int)((160 * 1024) / lds);
+  int grid = 256 * (per_cu < 1 ? 1 : per_cu);
+  if (grid > cdiv(M, nw)) grid = cdiv(M, nw);
+  quant_f32w_kernel<MODE, INPLACE><<<dim3(grid), dim3(64 * nw), lds, s>>>(
+      (float*)x, M, K, q_max, nga, (const u32x4*)ent, P, nonsal, Kn, sal, S, S_pad, cmax,
+      (float*)out);
+  SQMP_LAUNCH_CHECK();
+  return SQMP_OK;
 }
 
 static size_t quant_fp_wave_lds_bytes(int K, int P, int nga, int S_pad, int esize) {
@@ -813,6 +947,42 @@ static int quant_dispatch(void* x, int M, int K, int amode, int q_max, int G, in
   const int mode = amode == SQMP_ACT_PER_TOKEN    ? MODE_TOKEN
                    : amode == SQMP_ACT_PER_TENSOR ? MODE_TENSOR
                                                   : MODE_GROUP;
+  if constexpr (DT::id == SQMP_F32) {
+    // fp32 rows longer than the register-staged wave kernel holds, and the in-place output
+    // quantizer: one wave per row from LDS (quant_f32w_kernel)
+    if (ent && K % 8 == 0 && P % 8 == 0 && (((uintptr_t)x) % 16 == 0) &&
+        ((out_kind == SQMP_OUT_FP && (K > 4096 || P > 4096) && ((uintptr_t)out) % 16 == 0) ||
+         out_kind == SQMP_OUT_INPLACE)) {
+#define SQMP_QF32(MODE, INP)                                                                  \
+  quant_f32w_launch<MODE, INP>(x, M, K, q_max, nga, ent, P, nonsal, Kn, sal, S, S_pad, cmax, out, s)
+      int st32;
+      if (out_kind == SQMP_OUT_INPLACE)
+        st32 = mode == MODE_TOKEN ? SQMP_QF32(MODE_TOKEN, true)
+             : mode == MODE_TENSOR ? SQMP_QF32(MODE_TENSOR, true) : SQMP_QF32(MODE_GROUP, true);
+      else
+        st32 = mode == MODE_TOKEN ? SQMP_QF32(MODE_TOKEN, false)
+             : mode == MODE_TENSOR ? SQMP_QF32(MODE_TENSOR, false) : SQMP_QF32(MODE_GROUP, false);
+#undef SQMP_QF32
+      if (st32 != SQMP_EUNSUPPORTED) return st32;
+    }
+    // fp32 rows on the wave kernel (RCH = 16-B row chunks = 2 VCH): K, P <= 4096
+    if (ent && out_kind == SQMP_OUT_FP && K % 8 == 0 && K <= 4096 && P <= 4096 &&
+        (((uintptr_t)x) % 16 == 0)) {
+      const size_t lds = quant_fp_wave_lds_bytes(K, P, nga, S_pad, sizeof(typename DT::T));
+      if (lds <= 160 * 1024) {
+        const bool sm = K <= 2048 && P <= 2048;
+#define SQMP_QW32(MODE)                                                                        \
+  (sm ? quant_fpw_launch<DT, MODE, 8, 4>(x, M, K, q_max, nga, ent, P, nonsal, Kn, sal, S, S_pad, \
+                                         cmax, out, lds, s)                                   \
+      : quant_fpw_launch<DT, MODE, 16, 8>(x, M, K, q_max, nga, ent, P, nonsal, Kn, sal, S,     \
+                                          S_pad, cmax, out, lds, s))
+        if (mode == MODE_TOKEN) return SQMP_QW32(MODE_TOKEN);
+        if (mode == MODE_TENSOR) return SQMP_QW32(MODE_TENSOR);
+        return SQMP_QW32(MODE_GROUP);
+#undef SQMP_QW32
+      }
+    }
+  }
   if constexpr (DT::id != SQMP_F32) {
   if (ent && out_kind == SQMP_OUT_FP && K % 8 == 0 && K <= 12288 && P <= 12288 &&
       (((uintptr_t)x) % 16 == 0)) {
@@ -1085,7 +1255,8 @@ static int quant_act_impl(void* x, int dtype, int M, int K, int amode, int n_bit
   // entry table (read by the wave kernel) and rank_by_col (read by the block kernels)
   const int mode_e = group ? MODE_GROUP : MODE_TOKEN;
   const int Pe = out_kind == SQMP_OUT_INPLACE ? K : Kp;
-  const bool need_ent = out_kind == SQMP_OUT_FP && Pe % 8 == 0;
+  const bool need_ent = (out_kind == SQMP_OUT_FP || (out_kind == SQMP_OUT_INPLACE && dtype == SQMP_F32)) &&
+                        Pe % 8 == 0;
   if (need_ent || sorted || use_lc) {
     build_ent_kernel<<<dim3(cdiv(Pe, 256)), dim3(256), 0, s>>>(
         amap, Pe, nonsal, Kn, sorted ? part : nullptr, rank_tiles(Kn), (int)k64, mode_e,

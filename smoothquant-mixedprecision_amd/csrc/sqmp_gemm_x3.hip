@@ -17,7 +17,8 @@
 //    three bf16 planes [3][Np][L].
 // Tile 128 x 128, K stage 32, 4 waves (2 x 2, 64 x 64 each, 16 x 16 output tiles),
 // 96 MFMAs per wave per stage; single-buffered LDS (48 KiB) with the next stage's global
-// loads in flight over the MFMAs, two workgroups per CU.
+// loads in flight over the MFMAs, two workgroups per CU (8 waves of 64 x 32 in one
+// workgroup when the grid has fewer than two tiles per CU).
 #include "sqmp_mfma.h"
 
 namespace sqmp {
@@ -51,8 +52,10 @@ __device__ inline void split3(float v, uint32_t& h, uint32_t& m, uint32_t& l) {
   l = bf16_bits(r - bf16_val(m));   // exact, and exact in bf16
 }
 
-template <bool COLMAX>
-__global__ __launch_bounds__(256, 2) void gemm_x3_kernel(
+// WN = waves along N: 2 -> 4 waves of 64 x 64 (two workgroups per CU), 4 -> 8 waves of
+// 64 x 32 (grids of fewer than two tiles per CU: two waves per SIMD from one workgroup)
+template <bool COLMAX, int WN>
+__global__ __launch_bounds__(128 * WN, 4 / WN) void gemm_x3_kernel(
     const float* __restrict__ A, const uint16_t* __restrict__ B3, const float* __restrict__ bias,
     float* __restrict__ Y, int M, int N, int L, int Np, int tiles_m, int tiles_n,
     uint32_t* __restrict__ colmax) {
@@ -60,32 +63,33 @@ __global__ __launch_bounds__(256, 2) void gemm_x3_kernel(
   int tm, tn;
   tile_coords(tiles_m, tiles_n, 8, tm, tn);
   const int m0 = tm * X3_BM, n0 = tn * X3_BN;
+  constexpr int NT = 128 * WN, CW = X3_BN / WN, J = CW / 16;
+  constexpr int LA = 1024 / NT, LB = 1536 / NT;  // 16-B staging chunks per thread
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = wave / WN, wn = wave % WN;
   const int r16 = lane & 15, q = lane >> 4;
   const int nkt = L / X3_BK;
   const size_t plane = (size_t)Np * L;
 
-  // staging: A 128 rows x 8 chunks of 4 fp32 (4 per thread); B 3 planes x 128 rows x 4
-  // chunks of 8 bf16 (6 per thread)
-  u32x4 ra[4], rb[6];
+  // staging: A 128 rows x 8 chunks of 4 fp32; B 3 planes x 128 rows x 4 chunks of 8 bf16
+  u32x4 ra[LA], rb[LB];
   auto load = [&](int kt) {
     const int k0 = kt * X3_BK;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int idx = tid + 256 * i, row = idx >> 3, c = idx & 7;
+    for (int i = 0; i < LA; ++i) {
+      const int idx = tid + NT * i, row = idx >> 3, c = idx & 7;
       ra[i] = *(const u32x4*)(A + (size_t)(m0 + row) * L + k0 + 4 * c);
     }
 #pragma unroll
-    for (int i = 0; i < 6; ++i) {
-      const int idx = tid + 256 * i, p = idx >> 9, row = (idx >> 2) & 127, c = idx & 3;
+    for (int i = 0; i < LB; ++i) {
+      const int idx = tid + NT * i, p = idx >> 9, row = (idx >> 2) & 127, c = idx & 3;
       rb[i] = *(const u32x4*)(B3 + p * plane + (size_t)(n0 + row) * L + k0 + 8 * c);
     }
   };
   auto store = [&]() {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int idx = tid + 256 * i, row = idx >> 3, c = idx & 7;
+    for (int i = 0; i < LA; ++i) {
+      const int idx = tid + NT * i, row = idx >> 3, c = idx & 7;
       uint32_t h[4], m[4], l[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) split3(__uint_as_float(ra[i][e]), h[e], m[e], l[e]);
@@ -95,27 +99,27 @@ __global__ __launch_bounds__(256, 2) void gemm_x3_kernel(
       *(uint2*)(lds + 2 * X3_PLANE + off) = uint2{l[0] | (l[1] << 16), l[2] | (l[3] << 16)};
     }
 #pragma unroll
-    for (int i = 0; i < 6; ++i) {
-      const int idx = tid + 256 * i, p = idx >> 9, row = (idx >> 2) & 127, c = idx & 3;
+    for (int i = 0; i < LB; ++i) {
+      const int idx = tid + NT * i, p = idx >> 9, row = (idx >> 2) & 127, c = idx & 3;
       *(u32x4*)(lds + (3 + p) * X3_PLANE + x3_off(row, c)) = rb[i];
     }
   };
 
-  f32x4 acc[4][4];
+  f32x4 acc[4][J];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < J; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   auto compute = [&]() {
     // B fragments (output columns) in the MFMA's A slot: the lane's 4 results are 4
     // consecutive columns of one row (16-B stores)
-    u32x4 bf[3][4];
+    u32x4 bf[3][J];
 #pragma unroll
     for (int p = 0; p < 3; ++p)
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-        bf[p][j] = *(const u32x4*)(lds + (3 + p) * X3_PLANE + x3_off(wn * 64 + 16 * j + r16, q));
+      for (int j = 0; j < J; ++j)
+        bf[p][j] = *(const u32x4*)(lds + (3 + p) * X3_PLANE + x3_off(wn * CW + 16 * j + r16, q));
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       u32x4 af[3];
@@ -123,7 +127,7 @@ __global__ __launch_bounds__(256, 2) void gemm_x3_kernel(
       for (int p = 0; p < 3; ++p)
         af[p] = *(const u32x4*)(lds + p * X3_PLANE + x3_off(wm * 64 + 16 * i + r16, q));
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
+      for (int j = 0; j < J; ++j) {
         // smallest terms first
         Mfma<BF16>::run(acc[i][j], bf[1][j], af[1]);
         Mfma<BF16>::run(acc[i][j], bf[2][j], af[0]);
@@ -144,10 +148,10 @@ __global__ __launch_bounds__(256, 2) void gemm_x3_kernel(
     __syncthreads();
   }
 
-  // epilogue: acc[i][j][r] = C[m = m0 + 64 wm + 16 i + r16][n = n0 + 64 wn + 16 j + 4 q + r]
+  // epilogue: acc[i][j][r] = C[m = m0 + 64 wm + 16 i + r16][n = n0 + CW wn + 16 j + 4 q + r]
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int nb = n0 + wn * 64 + 16 * j + 4 * q;
+  for (int j = 0; j < J; ++j) {
+    const int nb = n0 + wn * CW + 16 * j + 4 * q;
     float bv[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) bv[r] = bias && nb + r < N ? bias[nb + r] : 0.f;
@@ -226,12 +230,16 @@ extern "C" int sqmp_gemm_x3(const float* a, const void* b3, const float* bias, f
   if (M == 0) return SQMP_OK;
   const int Np = pad_n(N);
   const int tiles_m = cdiv(M, X3_BM), tiles_n = cdiv(N, X3_BN);
-  if (colmax)
-    gemm_x3_kernel<true><<<tiles_m * tiles_n, 256, 0, (hipStream_t)stream>>>(
-        a, (const uint16_t*)b3, bias, y, M, N, L, Np, tiles_m, tiles_n, colmax);
-  else
-    gemm_x3_kernel<false><<<tiles_m * tiles_n, 256, 0, (hipStream_t)stream>>>(
-        a, (const uint16_t*)b3, bias, y, M, N, L, Np, tiles_m, tiles_n, nullptr);
+  const bool small = (long)tiles_m * tiles_n < 2L * 256;
+#define SQMP_X3(CM, WN)                                                                  \
+  gemm_x3_kernel<CM, WN><<<tiles_m * tiles_n, 128 * WN, 0, (hipStream_t)stream>>>(       \
+      a, (const uint16_t*)b3, bias, y, M, N, L, Np, tiles_m, tiles_n, colmax)
+  if (colmax) {
+    if (small) SQMP_X3(true, 4); else SQMP_X3(true, 2);
+  } else {
+    if (small) SQMP_X3(false, 4); else SQMP_X3(false, 2);
+  }
+#undef SQMP_X3
   SQMP_LAUNCH_CHECK();
   return SQMP_OK;
 }

@@ -28,11 +28,19 @@ CASES = [
     (64, 4096, 64, "per_group_mean3std", "fp16", 0.05, 4),
     (96, 8192, 128, "per_group", "fp16", 0.05, 4),
     (2, 4096, 32, "per_group", "fp16", 0.05, 4),
+    # fp32 (OPT): register-staged wave kernel (K <= 4096) and the LDS wave kernel (longer)
+    (64, 2048, 128, "per_group", "fp32", 0.05, 4),
+    (65, 8192, 128, "per_group", "fp32", 0.05, 4),
+    (64, 8192, 64, "per_token", "fp32", 0.05, 4),
+    (33, 6144, 128, "per_tensor", "fp32", 0.10, 4),
+    (64, 4096, 128, "per_group_mean3std", "fp32", 0.05, 4),
 ]
 
 
 def _bits(a, dtn):
     a = np.asarray(a, np.float32)
+    if dtn == "fp32":
+        return a.view(np.uint32)
     if dtn == "fp16":
         return a.astype(np.float16).view(np.uint16)
     return (a.view(np.uint32) >> 16).astype(np.uint16)
@@ -142,3 +150,42 @@ def test_sorted_groups_tie_order(case):
         want[:, pw.Kp:pw.Kp + pw.S] = qx[:, sal]
     bad = np.argwhere(_bits(a, dtn) != _bits(want, dtn))
     assert len(bad) == 0, f"{len(bad)} of {a.size} differ; first {bad[:5].tolist()}"
+
+
+INPLACE_CASES = [
+    # M, K, G, act, dtype, salient_prop -- the in-place output quantizer (fake_quant.py:308-316)
+    (64, 2048, 128, "per_group", "fp32", 0.05),
+    (33, 8192, 128, "per_group", "fp32", 0.05),
+    (64, 2048, 128, "per_token", "fp32", 0.0),
+    (64, 2048, 64, "per_tensor", "fp32", 0.10),
+    (64, 2048, 128, "per_group", "fp16", 0.05),
+]
+
+
+@pytest.mark.parametrize("case", INPLACE_CASES,
+                         ids=[f"{c[0]}x{c[1]}-G{c[2]}-{c[3]}-{c[4]}-p{c[5]}" for c in INPLACE_CASES])
+def test_inplace_output_quant_bit_exact(case):
+    """y quantized in place over its non-salient columns, salient columns passing through
+    (the oracle's quantize_input on y), bit-exact."""
+    dev = _dev()
+    from smoothquant import ops
+    from smoothquant.fake_quant import W4A4Linear
+    M, K, G, act, dtn, p = case
+    dt = O.DT(dtn)
+    g = np.random.default_rng(K + M + 7)
+    y = g.standard_normal((M, K)).astype(np.float32)
+    y[:, g.permutation(K)[: max(1, K // 100)]] *= 30
+    y = dt.rnd(y)
+    imp = np.abs(y).mean(0).astype(np.float32)
+    lin = torch.nn.Linear(K, K, bias=False).to(dev, TORCH_DT[dtn])
+    q = W4A4Linear.from_float(lin, weight_quant="per_group", act_quant=act,
+                              importance=torch.from_numpy(imp), salient_prop=p,
+                              quant_bits=4, group_size=G)
+    pw = q.packed()
+    yt = torch.from_numpy(y).to(dev, TORCH_DT[dtn])
+    ops.fake_quant_inplace(yt, act, 4, G, pw.amap_fq, pw.nonsal, pw.S)
+    got = yt.float().cpu().numpy()
+    want = O.quantize_input(y, act, 4, G, O.select_salient(imp, p), dt)
+    bad = np.argwhere(_bits(got, dtn) != _bits(want, dtn))
+    assert len(bad) == 0, (f"{len(bad)} of {got.size} differ; first "
+                           f"{[(int(m), int(c), float(got[m, c]), float(want[m, c])) for m, c in bad[:5]]}")
