@@ -768,26 +768,53 @@ __global__ __launch_bounds__(256) void quant_f32w_kernel(
   }
   const int nch4 = K / 4;
   for (int m = blockIdx.x * nwave + wave; m < M; m += gridDim.x * nwave) {
+    // the whole row by LDS-DMA (1 KiB per wave instruction, all in flight at once: one
+    // memory latency per row instead of one per register batch); the tail chunks (K % 256)
+    // through registers
     const u32x4* src = (const u32x4*)(x + (size_t)m * K);
-#pragma unroll 8
-    for (int c = lane; c < nch4; c += 64) ((u32x4*)row)[c] = src[c];
+    const int nfull = nch4 & ~63;
+    for (int c = 0; c < nfull; c += 64)
+      __builtin_amdgcn_global_load_lds((const void*)(src + c + lane),
+                                       (__attribute__((address_space(3))) void*)(row + 4 * c),
+                                       16, 0, 0);
+    if (nfull + lane < nch4) ((u32x4*)row)[nfull + lane] = src[nfull + lane];
     if (MODE == MODE_GROUP)
       for (int g = lane; g < nga; g += 64) gmax[g] = 0u;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-    float lmax = 0.f;
-    for (int c = lane; c < NCH; c += 64) {
-      const u32x4 e0 = ent[c], e1 = ent[NCH + c];
-      const uint32_t e[8] = {e0[0], e0[1], e0[2], e0[3], e1[0], e1[1], e1[2], e1[3]};
+    // entry-table chunks are loaded EB per lane at once (global / L2 latency once per
+    // batch, not once per chunk)
+    constexpr int EB = 8;
+    u32x4 ea[EB], eb[EB];
+    auto load_ent = [&](int c0) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const uint32_t g = e[j] >> 16;
-        if (g == G_ZERO) continue;
-        const float a = fabsf(row[e[j] & 0xFFFFu]);
-        if (MODE == MODE_GROUP) {
-          if (a > 0.f) atomicMax(&gmax[g], __float_as_uint(a));
-        } else {
-          lmax = fmaxf(lmax, a);
+      for (int b = 0; b < EB; ++b) {
+        const int c = c0 + 64 * b;
+        if (c < NCH) {
+          ea[b] = ent[c];
+          eb[b] = ent[NCH + c];
+        }
+      }
+    };
+    float lmax = 0.f;
+    for (int c0 = lane; c0 < NCH; c0 += 64 * EB) {
+      load_ent(c0);
+#pragma unroll
+      for (int b = 0; b < EB; ++b) {
+        if (c0 + 64 * b >= NCH) break;
+        const uint32_t e[8] = {ea[b][0], ea[b][1], ea[b][2], ea[b][3],
+                               eb[b][0], eb[b][1], eb[b][2], eb[b][3]};
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const uint32_t g = e[j] >> 16;
+          if (g == G_ZERO) continue;
+          const float a = fabsf(row[e[j] & 0xFFFFu]);
+          if (MODE == MODE_GROUP) {
+            if (a > 0.f) atomicMax(&gmax[g], __float_as_uint(a));
+          } else {
+            lmax = fmaxf(lmax, a);
+          }
         }
       }
     }
@@ -806,23 +833,29 @@ __global__ __launch_bounds__(256) void quant_f32w_kernel(
       __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     }
     float* o = (INPLACE ? x : out) + (size_t)m * W;
-    for (int c = lane; c < NCH; c += 64) {
-      const u32x4 e0 = ent[c], e1 = ent[NCH + c];
-      const uint32_t e[8] = {e0[0], e0[1], e0[2], e0[3], e1[0], e1[1], e1[2], e1[3]};
-      float r[8];
+    for (int c0 = lane; c0 < NCH; c0 += 64 * EB) {
+      load_ent(c0);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const uint32_t g = e[j] >> 16;
-        if (g == G_ZERO) {
-          r[j] = INPLACE ? row[8 * c + j] : 0.f;
-        } else {
-          const float2 sr = MODE == MODE_GROUP ? scr[g] : make_float2(s_row, r_row);
-          const float t = row[e[j] & 0xFFFFu];
-          r[j] = __builtin_copysignf(fast_code<F32>(t, sr.x, sr.y) * sr.x, t);
+      for (int b = 0; b < EB; ++b) {
+        const int c = c0 + 64 * b;
+        if (c >= NCH) break;
+        const uint32_t e[8] = {ea[b][0], ea[b][1], ea[b][2], ea[b][3],
+                               eb[b][0], eb[b][1], eb[b][2], eb[b][3]};
+        float r[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const uint32_t g = e[j] >> 16;
+          if (g == G_ZERO) {
+            r[j] = INPLACE ? row[8 * c + j] : 0.f;
+          } else {
+            const float2 sr = MODE == MODE_GROUP ? scr[g] : make_float2(s_row, r_row);
+            const float t = row[e[j] & 0xFFFFu];
+            r[j] = __builtin_copysignf(fast_code<F32>(t, sr.x, sr.y) * sr.x, t);
+          }
         }
+        ((u32x4*)o)[2 * c] = ((const u32x4*)r)[0];
+        ((u32x4*)o)[2 * c + 1] = ((const u32x4*)r)[1];
       }
-      ((u32x4*)o)[2 * c] = ((const u32x4*)r)[0];
-      ((u32x4*)o)[2 * c + 1] = ((const u32x4*)r)[1];
     }
     if (!INPLACE) {
       for (int c = NCH + lane; c < WCH; c += 64) {
