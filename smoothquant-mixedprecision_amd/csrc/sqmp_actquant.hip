@@ -1273,15 +1273,18 @@ static int quant_act_impl(void* x, int dtype, int M, int K, int amode, int n_bit
   }
 
   // ---- general path (fp32, 8-bit int output, large rows, other group sizes)
-  if ((amode == SQMP_ACT_PER_TENSOR || amode == SQMP_ACT_PER_GROUP) && !stats_given) {
+  // SQMP_QA_REUSE_STATS: the rank partials of the previous call on this workspace (a
+  // sibling layer on the same input, same K / Kp / salient set) are still in place
+  const bool reuse_part = sorted && (flags & SQMP_QA_REUSE_STATS) != 0;
+  if ((amode == SQMP_ACT_PER_TENSOR || amode == SQMP_ACT_PER_GROUP) && !stats_given && !reuse_part) {
     SQMP_HIP_CHECK(hipMemsetAsync(cmax, 0, sizeof(uint32_t) * k64, s));
     st = launch_colmax(x, dtype, M, K, cmax, s, false);
     if (st) return st;
-  } else if (amode == SQMP_ACT_PER_GROUP_MEAN3STD) {
+  } else if (amode == SQMP_ACT_PER_GROUP_MEAN3STD && !reuse_part) {
     st = launch_colkey_mean3std(x, dtype, M, K, sums, cmax, s, clean);
     if (st) return st;
   }
-  if (sorted) {
+  if (sorted && !reuse_part) {
     st = launch_rank_partial(cmax, nonsal, Kn, (int)k64, part, s);
     if (st) return st;
   }

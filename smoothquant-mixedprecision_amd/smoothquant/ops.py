@@ -231,8 +231,10 @@ def _ws_bytes(M: int, K: int, Kp: int) -> int:
     return n
 
 
-def _act_ws(device, stream_ptr: int, K: int, Kp: int, nbytes: int):
-    key = (device.index, stream_ptr, K, Kp)
+def _act_ws(device, stream_ptr: int, K: int, Kp: int, nbytes: int, tag: str = "in"):
+    # tag "out": the in-place output quantizer has workspaces of its own, so quantizing a
+    # layer's output (OPT q/k/v) leaves the input statistics for its sibling layers intact
+    key = (device.index, stream_ptr, K, Kp, tag)
     e = _WS.get(key)
     if e is None or e["buf"].numel() < nbytes:
         e = {"buf": torch.zeros(nbytes, dtype=torch.uint8, device=device), "stats": None}
@@ -277,7 +279,7 @@ def quant_act_fp(x2: torch.Tensor, pw: PackedWeight, act_quant: str, n_bits: int
                                    _lib.OUT_FP, _p(a), None, None, _p(e["buf"]),
                                    e["buf"].numel(), ctypes.c_void_p(stream))
     if status != _lib.SQMP_OK:
-        _WS.pop((x2.device.index, stream, K, pw.Kp), None)  # it may be left dirty
+        _WS.pop((x2.device.index, stream, K, pw.Kp, "in"), None)  # it may be left dirty
         check(status, "quant_act")
     if skey is not None:
         e["stats"] = (weakref.ref(stats_of if stats_of is not None else x2), skey,
@@ -345,7 +347,7 @@ def quant_act_c4(x2: torch.Tensor, pw: PackedWeight, act_quant: str, n_bits: int
                                    pw.N, pw.Gw, pw.ngw, _p(wp), _p(e["buf"]), e["buf"].numel(),
                                    ctypes.c_void_p(stream))
     if status != _lib.SQMP_OK:
-        _WS.pop((dev.index, stream, K, pw.Kp), None)
+        _WS.pop((dev.index, stream, K, pw.Kp, "in"), None)
         check(status, "quant_act_c4")
     if act_quant in _SORTED:
         e["stats"] = (weakref.ref(src), skey, pw.codes.data_ptr())
@@ -386,7 +388,7 @@ def out_quant_workspace(M: int, C: int, device):
     stream (its first C words: the column-maximum region sqmp_gemm_fq_colmax fills)."""
     nb = _ws_bytes(M, C, C)
     stream = torch.cuda.current_stream(device).cuda_stream
-    return _act_ws(device, stream, C, C, nb)
+    return _act_ws(device, stream, C, C, nb, "out")
 
 
 def fake_quant_inplace(t2: torch.Tensor, act_quant: str, n_bits: int, group_size: int,
@@ -400,14 +402,14 @@ def fake_quant_inplace(t2: torch.Tensor, act_quant: str, n_bits: int, group_size
     lib = load()
     nb = lib.sqmp_act_workspace_bytes(M, C, C)
     stream = torch.cuda.current_stream(t2.device).cuda_stream
-    e = _act_ws(t2.device, stream, C, C, nb)
+    e = _act_ws(t2.device, stream, C, C, nb, "out")
     flags = _lib.QA_CLEAN_WS | (_lib.QA_STATS_GIVEN if stats_given else 0)
     status = lib.sqmp_quant_act_v2(_p(t2), _dtype_code(t2.dtype), M, C, ACT_MODES[act_quant],
                                    n_bits, group_size, _p(amap_fq), C, _p(nonsal), None, S, 0,
                                    None, flags, _lib.OUT_INPLACE, None, None, None,
                                    _p(e["buf"]), e["buf"].numel(), ctypes.c_void_p(stream))
     if status != _lib.SQMP_OK:
-        _WS.pop((t2.device.index, stream, C, C), None)
+        _WS.pop((t2.device.index, stream, C, C, "out"), None)
         check(status, "fake_quant")
     e["stats"] = None  # the sorted-column list now describes t2, not a layer input
     # the kernel wrote t2 through a raw pointer: bump its version counter so statistics
@@ -583,7 +585,7 @@ def quant_act_f8(x2: torch.Tensor, pw: PackedWeight, act_quant: str, n_bits: int
                                    _p(a8), _p(sa), _p(xs), _p(e["buf"]), e["buf"].numel(),
                                    ctypes.c_void_p(stream))
     if status != _lib.SQMP_OK:
-        _WS.pop((x2.device.index, stream, K, pw.Kp), None)
+        _WS.pop((x2.device.index, stream, K, pw.Kp, "in"), None)
         check(status, "quant_act")
     return a8, sa, xs
 

@@ -83,24 +83,32 @@ def test_quant_act_operand_bit_exact(case):
                            f"{[(int(m), int(c), float(a[m, c]), float(want[m, c])) for m, c in bad[:5]]}")
 
 
-@pytest.mark.parametrize("act", ["per_group", "per_group_mean3std"])
-def test_sibling_layers_share_statistics(act):
+@pytest.mark.parametrize("act,dtn,oq", [("per_group", "fp16", False),
+                                         ("per_group_mean3std", "fp16", False),
+                                         ("per_group", "fp32", False),
+                                         ("per_group", "fp32", True),
+                                         ("per_group", "fp16", True)])
+def test_sibling_layers_share_statistics(act, dtn, oq):
     """q/k/v-style siblings (same input object, same salient set) reuse the first layer's
-    column statistics and rank: outputs are bit-identical to independent computation, and
-    an in-place change of the input between calls invalidates the reuse."""
+    column statistics and rank: outputs are bit-identical to independent computation (also
+    with the OPT pattern of each sibling quantizing its output in between, on workspaces of
+    its own), and an in-place change of the input between calls invalidates the reuse."""
     dev = _dev()
     from smoothquant.fake_quant import W4A4Linear
+    dt = TORCH_DT[dtn]
     g = torch.Generator(device=dev).manual_seed(3)
     K, M = 1024, 96
-    x = torch.randn(M, K, generator=g, device=dev).half()
+    N = K if oq else 320
+    x = torch.randn(M, K, generator=g, device=dev).to(dt)
     imp = x.float().abs().mean(0).cpu()
     layers = []
     for i in range(3):
-        lin = torch.nn.Linear(K, 320, bias=True).to(dev, torch.float16)
+        lin = torch.nn.Linear(K, N, bias=True).to(dev, dt)
         with torch.no_grad():
-            lin.weight.copy_(torch.randn(320, K, generator=g, device=dev) * 0.02)
+            lin.weight.copy_(torch.randn(N, K, generator=g, device=dev) * 0.02)
         layers.append(W4A4Linear.from_float(lin, weight_quant="per_group", act_quant=act,
-                                            importance=imp, salient_prop=0.05, group_size=64))
+                                            quantize_output=oq, importance=imp,
+                                            salient_prop=0.05, group_size=64))
     shared = [q(x) for q in layers]
     alone = [q(x.clone()) for q in layers]
     for a, b in zip(shared, alone):
