@@ -312,6 +312,25 @@ int sqmp_split3_bf16(const float* src, int R, int L, int ldr, void* dst, void* s
 int sqmp_gemm_x3(const float* a, const void* b3, const float* bias, float* y, int M, int N,
                  int L, uint32_t* colmax, void* stream);
 
+/* The fp32 faithful GEMM on the f16 MFMA (the default for fp32 layers): every row of A and
+ * of W is scaled by a power of two (exact) so that its maximum lies in [2^13, 2^14), each
+ * scaled value v is split as v = h + l + r with h = f16(v), l = f16(v - h) (|r| <= 2^-22 |v|,
+ * plus the f16 subnormal floor 2^-25), and y[m][n] = 2^-(aexp[m] + bexp[n]) (al.wh + ah.wl +
+ * ah.wh) + bias with fp32 accumulation: an error below 2^-21 of sum_k |a_k w_k| per output,
+ * under the fp32 accumulation error of the GEMM itself, at 3 f16 MFMAs per product.
+ * sqmp_split2_f16: src fp32 [R][L] -> dst f16 [2][ldr][L] (h, l of the scaled rows) and
+ * rexp int32 [ldr] (rows >= R: zero, exponent 0); once per layer (ldr = Np).
+ * sqmp_row_exp: rexp[r] = the scaling exponent of row r of src fp32 [R][L] (per forward, A).
+ * sqmp_gemm_h2: a / aexp: the SQMP_OUT_FP operand (fp32, roundup(M, 256) rows allocated) and
+ * its row exponents; b2 / bexp: sqmp_split2_f16 of the packed-order W_hat + salient slice.
+ * L % 32 == 0; colmax as sqmp_gemm_fq_colmax. */
+int sqmp_split2_f16(const float* src, int R, int L, int ldr, void* dst, int* rexp,
+                    void* stream);
+int sqmp_row_exp(const float* src, int R, int L, int* rexp, void* stream);
+int sqmp_gemm_h2(const float* a, const int* aexp, const void* b2, const int* bexp,
+                 const float* bias, float* y, int M, int N, int L, uint32_t* colmax,
+                 void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -27,7 +27,6 @@ namespace {
 
 constexpr int X3_BM = 128, X3_BN = 128, X3_BK = 32;
 constexpr int X3_PLANE = X3_BM * X3_BK * 2;  // one bf16 plane of a 128-row tile: 8 KiB
-constexpr int X3_LDS = 6 * X3_PLANE;         // A planes h, m, l then B planes h, m, l
 
 // 64-B rows (four 16-B chunks).  ds_read_b128 serves lanes in groups
 // {0-3,12-15,20-27}, {4-11,16-19,28-31} (+32): lane (r16, q) reads chunk q of row r16; the
@@ -54,25 +53,52 @@ __device__ inline void split3(float v, uint32_t& h, uint32_t& m, uint32_t& l) {
 
 // WN = waves along N: 2 -> 4 waves of 64 x 64 (two workgroups per CU), 4 -> 8 waves of
 // 64 x 32 (grids of fewer than two tiles per CU: two waves per SIMD from one workgroup)
-template <bool COLMAX, int WN>
+// H: the two-piece fp16 form (see sqmp_gemm_h2 below): A rows and B rows scaled by 2^aexp[m]
+// / 2^bexp[n] into [2^13, 2^14) at their maximum, v' = h + l with h = f16(v'),
+// l = f16(v' - h), three products (al.bh + ah.bl + ah.bh) on v_mfma_f32_16x16x32_f16, the
+// scales undone in the epilogue.
+// v (|v| < 2^14) -> (h, l) f16 bit patterns, h = f16(v), l = f16(v - h): v - h is exact in
+// fp32 and l keeps its 11 leading bits, so |v - h - l| <= 2^-22 |v| (+ the f16 subnormal
+// floor 2^-25)
+__device__ inline void split2h(float v, uint32_t& h, uint32_t& l) {
+  const _Float16 hh = (_Float16)v;
+  const _Float16 ll = (_Float16)(v - (float)hh);
+  h = (uint32_t)(*(const uint16_t*)&hh);
+  l = (uint32_t)(*(const uint16_t*)&ll);
+}
+
+// the exponent e with max |row| * 2^e in [2^13, 2^14) (0 for an all-zero row)
+__device__ inline int row_exp_of(float mx) {
+  // floor(log2 mx) from the exponent field (a subnormal mx counts as 2^-127: the scaled
+  // maximum then stays below 2^14 all the same)
+  return mx > 0.f ? 13 - ((int)((__float_as_uint(mx) >> 23) & 0xFFu) - 127) : 0;
+}
+
+template <bool COLMAX, int WN, bool H = false>
 __global__ __launch_bounds__(128 * WN, 4 / WN) void gemm_x3_kernel(
     const float* __restrict__ A, const uint16_t* __restrict__ B3, const float* __restrict__ bias,
     float* __restrict__ Y, int M, int N, int L, int Np, int tiles_m, int tiles_n,
-    uint32_t* __restrict__ colmax) {
-  __shared__ __attribute__((aligned(16))) unsigned char lds[X3_LDS];
+    uint32_t* __restrict__ colmax, const int* __restrict__ aexp, const int* __restrict__ bexp) {
+  constexpr int NPL = H ? 2 : 3;  // pieces per operand
+  __shared__ __attribute__((aligned(16))) unsigned char lds[2 * NPL * X3_PLANE];
   int tm, tn;
   tile_coords(tiles_m, tiles_n, 8, tm, tn);
   const int m0 = tm * X3_BM, n0 = tn * X3_BN;
   constexpr int NT = 128 * WN, CW = X3_BN / WN, J = CW / 16;
-  constexpr int LA = 1024 / NT, LB = 1536 / NT;  // 16-B staging chunks per thread
+  constexpr int LA = 1024 / NT, LB = 512 * NPL / NT;  // 16-B staging chunks per thread
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
   const int r16 = lane & 15, q = lane >> 4;
   const int nkt = L / X3_BK;
   const size_t plane = (size_t)Np * L;
 
-  // staging: A 128 rows x 8 chunks of 4 fp32; B 3 planes x 128 rows x 4 chunks of 8 bf16
+  // staging: A 128 rows x 8 chunks of 4 fp32; B NPL planes x 128 rows x 4 chunks of 8 x 16 bit
   u32x4 ra[LA], rb[LB];
+  int ae[LA];  // H: the row exponents of this thread's A chunks (fixed over the K loop)
+  if (H) {
+#pragma unroll
+    for (int i = 0; i < LA; ++i) ae[i] = aexp[min(m0 + ((tid + NT * i) >> 3), M - 1)];
+  }
   auto load = [&](int kt) {
     const int k0 = kt * X3_BK;
 #pragma unroll
@@ -90,18 +116,26 @@ __global__ __launch_bounds__(128 * WN, 4 / WN) void gemm_x3_kernel(
 #pragma unroll
     for (int i = 0; i < LA; ++i) {
       const int idx = tid + NT * i, row = idx >> 3, c = idx & 7;
-      uint32_t h[4], m[4], l[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) split3(__uint_as_float(ra[i][e]), h[e], m[e], l[e]);
       const int off = x3_off(row, c >> 1) + (c & 1) * 8;
-      *(uint2*)(lds + off) = uint2{h[0] | (h[1] << 16), h[2] | (h[3] << 16)};
-      *(uint2*)(lds + X3_PLANE + off) = uint2{m[0] | (m[1] << 16), m[2] | (m[3] << 16)};
-      *(uint2*)(lds + 2 * X3_PLANE + off) = uint2{l[0] | (l[1] << 16), l[2] | (l[3] << 16)};
+      if (H) {
+        uint32_t h[4], l[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) split2h(__builtin_ldexpf(__uint_as_float(ra[i][e]), ae[i]), h[e], l[e]);
+        *(uint2*)(lds + off) = uint2{h[0] | (h[1] << 16), h[2] | (h[3] << 16)};
+        *(uint2*)(lds + X3_PLANE + off) = uint2{l[0] | (l[1] << 16), l[2] | (l[3] << 16)};
+      } else {
+        uint32_t h[4], m[4], l[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) split3(__uint_as_float(ra[i][e]), h[e], m[e], l[e]);
+        *(uint2*)(lds + off) = uint2{h[0] | (h[1] << 16), h[2] | (h[3] << 16)};
+        *(uint2*)(lds + X3_PLANE + off) = uint2{m[0] | (m[1] << 16), m[2] | (m[3] << 16)};
+        *(uint2*)(lds + 2 * X3_PLANE + off) = uint2{l[0] | (l[1] << 16), l[2] | (l[3] << 16)};
+      }
     }
 #pragma unroll
     for (int i = 0; i < LB; ++i) {
       const int idx = tid + NT * i, p = idx >> 9, row = (idx >> 2) & 127, c = idx & 3;
-      *(u32x4*)(lds + (3 + p) * X3_PLANE + x3_off(row, c)) = rb[i];
+      *(u32x4*)(lds + (NPL + p) * X3_PLANE + x3_off(row, c)) = rb[i];
     }
   };
 
@@ -114,27 +148,33 @@ __global__ __launch_bounds__(128 * WN, 4 / WN) void gemm_x3_kernel(
   auto compute = [&]() {
     // B fragments (output columns) in the MFMA's A slot: the lane's 4 results are 4
     // consecutive columns of one row (16-B stores)
-    u32x4 bf[3][J];
+    u32x4 bf[NPL][J];
 #pragma unroll
-    for (int p = 0; p < 3; ++p)
+    for (int p = 0; p < NPL; ++p)
 #pragma unroll
       for (int j = 0; j < J; ++j)
-        bf[p][j] = *(const u32x4*)(lds + (3 + p) * X3_PLANE + x3_off(wn * CW + 16 * j + r16, q));
+        bf[p][j] = *(const u32x4*)(lds + (NPL + p) * X3_PLANE + x3_off(wn * CW + 16 * j + r16, q));
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      u32x4 af[3];
+      u32x4 af[NPL];
 #pragma unroll
-      for (int p = 0; p < 3; ++p)
+      for (int p = 0; p < NPL; ++p)
         af[p] = *(const u32x4*)(lds + p * X3_PLANE + x3_off(wm * 64 + 16 * i + r16, q));
 #pragma unroll
       for (int j = 0; j < J; ++j) {
         // smallest terms first
-        Mfma<BF16>::run(acc[i][j], bf[1][j], af[1]);
-        Mfma<BF16>::run(acc[i][j], bf[2][j], af[0]);
-        Mfma<BF16>::run(acc[i][j], bf[0][j], af[2]);
-        Mfma<BF16>::run(acc[i][j], bf[1][j], af[0]);
-        Mfma<BF16>::run(acc[i][j], bf[0][j], af[1]);
-        Mfma<BF16>::run(acc[i][j], bf[0][j], af[0]);
+        if (H) {
+          Mfma<F16>::run(acc[i][j], bf[0][j], af[1]);
+          Mfma<F16>::run(acc[i][j], bf[1][j], af[0]);
+          Mfma<F16>::run(acc[i][j], bf[0][j], af[0]);
+        } else {
+          Mfma<BF16>::run(acc[i][j], bf[1][j], af[1]);
+          Mfma<BF16>::run(acc[i][j], bf[2][j], af[0]);
+          Mfma<BF16>::run(acc[i][j], bf[0][j], af[2]);
+          Mfma<BF16>::run(acc[i][j], bf[1][j], af[0]);
+          Mfma<BF16>::run(acc[i][j], bf[0][j], af[1]);
+          Mfma<BF16>::run(acc[i][j], bf[0][j], af[0]);
+        }
       }
     }
   };
@@ -153,15 +193,21 @@ __global__ __launch_bounds__(128 * WN, 4 / WN) void gemm_x3_kernel(
   for (int j = 0; j < J; ++j) {
     const int nb = n0 + wn * CW + 16 * j + 4 * q;
     float bv[4];
+    int be[4] = {0, 0, 0, 0};
 #pragma unroll
-    for (int r = 0; r < 4; ++r) bv[r] = bias && nb + r < N ? bias[nb + r] : 0.f;
+    for (int r = 0; r < 4; ++r) {
+      bv[r] = bias && nb + r < N ? bias[nb + r] : 0.f;
+      if (H) be[r] = bexp[nb + r];  // [Np]
+    }
     float cm[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int gm = m0 + wm * 64 + 16 * i + r16;
+      const int aei = H ? aexp[min(gm, M - 1)] : 0;
       f32x4 v;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r] + bv[r];
+      for (int r = 0; r < 4; ++r)
+        v[r] = (H ? __builtin_ldexpf(acc[i][j][r], -(aei + be[r])) : acc[i][j][r]) + bv[r];
       if (gm < M) {
         if (nb + 4 <= N && (N & 3) == 0) {
           *(f32x4*)(Y + (size_t)gm * N + nb) = v;
@@ -206,11 +252,92 @@ __global__ void split3_kernel(const float* __restrict__ src, int R, int L, int l
   }
 }
 
+// one wave per row: exp[r] = row_exp_of(max_c |src[r][c]|)
+__global__ __launch_bounds__(256) void row_exp_kernel(const float* __restrict__ src, int R, int L,
+                                                      int* __restrict__ exp_out) {
+  const int lane = threadIdx.x & 63;
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= R) return;
+  const float* row = src + (size_t)r * L;
+  float mx = 0.f;
+  if ((L & 3) == 0) {
+    for (int c = lane; c < L / 4; c += 64) {
+      const f32x4 v = ((const f32x4*)row)[c];
+      mx = fmaxf(mx, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
+    }
+  } else {
+    for (int c = lane; c < L; c += 64) mx = fmaxf(mx, fabsf(row[c]));
+  }
+  mx = wave_max(mx);
+  if (lane == 0) exp_out[r] = row_exp_of(mx);
+}
+
+// [R][L] fp32 -> two f16 planes [2][ldr][L] of the row-scaled values + exp[ldr] (rows >= R
+// zero, exponent 0); one block per row
+__global__ __launch_bounds__(256) void split2h_kernel(const float* __restrict__ src, int R, int L,
+                                                      int ldr, uint16_t* __restrict__ dst,
+                                                      int* __restrict__ exp_out) {
+  __shared__ float red[16];
+  const int r = blockIdx.x;
+  const float* row = src + (size_t)r * L;
+  float mx = 0.f;
+  if (r < R)
+    for (int c = threadIdx.x; c < L; c += 256) mx = fmaxf(mx, fabsf(row[c]));
+  mx = block_max(mx, red);
+  const int e = row_exp_of(mx);
+  if (threadIdx.x == 0) exp_out[r] = e;
+  const size_t n = (size_t)ldr * L;
+  for (int c = threadIdx.x; c < L; c += 256) {
+    uint32_t h, l;
+    split2h(r < R ? __builtin_ldexpf(row[c], e) : 0.f, h, l);
+    dst[(size_t)r * L + c] = (uint16_t)h;
+    dst[n + (size_t)r * L + c] = (uint16_t)l;
+  }
+}
+
 }  // namespace
 
 }  // namespace sqmp
 
 using namespace sqmp;
+
+extern "C" int sqmp_split2_f16(const float* src, int R, int L, int ldr, void* dst, int* rexp,
+                               void* stream) {
+  if (!src || !dst || !rexp || R <= 0 || L <= 0 || ldr < R) return SQMP_EINVAL;
+  split2h_kernel<<<ldr, 256, 0, (hipStream_t)stream>>>(src, R, L, ldr, (uint16_t*)dst, rexp);
+  SQMP_LAUNCH_CHECK();
+  return SQMP_OK;
+}
+
+extern "C" int sqmp_row_exp(const float* src, int R, int L, int* rexp, void* stream) {
+  if (!src || !rexp || R < 0 || L <= 0) return SQMP_EINVAL;
+  if (R == 0) return SQMP_OK;
+  row_exp_kernel<<<cdiv(R, 4), 256, 0, (hipStream_t)stream>>>(src, R, L, rexp);
+  SQMP_LAUNCH_CHECK();
+  return SQMP_OK;
+}
+
+extern "C" int sqmp_gemm_h2(const float* a, const int* aexp, const void* b2, const int* bexp,
+                            const float* bias, float* y, int M, int N, int L, uint32_t* colmax,
+                            void* stream) {
+  if (!a || !aexp || !b2 || !bexp || !y || M < 0 || N <= 0 || L <= 0) return SQMP_EINVAL;
+  if (L % X3_BK != 0) return SQMP_EINVAL;
+  if (M == 0) return SQMP_OK;
+  const int Np = pad_n(N);
+  const int tiles_m = cdiv(M, X3_BM), tiles_n = cdiv(N, X3_BN);
+  const bool small = (long)tiles_m * tiles_n < 2L * 256;
+#define SQMP_H2(CM, WN)                                                                  \
+  gemm_x3_kernel<CM, WN, true><<<tiles_m * tiles_n, 128 * WN, 0, (hipStream_t)stream>>>( \
+      a, (const uint16_t*)b2, bias, y, M, N, L, Np, tiles_m, tiles_n, colmax, aexp, bexp)
+  if (colmax) {
+    if (small) SQMP_H2(true, 4); else SQMP_H2(true, 2);
+  } else {
+    if (small) SQMP_H2(false, 4); else SQMP_H2(false, 2);
+  }
+#undef SQMP_H2
+  SQMP_LAUNCH_CHECK();
+  return SQMP_OK;
+}
 
 extern "C" int sqmp_split3_bf16(const float* src, int R, int L, int ldr, void* dst,
                                 void* stream) {
@@ -233,7 +360,7 @@ extern "C" int sqmp_gemm_x3(const float* a, const void* b3, const float* bias, f
   const bool small = (long)tiles_m * tiles_n < 2L * 256;
 #define SQMP_X3(CM, WN)                                                                  \
   gemm_x3_kernel<CM, WN><<<tiles_m * tiles_n, 128 * WN, 0, (hipStream_t)stream>>>(       \
-      a, (const uint16_t*)b3, bias, y, M, N, L, Np, tiles_m, tiles_n, colmax)
+      a, (const uint16_t*)b3, bias, y, M, N, L, Np, tiles_m, tiles_n, colmax, nullptr, nullptr)
   if (colmax) {
     if (small) SQMP_X3(true, 4); else SQMP_X3(true, 2);
   } else {

@@ -64,6 +64,9 @@ SIGNATURES = {
                            _vp]),
     "sqmp_split3_bf16": (_i, [_vp, _i, _i, _i, _vp, _vp]),
     "sqmp_gemm_x3": (_i, [_vp, _vp, _vp, _vp, _i, _i, _i, _vp, _vp]),
+    "sqmp_split2_f16": (_i, [_vp, _i, _i, _i, _vp, _vp, _vp]),
+    "sqmp_row_exp": (_i, [_vp, _i, _i, _vp, _vp]),
+    "sqmp_gemm_h2": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _vp, _vp]),
 }
 
 _lock = threading.Lock()

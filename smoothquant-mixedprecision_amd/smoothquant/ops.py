@@ -94,6 +94,7 @@ class PackedWeight:
     w6: Optional[torch.Tensor] = field(default=None)     # uint8 [Np, Kp*3/4] e2m3 (f6 GEMM)
     fq7: Optional[tuple] = field(default=None)           # (codes_t, scale_t, sal_t, J) of gemm_fq7
     x3: Optional[torch.Tensor] = field(default=None)     # bf16 [3, Np, Kp + S_pad] (gemm_x3)
+    h2: Optional[tuple] = field(default=None)            # (f16 [2, Np, L], int32 [Np]) (gemm_h2)
 
     @property
     def gemm_operand(self):
@@ -462,25 +463,62 @@ def gemm_fq7(a: torch.Tensor, pw: PackedWeight, bias: Optional[torch.Tensor],
     return y
 
 
-# Whether fp32 layers run the faithful GEMM on the bf16 MFMA (sqmp_gemm_x3: exact
-# three-way bf16 splits, six piece products) instead of the f32 MFMA (1/16 of the rate).
-X3_AUTO = os.environ.get("SQMP_X3", "1") == "1"
+# The faithful GEMM of fp32 layers: "h2" (default) -- row-scaled two-piece fp16 splits on the
+# f16 MFMA (sqmp_gemm_h2, 3 MFMAs per product); "x3" -- exact three-piece bf16 splits on the
+# bf16 MFMA (sqmp_gemm_x3, 6 MFMAs); "f32" -- the f32 MFMA (1/16 of the bf16 rate).
+F32_GEMM = os.environ.get("SQMP_F32_GEMM", "h2")
+
+
+def _w_full(pw: PackedWeight) -> torch.Tensor:
+    """fp32 [N, Kp + S_pad]: the packed-order W_hat + exact salient slice (the GEMM's B)."""
+    w = pw.codes[:pw.N] if pw.n_bits == 0 and pw.dense is None else (
+        pw.dense if pw.dense is not None else dequant_weight_packed(pw))
+    full = torch.cat([w, pw.wsal], dim=1) if pw.S_pad else w
+    return full.contiguous()
 
 
 def x3_operand(pw: PackedWeight) -> torch.Tensor:
     """bf16 planes [3, Np, Kp + S_pad] of the packed-order W_hat + exact salient slice
     (sqmp_split3_bf16), built once per packed fp32 weight."""
     if pw.x3 is None:
-        w = pw.codes[:pw.N] if pw.n_bits == 0 and pw.dense is None else (
-            pw.dense if pw.dense is not None else dequant_weight_packed(pw))
-        full = torch.cat([w, pw.wsal], dim=1) if pw.S_pad else w
-        full = full.contiguous()
+        full = _w_full(pw)
         Np, L = pad_n(pw.N), pw.Kp + pw.S_pad
         planes = torch.empty((3, Np, L), dtype=torch.bfloat16, device=full.device)
         check(load().sqmp_split3_bf16(_p(full), pw.N, L, Np, _p(planes), _stream(full)),
               "split3_bf16")
         pw.x3 = planes
     return pw.x3
+
+
+def h2_operand(pw: PackedWeight):
+    """(f16 planes [2, Np, L], int32 row exponents [Np]) of the row-scaled packed-order
+    W_hat + salient slice (sqmp_split2_f16), built once per packed fp32 weight."""
+    if pw.h2 is None:
+        full = _w_full(pw)
+        Np, L = pad_n(pw.N), pw.Kp + pw.S_pad
+        planes = torch.empty((2, Np, L), dtype=torch.float16, device=full.device)
+        bexp = torch.empty(Np, dtype=torch.int32, device=full.device)
+        check(load().sqmp_split2_f16(_p(full), pw.N, L, Np, _p(planes), _p(bexp), _stream(full)),
+              "split2_f16")
+        pw.h2 = (planes, bexp)
+    return pw.h2
+
+
+def gemm_h2(a: torch.Tensor, pw: PackedWeight, bias: Optional[torch.Tensor],
+            colmax: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """gemm_fq for fp32 layers on the f16 MFMA (include/sqmp_w4a4.h sqmp_gemm_h2)."""
+    M = a.shape[0]
+    L = pw.Kp + pw.S_pad
+    if a.dtype != torch.float32 or a.shape[1] != L or a.stride(0) != L:
+        raise ValueError("gemm_h2: A must be fp32 [M, Kp + S_pad] with row stride Kp + S_pad")
+    planes, bexp = h2_operand(pw)
+    aexp = torch.empty(max(M, 1), dtype=torch.int32, device=a.device)
+    lib = load()
+    check(lib.sqmp_row_exp(_p(a), M, L, _p(aexp), _stream(a)), "row_exp")
+    y = torch.empty((M, pw.N), dtype=torch.float32, device=a.device)
+    check(lib.sqmp_gemm_h2(_p(a), _p(aexp), _p(planes), _p(bexp), _p(bias), _p(y), M, pw.N, L,
+                           _p(colmax) if colmax is not None else None, _stream(a)), "gemm_h2")
+    return y
 
 
 def gemm_x3(a: torch.Tensor, pw: PackedWeight, bias: Optional[torch.Tensor],
@@ -504,7 +542,9 @@ def gemm_fq(a: torch.Tensor, pw: PackedWeight, bias: Optional[torch.Tensor],
     epilogue max-reduces bits(|y|) per column into (fused output-quant statistics)."""
     if FQ7_AUTO and fq7_eligible(pw):
         return gemm_fq7(a, pw, bias, colmax)
-    if X3_AUTO and pw.dtype == torch.float32:
+    if pw.dtype == torch.float32 and F32_GEMM == "h2":
+        return gemm_h2(a, pw, bias, colmax)
+    if pw.dtype == torch.float32 and F32_GEMM == "x3":
         return gemm_x3(a, pw, bias, colmax)
     M = a.shape[0]
     y = torch.empty((M, pw.N), dtype=pw.dtype, device=a.device)

@@ -1,6 +1,7 @@
-"""GPU: the fp32 faithful GEMM on the bf16 MFMA (sqmp_gemm_x3, three-way exact bf16 splits,
-six piece products) -- the F.linear of fake_quant.py:306 for fp32 models (OPT runs in fp32 in
-the reference, run_experiments.py:146-156).
+"""GPU: the fp32 faithful GEMMs on 16-bit MFMAs -- sqmp_gemm_h2 (row-scaled two-piece fp16
+splits, three products; the default) and sqmp_gemm_x3 (exact three-piece bf16 splits, six
+products) -- the F.linear of fake_quant.py:306 for fp32 models (OPT runs in fp32 in the
+reference, run_experiments.py:146-156).
 
 * the split: h + m + l == v exactly for every fp32 value (random, huge, tiny, zero, signs);
 * the GEMM against an fp64 product of the SAME operands (the packed A operand and the
@@ -8,9 +9,11 @@ the reference, run_experiments.py:146-156).
   of an fp32 GEMM (the fp32 faithful tolerance of the parity tests is 1e-5); ragged M, N
   (N % 4 != 0, N < 128), with and without bias and salient tail;
 * the fused output-quant column maxima (colmax) equal max |y| per column;
-* the f32-MFMA kernel (SQMP_X3=0 path) and x3 agree to fp32 rounding level.
+* the f32-MFMA kernel (F32_GEMM = "f32") and both agree to fp32 rounding level;
+* the h2 split: h + l reproduces every scaled value within 2^-22 (+ the f16 subnormal floor),
+  and every row's scaled maximum lies in [2^13, 2^14).
 The layer-level fp32 cases of test_gpu_parity / test_gpu_configs (oracle, reference
-goldens, config 1 and 3 layers) run through this kernel by default (ops.X3_AUTO)."""
+goldens, config 1 and 3 layers) run through the default kernel (ops.F32_GEMM)."""
 import numpy as np
 import pytest
 import torch
@@ -53,10 +56,43 @@ CASES = [
 ]
 
 
+def test_split2_f16_bound():
+    from smoothquant import ops
+    from smoothquant._lib import load
+    dev = _dev()
+    g = torch.Generator().manual_seed(4)
+    R, L = 29, 160
+    v = torch.randn(R, L, generator=g, dtype=torch.float64)
+    v *= torch.exp2(torch.randint(-30, 30, (R, 1), generator=g).double())   # per-row range
+    v *= torch.exp2(torch.randint(-12, 1, (R, L), generator=g).double())    # in-row spread
+    v[3] = 0.0
+    v = v.float().to(dev)
+    ldr = 32
+    out = torch.empty((2, ldr, L), dtype=torch.float16, device=dev)
+    rexp = torch.empty(ldr, dtype=torch.int32, device=dev)
+    ops.check(load().sqmp_split2_f16(ops._p(v), R, L, ldr, ops._p(out), ops._p(rexp),
+                                     ops._stream(v)), "split2")
+    torch.cuda.synchronize()
+    e = rexp[:R].double().cpu()
+    vs = v.double().cpu() * torch.exp2(e)[:, None]
+    mx = vs.abs().amax(1)
+    nz = mx > 0
+    assert bool(((mx[nz] >= 2.0 ** 13) & (mx[nz] < 2.0 ** 14)).all())
+    assert int(rexp[3]) == 0 and bool((rexp[R:] == 0).all())
+    rec = out[0, :R].double().cpu() + out[1, :R].double().cpu()
+    err = (rec - vs).abs()
+    assert bool((err <= 2.0 ** -22 * vs.abs() + 2.0 ** -25).all()), err.max()
+
+
+GEMMS = ["h2", "x3"]
+
+
+@pytest.mark.parametrize("gemm", GEMMS)
 @pytest.mark.parametrize("case", CASES)
-def test_x3_matches_fp64_product(case):
+def test_x3_matches_fp64_product(case, gemm):
     from smoothquant import ops
     wq, act, p, G, M, K, N, has_bias, oq = case
+    run = ops.gemm_h2 if gemm == "h2" else ops.gemm_x3
     dev = _dev()
     rng = np.random.default_rng(11)
     W = (rng.standard_normal((N, K)) * 0.02).astype(np.float32)
@@ -69,34 +105,33 @@ def test_x3_matches_fp64_product(case):
     xt = torch.from_numpy(x).to(dev)
     a = ops.quant_act_fp(xt.clone(), pw, act, 4, G)
     bias = None if q.bias is None else q.bias.detach().reshape(-1)
-    y = ops.gemm_x3(a, pw, bias)
-    planes = ops.x3_operand(pw)
-    Wfull = (planes[0].double() + planes[1].double() + planes[2].double())[:N]
-    ref = a.double() @ Wfull.t()
+    y = run(a, pw, bias)
+    ref = a.double() @ ops._w_full(pw).double().t()
     if bias is not None:
         ref += bias.double()
     e = rel(y.double().cpu().numpy(), ref.cpu().numpy())
     assert e <= 2e-6, e
     # the f32-MFMA kernel on the same operands
-    old = ops.X3_AUTO
+    old = ops.F32_GEMM
     try:
-        ops.X3_AUTO = False
+        ops.F32_GEMM = "f32"
         y32 = ops.gemm_fq(a, pw, bias)
     finally:
-        ops.X3_AUTO = old
+        ops.F32_GEMM = old
     assert rel(y.double().cpu().numpy(), y32.double().cpu().numpy()) <= 2e-6
     # fused column maxima
     colmax = torch.zeros(N + 5, dtype=torch.int32, device=dev)
-    y2 = ops.gemm_x3(a, pw, bias, colmax=colmax)
+    y2 = run(a, pw, bias, colmax=colmax)
     assert torch.equal(y2, y)
     cm = colmax[:N].view(torch.float32)
     assert torch.equal(cm, y.abs().amax(0))
     assert bool((colmax[N:] == 0).all())
 
 
-def test_x3_layer_forward_uses_x3_and_matches_f32_kernel():
-    """W4A4Linear.forward on an fp32 layer takes gemm_x3 (ops.X3_AUTO) and agrees with the
-    f32-MFMA kernel to fp32 rounding level, output quantization included."""
+@pytest.mark.parametrize("gemm", GEMMS)
+def test_x3_layer_forward_uses_x3_and_matches_f32_kernel(gemm):
+    """W4A4Linear.forward on an fp32 layer takes the selected 16-bit-MFMA GEMM and agrees with
+    the f32-MFMA kernel to fp32 rounding level, output quantization included."""
     from smoothquant import ops
     dev = _dev()
     rng = np.random.default_rng(5)
@@ -106,15 +141,15 @@ def test_x3_layer_forward_uses_x3_and_matches_f32_kernel():
     q = make_layer(W, np.zeros(N, np.float32), "fp32", dev, weight_quant="per_group",
                    act_quant="per_group", quantize_output=True,
                    importance=x.abs().mean((0, 1)).cpu(), salient_prop=0.05, group_size=128)
-    assert ops.X3_AUTO
-    y = q(x.clone())
-    assert q.packed().x3 is not None
-    old = ops.X3_AUTO
+    old = ops.F32_GEMM
     try:
-        ops.X3_AUTO = False
+        ops.F32_GEMM = gemm
+        y = q(x.clone())
+        assert getattr(q.packed(), gemm) is not None
+        ops.F32_GEMM = "f32"
         y32 = q(x.clone())
     finally:
-        ops.X3_AUTO = old
+        ops.F32_GEMM = old
     # the group scales of the output quantizer follow last-bit differences of max |y| (every
     # value of a group moves by a few ulps), and a 4-bit code flips where y sits on a
     # rounding boundary: count the flips (differences far above fp32 rounding)
