@@ -46,7 +46,8 @@ import torch  # noqa: E402
 M, K, N, G, P = 16384, 4096, 4096, 128, 0.10
 # dense MFMA peaks (MI355X_MICROARCH.md: 256 CU @ 2.4 GHz): f16/bf16 2.5 PF, i8/fp8 5 PF,
 # fp6/fp4 10 PF
-PEAK_TFLOPS = {"f16": 2516.6, "bf16": 2516.6, "i8": 5033.2, "f8": 5033.2, "f6": 10066.3}
+PEAK_TFLOPS = {"f16": 2516.6, "bf16": 2516.6, "i8": 5033.2, "f8": 5033.2, "f6": 10066.3,
+               "f32": 157.3}
 HBM_PEAK_GBS = 8000.0
 
 
@@ -56,6 +57,9 @@ def parse(argv=None):
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=200)
     ap.add_argument("--act", default="per_group", choices=["per_group", "per_token"])
+    ap.add_argument("--dtype", default="fp16", choices=["fp16", "fp32"],
+                    help="model dtype of the layer (fp32: the reference's OPT dtype; the GEMM "
+                         "runs on the f16 MFMA as sqmp_gemm_h2)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--rehearsal", action="store_true",
                     help="CPU/gloo rehearsal of the launcher and timing path (no GPU): the "
@@ -138,11 +142,11 @@ def synthetic_layer(gen, dev, dtype):
     return W.to(dtype), b.to(dtype), x.to(dtype), imp
 
 
-def make_layer(dev, act, seed):
+def make_layer(dev, act, seed, dtype=torch.float16):
     from smoothquant.fake_quant import W4A4Linear
     gen = torch.Generator(device=dev).manual_seed(seed)
-    W, b, x, imp = synthetic_layer(gen, dev, torch.float16)
-    lin = torch.nn.Linear(K, N, bias=True).to(dev, torch.float16)
+    W, b, x, imp = synthetic_layer(gen, dev, dtype)
+    lin = torch.nn.Linear(K, N, bias=True).to(dev, dtype)
     with torch.no_grad():
         lin.weight.copy_(W)
         lin.bias.copy_(b)
@@ -248,7 +252,9 @@ def main(argv=None):
     torch.cuda.set_device(dev)
     from smoothquant import ops
 
-    q, x, lin = make_layer(dev, args.act, seed=1234 + rank)
+    fp32 = args.dtype == "fp32"
+    q, x, lin = make_layer(dev, args.act, seed=1234 + rank,
+                           dtype=torch.float32 if fp32 else torch.float16)
     pw = q.packed()
     # what W4A4Linear(kernel="auto") runs for this layer
     use_f8 = ops.F8_AUTO and ops.f8_eligible(pw, args.act, 4)
@@ -298,6 +304,10 @@ def main(argv=None):
         gemm = lambda: ops.gemm_fq(a, pw, lin.bias)  # noqa: E731
         quant = lambda: ops.quant_act_fp(x, pw, args.act, 4, G)  # noqa: E731
         kdt, kname = "f16", "sqmp::gemm_fq6_kernel<F16,1,256>"
+        if fp32:
+            kdt = "f32"
+            kname = ("sqmp::gemm_x3_kernel<H=true> (sqmp_gemm_h2: row-scaled two-piece fp16 "
+                     "splits, 3 f16 MFMAs per product)")
     quant_ms = time_events(quant, sec_iters, stream)
     for _ in range(10):
         gemm()
@@ -324,7 +334,8 @@ def main(argv=None):
     achieved = flops / (gemm_ms * 1e-3) / 1e12
     t_roof = contract_roofline_s(pw.S)
     # prepass algorithmic bytes: read x (stats) + read x (quantize) + write the operand(s)
-    xbytes = M * K * 2
+    esz = 4 if fp32 else 2
+    xbytes = M * K * esz
     if use_f8:
         wbytes = M * pw.Kp + M * 4 + M * pw.S_pad * 2
         reads = 2 if args.act == "per_tensor" else 1
@@ -336,12 +347,13 @@ def main(argv=None):
                   + N * (Kq + pw.S_pad) * 2 + N * pw.Kp // 2)
         reads = 2
     else:
-        wbytes = M * (pw.Kp + pw.S_pad) * 2
+        wbytes = M * (pw.Kp + pw.S_pad) * esz
         reads = 2 if args.act in ("per_group", "per_tensor") else 1
     prepass_bytes = reads * xbytes + wbytes
 
     traffic = None
     prof = os.path.join(ROOT, "profiles", "r02_pmc_gemm_f8v2_per_token.json" if kdt == "f8"
+                        else "r02_pmc_gemm_h2_fp32.json" if fp32
                         else "r02_pmc_gemm_fqt_per_group.json" if use_fqt
                         else f"r02_pmc_gemm_fq6_{args.act}.json")
     if os.path.exists(prof):
@@ -362,7 +374,9 @@ def main(argv=None):
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "e4m3 codes (fp32 accumulate) + fp16 salient tail" if use_f8 else "fp16",
+        "dtype": ("e4m3 codes (fp32 accumulate) + fp16 salient tail" if use_f8 else
+                  "fp32 (fp32-accurate products from fp16 pieces on the f16 MFMA)" if fp32
+                  else "fp16"),
         "data": "synthetic (random-init weights N(0,0.02^2), x N(0,1) with 1% outlier channels x30)",
         "config": {
             "workload": (f"W4A4Linear.forward: weight per_group(sorted) int4 + act {args.act} "
@@ -387,17 +401,21 @@ def main(argv=None):
             "frac_contract_gemm": round(t_roof / (gemm_ms * 1e-3), 4),
             "frac_contract_step": round(t_roof / (ms_per_step * 1e-3), 4),
             "note": ("frac = achieved / dense MFMA peak of the kernel's dtype; frac_contract_* "
-                     "= BASELINE.md §2 T_roof (2MNK'/P_i8 + 2MNS/P_f16) / GEMM time, / step time"),
+                     "= BASELINE.md §2 T_roof (2MNK'/P_i8 + 2MNS/P_f16) / GEMM time, / step time"
+                     + ("; fp32: peak = the f32 MFMA (the dtype's own); the kernel executes "
+                        "3 f16 MFMAs per product over Kp + S_pad positions: "
+                        f"executed_f16_frac = {3 * achieved * (pw.Kp + pw.S_pad) / K / PEAK_TFLOPS['f16']:.4f}"
+                        if fp32 else "")),
         },
         "reference_points": {
             "reference_fakequant_forward_ms": round(ref_ms, 4),
             "reference_fakequant_TFLOP_per_s": round(flops / (ref_ms * 1e-3) / 1e12, 1),
             "speedup_vs_reference_fakequant": round(ref_ms / ms_per_step, 2),
             "reference_vs_ours_rel_err": ref_rel,
-            "torch_fp16_linear_ms": round(dense_ms, 4),
-            "torch_fp16_linear_TFLOP_per_s": round(flops / (dense_ms * 1e-3) / 1e12, 1),
+            f"torch_{args.dtype}_linear_ms": round(dense_ms, 4),
+            f"torch_{args.dtype}_linear_TFLOP_per_s": round(flops / (dense_ms * 1e-3) / 1e12, 1),
             "note": "reference fake-quant forward restated in PyTorch ops (tools/torch_fakequant.py) on "
-                    "this GPU; fp16 F.linear = unquantized hipBLASLt GEMM of the same shape",
+                    f"this GPU; {args.dtype} F.linear = unquantized hipBLASLt GEMM of the same shape",
         },
         "prepass": {
             "avg_ms": round(quant_ms, 4),

@@ -1,5 +1,5 @@
 """Run only the W4A4 GEMM (and optionally the prepass) of BASELINE config 2 -- a target
-for rocprofv3 counter passes.  python tools/gemm_only.py [fq|fqt|i8|f8] [iters] [per_group|per_token] [prepass]"""
+for rocprofv3 counter passes.  python tools/gemm_only.py [fq|fqt|i8|f8|h2] [iters] [per_group|per_token] [prepass]"""
 import os
 import sys
 
@@ -16,7 +16,10 @@ extra = sys.argv[3:]
 prepass = "prepass" in extra
 dev = torch.device("cuda")
 act = next((a for a in extra if a.startswith("per_")), "per_group" if kind in ("fq", "fqt") else "per_token")
-q, x, lin = bench.make_layer(dev, act, seed=1)
+q, x, lin = bench.make_layer(dev, act, seed=1,
+                             dtype=torch.float32 if kind == "h2" else torch.float16)
+if kind == "h2":
+    kind = "fq"  # the fp32 layer's gemm_fq runs sqmp_gemm_h2
 pw = q.packed()
 if kind == "fq":
     a = ops.quant_act_fp(x, pw, act, 4, bench.G)
