@@ -19,6 +19,8 @@
 // 96 MFMAs per wave per stage; single-buffered LDS (48 KiB) with the next stage's global
 // loads in flight over the MFMAs, two workgroups per CU (8 waves of 64 x 32 in one
 // workgroup when the grid has fewer than two tiles per CU).
+#include <stdlib.h>
+
 #include "sqmp_mfma.h"
 
 namespace sqmp {
@@ -74,18 +76,22 @@ __device__ inline int row_exp_of(float mx) {
   return mx > 0.f ? 13 - ((int)((__float_as_uint(mx) >> 23) & 0xFFu) - 127) : 0;
 }
 
-template <bool COLMAX, int WN, bool H = false>
+template <bool COLMAX, int WN, bool H = false, int BN = 128>
 __global__ __launch_bounds__(128 * WN, 4 / WN) void gemm_x3_kernel(
     const float* __restrict__ A, const uint16_t* __restrict__ B3, const float* __restrict__ bias,
     float* __restrict__ Y, int M, int N, int L, int Np, int tiles_m, int tiles_n,
     uint32_t* __restrict__ colmax, const int* __restrict__ aexp, const int* __restrict__ bexp) {
   constexpr int NPL = H ? 2 : 3;  // pieces per operand
-  __shared__ __attribute__((aligned(16))) unsigned char lds[2 * NPL * X3_PLANE];
+  // A planes (NPL x 128 rows) then B planes (NPL x BN rows), 64-B rows
+  constexpr int BPL = X3_PLANE * BN / X3_BM;  // one B plane
+  __shared__ __attribute__((aligned(16))) unsigned char lds[NPL * (X3_PLANE + BPL)];
+  unsigned char* const ldsb = lds + NPL * X3_PLANE;
   int tm, tn;
   tile_coords(tiles_m, tiles_n, 8, tm, tn);
-  const int m0 = tm * X3_BM, n0 = tn * X3_BN;
-  constexpr int NT = 128 * WN, CW = X3_BN / WN, J = CW / 16;
-  constexpr int LA = 1024 / NT, LB = 512 * NPL / NT;  // 16-B staging chunks per thread
+  const int m0 = tm * X3_BM, n0 = tn * BN;
+  constexpr int NT = 128 * WN, CW = BN / WN, J = CW / 16;
+  constexpr int BSH = BN == 256 ? 10 : 9;  // log2(16-B chunks per B plane)
+  constexpr int LA = 1024 / NT, LB = 4 * BN * NPL / NT;  // 16-B staging chunks per thread
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
   const int r16 = lane & 15, q = lane >> 4;
@@ -108,7 +114,7 @@ __global__ __launch_bounds__(128 * WN, 4 / WN) void gemm_x3_kernel(
     }
 #pragma unroll
     for (int i = 0; i < LB; ++i) {
-      const int idx = tid + NT * i, p = idx >> 9, row = (idx >> 2) & 127, c = idx & 3;
+      const int idx = tid + NT * i, p = idx >> BSH, row = (idx >> 2) & (BN - 1), c = idx & 3;
       rb[i] = *(const u32x4*)(B3 + p * plane + (size_t)(n0 + row) * L + k0 + 8 * c);
     }
   };
@@ -134,8 +140,8 @@ __global__ __launch_bounds__(128 * WN, 4 / WN) void gemm_x3_kernel(
     }
 #pragma unroll
     for (int i = 0; i < LB; ++i) {
-      const int idx = tid + NT * i, p = idx >> 9, row = (idx >> 2) & 127, c = idx & 3;
-      *(u32x4*)(lds + (NPL + p) * X3_PLANE + x3_off(row, c)) = rb[i];
+      const int idx = tid + NT * i, p = idx >> BSH, row = (idx >> 2) & (BN - 1), c = idx & 3;
+      *(u32x4*)(ldsb + p * BPL + x3_off(row, c)) = rb[i];
     }
   };
 
@@ -153,7 +159,7 @@ __global__ __launch_bounds__(128 * WN, 4 / WN) void gemm_x3_kernel(
     for (int p = 0; p < NPL; ++p)
 #pragma unroll
       for (int j = 0; j < J; ++j)
-        bf[p][j] = *(const u32x4*)(lds + (NPL + p) * X3_PLANE + x3_off(wn * CW + 16 * j + r16, q));
+        bf[p][j] = *(const u32x4*)(ldsb + p * BPL + x3_off(wn * CW + 16 * j + r16, q));
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       u32x4 af[NPL];
@@ -162,7 +168,8 @@ __global__ __launch_bounds__(128 * WN, 4 / WN) void gemm_x3_kernel(
         af[p] = *(const u32x4*)(lds + p * X3_PLANE + x3_off(wm * 64 + 16 * i + r16, q));
 #pragma unroll
       for (int j = 0; j < J; ++j) {
-        // smallest terms first
+        // smallest terms first (one accumulator per chain: measured faster than term-major
+        // order over the accumulators)
         if (H) {
           Mfma<F16>::run(acc[i][j], bf[0][j], af[1]);
           Mfma<F16>::run(acc[i][j], bf[1][j], af[0]);
@@ -326,13 +333,21 @@ extern "C" int sqmp_gemm_h2(const float* a, const int* aexp, const void* b2, con
   const int Np = pad_n(N);
   const int tiles_m = cdiv(M, X3_BM), tiles_n = cdiv(N, X3_BN);
   const bool small = (long)tiles_m * tiles_n < 2L * 256;
-#define SQMP_H2(CM, WN)                                                                  \
-  gemm_x3_kernel<CM, WN, true><<<tiles_m * tiles_n, 128 * WN, 0, (hipStream_t)stream>>>( \
-      a, (const uint16_t*)b2, bias, y, M, N, L, Np, tiles_m, tiles_n, colmax, aexp, bexp)
+  // 128 x 256 tiles (8 waves of 64 x 64: half the A re-fetch and A split work per MFMA of
+  // 128 x 128 tiles) wherever they still give every CU a workgroup
+  const int tiles_n2 = cdiv(N, 256);
+  static const bool wide_ok = [] {  // SQMP_H2_WIDE=0: 128 x 128 tiles only (A/B knob)
+    const char* e = getenv("SQMP_H2_WIDE");
+    return !e || atoi(e) != 0;
+  }();
+  const bool wide = wide_ok && (long)tiles_m * tiles_n2 >= 256;
+#define SQMP_H2(CM, WN, BNV, TN)                                                                 \
+  gemm_x3_kernel<CM, WN, true, BNV><<<tiles_m * TN, 128 * WN, 0, (hipStream_t)stream>>>(        \
+      a, (const uint16_t*)b2, bias, y, M, N, L, Np, tiles_m, TN, colmax, aexp, bexp)
   if (colmax) {
-    if (small) SQMP_H2(true, 4); else SQMP_H2(true, 2);
+    if (wide) SQMP_H2(true, 4, 256, tiles_n2); else if (small) SQMP_H2(true, 4, 128, tiles_n); else SQMP_H2(true, 2, 128, tiles_n);
   } else {
-    if (small) SQMP_H2(false, 4); else SQMP_H2(false, 2);
+    if (wide) SQMP_H2(false, 4, 256, tiles_n2); else if (small) SQMP_H2(false, 4, 128, tiles_n); else SQMP_H2(false, 2, 128, tiles_n);
   }
 #undef SQMP_H2
   SQMP_LAUNCH_CHECK();
