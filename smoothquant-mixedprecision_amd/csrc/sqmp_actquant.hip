@@ -459,6 +459,29 @@ __global__ __launch_bounds__(256) void build_ent_kernel(
   }
 }
 
+
+// ---------------------------------------------------------------- entry table from lctab
+// The wave quantizers' chunk-major entry table built from the lane-contiguous table of the
+// same call (lctab[r] = column | packed position << 16 for rank r < Kn): rank threads
+// scatter (group << 16) | column to their position, position threads mark the positions
+// amap leaves empty (salient / padding: -1; in-place salient pass-through: -2) G_ZERO --
+// disjoint sets.  Also clears the column keys the rank table read (clean workspace).
+__global__ __launch_bounds__(256) void ent_from_lctab_kernel(
+    const uint32_t* __restrict__ lctab, int Kn, const int32_t* __restrict__ amap, int P,
+    int G, uint32_t* __restrict__ ent, uint32_t* __restrict__ key_clear, int clear_words) {
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  auto put = [&](int p, uint32_t e) {
+    const int c = p >> 3, j = p & 7;
+    ent[(size_t)(j >> 2) * (P / 2) + c * 4 + (j & 3)] = e;
+  };
+  if (t < Kn) {
+    const uint32_t e = lctab[t];
+    put((int)(e >> 16), ((uint32_t)(t / G) << 16) | (e & 0xFFFFu));
+  }
+  if (t < P && amap[t] < 0) put(t, G_ZERO << 16);
+  if (key_clear && t < clear_words) key_clear[t] = 0u;
+}
+
 // ---------------------------------------------------------------- lane-contiguous table
 // Per call, one thread per non-salient list entry i (column nonsal[i]):
 //   TAB_COUNTS  r = counts[col] (the stable rank), counts[col] = 0 afterwards, and the
@@ -1270,6 +1293,35 @@ static int quant_act_impl(void* x, int dtype, int M, int K, int amode, int n_bit
     if (st) return st;
     return launch_quant_lc(dtype, lmode, x, M, K, q_max, group_size, lctab, Kn, nullptr, K,
                            salient, 0, 0, cmax, nonsal, x, kc, (int)k64, s);
+  }
+
+  // ---- fp32 rows (OUT_FP, and the in-place output quantizer): the lane-contiguous
+  // pipeline's statistics and rank table (clean workspace, no memsets), the entry table
+  // scattered from it in one launch, the fp32 wave quantizers
+  if (dtype == SQMP_F32 && !lc_off && Kn > 0 && amode != SQMP_ACT_PER_TENSOR && K % 8 == 0 &&
+      (((uintptr_t)x) % 16 == 0) &&
+      ((out_kind == SQMP_OUT_FP && posmap && Kp % 8 == 0 && ((uintptr_t)out) % 16 == 0) ||
+       out_kind == SQMP_OUT_INPLACE) &&
+      (out_kind == SQMP_OUT_FP || clean)) {
+    const bool inplace = out_kind == SQMP_OUT_INPLACE;
+    const int P = inplace ? K : Kp;
+    const size_t wb = (size_t)round_up(4L * K, 16) + (size_t)round_up(12L * (group ? cdiv(Kn, group_size) : 1), 16);
+    if (wb <= 160 * 1024) {
+      uint32_t* kc;
+      const uint32_t none = inplace ? (uint32_t)K | ((uint32_t)(K + 1) << 16) : lc_none;
+      st = lc_prepare(inplace ? nullptr : posmap, none,
+                      !inplace && (flags & SQMP_QA_REUSE_STATS) != 0, kc);
+      if (st) return st;
+      const int nthr = P > Kn ? P : Kn;
+      const int cw = kc ? (int)k64 : 0;
+      ent_from_lctab_kernel<<<dim3(cdiv(nthr > cw ? nthr : cw, 256)), dim3(256), 0, s>>>(
+          lctab, Kn, amap, P, group ? group_size : (1 << 30), ent, kc, cw);
+      SQMP_LAUNCH_CHECK();
+      const int nga = group ? cdiv(Kn, group_size) : 1;
+      return quant_dispatch<F32>(x, M, K, amode, q_max, group_size, nga, amap, P, nonsal, Kn,
+                                 salient, S, S_pad, nullptr, cmax, ent, out_kind, out,
+                                 out_scale, out_xs, s);
+    }
   }
 
   // ---- general path (fp32, 8-bit int output, large rows, other group sizes)
