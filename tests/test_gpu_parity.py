@@ -455,3 +455,28 @@ def test_packed_checkpoint_loads_into_from_float_module(tmp_path):
     save_quantized(src, p)
     load_quantized(dst, p)
     assert bits_equal(to_np(dst(x.clone())), to_np(y0))
+
+
+def test_device_round_trip_keeps_packing_and_output():
+    """model.to("cpu") then .to("cuda") (nn.Module device moves, fake_quant.py:272-277 keeps
+    W_hat as a buffer): the packed buffers travel with the module, stay int4-packed, the
+    forward on the GPU afterwards is bit-identical, and a forward on the CPU raises (the
+    operator has no CPU path) instead of silently falling back."""
+    dev = _dev()
+    g = np.random.default_rng(29)
+    K, N, M = 512, 384, 48
+    W = g.standard_normal((N, K)).astype(np.float32) * 0.02
+    b = g.standard_normal(N).astype(np.float32) * 0.01
+    imp = torch.from_numpy(np.abs(g.standard_normal(K)).astype(np.float32))
+    for dtn in ("fp16", "fp32"):
+        q = make_layer(W, b, dtn, dev, weight_quant="per_group", act_quant="per_group",
+                       importance=imp, salient_prop=0.05, group_size=64)
+        x = to_t(g.standard_normal((M, K)), dtn, dev)
+        y0 = q(x.clone())
+        q.to("cpu")
+        assert q.w_codes.device.type == "cpu" and q.packed().n_bits == 4
+        with pytest.raises(RuntimeError):
+            q(x.cpu())
+        q.to(dev)
+        assert q.w_codes.device == x.device and q.packed().n_bits == 4
+        assert bits_equal(to_np(q(x.clone())), to_np(y0))
