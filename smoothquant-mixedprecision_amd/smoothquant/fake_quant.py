@@ -201,8 +201,9 @@ _PW_KEY = ("w_codes", "w_scale", "w_salient", "w_perm", "w_amap", "w_amap_fq", "
 class W4A4Linear(nn.Module):
     """Mixed-precision W4A4 linear: salient input channels in D, the rest int4/int8.
 
-    Forward kernels (chosen per layer, see `kernel`; "auto" = "f6" where ops.f6_eligible,
-    else "f8" where ops.f8_eligible, else "fq" unless ops.I8_AUTO):
+    Forward kernels (chosen per layer, see `kernel`; "auto" = "f8" where ops.f8_eligible
+    ("f6" instead when ops.F6_AUTO), "fqt" for large sorted per_group batches, else "fq"
+    unless ops.I8_AUTO):
       "f6"  as "f8" with both code operands in FP6 e2m3 (weight groups of whole 128-blocks):
             twice the MFMA rate, 0.75-byte operands, the same y bit for bit.
       "f8"  per_token / per_tensor 4-bit activations: e4m3 act codes x e4m3 weight codes on

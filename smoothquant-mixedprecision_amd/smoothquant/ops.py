@@ -688,8 +688,10 @@ I8_AUTO = False
 # Whether kernel="auto" takes the FP8 path for eligible layers (f8_eligible): on gfx950
 # it is 1.4x the fq GEMM at config 2.
 F8_AUTO = True
-# Whether kernel="auto" takes the FP6 path where f6_eligible (bit-identical to "f8").
-F6_AUTO = True
+# Whether kernel="auto" takes the FP6 path where f6_eligible (bit-identical to "f8").  Off:
+# measured at config 2 per_token, the f6 GEMM 310 us against f8v2's 285 us and the step
+# 0.386 against 0.343 ms (same box, interleaved runs); SQMP_F6=1 turns it on (A/B knob).
+F6_AUTO = os.environ.get("SQMP_F6", "0") == "1"
 
 
 def i8_eligible(pw: PackedWeight, act_quant: str, act_bits: int) -> bool:
