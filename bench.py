@@ -24,7 +24,11 @@ Also printed in the same JSON line:
                 host's cores: rank 0, N=1 only, median of 3 after 1 warm-up
   prepass       the activation-quantization kernels' time and algorithmic GB/s
 Secondary measurements (GEMM alone, prepass, vendor dense GEMM, reference fake-quant on
-the GPU) run BEFORE the W warm-up steps, so the timed region starts on a busy chip.
+the GPU) run BEFORE the W warm-up steps, followed by --settle-ms (default 300) of untimed
+steps, so the timed region starts on a chip that holds the clock it settles at under this
+load whatever W is (DVFS: a 20-step run right after a short warm-up measured the GEMM at
+510-680 us in its first milliseconds, 445 us once settled -- profiles/r02_bench_driver20_*).
+The timed region is still exactly K steps between barriers.
 """
 from __future__ import annotations
 
@@ -57,6 +61,8 @@ def parse(argv=None):
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=200)
     ap.add_argument("--act", default="per_group", choices=["per_group", "per_token"])
+    ap.add_argument("--settle-ms", type=float, default=300.0,
+                    help="untimed steps run for this long before the W warm-up steps")
     ap.add_argument("--dtype", default="fp16", choices=["fp16", "fp32"],
                     help="model dtype of the layer (fp32: the reference's OPT dtype; the GEMM "
                          "runs on the f16 MFMA as sqmp_gemm_h2)")
@@ -323,6 +329,11 @@ def main(argv=None):
     def step():
         return q(x)
 
+    t_settle = time.perf_counter()
+    while (time.perf_counter() - t_settle) * 1e3 < args.settle_ms:
+        for _ in range(10):
+            step()
+        torch.cuda.synchronize(dev)
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
