@@ -155,3 +155,26 @@ def test_x3_layer_forward_uses_x3_and_matches_f32_kernel(gemm):
     # rounding boundary: count the flips (differences far above fp32 rounding)
     flips = ((y - y32).abs() > 1e-4 * y32.abs().max()).float().mean().item()
     assert flips < 0.01, flips
+
+
+def test_h2_full_size_config2_fp32():
+    """BASELINE config 2 in fp32 (M = 16384, K = N = 4096, G = 128, 10 % salient): the
+    layer forward (quantizer + sqmp_gemm_h2) against the fp64 product of the same operands
+    (the packed A operand and the packed-order W_hat + salient slice)."""
+    from smoothquant import ops
+    dev = _dev()
+    M, K, N = 16384, 4096, 4096
+    g = torch.Generator(device=dev).manual_seed(9)
+    W = (torch.randn(N, K, generator=g, device=dev) * 0.02).cpu().numpy()
+    x = torch.randn(M, K, generator=g, device=dev)
+    x[:, torch.randperm(K, generator=g, device=dev)[:41]] *= 30.0
+    q = make_layer(W, np.zeros(N, np.float32), "fp32", dev, weight_quant="per_group",
+                   act_quant="per_group", importance=x[:2048].abs().mean(0).cpu(),
+                   salient_prop=0.10, group_size=128)
+    pw = q.packed()
+    with torch.no_grad():
+        y = q(x)
+        a = ops.quant_act_fp(x, pw, "per_group", 4, 128)
+        ref = a.double() @ ops._w_full(pw).double().t() + q.bias.detach().reshape(-1).double()
+    e = rel(y.double().cpu().numpy(), ref.cpu().numpy())
+    assert e <= 2e-6, e
