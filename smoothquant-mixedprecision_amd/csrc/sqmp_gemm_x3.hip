@@ -36,7 +36,16 @@ constexpr int X3_PLANE = X3_BM * X3_BK * 2;  // one bf16 plane of a 128-row tile
 // group on 16 distinct (row & 3, chunk) bank quarters -- conflict-free.
 __device__ inline int x3_off(int row, int chunk) {
   const int h = (0x1320 >> (4 * ((row >> 2) & 3))) & 3;  // H = {0, 2, 3, 1}
+
   return row * 64 + ((chunk ^ h) << 4);
+}
+
+// 128-B rows (K stage 64): chunk c of row r at c ^ (r & 7) -- conflict-free for the same
+// lane groups (fragment chunk 4 s + q of sub-step s)
+template <int BK>
+__device__ inline int xk_off(int row, int chunk) {
+  if (BK == 64) return row * 128 + ((chunk ^ (row & 7)) << 4);
+  return x3_off(row, chunk);
 }
 
 __device__ inline uint32_t bf16_bits(float v) {
@@ -76,26 +85,30 @@ __device__ inline int row_exp_of(float mx) {
   return mx > 0.f ? 13 - ((int)((__float_as_uint(mx) >> 23) & 0xFFu) - 127) : 0;
 }
 
-template <bool COLMAX, int WN, bool H = false, int BN = 128>
+template <bool COLMAX, int WN, bool H = false, int BN = 128, int BK = 32>
 __global__ __launch_bounds__(128 * WN, 4 / WN) void gemm_x3_kernel(
     const float* __restrict__ A, const uint16_t* __restrict__ B3, const float* __restrict__ bias,
     float* __restrict__ Y, int M, int N, int L, int Np, int tiles_m, int tiles_n,
     uint32_t* __restrict__ colmax, const int* __restrict__ aexp, const int* __restrict__ bexp) {
   constexpr int NPL = H ? 2 : 3;  // pieces per operand
-  // A planes (NPL x 128 rows) then B planes (NPL x BN rows), 64-B rows
-  constexpr int BPL = X3_PLANE * BN / X3_BM;  // one B plane
-  __shared__ __attribute__((aligned(16))) unsigned char lds[NPL * (X3_PLANE + BPL)];
-  unsigned char* const ldsb = lds + NPL * X3_PLANE;
+  // A planes (NPL x 128 rows) then B planes (NPL x BN rows), rows of BK 16-bit values
+  constexpr int APL = X3_BM * BK * 2;  // one A plane
+  constexpr int BPL = APL * BN / X3_BM;  // one B plane
+  constexpr int CPR = BK / 8;          // 16-B chunks per 16-bit row
+  constexpr int CSH = BK == 64 ? 3 : 2;
+  __shared__ __attribute__((aligned(16))) unsigned char lds[NPL * (APL + BPL)];
+  unsigned char* const ldsb = lds + NPL * APL;
   int tm, tn;
   tile_coords(tiles_m, tiles_n, 8, tm, tn);
   const int m0 = tm * X3_BM, n0 = tn * BN;
   constexpr int NT = 128 * WN, CW = BN / WN, J = CW / 16;
-  constexpr int BSH = BN == 256 ? 10 : 9;  // log2(16-B chunks per B plane)
-  constexpr int LA = 1024 / NT, LB = 4 * BN * NPL / NT;  // 16-B staging chunks per thread
+  constexpr int BSH = (BN == 256 ? 8 : 7) + CSH;  // log2(16-B chunks per B plane)
+  constexpr int LA = 2 * CPR * X3_BM / NT, LB = CPR * BN * NPL / NT;  // 16-B staging chunks per thread
+  constexpr int ASH = CSH + 1;  // log2(16-B fp32 chunks per A row)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
   const int r16 = lane & 15, q = lane >> 4;
-  const int nkt = L / X3_BK;
+  const int nkt = L / BK;
   const size_t plane = (size_t)Np * L;
 
   // staging: A 128 rows x 8 chunks of 4 fp32; B NPL planes x 128 rows x 4 chunks of 8 x 16 bit
@@ -103,45 +116,45 @@ __global__ __launch_bounds__(128 * WN, 4 / WN) void gemm_x3_kernel(
   int ae[LA];  // H: the row exponents of this thread's A chunks (fixed over the K loop)
   if (H) {
 #pragma unroll
-    for (int i = 0; i < LA; ++i) ae[i] = aexp[min(m0 + ((tid + NT * i) >> 3), M - 1)];
+    for (int i = 0; i < LA; ++i) ae[i] = aexp[min(m0 + ((tid + NT * i) >> ASH), M - 1)];
   }
   auto load = [&](int kt) {
-    const int k0 = kt * X3_BK;
+    const int k0 = kt * BK;
 #pragma unroll
     for (int i = 0; i < LA; ++i) {
-      const int idx = tid + NT * i, row = idx >> 3, c = idx & 7;
+      const int idx = tid + NT * i, row = idx >> ASH, c = idx & (2 * CPR - 1);
       ra[i] = *(const u32x4*)(A + (size_t)(m0 + row) * L + k0 + 4 * c);
     }
 #pragma unroll
     for (int i = 0; i < LB; ++i) {
-      const int idx = tid + NT * i, p = idx >> BSH, row = (idx >> 2) & (BN - 1), c = idx & 3;
+      const int idx = tid + NT * i, p = idx >> BSH, row = (idx >> CSH) & (BN - 1), c = idx & (CPR - 1);
       rb[i] = *(const u32x4*)(B3 + p * plane + (size_t)(n0 + row) * L + k0 + 8 * c);
     }
   };
   auto store = [&]() {
 #pragma unroll
     for (int i = 0; i < LA; ++i) {
-      const int idx = tid + NT * i, row = idx >> 3, c = idx & 7;
-      const int off = x3_off(row, c >> 1) + (c & 1) * 8;
+      const int idx = tid + NT * i, row = idx >> ASH, c = idx & (2 * CPR - 1);
+      const int off = xk_off<BK>(row, c >> 1) + (c & 1) * 8;
       if (H) {
         uint32_t h[4], l[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) split2h(__builtin_ldexpf(__uint_as_float(ra[i][e]), ae[i]), h[e], l[e]);
         *(uint2*)(lds + off) = uint2{h[0] | (h[1] << 16), h[2] | (h[3] << 16)};
-        *(uint2*)(lds + X3_PLANE + off) = uint2{l[0] | (l[1] << 16), l[2] | (l[3] << 16)};
+        *(uint2*)(lds + APL + off) = uint2{l[0] | (l[1] << 16), l[2] | (l[3] << 16)};
       } else {
         uint32_t h[4], m[4], l[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) split3(__uint_as_float(ra[i][e]), h[e], m[e], l[e]);
         *(uint2*)(lds + off) = uint2{h[0] | (h[1] << 16), h[2] | (h[3] << 16)};
-        *(uint2*)(lds + X3_PLANE + off) = uint2{m[0] | (m[1] << 16), m[2] | (m[3] << 16)};
-        *(uint2*)(lds + 2 * X3_PLANE + off) = uint2{l[0] | (l[1] << 16), l[2] | (l[3] << 16)};
+        *(uint2*)(lds + APL + off) = uint2{m[0] | (m[1] << 16), m[2] | (m[3] << 16)};
+        *(uint2*)(lds + 2 * APL + off) = uint2{l[0] | (l[1] << 16), l[2] | (l[3] << 16)};
       }
     }
 #pragma unroll
     for (int i = 0; i < LB; ++i) {
-      const int idx = tid + NT * i, p = idx >> BSH, row = (idx >> 2) & (BN - 1), c = idx & 3;
-      *(u32x4*)(ldsb + p * BPL + x3_off(row, c)) = rb[i];
+      const int idx = tid + NT * i, p = idx >> BSH, row = (idx >> CSH) & (BN - 1), c = idx & (CPR - 1);
+      *(u32x4*)(ldsb + p * BPL + xk_off<BK>(row, c)) = rb[i];
     }
   };
 
@@ -152,6 +165,8 @@ __global__ __launch_bounds__(128 * WN, 4 / WN) void gemm_x3_kernel(
     for (int j = 0; j < J; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   auto compute = [&]() {
+#pragma unroll
+   for (int sst = 0; sst < BK / 32; ++sst) {
     // B fragments (output columns) in the MFMA's A slot: the lane's 4 results are 4
     // consecutive columns of one row (16-B stores)
     u32x4 bf[NPL][J];
@@ -159,13 +174,13 @@ __global__ __launch_bounds__(128 * WN, 4 / WN) void gemm_x3_kernel(
     for (int p = 0; p < NPL; ++p)
 #pragma unroll
       for (int j = 0; j < J; ++j)
-        bf[p][j] = *(const u32x4*)(ldsb + p * BPL + x3_off(wn * CW + 16 * j + r16, q));
+        bf[p][j] = *(const u32x4*)(ldsb + p * BPL + xk_off<BK>(wn * CW + 16 * j + r16, 4 * sst + q));
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       u32x4 af[NPL];
 #pragma unroll
       for (int p = 0; p < NPL; ++p)
-        af[p] = *(const u32x4*)(lds + p * X3_PLANE + x3_off(wm * 64 + 16 * i + r16, q));
+        af[p] = *(const u32x4*)(lds + p * APL + xk_off<BK>(wm * 64 + 16 * i + r16, 4 * sst + q));
 #pragma unroll
       for (int j = 0; j < J; ++j) {
         // smallest terms first (one accumulator per chain: measured faster than term-major
@@ -184,6 +199,7 @@ __global__ __launch_bounds__(128 * WN, 4 / WN) void gemm_x3_kernel(
         }
       }
     }
+   }
   };
 
   load(0);
@@ -341,9 +357,16 @@ extern "C" int sqmp_gemm_h2(const float* a, const int* aexp, const void* b2, con
     return !e || atoi(e) != 0;
   }();
   const bool wide = wide_ok && (long)tiles_m * tiles_n2 >= 256;
+  static const bool bk64 = [] {  // SQMP_H2_BK64=0: K stages of 32 (A/B knob)
+    const char* e = getenv("SQMP_H2_BK64");
+    return !e || atoi(e) != 0;
+  }();
+  const bool k64 = bk64 && L % 64 == 0;
 #define SQMP_H2(CM, WN, BNV, TN)                                                                 \
-  gemm_x3_kernel<CM, WN, true, BNV><<<tiles_m * TN, 128 * WN, 0, (hipStream_t)stream>>>(        \
-      a, (const uint16_t*)b2, bias, y, M, N, L, Np, tiles_m, TN, colmax, aexp, bexp)
+  (k64 ? gemm_x3_kernel<CM, WN, true, BNV, 64><<<tiles_m * TN, 128 * WN, 0, (hipStream_t)stream>>>( \
+             a, (const uint16_t*)b2, bias, y, M, N, L, Np, tiles_m, TN, colmax, aexp, bexp)      \
+       : gemm_x3_kernel<CM, WN, true, BNV, 32><<<tiles_m * TN, 128 * WN, 0, (hipStream_t)stream>>>( \
+             a, (const uint16_t*)b2, bias, y, M, N, L, Np, tiles_m, TN, colmax, aexp, bexp))
   if (colmax) {
     if (wide) SQMP_H2(true, 4, 256, tiles_n2); else if (small) SQMP_H2(true, 4, 128, tiles_n); else SQMP_H2(true, 2, 128, tiles_n);
   } else {
