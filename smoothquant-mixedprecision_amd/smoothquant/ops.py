@@ -419,8 +419,10 @@ def fake_quant_inplace(t2: torch.Tensor, act_quant: str, n_bits: int, group_size
     return t2
 
 
-# Whether gemm_fq runs the register-operand kernel (sqmp_gemm_fq7) where fq7_eligible.
-FQ7_AUTO = os.environ.get("SQMP_FQ7", "0") == "1"
+# Whether gemm_fq runs the register-operand kernel (sqmp_gemm_fq7) where fq7_eligible: on by
+# default (same-box GEMM-only A/B, tools/gemm_ab.py: +8 to +10 % at the 2048-token Llama shapes,
+# +2.7 % at config 2 in packed order); SQMP_FQ7=0 selects fq6.
+FQ7_AUTO = os.environ.get("SQMP_FQ7", "1") == "1"
 # weight rows per wave / 16: 4 -> 128 x 512 tiles, 2 -> 256 x 256 tiles
 FQ7_J = int(os.environ.get("SQMP_FQ7_J", "2"))
 
