@@ -316,7 +316,9 @@ def main(argv=None):
         a = ops.quant_act_fp(x, pw, args.act, 4, G)
         gemm = lambda: ops.gemm_fq(a, pw, lin.bias)  # noqa: E731
         quant = lambda: ops.quant_act_fp(x, pw, args.act, 4, G)  # noqa: E731
-        kdt, kname = "f16", "sqmp::gemm_fq6_kernel<F16,1,256>"
+        kdt, kname = "f16", ("sqmp::fq7::gemm_fq7_kernel<F16,1,256,2> (weights in registers)"
+                             if ops.FQ7_AUTO and ops.fq7_eligible(pw)
+                             else "sqmp::gemm_fq6_kernel<F16,1,256>")
         if fp32:
             kdt = "f32"
             kname = ("sqmp::gemm_x3_kernel<H=true> (sqmp_gemm_h2: row-scaled two-piece fp16 "

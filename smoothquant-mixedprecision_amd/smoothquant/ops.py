@@ -294,7 +294,9 @@ def quant_act_fp(x2: torch.Tensor, pw: PackedWeight, act_quant: str, n_bits: int
 # quantizer writes 4-bit codes instead of D values.  It rebuilds the permuted weight per
 # forward (N x (Kq + S_pad) D values), so it pays from FQT_MIN_ROWS rows on.
 FQT_MODE = os.environ.get("SQMP_FQT", "auto")   # "auto" | "1" (whenever eligible) | "0"
-FQT_MIN_ROWS = int(os.environ.get("SQMP_FQT_MIN_ROWS", "8192"))
+# from 16384 rows: with fq7 as the packed-order GEMM, the packed order wins at 8192 rows (Llama
+# layer forward 3267 vs 3587 us) and the activation order at 16384 (config 2: 0.536 vs 0.556 ms)
+FQT_MIN_ROWS = int(os.environ.get("SQMP_FQT_MIN_ROWS", "16384"))
 
 
 def fqt_eligible(pw: PackedWeight, act_quant: str, act_bits: int, group_size: int,
