@@ -172,6 +172,9 @@ int sqmp_quant_act(void* x, int dtype, int M, int K, int amode, int n_bits,
                                  x -- sqmp_gemm_fq_colmax's epilogue -- so the column
                                  statistics pass is skipped (output quantization fused into
                                  the GEMM epilogue, fake_quant.py:308-316) */
+#define SQMP_QA_TILED 8       /* SQMP_OUT_C4: codes, group scales and salient x written in the
+                                 tile-major layouts of sqmp_gemm_fqt7 (sqmp_fq7_sizes with
+                                 J = 2 and N = M gives their sizes) instead of row-major */
 
 /* sqmp_quant_act with the per-weight map posmap (int32 [K]: packed position of column k,
  * the inverse of perm; NULL = derive it per call) and flags.  With posmap, OUT_FP on
@@ -297,6 +300,14 @@ int sqmp_quant_act_c4(void* x, int dtype, int M, int K, int amode, int n_bits, i
 int sqmp_gemm_fqt(const void* acodes, const void* ascale, const void* xs, const void* wp,
                   const void* bias, void* y, int dtype, int M, int N, int Kq, int S_pad,
                   int G, int ngq, void* stream);
+
+/* sqmp_gemm_fqt on the tile-major activation operands that sqmp_quant_act_c4 writes with
+ * SQMP_QA_TILED (codes [R][Kq/2], scales [R/32][ngq][32], xs [R][S_pad] in the layouts of
+ * sqmp_pack_fq7 with J = 2, R = roundup(M, 256)): the act codes ride in registers like
+ * sqmp_gemm_fq7's weight codes; the same values as sqmp_gemm_fqt.  Kq % 128 == 0. */
+int sqmp_gemm_fqt7(const void* codes_t, const void* scale_t, const void* sal_t, const void* wp,
+                   const void* bias, void* y, int dtype, int M, int N, int Kq, int S_pad,
+                   int G, int ngq, void* stream);
 
 /* fp32 models (the reference runs OPT in fp32): the faithful GEMM on the bf16 MFMA.
  * sqmp_split3_bf16: src fp32 [R][L] -> three bf16 planes dst [3][ldr][L] with

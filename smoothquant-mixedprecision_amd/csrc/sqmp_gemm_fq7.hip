@@ -105,7 +105,11 @@ __host__ __device__ inline int brev3(int c) { return ((c & 1) << 2) | (c & 2) | 
 // per-stage barrier
 // J = 16-row weight tiles per wave: tile TM x TN with TN = 8 * 16 J (J = 4: 128 x 512;
 // J = 2: 256 x 256, fq6's decode-optimal shape -- a decoded fragment feeds TM / 16 MFMAs)
-template <class DT, int GB, int TM, int J, int DIAG = 0>
+// TR (sqmp_gemm_fqt on the tile-major activation operands): A = the permuted weight wp,
+// the register operand = the activation codes / group scales / salient x in this kernel's
+// tile-major layouts (sqmp_quant_act_c4 writes them so with ldsc < 0); kernel M = weight
+// rows, kernel N = tokens, Y[n][m] stored transposed with the bias per kernel row.
+template <class DT, int GB, int TM, int J, int DIAG = 0, bool TR = false>
 __global__ __launch_bounds__(512, 1) void gemm_fq7_kernel(
     const typename DT::T* __restrict__ A, const uint32_t* __restrict__ Bt,
     const typename DT::T* __restrict__ St, const typename DT::T* __restrict__ Salt,
@@ -119,7 +123,8 @@ __global__ __launch_bounds__(512, 1) void gemm_fq7_kernel(
   constexpr int SLOT = TM * 128;        // TM rows x 64 positions x 2 B
   constexpr int NA = TM / 64;           // A pieces per wave per stage
   constexpr int PF = TM == 256 ? 2 : 3;  // A fragment read-ahead (blocks; 2 keeps TM = 256 spill-free)
-  constexpr int LDS_BYTES = NS * SLOT > TM * TN * 2 ? NS * SLOT : TM * TN * 2;
+  constexpr int EPI = TR ? TN * (2 * TM + 16) : TM * TN * 2;  // epilogue staging bytes
+  constexpr int LDS_BYTES = NS * SLOT > EPI ? NS * SLOT : EPI;
   static_assert(J <= I, "sub-step 1 decode must finish before block I");
   __shared__ __attribute__((aligned(16))) unsigned char lds[LDS_BYTES];
 
@@ -325,6 +330,32 @@ __global__ __launch_bounds__(512, 1) void gemm_fq7_kernel(
   // c ^ (m & 15)), stored as whole rows, one 16-B chunk per lane
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   barrier();  // every wave is past its last read of the ring
+  if constexpr (TR) {
+    // y^T staged [nl TN][ml TM] at a row stride of 2 TM + 16 bytes (the four q groups of a
+    // write land 16 banks apart), stored as TM-wide row pieces of Y[n][m]
+    constexpr int RS = 2 * TM + 16;
+#pragma unroll
+    for (int i = 0; i < I; ++i) {
+      const int ml = 16 * i + r16;
+      const float bv = bias && m0 + ml < M ? DT::to_f(bias[m0 + ml]) : 0.f;
+#pragma unroll
+      for (int j = 0; j < J; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          *(T*)(lds + (WR * wave + 16 * j + 4 * q + r) * RS + ml * 2) = DT::from_f(acc[i][j][r] + bv);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    barrier();
+    constexpr int CPR = TM / 8;  // 16-B chunks per staged row
+#pragma unroll 4
+    for (int k = tid; k < TN * CPR; k += 512) {
+      const int nl = k / CPR, c = k % CPR;
+      const int gn = n0 + nl, gm = m0 + c * 8;
+      if (gn < N && gm < M)  // M % 8 == 0 (launcher)
+        *(u32x4*)(Y + (size_t)gn * M + gm) = *(const u32x4*)(lds + nl * RS + c * 16);
+    }
+    return;
+  }
   float cmx[J][4] = {};
 #pragma unroll
   for (int j = 0; j < J; ++j) {
@@ -488,6 +519,21 @@ static int dispatch(const void* a, const void* bt, const void* st, const void* s
 #undef SQMP_FQ7
 }
 
+// the activation-order GEMM (TR): kernel M = weight rows N (wp rows), kernel N = tokens M
+template <class DT>
+static int dispatch_tr(const void* wp, const void* codes_t, const void* scale_t, const void* sal_t,
+                       const void* bias, void* y, int M, int N, int Kq, int S_pad, int G, int ngq,
+                       hipStream_t s) {
+  typedef typename DT::T T;
+  constexpr int TM = std::is_same<DT, BF16>::value ? 128 : 256;
+  const int tiles_m = cdiv(N, TM), tiles_n = cdiv(M, 256);
+  gemm_fq7_kernel<DT, 1, TM, 2, 0, true><<<dim3(tiles_m * tiles_n), dim3(512), 0, s>>>(
+      (const T*)wp, (const uint32_t*)codes_t, (const T*)scale_t, (const T*)sal_t, (const T*)bias,
+      (T*)y, N, M, Kq, S_pad, G, ngq, tiles_m, tiles_n, group_m_env(), nullptr);
+  SQMP_LAUNCH_CHECK();
+  return SQMP_OK;
+}
+
 }  // namespace fq7
 
 // rows of the tile-major copies: N rounded up to the 128 J-row tile
@@ -554,6 +600,24 @@ extern "C" int sqmp_gemm_fq7(const void* a, const void* codes_t, const void* sca
   if (dtype == SQMP_F16)
     return fq7::dispatch<F16>(a, codes_t, scale_t, sal_t, bias, y, M, N, Kp, S_pad, Gw, ngw, J, colmax, s);
   return fq7::dispatch<BF16>(a, codes_t, scale_t, sal_t, bias, y, M, N, Kp, S_pad, Gw, ngw, J, colmax, s);
+}
+
+// sqmp_gemm_fqt7: the activation-order GEMM (sqmp_gemm_fqt) on fq7's register-operand
+// structure, its activation operands in the tile-major layout (J = 2) that sqmp_quant_act_c4
+// writes when called with the SQMP_QA_TILED flag
+extern "C" int sqmp_gemm_fqt7(const void* codes_t, const void* scale_t, const void* sal_t,
+                              const void* wp, const void* bias, void* y, int dtype, int M, int N,
+                              int Kq, int S_pad, int G, int ngq, void* stream) {
+  if (!codes_t || !scale_t || !sal_t || !wp || !y) return SQMP_EINVAL;
+  if (M < 0 || N <= 0 || Kq <= 0 || Kq % 128 || S_pad < 0 || S_pad % 64 || G <= 0 || ngq <= 0)
+    return SQMP_EINVAL;
+  if (dtype != SQMP_F16 && dtype != SQMP_BF16) return SQMP_EUNSUPPORTED;
+  if (G % 64 || N % 8) return SQMP_EUNSUPPORTED;
+  if (M == 0) return SQMP_OK;
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == SQMP_F16)
+    return fq7::dispatch_tr<F16>(wp, codes_t, scale_t, sal_t, bias, y, M, N, Kq, S_pad, G, ngq, s);
+  return fq7::dispatch_tr<BF16>(wp, codes_t, scale_t, sal_t, bias, y, M, N, Kq, S_pad, G, ngq, s);
 }
 
 }  // namespace sqmp

@@ -297,6 +297,9 @@ FQT_MODE = os.environ.get("SQMP_FQT", "auto")   # "auto" | "1" (whenever eligibl
 # from 16384 rows: with fq7 as the packed-order GEMM, the packed order wins at 8192 rows (Llama
 # layer forward 3267 vs 3587 us) and the activation order at 16384 (config 2: 0.536 vs 0.556 ms)
 FQT_MIN_ROWS = int(os.environ.get("SQMP_FQT_MIN_ROWS", "16384"))
+# the activation-order GEMM on fq7's structure (sqmp_gemm_fqt7: tile-major activation
+# operands written by the quantizer) when Kq % 128 == 0, else on fq6's (sqmp_gemm_fqt)
+FQT7 = os.environ.get("SQMP_FQT7", "1") == "1"
 
 
 def fqt_eligible(pw: PackedWeight, act_quant: str, act_bits: int, group_size: int,
@@ -315,7 +318,10 @@ def quant_act_c4(x2: torch.Tensor, pw: PackedWeight, act_quant: str, n_bits: int
                  group_size: int, stats_of: Optional[torch.Tensor] = None):
     """x [M, K] -> the activation-order operands of gemm_fqt: (int4 codes [M, Kq/2] bytes,
     D group scales [Kq/G, Mp], exact salient x [M, S_pad], permuted weight [Np, Kq + S_pad])
-    with Kq = roundup(K - S, 64).  Statistics reuse as quant_act_fp."""
+    with Kq = roundup(K - S, 64).  With FQT7 and Kq % 128 == 0 the first three are in
+    sqmp_gemm_fqt7's tile-major layouts (SQMP_QA_TILED): codes [R, Kq/2], scales
+    [R/32, Kq/G, 32] (3-d marks the layout), xs [R, S_pad][:M], R = roundup(M, 256).
+    Statistics reuse as quant_act_fp."""
     _require_gpu(x2, "quant_act")
     M, K = x2.shape
     Mp = _pad_rows(M)
@@ -323,14 +329,20 @@ def quant_act_c4(x2: torch.Tensor, pw: PackedWeight, act_quant: str, n_bits: int
     Kq = (Kn + 63) // 64 * 64
     ngq = (Kn + group_size - 1) // group_size
     dev = x2.device
-    codes = torch.empty((Mp, Kq // 2), dtype=torch.uint8, device=dev)[:M]
-    scales = torch.empty((ngq, Mp), dtype=x2.dtype, device=dev)
-    xs = torch.empty((Mp, max(pw.S_pad, 8)), dtype=x2.dtype, device=dev)[:M]
+    tiled = FQT7 and Kq % 128 == 0
+    if tiled:
+        codes = torch.empty((Mp, Kq // 2), dtype=torch.uint8, device=dev)
+        scales = torch.empty((Mp // 32, ngq, 32), dtype=x2.dtype, device=dev)
+        xs = torch.empty((Mp, max(pw.S_pad, 64)), dtype=x2.dtype, device=dev)[:M]
+    else:
+        codes = torch.empty((Mp, Kq // 2), dtype=torch.uint8, device=dev)[:M]
+        scales = torch.empty((ngq, Mp), dtype=x2.dtype, device=dev)
+        xs = torch.empty((Mp, max(pw.S_pad, 8)), dtype=x2.dtype, device=dev)[:M]
     lib = load()
     nb = _ws_bytes(M, K, pw.Kp)
     stream = torch.cuda.current_stream(dev).cuda_stream
     e = _act_ws(dev, stream, K, pw.Kp, nb)
-    flags = _lib.QA_CLEAN_WS
+    flags = _lib.QA_CLEAN_WS | (_lib.QA_TILED if tiled else 0)
     src = x2 if stats_of is None else stats_of
     skey = (src.data_ptr(), tuple(src.shape), src.dtype, src._version, pw.sal_key, act_quant,
             M, K)
@@ -360,9 +372,14 @@ def quant_act_c4(x2: torch.Tensor, pw: PackedWeight, act_quant: str, n_bits: int
 def gemm_fqt(codes: torch.Tensor, scales: torch.Tensor, xs: torch.Tensor, wp: torch.Tensor,
              pw: PackedWeight, bias: Optional[torch.Tensor], group_size: int) -> torch.Tensor:
     """y = D(x_hat . W_hat^T + bias) on the activation-order operands of quant_act_c4."""
-    M = codes.shape[0]
+    M = xs.shape[0]
     y = torch.empty((M, pw.N), dtype=pw.dtype, device=codes.device)
     Kq = codes.shape[1] * 2
+    if scales.dim() == 3:   # tile-major (SQMP_QA_TILED)
+        check(load().sqmp_gemm_fqt7(_p(codes), _p(scales), _p(xs), _p(wp), _p(bias), _p(y),
+                                    _dtype_code(pw.dtype), M, pw.N, Kq, pw.S_pad, group_size,
+                                    scales.shape[1], _stream(codes)), "gemm_fqt7")
+        return y
     check(load().sqmp_gemm_fqt(_p(codes), _p(scales), _p(xs) if pw.S_pad else None, _p(wp),
                                _p(bias), _p(y), _dtype_code(pw.dtype), M, pw.N, Kq, pw.S_pad,
                                group_size, scales.shape[0], _stream(codes)), "gemm_fqt")

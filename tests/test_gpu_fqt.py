@@ -9,6 +9,9 @@ gemm_fq), whose operands are pinned bit-exactly to the reference (test_gpu_parit
     bit-exact that of the dequantized packed weight, zeros past K - S, wsal after;
   * y: the same products summed in another order, relative Frobenius vs gemm_fq 1e-3
     (fp16) / 8e-3 (bf16), and vs the fp32 product of the path's own operands 2e-3 / 1e-2.
+
+Both operand layouts: row-major (sqmp_gemm_fqt on fq6's structure) and tile-major
+(SQMP_QA_TILED + sqmp_gemm_fqt7, untiled here before the same checks).
 """
 import pytest
 import torch
@@ -60,6 +63,30 @@ def decode_c4(codes, scales, Kq, G, dt):
     return (code * s).to(dt)                                 # D(code * s): exact in fp32
 
 
+def untile_c4(codes_t, scales_t, xs_t, M, Kq, S_pad):
+    """The tile-major operands (sqmp_pack_fq7 layouts, J = 2) -> row-major codes [M, Kq/2],
+    scales [ngq, R], xs [M, S_pad]."""
+    R = codes_t.shape[0]
+    KB = Kq // 64
+    w = codes_t.contiguous().view(torch.int32).reshape(R // 32, KB, 4, 16, 2, 2)  # nb kb q r j s
+    codes = w.permute(0, 4, 3, 1, 2, 5).reshape(R, KB * 8).contiguous().view(torch.uint8)[:M]
+    ngq = scales_t.shape[1]
+    scales = scales_t.reshape(R // 32, ngq, 16, 2).permute(1, 0, 3, 2).reshape(ngq, R)
+    xs = None
+    if S_pad:
+        W = xs_t.stride(0)
+        flat = torch.as_strided(xs_t, (R * W,), (1,))[: R * S_pad]
+        t = flat.reshape(R // 32, S_pad // 64, 4, 16, 2, 2, 8)         # nb kd q r j s e
+        xs = torch.empty((R, S_pad), dtype=xs_t.dtype, device=xs_t.device)
+        v = xs.view(R // 32, 2, 16, S_pad // 64, 8, 8)                 # nb j r kd c e
+        for q in range(4):
+            for sl in range(2):
+                c = 4 * (q & 1) + 2 * sl + (q >> 1)
+                v[:, :, :, :, c, :] = t[:, :, q, :, :, sl, :].permute(0, 3, 2, 1, 4)
+        xs = xs[:M]
+    return codes, scales, xs
+
+
 CASES = [
     # M, K, N, G, p, dtype, act mode
     (64, 512, 256, 128, 0.10, torch.float16, "per_group"),
@@ -70,18 +97,31 @@ CASES = [
     (2048, 4096, 4096, 64, 0.05, torch.float16, "per_group"),
     (333, 768, 3072, 128, 0.10, torch.bfloat16, "per_group"),
     (513, 2048, 264, 64, 0.05, torch.float16, "per_group_unsorted"),
+    (777, 1024, 1032, 128, 0.05, torch.bfloat16, "per_group"),
 ]
 
 
+@pytest.mark.parametrize("tiled", [False, True], ids=["rowmajor", "tiled"])
 @pytest.mark.parametrize("M,K,N,Gs,p,dt,aq", CASES)
-def test_fqt_operands_exact_and_y(M, K, N, Gs, p, dt, aq):
+def test_fqt_operands_exact_and_y(M, K, N, Gs, p, dt, aq, tiled):
     dev = _dev()
     from smoothquant import ops
     q, lin, x = _layer(dev, M, K, N, Gs, p, dt, aq=aq)
     pw = q.packed()
     assert ops.fqt_eligible(pw, aq, 4, Gs, M, force=True)
-    codes, scales, xs, wp = ops.quant_act_c4(x, pw, aq, 4, Gs)
+    Kq = (pw.K - pw.S + 63) // 64 * 64
+    if tiled and Kq % 128:
+        pytest.skip("tile-major operands need Kq % 128 == 0")
+    fqt7 = ops.FQT7
+    ops.FQT7 = tiled
+    try:
+        codes, scales, xs, wp = ops.quant_act_c4(x, pw, aq, 4, Gs)
+    finally:
+        ops.FQT7 = fqt7
+    assert (scales.dim() == 3) == tiled
     y = ops.gemm_fqt(codes, scales, xs, wp, pw, lin.bias, Gs)
+    if tiled:
+        codes, scales, xs = untile_c4(codes, scales, xs, M, Kq, pw.S_pad)
     a = ops.quant_act_fp(x, pw, aq, 4, Gs)
     fq7 = ops.FQ7_AUTO
     ops.FQ7_AUTO = False
@@ -89,7 +129,7 @@ def test_fqt_operands_exact_and_y(M, K, N, Gs, p, dt, aq):
         y_fq = ops.gemm_fq(a, pw, lin.bias)
     finally:
         ops.FQ7_AUTO = fq7
-    Kn, Kq = pw.K - pw.S, codes.shape[1] * 2
+    Kn = pw.K - pw.S
     # activation operand: multisets per row over the non-salient columns, bit-exact
     xa = decode_c4(codes, scales, Kq, Gs, dt)
     assert (xa[:, Kn:] == 0).all()
