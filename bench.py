@@ -378,6 +378,7 @@ def main(argv=None):
     prof = os.path.join(ROOT, "profiles", "r02_pmc_gemm_f6_per_token.json" if kdt == "f6"
                         else "r02_pmc_gemm_f8v2_per_token.json" if kdt == "f8"
                         else "r02_pmc_gemm_h2_fp32.json" if fp32
+                        else "r02_pmc_gemm_fqt7_per_group.json" if use_fqt and "fqt7" in kname
                         else "r02_pmc_gemm_fqt_per_group.json" if use_fqt
                         else f"r02_pmc_gemm_fq6_{args.act}.json")
     if os.path.exists(prof):
