@@ -459,6 +459,16 @@ static int group_m_env() {
   return v;
 }
 
+// the activation-order (TR) launch: 4 weight-row tiles per raster group (same box, config 2:
+// GEMM 422.5 vs 429.8 us at 8, alternating runs); SQMP_FQT7_GROUP_M overrides
+static int group_m_tr_env() {
+  static int v = [] {
+    const char* e = getenv("SQMP_FQT7_GROUP_M");
+    return e && atoi(e) > 0 ? atoi(e) : 4;
+  }();
+  return v;
+}
+
 static int diag_env() {
   static int v = [] {
     const char* e = getenv("SQMP_FQ7_DIAG");
@@ -529,7 +539,7 @@ static int dispatch_tr(const void* wp, const void* codes_t, const void* scale_t,
   const int tiles_m = cdiv(N, TM), tiles_n = cdiv(M, 256);
   gemm_fq7_kernel<DT, 1, TM, 2, 0, true><<<dim3(tiles_m * tiles_n), dim3(512), 0, s>>>(
       (const T*)wp, (const uint32_t*)codes_t, (const T*)scale_t, (const T*)sal_t, (const T*)bias,
-      (T*)y, N, M, Kq, S_pad, G, ngq, tiles_m, tiles_n, group_m_env(), nullptr);
+      (T*)y, N, M, Kq, S_pad, G, ngq, tiles_m, tiles_n, group_m_tr_env(), nullptr);
   SQMP_LAUNCH_CHECK();
   return SQMP_OK;
 }
