@@ -277,7 +277,10 @@ class W4A4Linear(nn.Module):
         if self.output_quant_name != "None" and self.salient_indices is None:
             _, _, self.out_amap_fq, self.out_nonsal = ops.build_maps(pw.N, None, pw.codes.device)
 
-    def _pack_from(self, w: torch.Tensor, weight_quant: str):
+    def _pack_from(self, w: torch.Tensor, weight_quant: str, want_w_hat: bool = False):
+        """Pack w on the GPU (a CPU-resident w is packed on cuda and the module moved back
+        to w's device).  want_w_hat: also return W_hat (the reference's dequantized weight)
+        on w's device, computed on the GPU before any move back."""
         dev = w.device
         wg = w.detach()
         if dev.type != "cuda":
@@ -288,8 +291,10 @@ class W4A4Linear(nn.Module):
         pw = ops.pack_weight(wg, weight_quant if weight_quant in _WEIGHT_EXT else "none",
                              self.quant_bits, self.group_size, sal)
         self._install(pw, weight_quant)
+        w_hat = ops.dequant_weight(pw).to(dev) if want_w_hat else None
         if dev.type != "cuda":
             self.to(dev)
+        return w_hat
 
     def packed(self) -> PackedWeight:
         # One PackedWeight per buffer set: reused while every buffer is the same object and
@@ -427,10 +432,12 @@ class W4A4Linear(nn.Module):
     def _apply(self, fn, recurse=True):
         # A dtype cast (model.half(), .float(), .to(torch.bfloat16)) turns the reference's
         # dequantized W_hat buffer into cast(W_hat) (fake_quant.py:272-277 / nn.Module).
-        # The packed form survives the cast when cast(code * s) == code * cast(s) for every
-        # weight (e.g. fp16 / bf16 -> fp32 always): the codes stay, the scales and the
-        # salient slice are cast.  Otherwise the layer keeps the reference's values as a
-        # dense operand and says so (a dense GEMM moves 4x the weight bytes).
+        # The packed form is kept only when the check in _apply_cast passes, i.e.
+        # cast(W_hat) == D'(code * cast(s)) for every weight (D(code*s) may round, so even an
+        # up-cast is not guaranteed): the codes stay, the scales and the salient slice are
+        # cast.  Otherwise the layer keeps the reference's values as a dense operand and
+        # says so (a dense GEMM moves 4x the weight bytes).  The check dequantizes once per
+        # dtype cast, not per forward.
         if self._meta is not None and self.w_scale is not None:
             old = self._meta["dtype"]
             probe = fn(torch.empty(0, dtype=old, device=self.w_scale.device))
@@ -576,13 +583,15 @@ class W4A4Linear(nn.Module):
                                 group_size=group_size)
         if weight_quant not in _WEIGHT_EXT:
             raise ValueError(f"Invalid weight_quant: {weight_quant}")         # :361
-        new_module._pack_from(module.weight.data, weight_quant)
-        if weight_quant in ("per_channel", "per_tensor"):
+        in_place = weight_quant in ("per_channel", "per_tensor")
+        w_hat = new_module._pack_from(module.weight.data, weight_quant, want_w_hat=in_place)
+        if in_place:
             # the reference quantizes module.weight IN PLACE for these modes and then
             # restores the salient columns through the alias (:349-355, :363-365): the
-            # source Linear (and any weight tied to it) ends up holding W_hat
+            # source Linear (and any weight tied to it) ends up holding W_hat.  W_hat is
+            # dequantized on the GPU inside _pack_from, so a CPU-resident source works too.
             with torch.no_grad():
-                module.weight.data.copy_(new_module.weight.to(module.weight.device))
+                module.weight.data.copy_(w_hat)
         if module.bias is not None:
             new_module.bias = module.bias                                     # :369-370
         return new_module

@@ -308,10 +308,12 @@ def fqt_eligible(pw: PackedWeight, act_quant: str, act_bits: int, group_size: in
     threshold)."""
     if not force and (FQT_MODE == "0" or (FQT_MODE == "auto" and M < FQT_MIN_ROWS)):
         return False
+    # the C4 quantizer's limits (quant_lc_supported in sqmp_actquant_lc.hip): power-of-two
+    # groups of 64 .. 64 * LC_RPL = 1024 ranks (a group never straddles a wave's ranks)
     return (act_quant in _SORTED or act_quant == "per_group_unsorted") and act_bits <= 4 \
         and pw.n_bits == 4 and pw.dense is None and pw.dtype != torch.float32 \
-        and group_size % 64 == 0 and pw.N % 8 == 0 and pw.K % 8 == 0 and pw.K <= 16384 \
-        and pw.K - pw.S > 0
+        and 64 <= group_size <= 1024 and group_size & (group_size - 1) == 0 \
+        and pw.N % 8 == 0 and pw.K % 8 == 0 and pw.K <= 16384 and pw.K - pw.S > 0
 
 
 def quant_act_c4(x2: torch.Tensor, pw: PackedWeight, act_quant: str, n_bits: int,

@@ -6,7 +6,8 @@
 
 The split is joined with "\\n\\n" and tokenized once into a [1, T] id stream.  Window i is
 ids[:, i*B:(i+1)*B]; its negative log-likelihood is B x the mean cross-entropy of the
-B-1 next-token predictions (fp32 logits), and PPL = exp(sum of window NLLs / (n*B)).
+B-1 next-token predictions (fp32 logits) -- B = batch_size for every window, a short last
+window included, as the reference computes it -- and PPL = exp(sum of window NLLs / (n*B)).
 n_samples=None/0 means every full window.  Without hub access pass a dataset with a
 "text" column, or the token ids directly (`input_ids=`).  `last_tokens_per_s` is the
 throughput of the last evaluate() (windows x B tokens over its wall time).
@@ -25,13 +26,15 @@ except ImportError:  # pragma: no cover
         return it
 
 
-def window_nll(model, window: torch.Tensor) -> torch.Tensor:
-    """B x mean next-token cross-entropy of one [1, B] window (fp32 scalar tensor)."""
+def window_nll(model, window: torch.Tensor, batch_size=None) -> torch.Tensor:
+    """batch_size x mean next-token cross-entropy of one [1, B] window (fp32 scalar tensor).
+    The reference scales EVERY window by self.batch_size (run_experiments.py:120), also a
+    short last window; batch_size=None uses the window's own length."""
     logits = model(window).logits
     pred = logits[:, :-1, :].float()
     target = window[:, 1:].to(pred.device)
     ce = F.cross_entropy(pred.reshape(-1, pred.shape[-1]), target.reshape(-1))
-    return ce.float() * window.shape[1]
+    return ce.float() * (window.shape[1] if batch_size is None else batch_size)
 
 
 def _model_device(model, fallback):
@@ -63,7 +66,7 @@ class Evaluator:
         dev = _model_device(model, self.device)
         wins = self.windows()
         start = time.perf_counter()
-        total = torch.stack([window_nll(model, w.to(dev))
+        total = torch.stack([window_nll(model, w.to(dev), self.batch_size)
                              for w in _progress(wins, desc="Evaluating")]).sum()
         if torch.cuda.is_available():
             torch.cuda.synchronize()

@@ -32,6 +32,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 sys.path.insert(0, os.path.dirname(HERE))
 from gen_golden import _StableTorch, load_reference  # noqa: E402
+
+REF_SMOOTH = "/root/reference/smoothquant/smooth.py"
 import config_cases as C  # noqa: E402
 
 
@@ -78,21 +80,73 @@ def _rel(a, b):
     return float((a.double() - b.double()).norm() / b.double().norm())
 
 
+@torch.no_grad()
+def act_scales_of(model, blocks):
+    """{linear name: per-channel max|x| over the blocks, fp32} -- the statistic of
+    calibration.get_act_scales (calibration.py:13-51) on the given token blocks."""
+    scales = {}
+
+    def hook(name, m, inp, out):
+        x = inp[0] if isinstance(inp, tuple) else inp
+        cur = x.view(-1, x.shape[-1]).abs().max(dim=0)[0].float().cpu()
+        scales[name] = cur if name not in scales else torch.max(scales[name], cur)
+
+    hs = [m.register_forward_hook(lambda m, i, o, n=n: hook(n, m, i, o))
+          for n, m in model.named_modules() if isinstance(m, nn.Linear)]
+    for b in blocks:
+        model(b)
+    for h in hs:
+        h.remove()
+    return scales
+
+
+def load_smooth():
+    import importlib.util
+    sys.dont_write_bytecode = True
+    spec = importlib.util.spec_from_file_location("_ref_smooth", REF_SMOOTH)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
 def main():
     ref = load_reference()
     torch.set_num_threads(os.cpu_count() or 8)
     arrays, cases = {}, {}
+    only = None
+    if "--only" in sys.argv:
+        # regenerate the named cases, keep every other case of the existing fixture
+        only = set(sys.argv[sys.argv.index("--only") + 1].split(","))
+        old = np.load(C.GOLDEN, allow_pickle=False)
+        old_meta = json.loads(bytes(old["meta_json"]).decode())
+        for k in old.files:
+            if k != "meta_json" and k.split("__")[0] not in only:
+                arrays[k] = old[k]
+        cases = {k: v for k, v in old_meta["cases"].items() if k not in only}
     for case in C.CASES:
         t0 = time.time()
         key = case["key"]
+        if only is not None and key not in only:
+            continue
         model = C.build(case)
-        imp = importance_of(model, C.tokens(case, "cal"))
-        for n, v in imp.items():
-            arrays[f"{key}__imp__{n}"] = v.numpy()
-        # input_feat as the quantizers index it ("model." + module path); one-element lists
-        # so sum(...) returns the stored fp32 importance unchanged
-        feat = {n: [v] for n, v in imp.items()}
-        q = getattr(ref, case["quantizer"])(model, input_feat=feat, **case["kwargs"])
+        if case.get("smooth") is not None:
+            sc = act_scales_of(model, C.tokens(case, "cal"))
+            for n, v in sc.items():
+                arrays[f"{key}__act__{n}"] = v.numpy()
+            load_smooth().smooth_lm(model, sc, case["smooth"])
+        w_orig = {n: m.weight.detach().clone() for n, m in model.named_modules()
+                  if isinstance(m, nn.Linear)}
+        if case.get("input_feat", True):
+            imp = importance_of(model, C.tokens(case, "cal"))
+            for n, v in imp.items():
+                arrays[f"{key}__imp__{n}"] = v.numpy()
+            # input_feat as the quantizers index it ("model." + module path); one-element
+            # lists so sum(...) returns the stored fp32 importance unchanged
+            feat = {n: [v] for n, v in imp.items()}
+            q = getattr(ref, case["quantizer"])(model, input_feat=feat, **case["kwargs"])
+        else:
+            q = getattr(ref, case["quantizer"])(model, **case["kwargs"])
+        C.post_quantize(q, case, ref, w_orig)
         linears = {}
         for n, m in q.named_modules():
             if type(m).__name__ != "W4A4Linear":

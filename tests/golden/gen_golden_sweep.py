@@ -27,10 +27,14 @@ import numpy as np
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from gen_golden import TORCH_DT, load_reference, make_x, to_np  # noqa: E402
+import sweep_inputs as SI  # noqa: E402
 
 OUT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "sweep_golden.npz")
 
+# cases from this index on are stored by digest (inputs re-drawn: tests/sweep_inputs.py)
+DIGEST_FROM = 8
 # dtype, sort (max|none), act_bits, salient_prop, G, x_shape, K, N, bias
 CASES = [
     ("fp16", "max", 8, 0.05, 64, (48,), 256, 128, True),
@@ -41,23 +45,44 @@ CASES = [
     ("bf16", "max", 8, 0.05, 64, (48,), 256, 128, True),
     ("bf16", "none", 4, 0.05, 64, (48,), 256, 128, False),
     ("fp16", "max", 8, 0.0, 64, (48,), 256, 128, True),
+    # round 3: the sweep's larger groups (run_experiments.py:262 goes to 1024), including
+    # the Llama-2-7B down_proj width K = 11008 at G = 1024 (11 act groups, the weight's
+    # last group padded by 256 zero columns) for W4A8, sort=none and W4A4 max
+    ("fp16", "max", 8, 0.05, 256, (64,), 1024, 96, True),
+    ("fp16", "none", 4, 0.05, 256, (64,), 1024, 96, True),
+    ("fp16", "none", 8, 0.05, 256, (48,), 1000, 64, False),
+    ("fp16", "max", 8, 0.05, 1024, (16,), 11008, 16, True),
+    ("fp16", "none", 4, 0.05, 1024, (16,), 11008, 16, True),
+    ("fp16", "max", 4, 0.05, 1024, (16,), 11008, 16, True),
+    ("bf16", "none", 8, 0.05, 1024, (16,), 11008, 16, True),
+    ("fp32", "max", 8, 0.05, 256, (40,), 1024, 64, True),
+    ("fp16", "none", 8, 0.0, 1024, (24,), 4096, 32, False),
 ]
 
 
 def gen_case(ref, arrays, meta, i, case):
     dt, sort, abits, p, G, xshape, K, N, bias = case
-    gen = torch.Generator().manual_seed(5000 + i)
-    lin = torch.nn.Linear(K, N, bias=bias)
-    with torch.no_grad():
-        lin.weight.copy_(torch.randn(N, K, generator=gen) * 0.02)
-        if bias:
-            lin.bias.copy_(torch.randn(N, generator=gen) * 0.01)
-    lin = lin.to(TORCH_DT[dt])
+    if i >= DIGEST_FROM:
+        # inputs re-drawn by the tests from the same seed (tests/sweep_inputs.py)
+        w0, b0, x, imp = SI.case_inputs(i, case)
+        lin = torch.nn.Linear(K, N, bias=bias).to(TORCH_DT[dt])
+        with torch.no_grad():
+            lin.weight.copy_(w0)
+            if bias:
+                lin.bias.copy_(b0)
+    else:
+        gen = torch.Generator().manual_seed(5000 + i)
+        lin = torch.nn.Linear(K, N, bias=bias)
+        with torch.no_grad():
+            lin.weight.copy_(torch.randn(N, K, generator=gen) * 0.02)
+            if bias:
+                lin.bias.copy_(torch.randn(N, generator=gen) * 0.01)
+        lin = lin.to(TORCH_DT[dt])
+        n_out = max(1, K // 64)
+        x = make_x(gen, xshape, K, n_out, dt)
+        imp = make_x(gen, (64,), K, n_out, "fp32").abs().mean(0)
     w_in = lin.weight.detach().clone()
     b_in = lin.bias.detach().clone() if bias else None
-    n_out = max(1, K // 64)
-    x = make_x(gen, xshape, K, n_out, dt)
-    imp = make_x(gen, (64,), K, n_out, "fp32").abs().mean(0)
     q = ref.W4A4Linear.from_float(lin, weight_quant="per_group", act_quant="per_group",
                                   importance=imp if p > 0 else None, salient_prop=p,
                                   quant_bits=4, group_size=G)
@@ -83,6 +108,17 @@ def gen_case(ref, arrays, meta, i, case):
         qx = q.act_quant(x2.clone())
     y = q(x.clone())
     key = f"sweep{i}"
+    sal = q.salient_indices
+    if i >= DIGEST_FROM:
+        arrays[key + "_y"] = to_np(y, dt)
+        arrays[key + "_sal"] = (sal.numpy().astype(np.int64) if sal is not None
+                                else np.zeros((0,), np.int64))
+        meta.append(dict(key=key, dtype=dt, sort=sort, w_bits=4, act_bits=abits,
+                         salient_prop=p, group_size=G, x_shape=list(x.shape), K=K, N=N,
+                         bias=bias, has_salient=sal is not None, index=i,
+                         case=[dt, sort, abits, p, G, list(xshape), K, N, bias],
+                         what_sha256=SI.digest(q.weight), qx_sha256=SI.digest(qx)))
+        return
     arrays[key + "_W"] = to_np(w_in, dt)
     arrays[key + "_x"] = to_np(x, dt)
     arrays[key + "_imp"] = imp.numpy().astype(np.float32)
@@ -91,7 +127,6 @@ def gen_case(ref, arrays, meta, i, case):
     arrays[key + "_What"] = to_np(q.weight, dt)
     arrays[key + "_qx"] = to_np(qx, dt)
     arrays[key + "_y"] = to_np(y, dt)
-    sal = q.salient_indices
     arrays[key + "_sal"] = (sal.numpy().astype(np.int64) if sal is not None
                             else np.zeros((0,), np.int64))
     meta.append(dict(key=key, dtype=dt, sort=sort, w_bits=4, act_bits=abits, salient_prop=p,

@@ -96,3 +96,26 @@ def test_evaluator_formula():
             ces.append(torch.nn.functional.cross_entropy(lg.reshape(-1, lg.size(-1)), b[:, 1:].reshape(-1)))
     assert abs(ppl - float(torch.exp(torch.stack(ces).mean()))) <= 1e-3 * ppl
     assert ev.last_tokens_per_s and ev.last_tokens_per_s > 0
+
+
+def test_evaluator_short_last_window_scales_by_batch_size():
+    """n_samples beyond the full windows: the reference scales every window's mean CE by
+    self.batch_size, the short last one too (run_experiments.py:116-123)."""
+    case = MG.cases()[0]
+    model = build_model(case)
+    ids = torch.from_numpy(MG.arr(case["key"], "ev").copy())
+    B = case["eval_window"]
+    n_full = ids.size(1) // B - 1
+    assert n_full >= 1
+    ids = ids[:, : n_full * B + B // 2]          # one half window at the end
+    ev = Evaluator(None, None, "cpu", n_samples=n_full + 1, batch_size=B, input_ids=ids)
+    ppl = float(ev.evaluate(model))
+    nlls = []
+    with torch.no_grad():
+        for i in range(n_full + 1):
+            b = ids[:, i * B:(i + 1) * B]
+            lg = model(b).logits[:, :-1].float()
+            ce = torch.nn.functional.cross_entropy(lg.reshape(-1, lg.size(-1)), b[:, 1:].reshape(-1))
+            nlls.append(ce.float() * B)
+    want = float(torch.exp(torch.stack(nlls).sum() / ((n_full + 1) * B)))
+    assert abs(ppl - want) <= 1e-4 * want

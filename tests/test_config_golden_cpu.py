@@ -1,6 +1,6 @@
 """The PyTorch-CPU restatement (oracle/torch_cpu.py) reproduces the reference's salient
 choice and W_hat bit-exactly (sha256) at the real layer dimensions of BASELINE configs
-1, 3 and 4 (tests/golden/config_golden.npz, generated from the reference): the checker
+1, 3 and 4 and the round-3 config-5 / ppl_eval-flow layers (tests/golden/config_golden.npz, generated from the reference): the checker
 the GPU config tests use is pinned at full size, not only on the small layer goldens."""
 import numpy as np
 import pytest
@@ -14,16 +14,23 @@ CG = C.ConfigGolden()
 
 @pytest.mark.parametrize("case", C.CASES, ids=[c["key"] for c in C.CASES])
 def test_torch_cpu_what_matches_reference_at_full_size(case):
-    key, kw = case["key"], case["kwargs"]
+    key = case["key"]
+    kw = dict(salient_prop=0, quant_bits=4, group_size=128)
+    kw.update(case["kwargs"])
+    kw.update(case.get("test_kwargs", {}))
     meta = CG.case_meta(key)
     model = C.build(case)
+    if case.get("smooth") is not None:
+        # the ppl_eval flow smooths before quantizing (this repo's smooth_lm: plain torch)
+        from smoothquant.smooth import smooth_lm
+        smooth_lm(model, CG.act_scales(key), case["smooth"])
     imp = CG.importance(key)
     mods = dict(model.named_modules())
     assert meta["n_linears"] == len(meta["linears"])
     for n, lm in meta["linears"].items():
         lin = mods[n]
         assert isinstance(lin, torch.nn.Linear)
-        sal = T.select_salient(imp[n], kw["salient_prop"])
+        sal = T.select_salient(imp.get(n), kw["salient_prop"])
         if lm["n_salient"]:
             assert np.array_equal(sal.numpy(), CG.z[f"{key}__sal__{n}"]), n
         else:

@@ -29,7 +29,8 @@ from oracle import torch_cpu as T
 
 pytestmark = pytest.mark.gpu
 
-TOL_Y = {"fp32": 1e-5, "fp16": 2e-3}
+TOL_Y = {"fp32": 1e-5, "fp16": 2e-3, "bf16": 1e-2}
+TOL_F8 = {"fp16": 3e-3, "bf16": 2e-2}
 TOL_LOGITS, TOL_LOSS = 2e-2, 1e-3
 
 
@@ -67,8 +68,18 @@ def test_config_workload_matches_reference(case):
     key, dt = case["key"], case["dtype"]
     meta = CG.case_meta(key)
     model = C.build(case).to("cuda")
-    feat = {n: [v] for n, v in CG.importance(key).items()}
-    q = getattr(FQ, case["quantizer"])(model, input_feat=feat, **case["kwargs"])
+    if case.get("smooth") is not None:
+        # the ppl_eval.py flow: smooth_lm with the fixture's act scales first
+        from smoothquant.smooth import smooth_lm
+        smooth_lm(model, CG.act_scales(key), case["smooth"])
+    kwargs = dict(case["kwargs"])
+    kwargs.update(case.get("test_kwargs", {}))
+    if case.get("input_feat", True):
+        feat = {n: [v] for n, v in CG.importance(key).items()}
+        q = getattr(FQ, case["quantizer"])(model, input_feat=feat, **kwargs)
+    else:
+        q = getattr(FQ, case["quantizer"])(model, **kwargs)
+    C.post_quantize(q, case, FQ)
 
     # ---- surgery + W_hat bit-exact
     layers = {n: m for n, m in q.named_modules() if isinstance(m, W4A4Linear)}
@@ -129,13 +140,23 @@ def test_config_workload_matches_reference(case):
         # the GEMM: our y before any output quantization vs an fp64 product of the exact
         # operands (accumulation-order tolerance)
         bias = None if m.bias is None else m.bias.reshape(-1)
-        y_pre = ops.gemm_fq(a, pw, bias)
+        xin = x2.contiguous()
+        if (m.kernel == "auto" and ops.F8_AUTO and ops.f8_eligible(pw, amode, bits)
+                and ops.f8_input_ok(xin)):
+            # the forward's kernel for per_token / per_tensor 4-bit acts: the FP8 GEMM on
+            # the codes (scales factored out, D rounding of x_hat / W_hat skipped)
+            a8, sa, xs = ops.quant_act_f8(xin, pw, amode, bits)
+            y_pre = ops.gemm_f8(a8, sa, xs, pw, bias)
+            tol = TOL_F8[dt]
+        else:
+            y_pre = ops.gemm_fq(a, pw, bias)
+            tol = TOL_Y[dt]
         yr = qx_ref.cuda().double() @ m.weight.double().t()
         if bias is not None:
             yr = yr + bias.double()
         r = _rel(y_pre.float().cpu().numpy(), yr.cpu().numpy())
         worst = max(worst, r)
-        assert r < TOL_Y[dt], (n, r)
+        assert r < tol, (n, r)
         ospec = resolve_quantizer(m.output_quant)
         if ospec is None:
             assert torch.equal(y.reshape(y_pre.shape), y_pre), n  # forward = this GEMM

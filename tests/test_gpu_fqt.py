@@ -1,20 +1,27 @@
-"""GPU parity of the activation-order faithful path (SQMP_OUT_C4 quantizer,
-sqmp_perm_weight_c4, sqmp_gemm_fqt) against the packed-order path (quant_act_fp +
-gemm_fq), whose operands are pinned bit-exactly to the reference (test_gpu_parity.py).
+"""GPU parity of the activation-order faithful path (SQMP_OUT_C4 quantizer + per-forward
+weight permutation, sqmp_gemm_fqt / sqmp_gemm_fqt7) against the ORACLE
+(oracle/fake_quant_oracle.py, pinned bit-exact to the reference goldens):
 
-  * the activation operand: per row, the multiset of x_hat values over the non-salient
-    columns (decoded from the int4 codes and group scales) is BIT-EXACT that of the
-    packed-order operand, and the exact salient columns are identical;
-  * the permuted weight: per row, the multiset of W_hat over the non-salient columns is
-    bit-exact that of the dequantized packed weight, zeros past K - S, wsal after;
-  * y: the same products summed in another order, relative Frobenius vs gemm_fq 1e-3
-    (fp16) / 8e-3 (bf16), and vs the fp32 product of the path's own operands 2e-3 / 1e-2.
+  * the activation operand, COLUMN FOR COLUMN: act-order position j, decoded from the int4
+    codes and group scales, is bit-exact the oracle's q_x column nonsal[order[j]] (order =
+    the stable sort of the batch's column key, computed independently here); the exact
+    salient columns are x[:, S];
+  * the permuted weight, the same positions: the oracle's W_hat columns, zeros past K - S,
+    then W[:, S] exactly;
+  * y: relative Frobenius vs the fp64 product of the oracle's q_x and W_hat 2e-3 (fp16) /
+    1e-2 (bf16), and vs the packed-order gemm_fq 1e-3 / 8e-3;
+  * the BENCHMARKED kernel at full config-2 size (W4A4Linear.forward on the auto path =
+    fqt7): sampled rows of y against the fp64 product of the PyTorch-CPU restatement's q_x
+    (oracle/torch_cpu.py, batch-wide sort over all 16384 rows) and W_hat.
 
 Both operand layouts: row-major (sqmp_gemm_fqt on fq6's structure) and tile-major
 (SQMP_QA_TILED + sqmp_gemm_fqt7, untiled here before the same checks).
 """
+import numpy as np
 import pytest
 import torch
+
+from oracle import fake_quant_oracle as O
 
 pytestmark = pytest.mark.gpu
 
@@ -101,9 +108,47 @@ CASES = [
 ]
 
 
+def act_order_columns(x_np, sal, aq, D):
+    """The oracle's activation order: position j of the act-order operand holds original
+    column nonsal[order[j]] -- nonsal = the non-salient columns ascending (x[:, mask],
+    fake_quant.py:298), order = the stable ascending sort of their batch key (column
+    absmax :113; mean3std_key for the config-5 extension; identity when unsorted)."""
+    K = x_np.shape[1]
+    keep = np.ones(K, bool)
+    if sal is not None:
+        keep[sal] = False
+    nonsal = np.nonzero(keep)[0]
+    A = x_np[:, nonsal]
+    if aq == "per_group":
+        order = O.stable_argsort(D.f32(np.abs(A).max(axis=0)))
+    elif aq == "per_group_mean3std":
+        order = O.stable_argsort(O.mean3std_key(A, D))
+    else:
+        order = np.arange(len(nonsal))
+    return nonsal[order]
+
+
+def same_values(a, b):
+    """Equal value for value (-0.0 == +0.0: code 0 dequantizes to +0.0, the reference's
+    fake quantizer may give -0.0)."""
+    a = np.asarray(a, np.float32)
+    b = np.asarray(b, np.float32)
+    ok = a == b
+    if not ok.all():
+        idx = np.argwhere(~ok)[:5]
+        print(f"{(~ok).sum()} of {ok.size} differ; first {idx.tolist()}: "
+              f"{a[tuple(idx.T)]} vs {b[tuple(idx.T)]}")
+    return bool(ok.all())
+
+
 @pytest.mark.parametrize("tiled", [False, True], ids=["rowmajor", "tiled"])
 @pytest.mark.parametrize("M,K,N,Gs,p,dt,aq", CASES)
 def test_fqt_operands_exact_and_y(M, K, N, Gs, p, dt, aq, tiled):
+    """Column for column against the ORACLE (oracle/fake_quant_oracle.py, pinned to the
+    reference goldens): act-order position j of the decoded act operand is the oracle's
+    q_x column nonsal[order[j]] and of the permuted weight the oracle's W_hat column, both
+    bit-exact; the salient tails are x[:, S] and W[:, S] exactly; y is within the
+    accumulation-order tolerance of the fp64 product of the oracle's q_x and W_hat."""
     dev = _dev()
     from smoothquant import ops
     q, lin, x = _layer(dev, M, K, N, Gs, p, dt, aq=aq)
@@ -111,7 +156,8 @@ def test_fqt_operands_exact_and_y(M, K, N, Gs, p, dt, aq, tiled):
     assert ops.fqt_eligible(pw, aq, 4, Gs, M, force=True)
     Kq = (pw.K - pw.S + 63) // 64 * 64
     if tiled and Kq % 128:
-        pytest.skip("tile-major operands need Kq % 128 == 0")
+        pytest.skip("tile-major operands need Kq % 128 == 0 (the dispatcher then takes "
+                    "the row-major layout, covered by the rowmajor case)")
     fqt7 = ops.FQT7
     ops.FQT7 = tiled
     try:
@@ -122,6 +168,36 @@ def test_fqt_operands_exact_and_y(M, K, N, Gs, p, dt, aq, tiled):
     y = ops.gemm_fqt(codes, scales, xs, wp, pw, lin.bias, Gs)
     if tiled:
         codes, scales, xs = untile_c4(codes, scales, xs, M, Kq, pw.S_pad)
+    # ---- the oracle's operands (CPU, numpy)
+    Dn = {torch.float16: "fp16", torch.bfloat16: "bf16"}[dt]
+    D = O.DT(Dn)
+    x_np = x.float().cpu().numpy()
+    W_np = lin.weight.detach().float().cpu().numpy()
+    sal = None if q.salient_indices is None else q.salient_indices.numpy().astype(np.int64)
+    wq = "per_group"  # _layer packs the weight per_group (sorted) for every act mode
+    w_hat = D.f32(O.w4a4_from_float(W_np, wq, 4, Gs, sal, D))
+    qx = D.f32(O.quantize_input(D.rnd(x_np), aq, 4, Gs, sal, D))
+    cols = act_order_columns(x_np, sal, aq, D)
+    Kn = pw.K - pw.S
+    assert len(cols) == Kn
+    # act operand, position j <-> original column cols[j]
+    xa = decode_c4(codes, scales, Kq, Gs, dt).float().cpu().numpy()
+    assert same_values(xa[:, :Kn], qx[:, cols])
+    assert (xa[:, Kn:] == 0).all()
+    if pw.S:
+        assert same_values(xs[:, : pw.S].float().cpu().numpy(), x_np[:, pw.salient.cpu().numpy()])
+    # permuted weight, the same positions
+    wpn = wp[: pw.N].float().cpu().numpy()
+    assert same_values(wpn[:, :Kn], w_hat[:, cols])
+    assert (wpn[:, Kn:Kq] == 0).all()
+    if pw.S:
+        assert same_values(wpn[:, Kq: Kq + pw.S], W_np[:, pw.salient.cpu().numpy()])
+    # y against the fp64 product of the oracle's operands
+    bias = lin.bias.detach().double()
+    ref = torch.from_numpy(qx).to(dev).double() @ torch.from_numpy(w_hat).to(dev).double().t() + bias
+    tol = 2e-3 if dt == torch.float16 else 1e-2
+    assert rel(y, ref) < tol
+    # and against the packed-order GEMM (the same operands in another order)
     a = ops.quant_act_fp(x, pw, aq, 4, Gs)
     fq7 = ops.FQ7_AUTO
     ops.FQ7_AUTO = False
@@ -129,42 +205,47 @@ def test_fqt_operands_exact_and_y(M, K, N, Gs, p, dt, aq, tiled):
         y_fq = ops.gemm_fq(a, pw, lin.bias)
     finally:
         ops.FQ7_AUTO = fq7
-    Kn = pw.K - pw.S
-    # activation operand: multisets per row over the non-salient columns, bit-exact
-    xa = decode_c4(codes, scales, Kq, Gs, dt)
-    assert (xa[:, Kn:] == 0).all()
-    nonsal_pos = (pw.amap[: pw.Kp] >= 0).nonzero().flatten()
-    want = a[:, nonsal_pos].float().sort(dim=1).values
-    got = xa[:, :Kn].float().sort(dim=1).values
-    assert torch.equal(got, want)
-    if pw.S_pad:
-        assert torch.equal(xs[:, : pw.S], a[:, pw.Kp: pw.Kp + pw.S])
-    # permuted weight: multisets per row, zeros past Kn, wsal tail
-    w_hat = ops.dequant_weight_packed(pw)
-    wgot = wp[: pw.N, :Kn].float().sort(dim=1).values
-    wwant = w_hat[:, nonsal_pos].float().sort(dim=1).values
-    assert torch.equal(wgot, wwant)
-    assert (wp[: pw.N, Kn:Kq] == 0).all()
-    if pw.S_pad:
-        assert torch.equal(wp[: pw.N, Kq:], pw.wsal)
-    # y
-    ref = xa.float() @ wp[: pw.N, :Kq].float().t() + lin.bias.float()
-    if pw.S_pad:
-        ref = ref + xs[:, : pw.S_pad].float() @ pw.wsal.float().t()
-    tol = 2e-3 if dt == torch.float16 else 1e-2
-    assert rel(y, ref) < tol
     assert rel(y, y_fq) < (1e-3 if dt == torch.float16 else 8e-3)
 
 
 def test_fqt_forward_dispatch_and_full_size_config2():
-    """BASELINE config 2 through W4A4Linear.forward (kernel "fqt" via the auto row threshold)
-    against the packed-order forward."""
+    """BASELINE config 2 (M=16384, K=N=4096, G=128, 10 % salient) through
+    W4A4Linear.forward on the auto path -- the kernel bench.py times (fqt7 on tile-major
+    operands) -- against the oracle directly: sampled rows of y vs the fp64 product of the
+    PyTorch-CPU restatement's q_x (oracle/torch_cpu.py: the batch-wide column sort over all
+    16384 rows, fp16 rounding points of fake_quant.py:104-154) and its W_hat
+    (:156-207 + :347-365), tolerance 2e-3; and vs the packed-order forward 1e-3."""
     dev = _dev()
+    from oracle import torch_cpu as T
     from smoothquant import ops
     q, lin, x = _layer(dev, 16384, 4096, 4096, 128, 0.10, torch.float16)
     pw = q.packed()
     assert ops.fqt_eligible(pw, "per_group", 4, 128, 16384)
-    y_t = q(x)
+    seen = []
+    real = ops.gemm_fqt
+
+    def spy(codes, scales, *a, **k):
+        seen.append(scales.dim())
+        return real(codes, scales, *a, **k)
+
+    ops.gemm_fqt = spy
+    try:
+        y_t = q(x)
+    finally:
+        ops.gemm_fqt = real
+    assert seen == [3], "the auto path must run the tile-major fqt7 GEMM"
+    # the oracle on CPU: q_x over the whole batch, W_hat
+    xc = x.cpu()
+    sal = q.salient_indices.cpu()
+    keep = torch.ones(4096, dtype=torch.bool)
+    keep[sal] = False
+    qx = xc.clone()
+    qx[:, keep] = T.act_quant(xc[:, keep], "per_group", 4, 128)
+    w_hat = T.quantize_weight(lin.weight.detach().cpu(), "per_group", 4, 128, sal)
+    assert torch.equal(q.weight.cpu(), w_hat)
+    rows = torch.arange(0, 16384, 61)
+    ref = qx[rows].double() @ w_hat.double().t() + lin.bias.detach().cpu().double()
+    assert rel(y_t[rows.to(dev)].cpu(), ref) < 2e-3
     q.kernel = "fq"
     y_f = q(x)
     assert rel(y_t, y_f) < 1e-3

@@ -15,6 +15,7 @@ import numpy as np
 import pytest
 import torch
 
+import sweep_inputs as SI
 from oracle import fake_quant_oracle as O
 from test_gpu_parity import TOL_FQ, _dev, bits_equal, make_layer, rel, to_np, to_t
 
@@ -30,14 +31,26 @@ def arr(key, dt):
     return (a.astype(np.uint32) << 16).view(np.float32) if dt == "bf16" else a
 
 
-@pytest.mark.parametrize("m", CASES, ids=[f"{c['key']}-{c['dtype']}-{c['sort']}-a{c['act_bits']}" for c in CASES])
+def case_arrays(m):
+    """(W, x, b, importance) as float32 numpy: stored, or re-drawn for digest cases."""
+    key, dtn = m["key"], m["dtype"]
+    if "index" in m:
+        w, b, x, imp = SI.case_inputs(m["index"], m["case"])
+        f = lambda t: None if t is None else t.float().numpy()  # noqa: E731
+        return f(w), f(x), f(b), imp.numpy().astype(np.float32)
+    W, x = arr(key + "_W", dtn), arr(key + "_x", dtn)
+    b = arr(key + "_b", dtn) if m["bias"] else None
+    return W, x, b, Z[key + "_imp"]
+
+
+@pytest.mark.parametrize("m", CASES, ids=[f"{c['key']}-{c['dtype']}-{c['sort']}-a{c['act_bits']}-G{c['group_size']}-K{c['K']}" for c in CASES])
 def test_sweep_golden(m):
     dev = _dev()
     from smoothquant import fake_quant as FQ
     dtn, key, G = m["dtype"], m["key"], m["group_size"]
-    W, x = arr(key + "_W", dtn), arr(key + "_x", dtn)
-    b = arr(key + "_b", dtn) if m["bias"] else None
-    imp = torch.from_numpy(Z[key + "_imp"])
+    W, x, b, imp = case_arrays(m)
+    imp = torch.from_numpy(imp)
+    digest = "index" in m
     wq = "per_group" if m["sort"] == "max" else "per_group_unsorted"
     q = make_layer(W, b, dtn, dev, weight_quant=wq, act_quant="per_group", importance=imp,
                    salient_prop=m["salient_prop"], quant_bits=4, group_size=G)
@@ -45,12 +58,16 @@ def test_sweep_golden(m):
     fn = (FQ.quantize_activation_per_group_absmax_sort if m["sort"] == "max"
           else FQ.quantize_activation_per_group_absmax)
     q.act_quant = partial(fn, n_bits=m["act_bits"], group_size=G)
-    assert bits_equal(to_np(q.weight), arr(key + "_What", dtn))
-    xt = to_t(x, dtn, dev)
-    y = to_np(q(xt.clone()))
     sal = Z[key + "_sal"] if m["has_salient"] else None
     aq = "per_group" if m["sort"] == "max" else "per_group_unsorted"
-    w_hat = arr(key + "_What", dtn)
+    if digest:
+        assert SI.digest(q.weight) == m["what_sha256"]
+        w_hat = O.DT(dtn).f32(O.w4a4_from_float(W, wq, 4, G, sal, O.DT(dtn)))
+    else:
+        assert bits_equal(to_np(q.weight), arr(key + "_What", dtn))
+        w_hat = arr(key + "_What", dtn)
+    xt = to_t(x, dtn, dev)
+    y = to_np(q(xt.clone()))
     want = O.w4a4_forward(x, w_hat, b, aq, 4, G, sal, False, O.DT(dtn), act_bits=m["act_bits"])
     assert rel(y, want) < TOL_FQ[dtn]
     assert rel(y, arr(key + "_y", dtn)) < TOL_FQ[dtn] * 2
@@ -64,7 +81,10 @@ def test_sweep_golden(m):
         qx[:, mask] = q.act_quant(x2[:, mask].contiguous())
     else:
         qx = q.act_quant(x2.clone())
-    assert bits_equal(to_np(qx), arr(key + "_qx", dtn))
+    if digest:
+        assert SI.digest(qx) == m["qx_sha256"]
+    else:
+        assert bits_equal(to_np(qx), arr(key + "_qx", dtn))
 
 
 @pytest.mark.parametrize("dtn", ["fp16", "bf16", "fp32"])

@@ -13,6 +13,7 @@ import os
 import numpy as np
 import pytest
 
+import sweep_inputs as SI
 from oracle import fake_quant_oracle as O
 
 PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "sweep_golden.npz")
@@ -36,20 +37,38 @@ def modes(m):
     return ("per_group", "per_group") if m["sort"] == "max" else ("per_group_unsorted",) * 2
 
 
-@pytest.mark.parametrize("m", CASES, ids=[f"{c['key']}-{c['dtype']}-{c['sort']}-a{c['act_bits']}" for c in CASES])
+def case_arrays(m):
+    """(W, x, b, importance) of a sweep case as float32 numpy: stored arrays, or for the
+    digest cases re-drawn from the generator's seed (tests/sweep_inputs.py)."""
+    key, dtn = m["key"], m["dtype"]
+    if "index" in m:
+        w, b, x, imp = SI.case_inputs(m["index"], m["case"])
+        f = lambda t: None if t is None else t.float().numpy()  # noqa: E731
+        return f(w), f(x), f(b), imp.numpy().astype(np.float32)
+    W, x = arr(key + "_W", dtn), arr(key + "_x", dtn)
+    b = arr(key + "_b", dtn) if m["bias"] else None
+    return W, x, b, Z[key + "_imp"]
+
+
+@pytest.mark.parametrize("m", CASES, ids=[f"{c['key']}-{c['dtype']}-{c['sort']}-a{c['act_bits']}-G{c['group_size']}-K{c['K']}" for c in CASES])
 def test_sweep_case(m):
     dtn, key = m["dtype"], m["key"]
     dt = O.DT(dtn)
     wq, aq = modes(m)
-    W, x = arr(key + "_W", dtn), arr(key + "_x", dtn)
-    b = arr(key + "_b", dtn) if m["bias"] else None
+    W, x, b, imp = case_arrays(m)
     sal = Z[key + "_sal"] if m["has_salient"] else None
-    assert (O.select_salient(Z[key + "_imp"], m["salient_prop"]) is None) == (sal is None)
+    assert (O.select_salient(imp, m["salient_prop"]) is None) == (sal is None)
+    if sal is not None:
+        assert np.array_equal(O.select_salient(imp, m["salient_prop"]), sal)
     w_hat = O.w4a4_from_float(W, wq, m["w_bits"], m["group_size"], sal, dt)
-    assert np.array_equal(bits(w_hat, dtn), bits(arr(key + "_What", dtn), dtn))
     K = m["K"]
     qx = O.quantize_input(x.reshape(-1, K), aq, m["act_bits"], m["group_size"], sal, dt)
-    assert np.array_equal(bits(qx, dtn), bits(arr(key + "_qx", dtn), dtn))
+    if "index" in m:
+        assert SI.digest(dt.f32(w_hat)) == m["what_sha256"]
+        assert SI.digest(dt.f32(qx)) == m["qx_sha256"]
+    else:
+        assert np.array_equal(bits(w_hat, dtn), bits(arr(key + "_What", dtn), dtn))
+        assert np.array_equal(bits(qx, dtn), bits(arr(key + "_qx", dtn), dtn))
     y = O.w4a4_forward(x, w_hat, b, aq, m["w_bits"], m["group_size"], sal, False, dt,
                        act_bits=m["act_bits"])
     want = arr(key + "_y", dtn).astype(np.float64)

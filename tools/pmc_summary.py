@@ -1,4 +1,4 @@
-"""Summarise rocprofv3 --pmc passes (tools/gpu_pmc.sh layout: <dir>/<kind>_<pass>/
+"""Summarise rocprofv3 --pmc passes (tools/gpu.sh pmc:KIND layout: <dir>/<kind>_<pass>/
 run_counter_collection.csv) into one JSON per GEMM kind with the derived figures DESIGN.md
 quotes, so every fraction can be recomputed from profiles/ alone.
 
