@@ -263,7 +263,7 @@ def main(argv=None):
                            dtype=torch.float32 if fp32 else torch.float16)
     pw = q.packed()
     # what W4A4Linear(kernel="auto") runs for this layer
-    use_f8 = ops.F8_AUTO and ops.f8_eligible(pw, args.act, 4)
+    use_f8 = ops.f8_auto(pw, args.act, 4)
     use_f6 = use_f8 and ops.F6_AUTO and ops.f6_eligible(pw, args.act, 4)
     use_fqt = not use_f8 and ops.fqt_eligible(pw, args.act, 4, G, M)
     stream = torch.cuda.current_stream(dev)

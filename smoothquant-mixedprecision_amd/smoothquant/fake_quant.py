@@ -201,7 +201,7 @@ _PW_KEY = ("w_codes", "w_scale", "w_salient", "w_perm", "w_amap", "w_amap_fq", "
 class W4A4Linear(nn.Module):
     """Mixed-precision W4A4 linear: salient input channels in D, the rest int4/int8.
 
-    Forward kernels (chosen per layer, see `kernel`; "auto" = "f8" where ops.f8_eligible
+    Forward kernels (chosen per layer, see `kernel`; "auto" = "f8" where ops.f8_auto (fp16)
     ("f6" instead when ops.F6_AUTO), "fqt" for large sorted per_group batches, else "fq"
     unless ops.I8_AUTO):
       "f6"  as "f8" with both code operands in FP6 e2m3 (weight groups of whole 128-blocks):
@@ -510,7 +510,7 @@ class W4A4Linear(nn.Module):
                   (self.kernel == "auto" and ops.F6_AUTO and ops.f6_eligible(pw, amode, bits)
                    and ops.f8_input_ok(xc)))
         use_f8 = use_f6 or self.kernel == "f8" or (
-            self.kernel == "auto" and ops.F8_AUTO and ops.f8_eligible(pw, amode, bits)
+            self.kernel == "auto" and ops.f8_auto(pw, amode, bits)
             and ops.f8_input_ok(xc))
         use_i8 = not use_f8 and (
             self.kernel == "i8" or

@@ -711,6 +711,18 @@ I8_AUTO = False
 # Whether kernel="auto" takes the FP8 path for eligible layers (f8_eligible): on gfx950
 # it is 1.4x the fq GEMM at config 2.
 F8_AUTO = True
+
+
+def f8_auto(pw: PackedWeight, act_quant: str, act_bits: int) -> bool:
+    """Whether kernel="auto" runs this layer on the FP8 GEMM: fp16 layers only.  The FP8 path
+    factors the scales out and so skips the D rounding of x_hat = D(code * s) and W_hat; in
+    fp16 that is 2^-12 per product (y within 3e-3 of the reference).  In bf16 the rounding it
+    skips is 2^-9 per product -- the size of bf16's own output rounding -- so y differs from
+    the reference's bf16 F.linear in most low bits (2.4e-3 relative on the ppl_eval-flow
+    Llama layer) and a 4-bit per-token model amplifies that into 50 % logit differences
+    (tests/test_gpu_configs.py, llama7b_l_bf16_pplflow).  bf16 layers run the faithful fq
+    GEMM on the bit-exact operands instead; kernel="f8" still forces the FP8 path."""
+    return F8_AUTO and pw.dtype == torch.float16 and f8_eligible(pw, act_quant, act_bits)
 # Whether kernel="auto" takes the FP6 path where f6_eligible (bit-identical to "f8").  Off:
 # measured at config 2 per_token, the f6 GEMM 310 us against f8v2's 285 us and the step
 # 0.386 against 0.343 ms (same box, interleaved runs); SQMP_F6=1 turns it on (A/B knob).

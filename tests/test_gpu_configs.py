@@ -141,7 +141,7 @@ def test_config_workload_matches_reference(case):
         # operands (accumulation-order tolerance)
         bias = None if m.bias is None else m.bias.reshape(-1)
         xin = x2.contiguous()
-        if (m.kernel == "auto" and ops.F8_AUTO and ops.f8_eligible(pw, amode, bits)
+        if (m.kernel == "auto" and ops.f8_auto(pw, amode, bits)
                 and ops.f8_input_ok(xin)):
             # the forward's kernel for per_token / per_tensor 4-bit acts: the FP8 GEMM on
             # the codes (scales factored out, D rounding of x_hat / W_hat skipped)

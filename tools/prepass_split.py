@@ -1,0 +1,79 @@
+"""The config-2 activation-order prepass split into its kernels (for rocprofv3 --stats and
+HIP-event timing): the fused quant_act_c4 (column max + rank table + C4 quantizer with the
+weight permutation in one launch), then the quantizer alone (sqmp_quant_act_v2 OUT_C4) and
+the permutation alone (sqmp_perm_weight_c4), each ITERS times.
+
+    python tools/prepass_split.py [ITERS]
+"""
+import ctypes
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "smoothquant-mixedprecision_amd")]
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+from smoothquant import _lib, ops  # noqa: E402
+from smoothquant._lib import check, load  # noqa: E402
+
+iters = int(sys.argv[1]) if len(sys.argv) > 1 else 50
+dev = torch.device("cuda")
+q, x, lin = bench.make_layer(dev, "per_group", seed=1)
+pw = q.packed()
+G, M, K = bench.G, bench.M, bench.K
+lib = load()
+stream = torch.cuda.current_stream(dev)
+
+
+def t_us(fn, n=iters):
+    for _ in range(5):
+        fn()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record(stream)
+    for _ in range(n):
+        fn()
+    b.record(stream)
+    b.synchronize()
+    return a.elapsed_time(b) / n * 1e3
+
+
+fused = lambda: ops.quant_act_c4(x, pw, "per_group", 4, G)  # noqa: E731
+c4 = fused()
+codes, scales, xs, wp = c4
+Kq = codes.shape[1] * 2
+ngq = scales.shape[1]
+e = ops._act_ws(dev, stream.cuda_stream, K, pw.Kp, ops._ws_bytes(M, K, pw.Kp))
+
+
+def quant_only():
+    st = lib.sqmp_quant_act_v2(ops._p(x), ops._dtype_code(x.dtype), M, K, ops.ACT_MODES["per_group"],
+                               4, G, ops._p(pw.amap), pw.Kp, ops._p(pw.nonsal), ops._p(pw.salient),
+                               pw.S, pw.S_pad, ops._p(pw.posmap),
+                               _lib.QA_CLEAN_WS | _lib.QA_TILED, _lib.OUT_C4, ops._p(codes),
+                               ops._p(scales), ops._p(xs), ops._p(e["buf"]), e["buf"].numel(),
+                               ctypes.c_void_p(stream.cuda_stream))
+    check(st, "quant_act_v2 C4")
+
+
+def perm_only():
+    st = lib.sqmp_perm_weight_c4(ops._p(e["buf"]), pw.K, pw.Kp, pw.S, pw.S_pad, ops._p(pw.codes),
+                                 ops._p(pw.wscale), ops._p(pw.wsal), ops._dtype_code(pw.dtype),
+                                 pw.N, pw.Gw, pw.ngw, ops._p(wp), ctypes.c_void_p(stream.cuda_stream))
+    check(st, "perm_weight_c4")
+
+
+wp_ref = wp.clone()
+quant_only()
+perm_only()
+torch.cuda.synchronize()
+assert torch.equal(wp.view(torch.int16), wp_ref.view(torch.int16))
+xbytes = M * K * 2
+qbytes = xbytes + codes.numel() + M * ngq * 2 + M * pw.S_pad * 2
+pbytes = pw.N * pw.Kp // 2 + pw.N * (Kq + pw.S_pad) * 2
+tf = t_us(fused)
+tq = t_us(quant_only)
+tp = t_us(perm_only)
+print(f"fused quant_act_c4 (colmax + rank + quant|perm): {tf:7.1f} us")
+print(f"quant_act_v2 OUT_C4 (colmax + rank + quant):     {tq:7.1f} us   quant bytes {qbytes/1e6:.1f} MB")
+print(f"perm_weight_c4 alone:                             {tp:7.1f} us   {pbytes/1e6:.1f} MB = {pbytes/tp/1e3:.0f} GB/s")
