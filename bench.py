@@ -23,6 +23,9 @@ Also printed in the same JSON line:
                 torch_cpu.py, pinned bit-exact to the reference goldens) in fp32 on this
                 host's cores: rank 0, N=1 only, median of 3 after 1 warm-up
   prepass       the activation-quantization kernels' time and algorithmic GB/s
+  llama_layer   BASELINE config 4's workload: one Llama-2-7B decoder layer's 7 linears at
+                2048 tokens (G=64, 5 % salient), W4A4 vs unquantized fp16 F.linear, per
+                linear and in total (measured after the timed region)
 Secondary measurements (GEMM alone, prepass, vendor dense GEMM, reference fake-quant on
 the GPU) run BEFORE the W warm-up steps, followed by --settle-ms (default 300) of untimed
 steps, so the timed region starts on a chip that holds the clock it settles at under this
@@ -67,6 +70,8 @@ def parse(argv=None):
                     help="model dtype of the layer (fp32: the reference's OPT dtype; the GEMM "
                          "runs on the f16 MFMA as sqmp_gemm_h2)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--no-layer", action="store_true",
+                    help="skip the Llama-2-7B decoder-layer line (llama_layer)")
     ap.add_argument("--rehearsal", action="store_true",
                     help="CPU/gloo rehearsal of the launcher and timing path (no GPU): the "
                          "step is the CPU fake-quant layer on a 64-row batch")
@@ -211,6 +216,87 @@ def cpu_baseline(act, rows=M, runs=3):
                    f"bit-exact to its goldens), fp32, weight per_group + act {act}, "
                    f"{rows}x{K}->{N}, G={G}, p={P}; median of {runs} after 1 warm-up: "
                    f"{dt:.3f} s per forward (runs {', '.join(f'{t:.3f}' for t in ts)})"),
+    }
+
+
+# ------------------------------------------------------------------ Llama-2-7B layer
+# BASELINE config 4's linears (the north star's end-to-end workload): one decoder layer of
+# Llama-2-7B at 2048 tokens (one prefill window), G=64, 5 % salient, max-sorted per_group
+# weights and activations, fp16.  The 7 linears run in the order a LlamaDecoderLayer calls
+# them, q/k/v on one input object and gate/up on another, so k, v and up reuse the column
+# statistics of their sibling (fake_quant.py:479-561 swaps them one by one; the reference
+# recomputes the identical sort per layer).
+LLAMA_LINEARS = [  # name, K, N, input
+    ("q_proj", 4096, 4096, "attn"), ("k_proj", 4096, 4096, "attn"),
+    ("v_proj", 4096, 4096, "attn"), ("o_proj", 4096, 4096, "o"),
+    ("gate_proj", 4096, 11008, "mlp"), ("up_proj", 4096, 11008, "mlp"),
+    ("down_proj", 11008, 4096, "down"),
+]
+LLAMA_T, LLAMA_G, LLAMA_P = 2048, 64, 0.05
+
+
+def llama_layer(dev, iters=40):
+    """Per-linear and whole-layer time of the W4A4 layer against the same 7 unquantized fp16
+    F.linear calls (hipBLASLt), HIP events on the launch stream."""
+    from smoothquant.fake_quant import W4A4Linear
+    gen = torch.Generator(device=dev).manual_seed(7)
+    dt = torch.float16
+    xs = {}
+    for name, K in (("attn", 4096), ("o", 4096), ("mlp", 4096), ("down", 11008)):
+        x = torch.randn(LLAMA_T, K, generator=gen, device=dev)
+        x[:, torch.randperm(K, generator=gen, device=dev)[: K // 100]] *= 30.0
+        xs[name] = x.to(dt)
+    layers = []
+    for name, K, N, src in LLAMA_LINEARS:
+        lin = torch.nn.Linear(K, N, bias=False).to(dev, dt)
+        with torch.no_grad():
+            lin.weight.copy_((torch.randn(N, K, generator=gen, device=dev) * 0.02).to(dt))
+        imp = xs[src][:512].float().abs().mean(0).cpu()
+        q = W4A4Linear.from_float(lin, weight_quant="per_group", act_quant="per_group",
+                                  importance=imp, salient_prop=LLAMA_P, group_size=LLAMA_G)
+        layers.append((name, q, lin.weight.detach(), xs[src]))
+    stream = torch.cuda.current_stream(dev)
+
+    def run(fp16, ev=None):
+        for i, (_, q, w, x) in enumerate(layers):
+            if fp16:
+                torch.nn.functional.linear(x, w)
+            else:
+                q(x)
+            if ev is not None:
+                ev[i + 1].record(stream)
+
+    out = {}
+    for kind in (False, True, False, True):  # interleaved rounds, best of each
+        for _ in range(5):
+            run(kind)
+        evs = [[torch.cuda.Event(enable_timing=True) for _ in range(len(layers) + 1)]
+               for _ in range(iters)]
+        for ev in evs:
+            ev[0].record(stream)
+            run(kind, ev)
+        evs[-1][-1].synchronize()
+        per = [sorted(ev[i].elapsed_time(ev[i + 1]) for ev in evs)[iters // 2]
+               for i in range(len(layers))]
+        tot = sorted(ev[0].elapsed_time(ev[-1]) for ev in evs)[iters // 2]
+        key = "fp16" if kind else "w4a4"
+        if key not in out or tot < out[key][1]:
+            out[key] = (per, tot)
+    flops = sum(2.0 * LLAMA_T * K * N for _, K, N, _ in LLAMA_LINEARS)
+    (pw4, tw4), (pf16, tf16) = out["w4a4"], out["fp16"]
+    return {
+        "workload": (f"Llama-2-7B decoder layer linears, {LLAMA_T} tokens, W4A4 G={LLAMA_G}, "
+                     f"{int(LLAMA_P * 100)}% salient, per_group(sorted) W and A, fp16; "
+                     "q/k/v and gate/up share their input (sibling statistics reuse)"),
+        "w4a4_ms": round(tw4, 4), "fp16_linear_ms": round(tf16, 4),
+        "w4a4_over_fp16_speed": round(tf16 / tw4, 4),
+        "w4a4_TFLOP_per_s": round(flops / (tw4 * 1e-3) / 1e12, 1),
+        "per_linear": {name: {"w4a4_ms": round(a, 4), "fp16_ms": round(b, 4),
+                              "fp16_over_w4a4": round(b / a, 3)}
+                       for (name, _, _, _), a, b in zip(LLAMA_LINEARS, pw4, pf16)},
+        "note": "median of 40 layer passes, best of 2 interleaved rounds; per-linear times "
+                "include each layer's own prepass (column max / rank only on the first "
+                "sibling)",
     }
 
 
@@ -451,6 +537,8 @@ def main(argv=None):
             "hbm_peak_GB_per_s": HBM_PEAK_GBS,
         },
     }
+    if not fp32 and not args.no_layer:
+        out["llama_layer"] = llama_layer(dev)
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(args.act)
     if rank == 0:

@@ -67,6 +67,7 @@ def test_from_float_cpu_source_linear(wq):
     K, N = 512, 192
     lin = torch.nn.Linear(K, N).half()                      # stays on the CPU
     w0 = lin.weight.detach().clone()
+    b0 = lin.bias.detach().clone()   # from_float aliases the bias Parameter (:369-370)
     imp = torch.rand(K)
     q = W4A4Linear.from_float(lin, weight_quant=wq, act_quant="per_token", importance=imp,
                               salient_prop=0.05, group_size=128)
@@ -85,5 +86,5 @@ def test_from_float_cpu_source_linear(wq):
     keep[sal] = False
     qx = x.clone()
     qx[:, keep] = T.act_quant(x[:, keep], "per_token", 4, 128)
-    ref = qx.double() @ w_hat.double().t() + lin.bias.detach().double()
+    ref = qx.double() @ w_hat.double().t() + b0.double()
     assert _rel(y, ref) < 3e-3
