@@ -233,6 +233,15 @@ int sqmp_gemm_f8(const void* a8, const float* ascale, const void* xs, const void
                  const float* ws32, const void* wsal, const void* bias, void* y, int dtype,
                  int M, int N, int Kp, int S_pad, int Gw, int ngw, void* stream);
 
+/* sqmp_gemm_f8 with the output quantizer's column statistics fused into its epilogue, as
+ * sqmp_gemm_fq_colmax: colmax[n] = max(colmax[n], bits(|y[m][n]|)) over every row m
+ * (fake_quant.py:308-316 then skips its statistics pass: SQMP_QA_STATS_GIVEN).
+ * Gw % 128 == 0 (the 16x16x128 kernel). */
+int sqmp_gemm_f8_colmax(const void* a8, const float* ascale, const void* xs, const void* w8,
+                        const float* ws32, const void* wsal, const void* bias, void* y,
+                        int dtype, int M, int N, int Kp, int S_pad, int Gw, int ngw,
+                        uint32_t* colmax, void* stream);
+
 /* FP6 weight operand of sqmp_gemm_f6: the int4 codes as OCP FP6 e2m3 [Np][Kp*3/4] bytes
  * in the f6-packed format of SQMP_OUT_F6 (Np = roundup(N, 256)); the scales are
  * sqmp_pack_f8's ws32.  Once per layer. */
@@ -308,6 +317,11 @@ int sqmp_gemm_fqt(const void* acodes, const void* ascale, const void* xs, const 
 int sqmp_gemm_fqt7(const void* codes_t, const void* scale_t, const void* sal_t, const void* wp,
                    const void* bias, void* y, int dtype, int M, int N, int Kq, int S_pad,
                    int G, int ngq, void* stream);
+
+/* sqmp_gemm_fqt7 with the fused output-quant column statistics (as sqmp_gemm_fq_colmax). */
+int sqmp_gemm_fqt7_colmax(const void* codes_t, const void* scale_t, const void* sal_t,
+                          const void* wp, const void* bias, void* y, int dtype, int M, int N,
+                          int Kq, int S_pad, int G, int ngq, uint32_t* colmax, void* stream);
 
 /* fp32 models (the reference runs OPT in fp32): the faithful GEMM on the bf16 MFMA.
  * sqmp_split3_bf16: src fp32 [R][L] -> three bf16 planes dst [3][ldr][L] with

@@ -296,7 +296,8 @@ __global__ __launch_bounds__(512, 1) void gemm_f8v2_kernel(
     const typename DT::T* __restrict__ XS, const unsigned char* __restrict__ W8,
     const float* __restrict__ ws32, const typename DT::T* __restrict__ wsal,
     const typename DT::T* __restrict__ bias, typename DT::T* __restrict__ Y, int M, int N,
-    int Kp, int S_pad, int Gw, int ngw, int tiles_m, int tiles_n, int group_m) {
+    int Kp, int S_pad, int Gw, int ngw, int tiles_m, int tiles_n, int group_m,
+    uint32_t* __restrict__ colmax) {
   typedef typename DT::T T;
   __shared__ __attribute__((aligned(16))) unsigned char lds[V2_NSLOT * V2_SLOT];
 
@@ -457,6 +458,33 @@ __global__ __launch_bounds__(512, 1) void gemm_f8v2_kernel(
       const float s = gm < M ? ascale[gm] : 0.f;
 #pragma unroll
       for (int j = 0; j < 4; ++j) tot[i][j] *= s;
+    }
+  }
+
+  // fused output-quant statistics (sqmp_gemm_f8_colmax): per output column the max of
+  // |D(y)| over the lane's rows, the 16 r16 lanes, then one atomic per column and wave
+  if (colmax) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int nl = wn * 64 + 16 * j + 4 * q;
+      float cm[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float bv = (bias && n0 + nl + r < N) ? DT::to_f(bias[n0 + nl + r]) : 0.f;
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+          if (m0 + xrow0 + 16 * i < M)
+            cm[r] = fmaxf(cm[r], fabsf(DT::to_f(DT::from_f(tot[i][j][r] + bv))));
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float v = cm[r];
+        v = fmaxf(v, __shfl_xor(v, 1, 64));
+        v = fmaxf(v, __shfl_xor(v, 2, 64));
+        v = fmaxf(v, __shfl_xor(v, 4, 64));
+        v = fmaxf(v, __shfl_xor(v, 8, 64));
+        if (r16 == 0 && n0 + nl + r < N) atomicMax(colmax + n0 + nl + r, __float_as_uint(v));
+      }
     }
   }
 
@@ -880,10 +908,10 @@ extern "C" int sqmp_pack_f8(const void* codes, const void* wscale, int dtype, in
   return SQMP_OK;
 }
 
-extern "C" int sqmp_gemm_f8(const void* a8, const float* ascale, const void* xs, const void* w8,
-                            const float* ws32, const void* wsal, const void* bias, void* y,
-                            int dtype, int M, int N, int Kp, int S_pad, int Gw, int ngw,
-                            void* stream) {
+static int gemm_f8_impl(const void* a8, const float* ascale, const void* xs, const void* w8,
+                        const float* ws32, const void* wsal, const void* bias, void* y,
+                        int dtype, int M, int N, int Kp, int S_pad, int Gw, int ngw,
+                        uint32_t* colmax, void* stream) {
   if (M < 0 || N <= 0 || Kp <= 0 || Kp % 128 != 0 || S_pad < 0 || S_pad % 64 != 0)
     return SQMP_EINVAL;
   if (!a8 || !ascale || !w8 || !ws32 || !y || (S_pad > 0 && (!xs || !wsal))) return SQMP_EINVAL;
@@ -899,6 +927,7 @@ extern "C" int sqmp_gemm_f8(const void* a8, const float* ascale, const void* xs,
     return e && atoi(e) != 0;
   }();
   const bool v2 = Gw % 128 == 0 && !v1_only;
+  if (colmax && !v2) return SQMP_EUNSUPPORTED;  // fused statistics: the 16x16x128 kernel only
   static const int group_m = [] {  // M-tiles per raster group (SQMP_GROUP_M: A/B knob)
     const char* e = getenv("SQMP_GROUP_M");
     return e && atoi(e) > 0 ? atoi(e) : 4;
@@ -907,7 +936,7 @@ extern "C" int sqmp_gemm_f8(const void* a8, const float* ascale, const void* xs,
   if (v2) gemm_f8v2_kernel<DTT><<<grid, block, 0, s>>>(                                      \
       (const unsigned char*)a8, ascale, (const DTT::T*)xs, (const unsigned char*)w8, ws32,   \
       (const DTT::T*)wsal, (const DTT::T*)bias, (DTT::T*)y, M, N, Kp, S_pad, Gw, ngw, tiles_m, \
-      tiles_n, group_m);                                                                     \
+      tiles_n, group_m, colmax);                                                             \
   else gemm_f8_kernel<DTT><<<grid, block, 0, s>>>(                                           \
       (const unsigned char*)a8, ascale, (const DTT::T*)xs, (const unsigned char*)w8, ws32,   \
       (const DTT::T*)wsal, (const DTT::T*)bias, (DTT::T*)y, M, N, Kp, S_pad, Gw, ngw, tiles_m, \
@@ -920,6 +949,24 @@ extern "C" int sqmp_gemm_f8(const void* a8, const float* ascale, const void* xs,
 #undef SQMP_F8L
   SQMP_LAUNCH_CHECK();
   return SQMP_OK;
+}
+
+extern "C" int sqmp_gemm_f8(const void* a8, const float* ascale, const void* xs, const void* w8,
+                            const float* ws32, const void* wsal, const void* bias, void* y,
+                            int dtype, int M, int N, int Kp, int S_pad, int Gw, int ngw,
+                            void* stream) {
+  return gemm_f8_impl(a8, ascale, xs, w8, ws32, wsal, bias, y, dtype, M, N, Kp, S_pad, Gw, ngw,
+                      nullptr, stream);
+}
+
+// sqmp_gemm_f8 with the fused output-quant statistics (as sqmp_gemm_fq_colmax); Gw % 128 == 0
+extern "C" int sqmp_gemm_f8_colmax(const void* a8, const float* ascale, const void* xs,
+                                   const void* w8, const float* ws32, const void* wsal,
+                                   const void* bias, void* y, int dtype, int M, int N, int Kp,
+                                   int S_pad, int Gw, int ngw, uint32_t* colmax, void* stream) {
+  if (!colmax) return SQMP_EINVAL;
+  return gemm_f8_impl(a8, ascale, xs, w8, ws32, wsal, bias, y, dtype, M, N, Kp, S_pad, Gw, ngw,
+                      colmax, stream);
 }
 
 extern "C" int sqmp_pack_f6(const void* codes, int N, int Kp, void* w6, void* stream) {

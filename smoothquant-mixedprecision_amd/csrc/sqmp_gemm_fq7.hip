@@ -338,11 +338,23 @@ __global__ __launch_bounds__(512, 1) void gemm_fq7_kernel(
     for (int i = 0; i < I; ++i) {
       const int ml = 16 * i + r16;
       const float bv = bias && m0 + ml < M ? DT::to_f(bias[m0 + ml]) : 0.f;
+      float cm = 0.f;  // |y| max of output column m0 + ml over this lane's tokens
 #pragma unroll
       for (int j = 0; j < J; ++j)
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
-          *(T*)(lds + (WR * wave + 16 * j + 4 * q + r) * RS + ml * 2) = DT::from_f(acc[i][j][r] + bv);
+        for (int r = 0; r < 4; ++r) {
+          const T v = DT::from_f(acc[i][j][r] + bv);
+          *(T*)(lds + (WR * wave + 16 * j + 4 * q + r) * RS + ml * 2) = v;
+          if (colmax && n0 + WR * wave + 16 * j + 4 * q + r < N) cm = fmaxf(cm, fabsf(DT::to_f(v)));
+        }
+      if (colmax) {
+        // fused output-quant statistics (sqmp_gemm_fqt7_colmax): max over the lane's tokens,
+        // the four q lane groups, then one atomic per column and wave (bits of |y| order
+        // like unsigned integers)
+        cm = fmaxf(cm, __shfl_xor(cm, 16, 64));
+        cm = fmaxf(cm, __shfl_xor(cm, 32, 64));
+        if (q == 0 && m0 + ml < M) atomicMax(colmax + m0 + ml, __float_as_uint(cm));
+      }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     barrier();
@@ -533,13 +545,13 @@ static int dispatch(const void* a, const void* bt, const void* st, const void* s
 template <class DT>
 static int dispatch_tr(const void* wp, const void* codes_t, const void* scale_t, const void* sal_t,
                        const void* bias, void* y, int M, int N, int Kq, int S_pad, int G, int ngq,
-                       hipStream_t s) {
+                       uint32_t* colmax, hipStream_t s) {
   typedef typename DT::T T;
   constexpr int TM = std::is_same<DT, BF16>::value ? 128 : 256;
   const int tiles_m = cdiv(N, TM), tiles_n = cdiv(M, 256);
   gemm_fq7_kernel<DT, 1, TM, 2, 0, true><<<dim3(tiles_m * tiles_n), dim3(512), 0, s>>>(
       (const T*)wp, (const uint32_t*)codes_t, (const T*)scale_t, (const T*)sal_t, (const T*)bias,
-      (T*)y, N, M, Kq, S_pad, G, ngq, tiles_m, tiles_n, group_m_tr_env(), nullptr);
+      (T*)y, N, M, Kq, S_pad, G, ngq, tiles_m, tiles_n, group_m_tr_env(), colmax);
   SQMP_LAUNCH_CHECK();
   return SQMP_OK;
 }
@@ -615,9 +627,9 @@ extern "C" int sqmp_gemm_fq7(const void* a, const void* codes_t, const void* sca
 // sqmp_gemm_fqt7: the activation-order GEMM (sqmp_gemm_fqt) on fq7's register-operand
 // structure, its activation operands in the tile-major layout (J = 2) that sqmp_quant_act_c4
 // writes when called with the SQMP_QA_TILED flag
-extern "C" int sqmp_gemm_fqt7(const void* codes_t, const void* scale_t, const void* sal_t,
-                              const void* wp, const void* bias, void* y, int dtype, int M, int N,
-                              int Kq, int S_pad, int G, int ngq, void* stream) {
+static int gemm_fqt7_impl(const void* codes_t, const void* scale_t, const void* sal_t,
+                          const void* wp, const void* bias, void* y, int dtype, int M, int N,
+                          int Kq, int S_pad, int G, int ngq, uint32_t* colmax, void* stream) {
   if (!codes_t || !scale_t || !sal_t || !wp || !y) return SQMP_EINVAL;
   if (M < 0 || N <= 0 || Kq <= 0 || Kq % 128 || S_pad < 0 || S_pad % 64 || G <= 0 || ngq <= 0)
     return SQMP_EINVAL;
@@ -626,8 +638,26 @@ extern "C" int sqmp_gemm_fqt7(const void* codes_t, const void* scale_t, const vo
   if (M == 0) return SQMP_OK;
   hipStream_t s = (hipStream_t)stream;
   if (dtype == SQMP_F16)
-    return fq7::dispatch_tr<F16>(wp, codes_t, scale_t, sal_t, bias, y, M, N, Kq, S_pad, G, ngq, s);
-  return fq7::dispatch_tr<BF16>(wp, codes_t, scale_t, sal_t, bias, y, M, N, Kq, S_pad, G, ngq, s);
+    return fq7::dispatch_tr<F16>(wp, codes_t, scale_t, sal_t, bias, y, M, N, Kq, S_pad, G, ngq, colmax, s);
+  return fq7::dispatch_tr<BF16>(wp, codes_t, scale_t, sal_t, bias, y, M, N, Kq, S_pad, G, ngq, colmax, s);
+}
+
+extern "C" int sqmp_gemm_fqt7(const void* codes_t, const void* scale_t, const void* sal_t,
+                              const void* wp, const void* bias, void* y, int dtype, int M, int N,
+                              int Kq, int S_pad, int G, int ngq, void* stream) {
+  return gemm_fqt7_impl(codes_t, scale_t, sal_t, wp, bias, y, dtype, M, N, Kq, S_pad, G, ngq,
+                        nullptr, stream);
+}
+
+// the same with the fused output-quant statistics (as sqmp_gemm_fq_colmax): colmax[n] =
+// max(colmax[n], bits(|y[m][n]|)) over every row m
+extern "C" int sqmp_gemm_fqt7_colmax(const void* codes_t, const void* scale_t, const void* sal_t,
+                                     const void* wp, const void* bias, void* y, int dtype, int M,
+                                     int N, int Kq, int S_pad, int G, int ngq, uint32_t* colmax,
+                                     void* stream) {
+  if (!colmax) return SQMP_EINVAL;
+  return gemm_fqt7_impl(codes_t, scale_t, sal_t, wp, bias, y, dtype, M, N, Kq, S_pad, G, ngq,
+                        colmax, stream);
 }
 
 }  // namespace sqmp

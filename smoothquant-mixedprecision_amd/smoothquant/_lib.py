@@ -50,6 +50,8 @@ SIGNATURES = {
     "sqmp_pack_f8": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _vp, _vp]),
     "sqmp_gemm_f8": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i,
                           _vp]),
+    "sqmp_gemm_f8_colmax": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i,
+                                 _i, _vp, _vp]),
     "sqmp_pack_f6": (_i, [_vp, _i, _i, _vp, _vp]),
     "sqmp_gemm_f6": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i,
                           _vp]),
@@ -58,6 +60,8 @@ SIGNATURES = {
     "sqmp_perm_weight_c4": (_i, [_vp, _i, _i, _i, _i, _vp, _vp, _vp, _i, _i, _i, _i, _vp, _vp]),
     "sqmp_gemm_fqt": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _vp]),
     "sqmp_gemm_fqt7": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _vp]),
+    "sqmp_gemm_fqt7_colmax": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i,
+                                   _vp, _vp]),
     "sqmp_fq7_sizes": (_i, [_i, _i, _i, _i, _i, ctypes.POINTER(_sz), ctypes.POINTER(_sz),
                             ctypes.POINTER(_sz)]),
     "sqmp_pack_fq7": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp]),

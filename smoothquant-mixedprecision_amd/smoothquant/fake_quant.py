@@ -539,22 +539,21 @@ class W4A4Linear(nn.Module):
         # per_group (sorted) / per_tensor the faithful GEMM also writes the column maxima of
         # y into the output quantizer's workspace, which then skips its statistics pass
         fuse = (ospec is not None and ospec[0] in ("per_group", "per_tensor") and _OQ_FUSE
-                and not use_f8
-                and not use_i8 and not use_fqt
+                and not use_i8 and not use_f6
+                and (not use_f8 or pw.Gw % 128 == 0)           # the 16x16x128 FP8 kernel
+                and (not use_fqt or c4[1].dim() == 3)          # the tile-major fqt7 GEMM
                 and (self.salient_indices is None or pw.K - pw.S > 0))
+        colmax = ops.out_quant_workspace(x2.shape[0], pw.N, x2.device)["buf"] if fuse else None
         if use_f6:
             y = ops.gemm_f6(a8, sa, xs, pw, bias)
         elif use_f8:
-            y = ops.gemm_f8(a8, sa, xs, pw, bias)
+            y = ops.gemm_f8(a8, sa, xs, pw, bias, colmax=colmax)
         elif use_i8:
             y = ops.gemm_i8(a8, sa, xs, pw, bias)
         elif use_fqt:
-            y = ops.gemm_fqt(*c4, pw, bias, ag)
-        elif fuse:
-            ws = ops.out_quant_workspace(x2.shape[0], pw.N, x2.device)
-            y = ops.gemm_fq(a, pw, bias, colmax=ws["buf"])
+            y = ops.gemm_fqt(*c4, pw, bias, ag, colmax=colmax)
         else:
-            y = ops.gemm_fq(a, pw, bias)
+            y = ops.gemm_fq(a, pw, bias, colmax=colmax)
         if ospec is not None:                                                # :308-316
             omode, obits, og = ospec
             if self.salient_indices is not None:

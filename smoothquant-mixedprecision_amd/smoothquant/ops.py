@@ -372,16 +372,23 @@ def quant_act_c4(x2: torch.Tensor, pw: PackedWeight, act_quant: str, n_bits: int
 
 
 def gemm_fqt(codes: torch.Tensor, scales: torch.Tensor, xs: torch.Tensor, wp: torch.Tensor,
-             pw: PackedWeight, bias: Optional[torch.Tensor], group_size: int) -> torch.Tensor:
-    """y = D(x_hat . W_hat^T + bias) on the activation-order operands of quant_act_c4."""
+             pw: PackedWeight, bias: Optional[torch.Tensor], group_size: int,
+             colmax: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """y = D(x_hat . W_hat^T + bias) on the activation-order operands of quant_act_c4.
+    colmax (tile-major operands only): as gemm_fq's fused output-quant statistics."""
     M = xs.shape[0]
     y = torch.empty((M, pw.N), dtype=pw.dtype, device=codes.device)
     Kq = codes.shape[1] * 2
     if scales.dim() == 3:   # tile-major (SQMP_QA_TILED)
-        check(load().sqmp_gemm_fqt7(_p(codes), _p(scales), _p(xs), _p(wp), _p(bias), _p(y),
-                                    _dtype_code(pw.dtype), M, pw.N, Kq, pw.S_pad, group_size,
-                                    scales.shape[1], _stream(codes)), "gemm_fqt7")
+        args = (_p(codes), _p(scales), _p(xs), _p(wp), _p(bias), _p(y), _dtype_code(pw.dtype), M,
+                pw.N, Kq, pw.S_pad, group_size, scales.shape[1])
+        if colmax is None:
+            check(load().sqmp_gemm_fqt7(*args, _stream(codes)), "gemm_fqt7")
+        else:
+            check(load().sqmp_gemm_fqt7_colmax(*args, _p(colmax), _stream(codes)), "gemm_fqt7")
         return y
+    if colmax is not None:
+        raise ValueError("gemm_fqt: fused column statistics need the tile-major operands")
     check(load().sqmp_gemm_fqt(_p(codes), _p(scales), _p(xs) if pw.S_pad else None, _p(wp),
                                _p(bias), _p(y), _dtype_code(pw.dtype), M, pw.N, Kq, pw.S_pad,
                                group_size, scales.shape[0], _stream(codes)), "gemm_fqt")
@@ -654,14 +661,18 @@ def quant_act_f8(x2: torch.Tensor, pw: PackedWeight, act_quant: str, n_bits: int
 
 
 def gemm_f8(a8: torch.Tensor, sa: torch.Tensor, xs: torch.Tensor, pw: PackedWeight,
-            bias: Optional[torch.Tensor]) -> torch.Tensor:
+            bias: Optional[torch.Tensor], colmax: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """colmax (Gw % 128 == 0): as gemm_fq's fused output-quant statistics."""
     M = a8.shape[0]
     w8, ws32 = f8_operands(pw)
     y = torch.empty((M, pw.N), dtype=pw.dtype, device=a8.device)
-    check(load().sqmp_gemm_f8(_p(a8), _p(sa), _p(xs) if pw.S_pad else None, _p(w8), _p(ws32),
-                              _p(pw.wsal) if pw.S_pad else None, _p(bias), _p(y),
-                              _dtype_code(pw.dtype), M, pw.N, pw.Kp, pw.S_pad, pw.Gw, pw.ngw,
-                              _stream(a8)), "gemm_f8")
+    args = (_p(a8), _p(sa), _p(xs) if pw.S_pad else None, _p(w8), _p(ws32),
+            _p(pw.wsal) if pw.S_pad else None, _p(bias), _p(y), _dtype_code(pw.dtype), M, pw.N,
+            pw.Kp, pw.S_pad, pw.Gw, pw.ngw)
+    if colmax is None:
+        check(load().sqmp_gemm_f8(*args, _stream(a8)), "gemm_f8")
+    else:
+        check(load().sqmp_gemm_f8_colmax(*args, _p(colmax), _stream(a8)), "gemm_f8")
     return y
 
 
