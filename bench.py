@@ -52,8 +52,8 @@ import torch  # noqa: E402
 
 M, K, N, G, P = 16384, 4096, 4096, 128, 0.10
 # dense MFMA peaks (MI355X_MICROARCH.md: 256 CU @ 2.4 GHz): f16/bf16 2.5 PF, i8/fp8 5 PF,
-# fp6/fp4 10 PF
-PEAK_TFLOPS = {"f16": 2516.6, "bf16": 2516.6, "i8": 5033.2, "f8": 5033.2, "f6": 10066.3,
+# (fp6/fp4 10 PF: no kernel here)
+PEAK_TFLOPS = {"f16": 2516.6, "bf16": 2516.6, "i8": 5033.2, "f8": 5033.2,
                "f32": 157.3}
 HBM_PEAK_GBS = 8000.0
 
@@ -350,7 +350,6 @@ def main(argv=None):
     pw = q.packed()
     # what W4A4Linear(kernel="auto") runs for this layer
     use_f8 = ops.f8_auto(pw, args.act, 4)
-    use_f6 = use_f8 and ops.F6_AUTO and ops.f6_eligible(pw, args.act, 4)
     use_fqt = not use_f8 and ops.fqt_eligible(pw, args.act, 4, G, M)
     stream = torch.cuda.current_stream(dev)
     flops = 2.0 * M * N * K
@@ -379,13 +378,7 @@ def main(argv=None):
         dense()
     dense_ms = time_events(dense, sec_iters, stream)
     # dominant kernel: the GEMM, timed alone on the stream it is launched on
-    if use_f6:
-        a6, sa, xs = ops.quant_act_f6(x, pw, args.act, 4)
-        gemm = lambda: ops.gemm_f6(a6, sa, xs, pw, lin.bias)  # noqa: E731
-        quant = lambda: ops.quant_act_f6(x, pw, args.act, 4)  # noqa: E731
-        kdt = "f6"
-        kname = "sqmp::gemm_f6_kernel<F16> (e2m3 on v_mfma_scale_f32_16x16x128_f8f6f4)"
-    elif use_f8:
+    if use_f8:
         a8, sa, xs = ops.quant_act_f8(x, pw, args.act, 4)
         gemm = lambda: ops.gemm_f8(a8, sa, xs, pw, lin.bias)  # noqa: E731
         quant = lambda: ops.quant_act_f8(x, pw, args.act, 4)  # noqa: E731
@@ -446,7 +439,7 @@ def main(argv=None):
     esz = 4 if fp32 else 2
     xbytes = M * K * esz
     if use_f8:
-        wbytes = (M * pw.Kp * 3 // 4 if use_f6 else M * pw.Kp) + M * 4 + M * pw.S_pad * 2
+        wbytes = M * pw.Kp + M * 4 + M * pw.S_pad * 2
         reads = 2 if args.act == "per_tensor" else 1
     elif use_fqt:
         Kq = (K - pw.S + 63) // 64 * 64
@@ -461,8 +454,7 @@ def main(argv=None):
     prepass_bytes = reads * xbytes + wbytes
 
     traffic = None
-    prof = os.path.join(ROOT, "profiles", "r02_pmc_gemm_f6_per_token.json" if kdt == "f6"
-                        else "r02_pmc_gemm_f8v2_per_token.json" if kdt == "f8"
+    prof = os.path.join(ROOT, "profiles", "r02_pmc_gemm_f8v2_per_token.json" if kdt == "f8"
                         else "r02_pmc_gemm_h2_fp32.json" if fp32
                         else "r02_pmc_gemm_fqt7_per_group.json" if use_fqt and "fqt7" in kname
                         else "r02_pmc_gemm_fqt_per_group.json" if use_fqt
@@ -485,8 +477,7 @@ def main(argv=None):
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": ("e2m3 codes (fp32 accumulate) + fp16 salient tail" if use_f6 else
-                  "e4m3 codes (fp32 accumulate) + fp16 salient tail" if use_f8 else
+        "dtype": ("e4m3 codes (fp32 accumulate) + fp16 salient tail" if use_f8 else
                   "fp32 (fp32-accurate products from fp16 pieces on the f16 MFMA)" if fp32
                   else "fp16"),
         "data": "synthetic (random-init weights N(0,0.02^2), x N(0,1) with 1% outlier channels x30)",
@@ -496,7 +487,7 @@ def main(argv=None):
                          f"{int(P * 100)}% salient fp16 side-GEMM"),
             "M": M, "K": K, "N": N, "group_size": G, "salient_prop": P,
             "salient_channels": pw.S,
-            "kernel": ("gemm_f6" if use_f6 else "gemm_f8" if use_f8 else "gemm_fqt" if use_fqt
+            "kernel": ("gemm_f8" if use_f8 else "gemm_fqt" if use_fqt
                        else "gemm_fq"),
             "parallelism": f"replicas x{world}",
         },

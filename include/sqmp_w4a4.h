@@ -96,10 +96,7 @@ enum sqmp_act_out {
                            packed order (0 at salient / padding positions); out_scale: fp32
                            [M] (the D scale); out_xs: D [M][S_pad] exact salient x
                            (operands of sqmp_gemm_f8) */
-  SQMP_OUT_F6 = 4,      /* as SQMP_OUT_F8 with the codes as OCP FP6 e2m3 in the "f6
-                           packed" format: per row, every 32 consecutive packed positions
-                           one 24-byte block, value e at bits [6e, 6e+6); out [M][Kp*3/4]
-                           bytes (operand of sqmp_gemm_f6) */
+  /* 4: reserved (the removed FP6 code output) */
   SQMP_OUT_C4 = 5       /* per_group activations in ACTIVATION order (operands of
                            sqmp_gemm_fqt): out = int4 codes [roundup(M, 256)][Kq / 2] bytes,
                            Kq = roundup(K - S, 64), bpack rows whose position j is the
@@ -219,8 +216,7 @@ int sqmp_gemm_i8(const int8_t* a8, const float* ascale, const void* xs,
 
 /* e4m3 operands of sqmp_gemm_f8 from a packed 4-bit weight: w8 = the int4 codes as OCP
  * e4m3 bytes [Np][Kp] in packed order, ws32 = the D group scales as fp32 [ngw][Np]
- * (Np = roundup(N, 256)).  Once per layer.  w8 = NULL builds the scales only (the f6
- * GEMM's ws32). */
+ * (Np = roundup(N, 256)).  Once per layer.  w8 = NULL builds the scales only. */
 int sqmp_pack_f8(const void* codes, const void* wscale, int dtype, int N, int Kp, int ngw,
                  void* w8, float* ws32, void* stream);
 
@@ -241,19 +237,6 @@ int sqmp_gemm_f8_colmax(const void* a8, const float* ascale, const void* xs, con
                         const float* ws32, const void* wsal, const void* bias, void* y,
                         int dtype, int M, int N, int Kp, int S_pad, int Gw, int ngw,
                         uint32_t* colmax, void* stream);
-
-/* FP6 weight operand of sqmp_gemm_f6: the int4 codes as OCP FP6 e2m3 [Np][Kp*3/4] bytes
- * in the f6-packed format of SQMP_OUT_F6 (Np = roundup(N, 256)); the scales are
- * sqmp_pack_f8's ws32.  Once per layer. */
-int sqmp_pack_f6(const void* codes, int N, int Kp, void* w6, void* stream);
-
-/* sqmp_gemm_f8 on FP6 e2m3 operands (SQMP_OUT_F6 codes x sqmp_pack_f6 codes) through the
- * same block-scaled MFMA at twice the e4m3 rate: the same exact integer block sums and
- * fp32 fold order, so y is bit-identical to sqmp_gemm_f8's.  Gw % 128 == 0, fp16/bf16;
- * a6 and xs: roundup(M, 256) rows allocated. */
-int sqmp_gemm_f6(const void* a6, const float* ascale, const void* xs, const void* w6,
-                 const float* ws32, const void* wsal, const void* bias, void* y, int dtype,
-                 int M, int N, int Kp, int S_pad, int Gw, int ngw, void* stream);
 
 /* Register-operand copy of a packed 4-bit weight for sqmp_gemm_fq7 (same values, tile-major
  * order; once per layer), for J (2 or 4) 16-row weight tiles per wave (WR = 16 J rows per
@@ -322,20 +305,6 @@ int sqmp_gemm_fqt7(const void* codes_t, const void* scale_t, const void* sal_t, 
 int sqmp_gemm_fqt7_colmax(const void* codes_t, const void* scale_t, const void* sal_t,
                           const void* wp, const void* bias, void* y, int dtype, int M, int N,
                           int Kq, int S_pad, int G, int ngq, uint32_t* colmax, void* stream);
-
-/* fp32 models (the reference runs OPT in fp32): the faithful GEMM on the bf16 MFMA.
- * sqmp_split3_bf16: src fp32 [R][L] -> three bf16 planes dst [3][ldr][L] with
- * src == h + m + l exactly (h = bf16(v), m = bf16(v - h), l = v - h - m); rows R..ldr-1
- * are zero.  Once per layer, on the packed-order W_hat + salient slice (ldr = Np).
- * sqmp_gemm_x3: y[M][N] = A[M][L] . W^T + bias in fp32, A = the packed-order x_hat +
- * exact salient columns (SQMP_OUT_FP output, fp32, roundup(M, 256) rows allocated), W
- * given as the planes b3 [3][roundup(N, 256)][L]; every product a.w is summed as the six
- * largest of its nine exact piece products (ah.wh + ah.wm + am.wh + ah.wl + al.wh + am.wm,
- * fp32 accumulation): a relative error per product of a few 2^-24, the rounding of an
- * fp32 FMA.  L % 32 == 0.  colmax (may be NULL): as sqmp_gemm_fq_colmax. */
-int sqmp_split3_bf16(const float* src, int R, int L, int ldr, void* dst, void* stream);
-int sqmp_gemm_x3(const float* a, const void* b3, const float* bias, float* y, int M, int N,
-                 int L, uint32_t* colmax, void* stream);
 
 /* The fp32 faithful GEMM on the f16 MFMA (the default for fp32 layers): every row of A and
  * of W is scaled by a power of two (exact) so that its maximum lies in [2^13, 2^14), each

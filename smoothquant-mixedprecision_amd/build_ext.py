@@ -25,6 +25,10 @@ ARCH = os.environ.get("SQMP_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I", INCLUDE,
           "-Wno-unused-result"]
+# SQMP_DIAG=1: also instantiate the timing-diagnostic kernel variants (wrong results by
+# design; never in the product build)
+if os.environ.get("SQMP_DIAG") == "1":
+    CFLAGS.append("-DSQMP_DIAG_BUILD")
 
 
 def _headers():

@@ -153,17 +153,6 @@ __device__ inline uint32_t f8_pair(uint32_t v, const PairScale& c) {
   return (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(code[1], 0.f, w, true);
 }
 
-// F6 output: the codes as OCP FP6 e2m3 bit patterns (|code| <= 7 exact), row m0 in byte 0,
-// row m0 + 1 in byte 2; |code| -> magnitude bits through a byte table (v_perm_b32):
-// 0 8 16 20 24 26 28 30, sign bit 0x20.
-template <class DT>
-__device__ inline uint32_t f6_pair(uint32_t v, const PairScale& c) {
-  const f32x2 code = code_pair<DT>(v, c);
-  const uint32_t a0 = (uint32_t)fabsf(code[0]), a1 = (uint32_t)fabsf(code[1]);
-  const uint32_t mag = __builtin_amdgcn_perm(0x1E1C1A18u, 0x14100800u, a0 | (a1 << 16));
-  return (mag & 0x00FF00FFu) | (code[0] < 0.f ? 0x20u : 0u) | (code[1] < 0.f ? 0x200000u : 0u);
-}
-
 }  // namespace
 
 // RPL = ranks per thread; GS = the group size when it is below RPL (RPL / GS groups per
@@ -390,7 +379,7 @@ __device__ __forceinline__ void quant_lc_body(
       } else if (F8) {
 #pragma unroll
         for (int i = 0; i < RPL; ++i)
-          lc_buf[tab[i] >> 16] = F8 == 2 ? f6_pair<DT>(v[i], c) : f8_pair<DT>(v[i], c);
+          lc_buf[tab[i] >> 16] = f8_pair<DT>(v[i], c);
         if (tid == 0) {
           out_scale[m0] = c.s[0];
           if (has1) out_scale[m0 + 1] = c.s[1];
@@ -406,35 +395,6 @@ __device__ __forceinline__ void quant_lc_body(
     if (rp + nblk < npair) load_pair(rp + nblk);  // prefetch the next pair
     __syncthreads();
 
-    if (F8 == 2) {
-      // f6-packed codes: 32 positions per 24-byte block, value e at bits [6e, 6e + 6)
-      const size_t rowb = (size_t)P / 32 * 24;
-      unsigned char* b0 = (unsigned char*)out + (size_t)m0 * rowb;
-      unsigned char* b1 = (unsigned char*)out + (size_t)(m0 + 1) * rowb;
-      for (int c = tid; c < P / 32; c += nthr) {
-        uint32_t o0[6] = {0u, 0u, 0u, 0u, 0u, 0u}, o1[6] = {0u, 0u, 0u, 0u, 0u, 0u};
-#pragma unroll
-        for (int h = 0; h < 8; ++h) {
-          const u32x4 w = ((const u32x4*)lc_buf)[8 * c + h];
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            const int bit = 6 * (4 * h + k);
-            const uint32_t v0 = w[k] & 0x3Fu, v1 = (w[k] >> 16) & 0x3Fu;
-            o0[bit >> 5] |= v0 << (bit & 31);
-            o1[bit >> 5] |= v1 << (bit & 31);
-            if ((bit & 31) > 26) {
-              o0[(bit >> 5) + 1] |= v0 >> (32 - (bit & 31));
-              o1[(bit >> 5) + 1] |= v1 >> (32 - (bit & 31));
-            }
-          }
-        }
-#pragma unroll
-        for (int i = 0; i < 3; ++i) {
-          ((uint2*)(b0 + 24 * (size_t)c))[i] = uint2{o0[2 * i], o0[2 * i + 1]};
-          if (has1) ((uint2*)(b1 + 24 * (size_t)c))[i] = uint2{o1[2 * i], o1[2 * i + 1]};
-        }
-      }
-    }
     if (F8 == 1) {
       // codes: 16 positions per chunk, byte 0 / byte 2 of each word -> rows m0 / m0 + 1
       unsigned char* b0 = (unsigned char*)out + (size_t)m0 * P;
@@ -665,16 +625,13 @@ int launch_quant_lc(int dtype, int mode, const void* x, int M, int K, int q_max,
                     const uint32_t* lctab, int Kn, const int32_t* amap, int P,
                     const int32_t* sal, int S, int S_pad, const uint32_t* cmax,
                     const int32_t* nonsal, void* out, uint32_t* key_clear, int clear_words,
-                    hipStream_t s, float* out_scale, void* out_xs, bool f6) {
+                    hipStream_t s, float* out_scale, void* out_xs) {
 #define SQMP_LC(DTT, MD, GSV, F8V)                                                           \
   quant_lc_launch<DTT, MD, GSV, F8V>(x, M, K, q_max, G, lctab, Kn, amap, P, sal, S, S_pad,   \
                                      cmax, nonsal, out, key_clear, clear_words, out_scale,  \
                                      out_xs, s)
 #define SQMP_LC_MODE(DTT)                                                                  \
-  (out_scale && f6 ? (mode == LC_MODE_TOKEN    ? SQMP_LC(DTT, LC_MODE_TOKEN, 0, 2)         \
-                      : mode == LC_MODE_TENSOR ? SQMP_LC(DTT, LC_MODE_TENSOR, 0, 2)        \
-                                               : SQMP_EUNSUPPORTED)                        \
-   : out_scale ? (mode == LC_MODE_TOKEN    ? SQMP_LC(DTT, LC_MODE_TOKEN, 0, 1)             \
+  (out_scale ? (mode == LC_MODE_TOKEN    ? SQMP_LC(DTT, LC_MODE_TOKEN, 0, 1)               \
                 : mode == LC_MODE_TENSOR ? SQMP_LC(DTT, LC_MODE_TENSOR, 0, 1)              \
                                          : SQMP_EUNSUPPORTED)                              \
    : mode == LC_MODE_TOKEN ? SQMP_LC(DTT, LC_MODE_TOKEN, 0, 0)                             \

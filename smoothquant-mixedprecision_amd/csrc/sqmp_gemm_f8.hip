@@ -550,312 +550,6 @@ __global__ __launch_bounds__(512, 1) void gemm_f8v2_kernel(
   }
 }
 
-// ================================================================= gemm_f6
-// The v2 contraction with both code operands in OCP FP6 e2m3 (every 4-bit code |c| <= 7 is
-// exact: 1.5 mantissa bits suffice) on v_mfma_scale_f32_16x16x128_f8f6f4 with fmt 2/2: the
-// same exact integer block sums (|sum| <= 128 * 49, exact in fp32), the same fp32 fold
-// order and the same tail, so y is bit-identical to gemm_f8v2 -- at twice its MFMA rate
-// (the e2m3 instruction runs at the FP4 rate) and with 0.75-byte operands.
-//
-// Operand format "f6 packed": per row, every 32 consecutive packed positions are one
-// 24-byte block, value e at bits [6 e, 6 e + 6) of the little-endian 192-bit block; a
-// 128-position block (one MFMA K step) is 96 bytes, lane group q taking block q.
-// Ring: 3 slots of A 24 KiB + B 24 KiB (256 rows x 96 B) + S 1 KiB, the DMA of stage k + 2
-// running under the compute of stage k (the f8v2 kernel's 2-slot ring left 40 % of wave
-// cycles waiting).  An image row is 96 B = 6 chunks of 16 B, stored contiguously (LDS-DMA
-// writes 16 B per lane in order); rows with bit 3 set hold their chunks rotated by one
-// (physical chunk (c + 1) mod 6), which makes the three ds_read_b64 of every fragment
-// (8-B units 3 q + t) conflict-free.  Salient tail stages are 32 D columns (64-B rows,
-// chunk q at q ^ 2 bit3(row), conflict-free for ds_read_b128).
-namespace {
-constexpr int F6_A = 0, F6_B = 24576, F6_S = 49152;
-constexpr int F6_SLOT = 50176;  // A 24 KiB + B 24 KiB + S 1 KiB
-constexpr int F6_NSLOT = 3;     // 150528 B
-
-__device__ inline int f6_rot(int r) { return (r >> 3) & 1; }
-// byte offset of 8-B unit u (0..11) of image row r
-__device__ inline int f6_unit(int r, int u) {
-  int pc = (u >> 1) + f6_rot(r);
-  pc = pc >= 6 ? pc - 6 : pc;
-  return r * 96 + pc * 16 + (u & 1) * 8;
-}
-__device__ inline int f6_tail(int r, int c) { return r * 64 + ((c ^ (f6_rot(r) << 1)) << 4); }
-}  // namespace
-
-// PROBE (tools/probe/f6_rate_probe.hip only): 1 = no compute, 2 = no DMA -- the two rates
-// the kernel overlaps, measured apart.  The library instantiates PROBE = 0.
-template <class DT, int PROBE = 0>
-__global__ __launch_bounds__(512, 1) void gemm_f6_kernel(
-    const unsigned char* __restrict__ A6, const float* __restrict__ ascale,
-    const typename DT::T* __restrict__ XS, const unsigned char* __restrict__ W6,
-    const float* __restrict__ ws32, const typename DT::T* __restrict__ wsal,
-    const typename DT::T* __restrict__ bias, typename DT::T* __restrict__ Y, int M, int N,
-    int Kp, int S_pad, int Gw, int ngw, int tiles_m, int tiles_n, int group_m) {
-  typedef typename DT::T T;
-  __shared__ __attribute__((aligned(16))) unsigned char lds[F6_NSLOT * F6_SLOT];
-
-  int tm, tn;
-  tile_coords(tiles_m, tiles_n, group_m, tm, tn);
-  const int m0 = tm * 256, n0 = tn * 256;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 2, wn = wave & 3;
-  const int r16 = lane & 15, q = lane >> 4;
-  const int nk = Kp / 128, nkt = nk + S_pad / 32;
-  const int Np = pad_n(N);
-  const uint32_t rp = (uint32_t)(Kp / 128) * 96u;  // operand row pitch (bytes)
-
-  // ---- DMA geometry, code stages: piece 3 wave + j = image bytes [1024 p, 1024 p + 1024),
-  // lane L's 16 B at image byte 1024 p + 16 L = row R, physical chunk pc, which holds
-  // logical chunk (pc - rot(R)) mod 6.  A and B share the row pitch, hence the offsets.
-  // (recomputed per stage: a few VALU ops instead of 3 live VGPRs)
-  auto voff = [&](int j) {
-    const int b = 1024 * (3 * wave + j) + 16 * lane;
-    const int R = b / 96, pc = (b % 96) / 16;
-    int lc = pc - f6_rot(R);
-    lc = lc < 0 ? lc + 6 : lc;
-    return (uint32_t)R * rp + (uint32_t)lc * 16u;
-  };
-  // tail stages: piece 2 wave + j = rows 16 p .. 16 p + 15, lane L row 16 p + (L >> 2)
-  auto trow = [&](int j) { return 16 * (2 * wave + j) + (lane >> 2); };
-  auto tchunk = [&](int j) { return (uint32_t)(((lane & 3) ^ (f6_rot(trow(j)) << 1)) << 4); };
-  const i32x4b rA = rsrc_of(A6 + (size_t)m0 * rp, 0xFFFFFFFFu);
-  const i32x4b rW = rsrc_of(W6 + (size_t)n0 * rp, 0xFFFFFFFFu);
-  const i32x4b rX = rsrc_of(XS + (size_t)m0 * S_pad, 0xFFFFFFFFu);
-  const i32x4b rL = rsrc_of(wsal, 0xFFFFFFFFu);
-  const i32x4b rS = rsrc_of(ws32 + n0, 0xFFFFFFFFu);
-  const i32x4b rR = rsrc_of(ascale + m0, (uint32_t)(M - m0) * 4u);  // rows >= M read 0
-
-  auto issue = [&](int kt) {
-    unsigned char* slot = lds + (kt % F6_NSLOT) * F6_SLOT;
-    if (kt < nk) {
-      const uint32_t so = (uint32_t)kt * 96u;
-#pragma unroll
-      for (int j = 0; j < 3; ++j) {
-        const uint32_t v = voff(j);
-        dma16(rA, v, so, slot + F6_A + (3 * wave + j) * 1024);
-        dma16(rW, v, so, slot + F6_B + (3 * wave + j) * 1024);
-      }
-      if (wave == 0) {
-        const int g = min((kt * 128) / Gw, ngw - 1);
-        dma16(rS, (uint32_t)lane * 16, (uint32_t)g * Np * 4, slot + F6_S);
-      }
-    } else {
-      const uint32_t so = (uint32_t)(kt - nk) * 32 * sizeof(T);
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const uint32_t c = tchunk(j);
-        dma16(rX, (uint32_t)trow(j) * S_pad * sizeof(T) + c, so, slot + F6_A + (2 * wave + j) * 1024);
-        dma16(rL, (uint32_t)min(n0 + trow(j), N - 1) * S_pad * sizeof(T) + c, so,
-              slot + F6_B + (2 * wave + j) * 1024);
-      }
-      if (wave == 0 && kt == nk) dma16(rR, (uint32_t)lane * 16, 0u, slot + F6_S);
-    }
-  };
-  // DMA ops this wave issued for stage kt (the vmcnt of the stage behind it)
-  auto wait_for = [&](int kt) {  // every piece of stage kt landed, stage kt + 1 may fly
-    if (kt + 1 >= nkt) {
-      vmw<0>();
-    } else if (kt + 1 < nk) {
-      if (wave == 0) vmw<7>(); else vmw<6>();
-    } else if (kt + 1 == nk) {
-      if (wave == 0) vmw<5>(); else vmw<4>();
-    } else {
-      vmw<4>();
-    }
-  };
-
-  f32x4 tot[8][4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) tot[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const int wcol0 = wn * 64 + r16;   // + 16 j: the lane's weight row in the B image
-  const int xrow0 = wm * 128 + r16;  // + 16 i: the lane's activation row in the A image
-  // the three 8-B units of the lane's fragment within its row (rows 16 i + r16 share the
-  // rotation: it depends on bit 3 of the row only), so fragment t of tile i is at
-  // (row0 + 16 i) * 96 + uo(t) -- an immediate offset per tile
-  const int uo0 = f6_unit(r16, 3 * q) - r16 * 96, uo1 = f6_unit(r16, 3 * q + 1) - r16 * 96,
-            uo2 = f6_unit(r16, 3 * q + 2) - r16 * 96;
-  auto frag = [&](const unsigned char* __restrict__ img, int r) {
-    const unsigned char* row = img + r * 96;
-    const uint2 a = *(const uint2*)(row + uo0);
-    const uint2 b = *(const uint2*)(row + uo1);
-    const uint2 c = *(const uint2*)(row + uo2);
-    return i32x8b{(int)a.x, (int)a.y, (int)b.x, (int)b.y, (int)c.x, (int)c.y, 0, 0};
-  };
-  auto compute_f6 = [&](const unsigned char* __restrict__ slot) {
-    i32x8b bw[4];
-    f32x4 sv[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      bw[j] = frag(slot + F6_B, wcol0 + 16 * j);
-      sv[j] = *(const f32x4*)(slot + F6_S + (wn * 64 + 16 * j + 4 * q) * 4);
-    }
-    const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
-    i32x8b ax = frag(slot + F6_A, xrow0);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const i32x8b cur = ax;
-      if (i + 1 < 8) ax = frag(slot + F6_A, xrow0 + 16 * (i + 1));
-      f32x4 t0 = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(bw[0], cur, zero, 2, 2, 0, 127, 0, 127);
-      f32x4 t1 = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(bw[1], cur, zero, 2, 2, 0, 127, 0, 127);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) tot[i][0][r] = __builtin_fmaf(t0[r], sv[0][r], tot[i][0][r]);
-      t0 = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(bw[2], cur, zero, 2, 2, 0, 127, 0, 127);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) tot[i][1][r] = __builtin_fmaf(t1[r], sv[1][r], tot[i][1][r]);
-      t1 = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(bw[3], cur, zero, 2, 2, 0, 127, 0, 127);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) tot[i][2][r] = __builtin_fmaf(t0[r], sv[2][r], tot[i][2][r]);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) tot[i][3][r] = __builtin_fmaf(t1[r], sv[3][r], tot[i][3][r]);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  };
-  auto apply_row_scales = [&](const float* rs) {
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const float s = rs[wm * 128 + 16 * i + r16];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) tot[i][j] *= s;
-    }
-  };
-  auto compute_tail = [&](const unsigned char* __restrict__ slot) {
-    u32x4 bf[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) bf[j] = *(const u32x4*)(slot + F6_B + f6_tail(wcol0 + 16 * j, q));
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const u32x4 af = *(const u32x4*)(slot + F6_A + f6_tail(xrow0 + 16 * i, q));
-#pragma unroll
-      for (int j = 0; j < 4; ++j) Mfma<DT>::run(tot[i][j], bf[j], af);
-    }
-  };
-
-  // ---- three-slot ring: stages k + 1 and k + 2 in flight while stage k computes
-  auto top = [&](int kt) {
-    if (!(PROBE & 2)) wait_for(kt);
-    __builtin_amdgcn_s_barrier();  // every wave's pieces of stage kt have landed; every
-    asm volatile("" ::: "memory");  // wave is past its reads of slot (kt + 2) % 3
-    __builtin_amdgcn_sched_barrier(0);
-    return (const unsigned char*)(lds + (kt % F6_NSLOT) * F6_SLOT);
-  };
-  constexpr bool DMA = !(PROBE & 2), COMPUTE = !(PROBE & 1);
-  if (DMA) issue(0);
-  if (DMA && nkt > 1) issue(1);
-  int kt = 0;
-  for (; kt < nk; ++kt) {
-    const unsigned char* slot = top(kt);
-    if (DMA && kt + 2 < nkt) issue(kt + 2);
-    if (COMPUTE) compute_f6(slot);
-  }
-  for (; kt < nkt; ++kt) {
-    const unsigned char* slot = top(kt);
-    if (DMA && kt + 2 < nkt) issue(kt + 2);
-    if (COMPUTE && kt == nk) apply_row_scales((const float*)(slot + F6_S));
-    if (COMPUTE) compute_tail(slot);
-  }
-  if (nkt == nk) {  // no salient tail: row scales straight from global memory
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int gm = m0 + wm * 128 + 16 * i + r16;
-      const float s = gm < M ? ascale[gm] : 0.f;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) tot[i][j] *= s;
-    }
-  }
-
-  // ---- epilogue (as gemm_f8v2): full-width tiles staged in LDS, 512-B row stores
-  if (n0 + 256 <= N && (N & 7) == 0) {
-    __builtin_amdgcn_s_barrier();  // every wave is past its last fragment read
-    asm volatile("" ::: "memory");
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int nl = wn * 64 + 16 * j + 4 * q;
-      float bv[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) bv[r] = bias ? DT::to_f(bias[n0 + nl + r]) : 0.f;
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int ml = xrow0 + 16 * i;
-        T v[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = DT::from_f(tot[i][j][r] + bv[r]);
-        *(uint2*)(lds + ml * 512 + (((nl >> 3) ^ (ml & 31)) << 4) + (nl & 4) * 2) =
-            *(const uint2*)v;
-      }
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's tile writes landed
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    const int c = tid & 31;
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      const int ml = 16 * k + (tid >> 5);
-      const u32x4 val = *(const u32x4*)(lds + ml * 512 + ((c ^ (ml & 31)) << 4));
-      if (m0 + ml < M) *(u32x4*)(Y + (size_t)(m0 + ml) * N + n0 + c * 8) = val;
-    }
-    return;
-  }
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int nb = n0 + wn * 64 + 16 * j + 4 * q;
-    if (nb >= N) continue;
-    float bv[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) bv[r] = (bias && nb + r < N) ? DT::to_f(bias[nb + r]) : 0.f;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int gm = m0 + xrow0 + 16 * i;
-      if (gm >= M) continue;
-      T v[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = DT::from_f(tot[i][j][r] + bv[r]);
-      T* dst = Y + (size_t)gm * N + nb;
-      if (nb + 4 <= N && (N & 3) == 0) {
-        *(uint2*)dst = *(const uint2*)v;
-      } else {
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          if (nb + r < N) dst[r] = v[r];
-      }
-    }
-  }
-}
-
-// bpack int4 codes -> f6-packed e2m3 rows [Np][Kp * 3 / 4]: one 24-byte block (32
-// positions) per thread.
-__device__ inline uint32_t e2m3_of_code(int c) {
-  // |c| -> e2m3 magnitude bits through a byte table (v_perm_b32): 0 8 16 20 24 26 28 30
-  const uint32_t a = (uint32_t)(c < 0 ? -c : c);
-  return (__builtin_amdgcn_perm(0x1E1C1A18u, 0x14100800u, a) & 0xFFu) | (c < 0 ? 0x20u : 0u);
-}
-
-__global__ __launch_bounds__(256) void pack_f6_kernel(const uint32_t* __restrict__ codes,
-                                                      int Np, int Kp,
-                                                      uint32_t* __restrict__ w6) {
-  const size_t t = (size_t)blockIdx.x * 256 + threadIdx.x;
-  const int nblk = Kp / 32;
-  if (t >= (size_t)Np * nblk) return;
-  const int n = (int)(t / nblk);
-  const int p0 = (int)(t % nblk) * 32;
-  uint32_t o[6] = {0u, 0u, 0u, 0u, 0u, 0u};
-#pragma unroll
-  for (int e = 0; e < 32; ++e) {
-    const int p = p0 + e;
-    const uint32_t wd = codes[(size_t)n * (Kp / 8) + bpack_dword(p)];
-    const uint32_t v = e2m3_of_code((int)((wd >> bpack_shift(p)) & 0xFu) - 8);
-    const int bit = 6 * e;
-    o[bit >> 5] |= v << (bit & 31);
-    if ((bit & 31) > 26) o[(bit >> 5) + 1] |= v >> (32 - (bit & 31));
-  }
-  uint32_t* dst = w6 + t * 6;
-#pragma unroll
-  for (int i = 0; i < 6; ++i) dst[i] = o[i];
-}
-
 // bpack int4 codes -> e4m3 bytes [Np][Kp] (natural packed order), D scales -> fp32.
 template <class DT>
 __global__ __launch_bounds__(256) void pack_f8_kernel(const uint32_t* __restrict__ codes,
@@ -967,45 +661,4 @@ extern "C" int sqmp_gemm_f8_colmax(const void* a8, const float* ascale, const vo
   if (!colmax) return SQMP_EINVAL;
   return gemm_f8_impl(a8, ascale, xs, w8, ws32, wsal, bias, y, dtype, M, N, Kp, S_pad, Gw, ngw,
                       colmax, stream);
-}
-
-extern "C" int sqmp_pack_f6(const void* codes, int N, int Kp, void* w6, void* stream) {
-  if (!codes || !w6 || N <= 0 || Kp <= 0 || Kp % 128 != 0) return SQMP_EINVAL;
-  const int Np = pad_n(N);
-  const size_t n = (size_t)Np * (Kp / 32);
-  pack_f6_kernel<<<dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream>>>(
-      (const uint32_t*)codes, Np, Kp, (uint32_t*)w6);
-  SQMP_LAUNCH_CHECK();
-  return SQMP_OK;
-}
-
-extern "C" int sqmp_gemm_f6(const void* a6, const float* ascale, const void* xs, const void* w6,
-                            const float* ws32, const void* wsal, const void* bias, void* y,
-                            int dtype, int M, int N, int Kp, int S_pad, int Gw, int ngw,
-                            void* stream) {
-  if (M < 0 || N <= 0 || Kp <= 0 || Kp % 128 != 0 || S_pad < 0 || S_pad % 64 != 0)
-    return SQMP_EINVAL;
-  if (!a6 || !ascale || !w6 || !ws32 || !y || (S_pad > 0 && (!xs || !wsal))) return SQMP_EINVAL;
-  if (Gw <= 0 || Gw % 128 != 0 || ngw <= 0) return SQMP_EUNSUPPORTED;
-  if (dtype != SQMP_F16 && dtype != SQMP_BF16) return SQMP_EUNSUPPORTED;
-  if (M == 0) return SQMP_OK;
-  hipStream_t s = (hipStream_t)stream;
-  const int tiles_m = cdiv(M, 256), tiles_n = cdiv(N, 256);
-  const dim3 grid(tiles_m * tiles_n), block(512);
-  static const int group_m = [] {
-    const char* e = getenv("SQMP_GROUP_M");
-    return e && atoi(e) > 0 ? atoi(e) : 4;
-  }();
-  if (dtype == SQMP_F16)
-    gemm_f6_kernel<F16><<<grid, block, 0, s>>>(
-        (const unsigned char*)a6, ascale, (const F16::T*)xs, (const unsigned char*)w6, ws32,
-        (const F16::T*)wsal, (const F16::T*)bias, (F16::T*)y, M, N, Kp, S_pad, Gw, ngw,
-        tiles_m, tiles_n, group_m);
-  else
-    gemm_f6_kernel<BF16><<<grid, block, 0, s>>>(
-        (const unsigned char*)a6, ascale, (const BF16::T*)xs, (const unsigned char*)w6, ws32,
-        (const BF16::T*)wsal, (const BF16::T*)bias, (BF16::T*)y, M, N, Kp, S_pad, Gw, ngw,
-        tiles_m, tiles_n, group_m);
-  SQMP_LAUNCH_CHECK();
-  return SQMP_OK;
 }

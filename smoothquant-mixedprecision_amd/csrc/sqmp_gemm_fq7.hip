@@ -100,7 +100,8 @@ __device__ inline void fence(V& v) {
 
 __host__ __device__ inline int brev3(int c) { return ((c & 1) << 2) | (c & 2) | ((c >> 2) & 1); }
 
-// DIAG (timing diagnostics, wrong results by design; 0 = the product kernel): 1 no weight
+// DIAG (timing diagnostics, wrong results by design, instantiated only in a SQMP_DIAG_BUILD;
+// 0 = the product kernel): 1 no weight
 // register loads after the prologue, 2 no A DMA after the prologue, 3 no int4 decode, 4 no
 // per-stage barrier
 // J = 16-row weight tiles per wave: tile TM x TN with TN = 8 * 16 J (J = 4: 128 x 512;
@@ -481,6 +482,9 @@ static int group_m_tr_env() {
   return v;
 }
 
+#ifdef SQMP_DIAG_BUILD
+// timing-diagnostic variants (wrong results by design) only in a diagnostics build:
+// SQMP_DIAG=1 python smoothquant-mixedprecision_amd/build_ext.py --force
 static int diag_env() {
   static int v = [] {
     const char* e = getenv("SQMP_FQ7_DIAG");
@@ -488,6 +492,7 @@ static int diag_env() {
   }();
   return v;
 }
+#endif
 
 template <class DT, int GB, int TM, int J, int DIAG = 0>
 static int launch_k(const void* a, const void* bt, const void* st, const void* salt,
@@ -507,6 +512,7 @@ static int launch(const void* a, const void* bt, const void* st, const void* sal
                   const void* bias, void* y, int M, int N, int Kp, int S_pad, int Gw, int ngw,
                   uint32_t* colmax, hipStream_t s) {
 #define SQMP_L(D) launch_k<DT, GB, TM, J, D>(a, bt, st, salt, bias, y, M, N, Kp, S_pad, Gw, ngw, colmax, s)
+#ifdef SQMP_DIAG_BUILD
   if (std::is_same<DT, F16>::value && GB == 1 && TM == 128 * 4 / J) {
     switch (diag_env()) {
       case 1: return SQMP_L(1);
@@ -516,6 +522,7 @@ static int launch(const void* a, const void* bt, const void* st, const void* sal
       default: break;
     }
   }
+#endif
   return SQMP_L(0);
 #undef SQMP_L
 }

@@ -259,22 +259,6 @@ __global__ __launch_bounds__(128 * WN, 4 / WN) void gemm_x3_kernel(
   }
 }
 
-// [R][L] fp32 (row stride L) -> three bf16 planes [3][ldr rows][L]; rows >= R zero-filled
-__global__ void split3_kernel(const float* __restrict__ src, int R, int L, int ldr,
-                              uint16_t* __restrict__ dst) {
-  const size_t n = (size_t)ldr * L;
-  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
-       i += (size_t)gridDim.x * blockDim.x) {
-    const size_t row = i / L;
-    const float v = row < (size_t)R ? src[i] : 0.f;
-    uint32_t h, m, l;
-    split3(v, h, m, l);
-    dst[i] = (uint16_t)h;
-    dst[n + i] = (uint16_t)m;
-    dst[2 * n + i] = (uint16_t)l;
-  }
-}
-
 // one wave per row: exp[r] = row_exp_of(max_c |src[r][c]|)
 __global__ __launch_bounds__(256) void row_exp_kernel(const float* __restrict__ src, int R, int L,
                                                       int* __restrict__ exp_out) {
@@ -373,38 +357,6 @@ extern "C" int sqmp_gemm_h2(const float* a, const int* aexp, const void* b2, con
     if (wide) SQMP_H2(false, 4, 256, tiles_n2); else if (small) SQMP_H2(false, 4, 128, tiles_n); else SQMP_H2(false, 2, 128, tiles_n);
   }
 #undef SQMP_H2
-  SQMP_LAUNCH_CHECK();
-  return SQMP_OK;
-}
-
-extern "C" int sqmp_split3_bf16(const float* src, int R, int L, int ldr, void* dst,
-                                void* stream) {
-  if (!src || !dst || R <= 0 || L <= 0 || ldr < R) return SQMP_EINVAL;
-  const size_t n = (size_t)ldr * L;
-  const size_t nb = (n + 255) / 256;
-  const int blocks = (int)(nb < 8192 ? nb : 8192);
-  split3_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(src, R, L, ldr, (uint16_t*)dst);
-  SQMP_LAUNCH_CHECK();
-  return SQMP_OK;
-}
-
-extern "C" int sqmp_gemm_x3(const float* a, const void* b3, const float* bias, float* y, int M,
-                            int N, int L, uint32_t* colmax, void* stream) {
-  if (!a || !b3 || !y || M < 0 || N <= 0 || L <= 0) return SQMP_EINVAL;
-  if (L % X3_BK != 0) return SQMP_EINVAL;
-  if (M == 0) return SQMP_OK;
-  const int Np = pad_n(N);
-  const int tiles_m = cdiv(M, X3_BM), tiles_n = cdiv(N, X3_BN);
-  const bool small = (long)tiles_m * tiles_n < 2L * 256;
-#define SQMP_X3(CM, WN)                                                                  \
-  gemm_x3_kernel<CM, WN><<<tiles_m * tiles_n, 128 * WN, 0, (hipStream_t)stream>>>(       \
-      a, (const uint16_t*)b3, bias, y, M, N, L, Np, tiles_m, tiles_n, colmax, nullptr, nullptr)
-  if (colmax) {
-    if (small) SQMP_X3(true, 4); else SQMP_X3(true, 2);
-  } else {
-    if (small) SQMP_X3(false, 4); else SQMP_X3(false, 2);
-  }
-#undef SQMP_X3
   SQMP_LAUNCH_CHECK();
   return SQMP_OK;
 }

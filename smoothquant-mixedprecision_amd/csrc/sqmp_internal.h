@@ -43,8 +43,7 @@ int launch_quant_lc(int dtype, int mode, const void* x, int M, int K, int q_max,
                     const uint32_t* lctab, int Kn, const int32_t* amap, int P,
                     const int32_t* sal, int S, int S_pad, const uint32_t* cmax,
                     const int32_t* nonsal, void* out, uint32_t* key_clear, int clear_words,
-                    hipStream_t s, float* out_scale = nullptr, void* out_xs = nullptr,
-                    bool f6 = false);
+                    hipStream_t s, float* out_scale = nullptr, void* out_xs = nullptr);
 // key_clear: zeroed (clear_words % 4 == 0), may be NULL.  out_scale != NULL selects the
 // e4m3 code output (token / tensor modes): out = codes [M][P], out_xs = D [M][S_pad].
 

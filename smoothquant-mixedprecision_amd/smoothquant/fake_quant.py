@@ -201,11 +201,8 @@ _PW_KEY = ("w_codes", "w_scale", "w_salient", "w_perm", "w_amap", "w_amap_fq", "
 class W4A4Linear(nn.Module):
     """Mixed-precision W4A4 linear: salient input channels in D, the rest int4/int8.
 
-    Forward kernels (chosen per layer, see `kernel`; "auto" = "f8" where ops.f8_auto (fp16)
-    ("f6" instead when ops.F6_AUTO), "fqt" for large sorted per_group batches, else "fq"
-    unless ops.I8_AUTO):
-      "f6"  as "f8" with both code operands in FP6 e2m3 (weight groups of whole 128-blocks):
-            twice the MFMA rate, 0.75-byte operands, the same y bit for bit.
+    Forward kernels (chosen per layer, see `kernel`; "auto" = "f8" where ops.f8_auto (fp16),
+    "fqt" for large sorted per_group batches, else "fq" unless ops.I8_AUTO):
       "f8"  per_token / per_tensor 4-bit activations: e4m3 act codes x e4m3 weight codes on
             the block-scaled FP8 MFMA (exact integer block sums), per-group fp32 folds.
       "i8"  per_token / per_tensor activations: int8 act codes x int4 weight codes on the
@@ -506,12 +503,8 @@ class W4A4Linear(nn.Module):
         if bias is not None and bias.device != x.device:
             raise RuntimeError(f"bias on {bias.device}, input on {x.device}: move the module "
                                "to the input's device")
-        use_f6 = (self.kernel == "f6" or
-                  (self.kernel == "auto" and ops.F6_AUTO and ops.f6_eligible(pw, amode, bits)
-                   and ops.f8_input_ok(xc)))
-        use_f8 = use_f6 or self.kernel == "f8" or (
-            self.kernel == "auto" and ops.f8_auto(pw, amode, bits)
-            and ops.f8_input_ok(xc))
+        use_f8 = self.kernel == "f8" or (
+            self.kernel == "auto" and ops.f8_auto(pw, amode, bits) and ops.f8_input_ok(xc))
         use_i8 = not use_f8 and (
             self.kernel == "i8" or
             (self.kernel == "auto" and ops.I8_AUTO and ops.i8_eligible(pw, amode, bits)))
@@ -519,9 +512,7 @@ class W4A4Linear(nn.Module):
                    and ops.fqt_eligible(pw, amode, bits, ag, x2.shape[0],
                                         force=self.kernel == "fqt")
                    and ops.f8_input_ok(xc))
-        if use_f6:
-            a8, sa, xs = ops.quant_act_f6(xc, pw, amode, bits)
-        elif use_f8:
+        if use_f8:
             a8, sa, xs = ops.quant_act_f8(xc, pw, amode, bits)
         elif use_i8:
             a8, sa, xs = ops.quant_act_i8(xc, pw, amode, bits)
@@ -539,14 +530,12 @@ class W4A4Linear(nn.Module):
         # per_group (sorted) / per_tensor the faithful GEMM also writes the column maxima of
         # y into the output quantizer's workspace, which then skips its statistics pass
         fuse = (ospec is not None and ospec[0] in ("per_group", "per_tensor") and _OQ_FUSE
-                and not use_i8 and not use_f6
+                and not use_i8
                 and (not use_f8 or pw.Gw % 128 == 0)           # the 16x16x128 FP8 kernel
                 and (not use_fqt or c4[1].dim() == 3)          # the tile-major fqt7 GEMM
                 and (self.salient_indices is None or pw.K - pw.S > 0))
         colmax = ops.out_quant_workspace(x2.shape[0], pw.N, x2.device)["buf"] if fuse else None
-        if use_f6:
-            y = ops.gemm_f6(a8, sa, xs, pw, bias)
-        elif use_f8:
+        if use_f8:
             y = ops.gemm_f8(a8, sa, xs, pw, bias, colmax=colmax)
         elif use_i8:
             y = ops.gemm_i8(a8, sa, xs, pw, bias)

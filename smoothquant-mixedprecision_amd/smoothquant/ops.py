@@ -90,10 +90,8 @@ class PackedWeight:
     posmap: Optional[torch.Tensor] = field(default=None)  # int32 [K]: packed position of column k
     sal_key: Optional[tuple] = field(default=None)        # identity of the salient set (host)
     w8: Optional[torch.Tensor] = field(default=None)     # uint8 [Np, Kp] e4m3 codes (f8 GEMM)
-    ws32: Optional[torch.Tensor] = field(default=None)   # fp32 [ngw, Np] scales (f8/f6 GEMM)
-    w6: Optional[torch.Tensor] = field(default=None)     # uint8 [Np, Kp*3/4] e2m3 (f6 GEMM)
+    ws32: Optional[torch.Tensor] = field(default=None)   # fp32 [ngw, Np] scales (f8 GEMM)
     fq7: Optional[tuple] = field(default=None)           # (codes_t, scale_t, sal_t, J) of gemm_fq7
-    x3: Optional[torch.Tensor] = field(default=None)     # bf16 [3, Np, Kp + S_pad] (gemm_x3)
     h2: Optional[tuple] = field(default=None)            # (f16 [2, Np, L], int32 [Np]) (gemm_h2)
 
     @property
@@ -494,8 +492,7 @@ def gemm_fq7(a: torch.Tensor, pw: PackedWeight, bias: Optional[torch.Tensor],
 
 
 # The faithful GEMM of fp32 layers: "h2" (default) -- row-scaled two-piece fp16 splits on the
-# f16 MFMA (sqmp_gemm_h2, 3 MFMAs per product); "x3" -- exact three-piece bf16 splits on the
-# bf16 MFMA (sqmp_gemm_x3, 6 MFMAs); "f32" -- the f32 MFMA (1/16 of the bf16 rate).
+# f16 MFMA (sqmp_gemm_h2, 3 MFMAs per product); "f32" -- the f32 MFMA (1/16 of the bf16 rate).
 F32_GEMM = os.environ.get("SQMP_F32_GEMM", "h2")
 
 
@@ -505,19 +502,6 @@ def _w_full(pw: PackedWeight) -> torch.Tensor:
         pw.dense if pw.dense is not None else dequant_weight_packed(pw))
     full = torch.cat([w, pw.wsal], dim=1) if pw.S_pad else w
     return full.contiguous()
-
-
-def x3_operand(pw: PackedWeight) -> torch.Tensor:
-    """bf16 planes [3, Np, Kp + S_pad] of the packed-order W_hat + exact salient slice
-    (sqmp_split3_bf16), built once per packed fp32 weight."""
-    if pw.x3 is None:
-        full = _w_full(pw)
-        Np, L = pad_n(pw.N), pw.Kp + pw.S_pad
-        planes = torch.empty((3, Np, L), dtype=torch.bfloat16, device=full.device)
-        check(load().sqmp_split3_bf16(_p(full), pw.N, L, Np, _p(planes), _stream(full)),
-              "split3_bf16")
-        pw.x3 = planes
-    return pw.x3
 
 
 def h2_operand(pw: PackedWeight):
@@ -551,21 +535,6 @@ def gemm_h2(a: torch.Tensor, pw: PackedWeight, bias: Optional[torch.Tensor],
     return y
 
 
-def gemm_x3(a: torch.Tensor, pw: PackedWeight, bias: Optional[torch.Tensor],
-            colmax: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """gemm_fq for fp32 layers on the bf16 MFMA (fp32-accurate products, see
-    include/sqmp_w4a4.h sqmp_gemm_x3)."""
-    M = a.shape[0]
-    L = pw.Kp + pw.S_pad
-    if a.dtype != torch.float32 or a.shape[1] != L or a.stride(0) != L:
-        raise ValueError("gemm_x3: A must be fp32 [M, Kp + S_pad] with row stride Kp + S_pad")
-    y = torch.empty((M, pw.N), dtype=torch.float32, device=a.device)
-    check(load().sqmp_gemm_x3(_p(a), _p(x3_operand(pw)), _p(bias), _p(y), M, pw.N, L,
-                              _p(colmax) if colmax is not None else None, _stream(a)),
-          "gemm_x3")
-    return y
-
-
 def gemm_fq(a: torch.Tensor, pw: PackedWeight, bias: Optional[torch.Tensor],
             colmax: Optional[torch.Tensor] = None) -> torch.Tensor:
     """y = D(A . W_hat^T + bias).  colmax: a zeroed uint32 buffer of >= N words that the
@@ -574,8 +543,6 @@ def gemm_fq(a: torch.Tensor, pw: PackedWeight, bias: Optional[torch.Tensor],
         return gemm_fq7(a, pw, bias, colmax)
     if pw.dtype == torch.float32 and F32_GEMM == "h2":
         return gemm_h2(a, pw, bias, colmax)
-    if pw.dtype == torch.float32 and F32_GEMM == "x3":
-        return gemm_x3(a, pw, bias, colmax)
     M = a.shape[0]
     y = torch.empty((M, pw.N), dtype=pw.dtype, device=a.device)
     b_op, nb = pw.gemm_operand
@@ -600,7 +567,7 @@ def gemm_i8(a8: torch.Tensor, sa: torch.Tensor, xs: torch.Tensor, pw: PackedWeig
 
 
 def _ws32(pw: PackedWeight) -> torch.Tensor:
-    """fp32 [ngw, Np] weight scales of the f8 / f6 GEMMs, built once per packed weight."""
+    """fp32 [ngw, Np] weight scales of the f8 GEMM, built once per packed weight."""
     if pw.ws32 is None:
         ws32 = torch.empty((pw.ngw, pad_n(pw.N)), dtype=torch.float32, device=pw.codes.device)
         check(load().sqmp_pack_f8(_p(pw.codes), _p(pw.wscale), _dtype_code(pw.dtype), pw.N,
@@ -620,26 +587,13 @@ def f8_operands(pw: PackedWeight):
     return pw.w8, _ws32(pw)
 
 
-def f6_operands(pw: PackedWeight):
-    """(w6, ws32) of the f6 GEMM, built once per packed weight."""
-    if pw.w6 is None:
-        w6 = torch.empty((pad_n(pw.N), pw.Kp // 32 * 24), dtype=torch.uint8,
-                         device=pw.codes.device)
-        check(load().sqmp_pack_f6(_p(pw.codes), pw.N, pw.Kp, _p(w6), _stream(pw.codes)),
-              "pack_f6")
-        pw.w6 = w6
-    return pw.w6, _ws32(pw)
-
-
-def quant_act_f8(x2: torch.Tensor, pw: PackedWeight, act_quant: str, n_bits: int,
-                 out_kind: int = _lib.OUT_F8):
+def quant_act_f8(x2: torch.Tensor, pw: PackedWeight, act_quant: str, n_bits: int):
     """x [M, K] -> (e4m3 codes [M, Kp] in packed order, fp32 row scales [M], exact salient
-    x [M, S_pad]) for gemm_f8 (per_token / per_tensor, n_bits <= 4).  out_kind OUT_F6: the
-    codes as f6-packed e2m3 [M, Kp * 3 / 4] bytes for gemm_f6."""
+    x [M, S_pad]) for gemm_f8 (per_token / per_tensor, n_bits <= 4)."""
     _require_gpu(x2, "quant_act")
     M, K = x2.shape
     Mp = _pad_rows(M)
-    width = pw.Kp // 32 * 24 if out_kind == _lib.OUT_F6 else pw.Kp
+    width = pw.Kp
     a8 = torch.empty((Mp, width), dtype=torch.uint8, device=x2.device)[:M]
     sa = torch.empty((M,), dtype=torch.float32, device=x2.device)
     xs = torch.empty((Mp, max(pw.S_pad, 8)), dtype=x2.dtype, device=x2.device)[:M]
@@ -651,7 +605,7 @@ def quant_act_f8(x2: torch.Tensor, pw: PackedWeight, act_quant: str, n_bits: int
         pw.posmap = build_posmap(pw.perm, K)
     status = lib.sqmp_quant_act_v2(_p(x2), _dtype_code(x2.dtype), M, K, ACT_MODES[act_quant],
                                    n_bits, 0, _p(pw.amap), pw.Kp, _p(pw.nonsal), _p(pw.salient),
-                                   pw.S, pw.S_pad, _p(pw.posmap), _lib.QA_CLEAN_WS, out_kind,
+                                   pw.S, pw.S_pad, _p(pw.posmap), _lib.QA_CLEAN_WS, _lib.OUT_F8,
                                    _p(a8), _p(sa), _p(xs), _p(e["buf"]), e["buf"].numel(),
                                    ctypes.c_void_p(stream))
     if status != _lib.SQMP_OK:
@@ -674,30 +628,6 @@ def gemm_f8(a8: torch.Tensor, sa: torch.Tensor, xs: torch.Tensor, pw: PackedWeig
     else:
         check(load().sqmp_gemm_f8_colmax(*args, _p(colmax), _stream(a8)), "gemm_f8")
     return y
-
-
-def quant_act_f6(x2: torch.Tensor, pw: PackedWeight, act_quant: str, n_bits: int):
-    """quant_act_f8 with the codes as f6-packed e2m3 (operands of gemm_f6)."""
-    return quant_act_f8(x2, pw, act_quant, n_bits, _lib.OUT_F6)
-
-
-def gemm_f6(a6: torch.Tensor, sa: torch.Tensor, xs: torch.Tensor, pw: PackedWeight,
-            bias: Optional[torch.Tensor]) -> torch.Tensor:
-    """gemm_f8 on FP6 e2m3 operands (twice the MFMA rate; the same y bit for bit)."""
-    M = a6.shape[0]
-    w6, ws32 = f6_operands(pw)
-    y = torch.empty((M, pw.N), dtype=pw.dtype, device=a6.device)
-    check(load().sqmp_gemm_f6(_p(a6), _p(sa), _p(xs) if pw.S_pad else None, _p(w6), _p(ws32),
-                              _p(pw.wsal) if pw.S_pad else None, _p(bias), _p(y),
-                              _dtype_code(pw.dtype), M, pw.N, pw.Kp, pw.S_pad, pw.Gw, pw.ngw,
-                              _stream(a6)), "gemm_f6")
-    return y
-
-
-def f6_eligible(pw: PackedWeight, act_quant: str, act_bits: int) -> bool:
-    """f8_eligible with weight groups of whole 128-position blocks (one 16x16x128 MFMA per
-    group block)."""
-    return f8_eligible(pw, act_quant, act_bits) and pw.Gw % 128 == 0
 
 
 def f8_eligible(pw: PackedWeight, act_quant: str, act_bits: int) -> bool:
@@ -734,10 +664,6 @@ def f8_auto(pw: PackedWeight, act_quant: str, act_bits: int) -> bool:
     (tests/test_gpu_configs.py, llama7b_l_bf16_pplflow).  bf16 layers run the faithful fq
     GEMM on the bit-exact operands instead; kernel="f8" still forces the FP8 path."""
     return F8_AUTO and pw.dtype == torch.float16 and f8_eligible(pw, act_quant, act_bits)
-# Whether kernel="auto" takes the FP6 path where f6_eligible (bit-identical to "f8").  Off:
-# measured at config 2 per_token, the f6 GEMM 310 us against f8v2's 285 us and the step
-# 0.386 against 0.343 ms (same box, interleaved runs); SQMP_F6=1 turns it on (A/B knob).
-F6_AUTO = os.environ.get("SQMP_F6", "0") == "1"
 
 
 def i8_eligible(pw: PackedWeight, act_quant: str, act_bits: int) -> bool:

@@ -117,7 +117,7 @@ def test_f8_full_size_config2_per_token():
                               importance=imp, salient_prop=p, group_size=Gs)
     pw = q.packed()
     assert ops.f8_eligible(pw, "per_token", 4)
-    q.kernel = "f8"  # (the bit-identical FP6 path is test_gpu_f6)
+    q.kernel = "f8"
     y = q(x)
     a = ops.quant_act_fp(x, pw, "per_token", 4, Gs)
     b_full = torch.cat([ops.dequant_weight_packed(pw), pw.wsal], dim=1)

@@ -1,5 +1,5 @@
 """Time the W4A4 GEMM alone on BASELINE config 2 (HIP events, GEMM on torch's current
-stream).  python tools/gemm_time.py [fq|fq7|fqt|i8|f8|f6] [iters]  -> one line: kind, avg ms, TFLOP/s."""
+stream).  python tools/gemm_time.py [fq|fq7|fqt|i8|f8] [iters]  -> one line: kind, avg ms, TFLOP/s."""
 import os
 import sys
 
@@ -26,9 +26,6 @@ elif kind == "fqt":
 elif kind == "fq7":
     a = ops.quant_act_fp(x, pw, act, 4, bench.G)
     run = lambda: ops.gemm_fq7(a, pw, lin.bias)  # noqa: E731
-elif kind == "f6":
-    a6, sa, xs = ops.quant_act_f6(x, pw, act, 4)
-    run = lambda: ops.gemm_f6(a6, sa, xs, pw, lin.bias)  # noqa: E731
 elif kind == "f8":
     a8, sa, xs = ops.quant_act_f8(x, pw, act, 4)
     run = lambda: ops.gemm_f8(a8, sa, xs, pw, lin.bias)  # noqa: E731
