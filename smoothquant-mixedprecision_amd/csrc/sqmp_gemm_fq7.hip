@@ -60,6 +60,13 @@ __device__ inline void vmwait_dyn(int n) {
     case 4: vmwait<4>(); break;
     case 5: vmwait<5>(); break;
     case 6: vmwait<6>(); break;
+    case 7: vmwait<7>(); break;
+    case 8: vmwait<8>(); break;
+    case 9: vmwait<9>(); break;
+    case 10: vmwait<10>(); break;
+    case 11: vmwait<11>(); break;
+    case 12: vmwait<12>(); break;
+    case 16: vmwait<16>(); break;
     default: vmwait<0>(); break;
   }
 }
@@ -110,7 +117,11 @@ __host__ __device__ inline int brev3(int c) { return ((c & 1) << 2) | (c & 2) | 
 // the register operand = the activation codes / group scales / salient x in this kernel's
 // tile-major layouts (sqmp_quant_act_c4 writes them so with ldsc < 0); kernel M = weight
 // rows, kernel N = tokens, Y[n][m] stored transposed with the bias per kernel row.
-template <class DT, int GB, int TM, int J, int DIAG = 0, bool TR = false>
+// OPT (the activation-order launch, A/B knob SQMP_FQT7_OPT): bit 0 -- waves 4-7 run at
+// s_setprio 1 through the K loop (MI355X_MICROARCH.md "Two waves per SIMD" item 4); bit 1 --
+// loader split: waves 0-3 issue every LDS-DMA piece of a stage (their own and those of
+// waves 4-7), waves 4-7 only wait, read and multiply (gemm_fq6's split)
+template <class DT, int GB, int TM, int J, int DIAG = 0, bool TR = false, int OPT = 0>
 __global__ __launch_bounds__(512, 1) void gemm_fq7_kernel(
     const typename DT::T* __restrict__ A, const uint32_t* __restrict__ Bt,
     const typename DT::T* __restrict__ St, const typename DT::T* __restrict__ Salt,
@@ -141,19 +152,29 @@ __global__ __launch_bounds__(512, 1) void gemm_fq7_kernel(
 
   // ---- A (x_hat) by LDS-DMA: piece i of wave w = rows 64 i + 8 w + (lane >> 3), the lane
   // moving logical chunk brev3(p ^ ((row >> 1) & 7)) into physical chunk p = lane & 7
-  const int arow = 8 * wave + (lane >> 3);
+  constexpr bool SPLIT = (OPT & 2) != 0;
+  constexpr int NO = SPLIT ? 2 : 1;       // waves whose pieces this wave issues
   const rsrc_t rA = make_rsrc(A + (size_t)m0 * lda);
-  uint32_t a_off[NA];
+  uint32_t a_off[NO][NA];
 #pragma unroll
-  for (int i = 0; i < NA; ++i)
-    a_off[i] = (uint32_t)((size_t)(arow + 64 * i) * lda * sizeof(T)) +
-               (uint32_t)(brev3((lane & 7) ^ ((arow >> 1) & 7)) << 4);
+  for (int o = 0; o < NO; ++o) {
+    const int arow = 8 * (wave + 4 * o) + (lane >> 3);
+#pragma unroll
+    for (int i = 0; i < NA; ++i)
+      a_off[o][i] = (uint32_t)((size_t)(arow + 64 * i) * lda * sizeof(T)) +
+                    (uint32_t)(brev3((lane & 7) ^ ((arow >> 1) & 7)) << 4);
+  }
+  // A pieces this wave issues per stage (the vmcnt of one stage's DMA)
+  const int na_w = SPLIT ? (wave < 4 ? 2 * NA : 0) : NA;
   auto issue_a = [&](int kt) {
-    if (kt < nkt && (DIAG != 2 || kt < PA)) {
+    if (kt < nkt && (DIAG != 2 || kt < PA) && (!SPLIT || wave < 4)) {
       unsigned char* slot = lds + (kt % NS) * SLOT;
       const uint32_t so = (uint32_t)kt * 64 * sizeof(T);
 #pragma unroll
-      for (int i = 0; i < NA; ++i) dma16(rA, a_off[i], so, slot + (i * 8 + wave) * 1024);
+      for (int o = 0; o < NO; ++o)
+#pragma unroll
+        for (int i = 0; i < NA; ++i)
+          dma16(rA, a_off[o][i], so, slot + (i * 8 + wave + 4 * o) * 1024);
     }
   };
 
@@ -263,7 +284,7 @@ __global__ __launch_bounds__(512, 1) void gemm_fq7_kernel(
   // ops issued after B(kt) when stage kt starts: A(kt - 1 + PA) (or, at kt = 0, the
   // prologue's A(1 .. PA-1)); A(kt) is older than B(kt) and so covered by the same wait
   auto wait_stage = [&](int kt) {
-    const int n = kt == 0 ? NA * min(PA - 1, nkt - 1) : (kt - 1 + PA < nkt ? NA : 0);
+    const int n = kt == 0 ? na_w * min(PA - 1, nkt - 1) : (kt - 1 + PA < nkt ? na_w : 0);
     vmwait_dyn(n);
   };
 
@@ -293,6 +314,7 @@ __global__ __launch_bounds__(512, 1) void gemm_fq7_kernel(
       issue_dense(0, dd, O());
     }
   };
+  if ((OPT & 1) && wave >= 4) __builtin_amdgcn_s_setprio(1);
   int kt = 0;
   for (; kt + 2 < nkm; kt += 2) {
     codes_step(kt, Z(), false);
@@ -316,7 +338,7 @@ __global__ __launch_bounds__(512, 1) void gemm_fq7_kernel(
     compute_dense(lds + (k % NS) * SLOT, dd, [&](int t) {
       if (t == I - 1) {
         if (k + PA < nkt)
-          vmwait<NA>();
+          vmwait_dyn(na_w);
         else
           vmwait<0>();
 #pragma unroll
@@ -482,6 +504,12 @@ static int group_m_tr_env() {
   return v;
 }
 
+// the activation-order launch's OPT variant (A/B knob, see gemm_fq7_kernel)
+static int opt_tr_env() {  // read per launch (in-process A/B)
+  const char* e = getenv("SQMP_FQT7_OPT");
+  return e ? atoi(e) : 0;
+}
+
 #ifdef SQMP_DIAG_BUILD
 // timing-diagnostic variants (wrong results by design) only in a diagnostics build:
 // SQMP_DIAG=1 python smoothquant-mixedprecision_amd/build_ext.py --force
@@ -556,9 +584,17 @@ static int dispatch_tr(const void* wp, const void* codes_t, const void* scale_t,
   typedef typename DT::T T;
   constexpr int TM = std::is_same<DT, BF16>::value ? 128 : 256;
   const int tiles_m = cdiv(N, TM), tiles_n = cdiv(M, 256);
-  gemm_fq7_kernel<DT, 1, TM, 2, 0, true><<<dim3(tiles_m * tiles_n), dim3(512), 0, s>>>(
-      (const T*)wp, (const uint32_t*)codes_t, (const T*)scale_t, (const T*)sal_t, (const T*)bias,
-      (T*)y, N, M, Kq, S_pad, G, ngq, tiles_m, tiles_n, group_m_tr_env(), colmax);
+#define SQMP_TR(O)                                                                              \
+  gemm_fq7_kernel<DT, 1, TM, 2, 0, true, O><<<dim3(tiles_m * tiles_n), dim3(512), 0, s>>>(      \
+      (const T*)wp, (const uint32_t*)codes_t, (const T*)scale_t, (const T*)sal_t, (const T*)bias, \
+      (T*)y, N, M, Kq, S_pad, G, ngq, tiles_m, tiles_n, group_m_tr_env(), colmax)
+  switch (opt_tr_env()) {
+    case 1: SQMP_TR(1); break;
+    case 2: SQMP_TR(2); break;
+    case 3: SQMP_TR(3); break;
+    default: SQMP_TR(0); break;
+  }
+#undef SQMP_TR
   SQMP_LAUNCH_CHECK();
   return SQMP_OK;
 }
