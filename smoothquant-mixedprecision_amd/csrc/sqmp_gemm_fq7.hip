@@ -120,7 +120,8 @@ __host__ __device__ inline int brev3(int c) { return ((c & 1) << 2) | (c & 2) | 
 // OPT (the activation-order launch, A/B knob SQMP_FQT7_OPT): bit 0 -- waves 4-7 run at
 // s_setprio 1 through the K loop (MI355X_MICROARCH.md "Two waves per SIMD" item 4); bit 1 --
 // loader split: waves 0-3 issue every LDS-DMA piece of a stage (their own and those of
-// waves 4-7), waves 4-7 only wait, read and multiply (gemm_fq6's split)
+// waves 4-7), waves 4-7 only wait, read and multiply (gemm_fq6's split); bit 2 -- A fragments
+// read 3 blocks ahead instead of 2
 template <class DT, int GB, int TM, int J, int DIAG = 0, bool TR = false, int OPT = 0>
 __global__ __launch_bounds__(512, 1) void gemm_fq7_kernel(
     const typename DT::T* __restrict__ A, const uint32_t* __restrict__ Bt,
@@ -134,7 +135,9 @@ __global__ __launch_bounds__(512, 1) void gemm_fq7_kernel(
   constexpr int PA = 3, NS = PA + 1;    // A stages in flight, ring slots
   constexpr int SLOT = TM * 128;        // TM rows x 64 positions x 2 B
   constexpr int NA = TM / 64;           // A pieces per wave per stage
-  constexpr int PF = TM == 256 ? 2 : 3;  // A fragment read-ahead (blocks; 2 keeps TM = 256 spill-free)
+  // A fragment read-ahead (blocks; 2 keeps the packed-order TM = 256 kernel spill-free;
+  // OPT bit 2: 3 on the activation-order kernel)
+  constexpr int PF = (TM == 256 && !(OPT & 4)) ? 2 : 3;
   constexpr int EPI = TR ? TN * (2 * TM + 16) : TM * TN * 2;  // epilogue staging bytes
   constexpr int LDS_BYTES = NS * SLOT > EPI ? NS * SLOT : EPI;
   static_assert(J <= I, "sub-step 1 decode must finish before block I");
@@ -592,6 +595,10 @@ static int dispatch_tr(const void* wp, const void* codes_t, const void* scale_t,
     case 1: SQMP_TR(1); break;
     case 2: SQMP_TR(2); break;
     case 3: SQMP_TR(3); break;
+    case 4: SQMP_TR(4); break;
+    case 5: SQMP_TR(5); break;
+    case 6: SQMP_TR(6); break;
+    case 7: SQMP_TR(7); break;
     default: SQMP_TR(0); break;
   }
 #undef SQMP_TR

@@ -11,7 +11,7 @@ import torch  # noqa: E402
 import bench  # noqa: E402
 from smoothquant import ops  # noqa: E402
 
-variants = (sys.argv[1] if len(sys.argv) > 1 else "0,1,2,3").split(",")
+variants = (sys.argv[1] if len(sys.argv) > 1 else "0,1,2,3,4,5").split(",")
 rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 4
 iters = int(sys.argv[3]) if len(sys.argv) > 3 else 200
 dev = torch.device("cuda")
