@@ -391,7 +391,7 @@ def main(argv=None):
         gemm = lambda: ops.gemm_fqt(*c4, pw, lin.bias, G)  # noqa: E731
         quant = lambda: ops.quant_act_c4(x, pw, args.act, 4, G)  # noqa: E731
         kdt = "f16"
-        kname = ("sqmp::fq7::gemm_fq7_kernel<F16,1,256,2,0,true> (activation order, sqmp_gemm_fqt7)"
+        kname = ("sqmp::fq7::gemm_fq7_kernel<F16,1,256,2,0,true,3> (activation order, sqmp_gemm_fqt7)"
                  if c4[1].dim() == 3 else
                  "sqmp::gemm_fq6_kernel<F16,1,256,true> (activation order, sqmp_gemm_fqt)")
     else:

@@ -508,9 +508,12 @@ static int group_m_tr_env() {
 }
 
 // the activation-order launch's OPT variant (A/B knob, see gemm_fq7_kernel)
+// default 3 (setprio + loader split): same box, interleaved rounds at config 2, 421.6 us
+// against 431.4 us for 0 (either bit alone +-0.3 %, PF = 3 +-0.1 %; tools/ab_fqt7.py,
+// profiles/r03_ab_fqt7.txt)
 static int opt_tr_env() {  // read per launch (in-process A/B)
   const char* e = getenv("SQMP_FQT7_OPT");
-  return e ? atoi(e) : 0;
+  return e ? atoi(e) : 3;
 }
 
 #ifdef SQMP_DIAG_BUILD
