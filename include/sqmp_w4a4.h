@@ -229,18 +229,6 @@ int sqmp_gemm_f8(const void* a8, const float* ascale, const void* xs, const void
                  const float* ws32, const void* wsal, const void* bias, void* y, int dtype,
                  int M, int N, int Kp, int S_pad, int Gw, int ngw, void* stream);
 
-/* sqmp_gemm_f8 with the weight operand in registers (Gw % 128 == 0, N % 8 == 0): the same
- * y bit for bit.  Weight operands from sqmp_pack_f8t once per layer: w8t = sqmp_pack_f8's
- * e4m3 codes tile-major ([Np/32][Kp/128][2][2][64][16 B], Np = roundup(N, 256) rows),
- * salt = wsal tile-major ([Np/32][S_pad/64][2][2][64][8 D]; NULL when S_pad == 0); ws32 as
- * sqmp_gemm_f8.  colmax (may be NULL): as sqmp_gemm_fq_colmax. */
-int sqmp_pack_f8t(const void* w8, const void* wsal, int dtype, int N, int Kp, int S_pad,
-                  void* w8t, void* salt, void* stream);
-int sqmp_gemm_f8t(const void* a8, const float* ascale, const void* xs, const void* w8t,
-                  const float* ws32, const void* salt, const void* bias, void* y, int dtype,
-                  int M, int N, int Kp, int S_pad, int Gw, int ngw, uint32_t* colmax,
-                  void* stream);
-
 /* sqmp_gemm_f8 with the output quantizer's column statistics fused into its epilogue, as
  * sqmp_gemm_fq_colmax: colmax[n] = max(colmax[n], bits(|y[m][n]|)) over every row m
  * (fake_quant.py:308-316 then skips its statistics pass: SQMP_QA_STATS_GIVEN).

@@ -50,9 +50,6 @@ SIGNATURES = {
     "sqmp_pack_f8": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _vp, _vp]),
     "sqmp_gemm_f8": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i,
                           _vp]),
-    "sqmp_pack_f8t": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _vp, _vp]),
-    "sqmp_gemm_f8t": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i,
-                           _vp, _vp]),
     "sqmp_gemm_f8_colmax": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i,
                                  _i, _vp, _vp]),
     "sqmp_quant_act_c4": (_i, [_vp, _i, _i, _i, _i, _i, _i, _vp, _i, _vp, _vp, _i, _i, _vp, _i,

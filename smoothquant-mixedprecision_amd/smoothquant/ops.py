@@ -91,7 +91,6 @@ class PackedWeight:
     sal_key: Optional[tuple] = field(default=None)        # identity of the salient set (host)
     w8: Optional[torch.Tensor] = field(default=None)     # uint8 [Np, Kp] e4m3 codes (f8 GEMM)
     ws32: Optional[torch.Tensor] = field(default=None)   # fp32 [ngw, Np] scales (f8 GEMM)
-    f8t: Optional[tuple] = field(default=None)           # (w8t, salt) of gemm_f8t
     fq7: Optional[tuple] = field(default=None)           # (codes_t, scale_t, sal_t, J) of gemm_fq7
     h2: Optional[tuple] = field(default=None)            # (f16 [2, Np, L], int32 [Np]) (gemm_h2)
 
@@ -615,41 +614,10 @@ def quant_act_f8(x2: torch.Tensor, pw: PackedWeight, act_quant: str, n_bits: int
     return a8, sa, xs
 
 
-# Whether gemm_f8 runs the register-weight FP8 kernel (sqmp_gemm_f8t) where it applies
-# (Gw % 128 == 0, N % 8 == 0); the same y bit for bit as sqmp_gemm_f8.  Off until measured
-# (SQMP_F8T=1: A/B).
-F8T = os.environ.get("SQMP_F8T", "0") == "1"
-
-
-def f8t_operands(pw: PackedWeight):
-    """(w8t, salt) of gemm_f8t: tile-major copies of the e4m3 weight codes and the salient
-    slice, built once per packed weight."""
-    if pw.f8t is None:
-        w8, _ = f8_operands(pw)
-        dev = pw.codes.device
-        w8t = torch.empty_like(w8)
-        salt = (torch.empty((pad_n(pw.N), pw.S_pad), dtype=pw.dtype, device=dev)
-                if pw.S_pad else None)
-        check(load().sqmp_pack_f8t(_p(w8), _p(pw.wsal) if pw.S_pad else None,
-                                   _dtype_code(pw.dtype), pw.N, pw.Kp, pw.S_pad, _p(w8t),
-                                   _p(salt), _stream(w8)), "pack_f8t")
-        pw.f8t = (w8t, salt)
-    return pw.f8t
-
-
 def gemm_f8(a8: torch.Tensor, sa: torch.Tensor, xs: torch.Tensor, pw: PackedWeight,
             bias: Optional[torch.Tensor], colmax: Optional[torch.Tensor] = None) -> torch.Tensor:
     """colmax (Gw % 128 == 0): as gemm_fq's fused output-quant statistics."""
     M = a8.shape[0]
-    if F8T and pw.Gw % 128 == 0 and pw.N % 8 == 0:
-        _, ws32 = f8_operands(pw)
-        w8t, salt = f8t_operands(pw)
-        y = torch.empty((M, pw.N), dtype=pw.dtype, device=a8.device)
-        check(load().sqmp_gemm_f8t(_p(a8), _p(sa), _p(xs) if pw.S_pad else None, _p(w8t),
-                                   _p(ws32), _p(salt), _p(bias), _p(y), _dtype_code(pw.dtype), M,
-                                   pw.N, pw.Kp, pw.S_pad, pw.Gw, pw.ngw, _p(colmax),
-                                   _stream(a8)), "gemm_f8t")
-        return y
     w8, ws32 = f8_operands(pw)
     y = torch.empty((M, pw.N), dtype=pw.dtype, device=a8.device)
     args = (_p(a8), _p(sa), _p(xs) if pw.S_pad else None, _p(w8), _p(ws32),
