@@ -205,8 +205,16 @@ __device__ __forceinline__ void quant_lc_body(
       }
     }
   };
-  int rp = bid;
-  if (rp < npair) load_pair(rp);
+  // Row pairs in contiguous runs per workgroup, consecutive runs on one XCD (blocks are dealt
+  // round-robin over the 8 XCDs): the workgroups that write one 32-row block of the
+  // tile-major outputs (and neighbouring rows of the row-major ones) share an L2, so its
+  // partial-line writes merge there instead of leaving eight XCDs as masked writes.
+  const int xcd = bid & 7, per = nblk >> 3, rem = nblk & 7;
+  const int wg = (xcd < rem ? xcd * (per + 1) : rem * (per + 1) + (xcd - rem) * per) + (bid >> 3);
+  const int run = (npair + nblk - 1) / nblk;
+  const int rp_end = min(npair, (wg + 1) * run);
+  int rp = wg * run;
+  if (rp < rp_end) load_pair(rp);
 
   // ---- once per workgroup: salient-position mask, zeroed buffer (+ two spare words: W =
   // a zero read by padding table entries, W + 1 = a write-only sink for their scatter)
@@ -247,7 +255,7 @@ __device__ __forceinline__ void quant_lc_body(
   }
   __syncthreads();
 
-  for (; rp < npair; rp += nblk) {
+  for (; rp < rp_end; ++rp) {
     const int m0 = 2 * rp;
     const bool has1 = m0 + 1 < M;
     // ---- this thread's RPL table entries (L1/L2-resident, padded to whole rounds with
@@ -392,7 +400,7 @@ __device__ __forceinline__ void quant_lc_body(
     // salient columns' own packed positions hold 0 (their weight codes are 0 too)
     if (F8 != 3)
       for (uint64_t zm = zmask; zm; zm &= zm - 1) lc_buf[zp0 + __builtin_ctzll(zm)] = 0u;
-    if (rp + nblk < npair) load_pair(rp + nblk);  // prefetch the next pair
+    if (rp + 1 < rp_end) load_pair(rp + 1);  // prefetch the next pair
     __syncthreads();
 
     if (F8 == 1) {
@@ -485,18 +493,22 @@ __global__ __launch_bounds__(1024) void quant_lc_kernel(
 
 // ---- the activation-order weight operand (sqmp_gemm_fqt): wp[n][j] = W_hat[n][pos_j],
 // pos_j = lctab[j] >> 16 (the weight-packed position of the column of activation rank j),
-// 0 past Kn, then wsal[n][:].  Workgroup `bid` dequantizes its RB codes rows into LDS in
-// packed order (one bpack dword -> 8 D values D(code * scale), one 16-B LDS write), then
-// gathers them in rank order (an output chunk's table entries are read once for all RB
-// rows) and stores 16-B chunks.  Latency-bound rather than byte-bound, so it runs in the
-// same launch as the C4 quantizer (quant_c4_fused_kernel), on workgroups of its own.
+// 0 past Kn, then wsal[n][:].  Workgroup `bid` owns RW consecutive rows and walks them in
+// batches of RB: each batch is dequantized into LDS in packed order (one bpack dword -> 8 D
+// values D(code * scale), one 16-B LDS write), then gathered in rank order and stored as
+// 16-B chunks.  A thread's table entries (the packed positions of its output chunks) are
+// read once per workgroup and kept in registers for every batch: with one batch per
+// workgroup the table reads (4 B per element and batch) matched the output bytes.  It runs
+// in the same launch as the C4 quantizer (quant_c4_fused_kernel), on workgroups of its own.
 struct PermArgs {
   const uint32_t* codes;  // bpack [Np][Kp/2]
   const void* wscale;     // D [ngw][Np]
   const void* wsal;       // D [N][S_pad]
   void* wp;               // D [Np][Kq + S_pad]
-  int N, Np, Kp, Gw, ngw, Kn, Kq, S_pad, RB;
+  int N, Np, Kp, Gw, ngw, Kn, Kq, S_pad, RB, RW;
 };
+
+constexpr int PW_CH = 4;  // output chunks per thread whose table entries stay in registers
 
 template <class DT>
 __device__ __forceinline__ void perm_weight_body(const PermArgs& a, const uint32_t* __restrict__ lctab,
@@ -507,47 +519,79 @@ __device__ __forceinline__ void perm_weight_body(const PermArgs& a, const uint32
   const T* wscale = (const T*)a.wscale;
   const T* wsal = (const T*)a.wsal;
   T* wp = (T*)a.wp;
-  const int RB = a.RB, Kp = a.Kp, n0 = bid * RB, tid = threadIdx.x;
+  const int RB = a.RB, Kp = a.Kp, tid = threadIdx.x, nt = blockDim.x;
   const int dw = Kp / 8;  // bpack dwords per codes row
-#pragma unroll 4
-  for (int i = tid; i < RB * dw; i += blockDim.x) {
-    const int r = i / dw, d = i - r * dw, n = n0 + r;
-    const int p0 = bpack_pos(d, 0);  // its 8 positions p0 .. p0 + 7 (one group: Gw % 8 == 0)
-    T v[8];
-    if (n < a.N) {
-      const uint32_t w = a.codes[(size_t)n * dw + d];
-      const float sc = DT::to_f(wscale[(size_t)min(p0 / a.Gw, a.ngw - 1) * a.Np + n]);
-#pragma unroll
-      for (int e = 0; e < 8; ++e)
-        v[e] = DT::from_f((float)((int)((w >> bpack_shift(e)) & 0xFu) - 8) * sc);
-    } else {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = DT::from_f(0.f);
-    }
-    *(u32x4*)(wl + (size_t)r * Kp + p0) = *(const u32x4*)v;
-  }
-  __syncthreads();
   const int W = a.Kq + a.S_pad, nch = W / 8;
-  for (int c = tid; c < nch; c += blockDim.x) {
+  // the packed positions of output chunk c (two 16-bit positions per word; 0xFFFF: zero)
+  auto load_pos = [&](int c, uint32_t* pc) {
     const int j0 = 8 * c;
-    if (j0 < a.Kq) {
-      int pos[8];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) pos[e] = j0 + e < a.Kn ? (int)(lctab[j0 + e] >> 16) : -1;
-      for (int r = 0; r < RB; ++r) {
-        T v[8];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = pos[e] >= 0 ? wl[(size_t)r * Kp + pos[e]] : DT::from_f(0.f);
-        *(u32x4*)(wp + (size_t)(n0 + r) * W + j0) = *(const u32x4*)v;
+    for (int h = 0; h < 4; ++h) {
+      uint32_t v = 0xFFFFFFFFu;
+      if (j0 < a.Kq) {
+        const uint32_t lo = j0 + 2 * h < a.Kn ? lctab[j0 + 2 * h] >> 16 : 0xFFFFu;
+        const uint32_t hi = j0 + 2 * h + 1 < a.Kn ? lctab[j0 + 2 * h + 1] >> 16 : 0xFFFFu;
+        v = lo | (hi << 16);
       }
-    } else {
-      for (int r = 0; r < RB; ++r) {
-        const int n = n0 + r;
-        u32x4 v = u32x4{0u, 0u, 0u, 0u};
-        if (n < a.N) v = *(const u32x4*)(wsal + (size_t)n * a.S_pad + (j0 - a.Kq));
-        *(u32x4*)(wp + (size_t)n * W + j0) = v;
-      }
+      pc[h] = v;
     }
+  };
+  // this thread's first PW_CH output chunks c = tid + nt * t, positions cached in registers
+  uint32_t pos[PW_CH][4];
+#pragma unroll
+  for (int t = 0; t < PW_CH; ++t) load_pos(tid + nt * t, pos[t]);
+  for (int nb0 = bid * a.RW; nb0 < min((bid + 1) * a.RW, a.Np); nb0 += RB) {
+#pragma unroll 4
+    for (int i = tid; i < RB * dw; i += nt) {
+      const int r = i / dw, d = i - r * dw, n = nb0 + r;
+      const int p0 = bpack_pos(d, 0);  // its 8 positions p0 .. p0 + 7 (one group: Gw % 8 == 0)
+      T v[8];
+      if (n < a.N) {
+        const uint32_t w = a.codes[(size_t)n * dw + d];
+        const float sc = DT::to_f(wscale[(size_t)min(p0 / a.Gw, a.ngw - 1) * a.Np + n]);
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          v[e] = DT::from_f((float)((int)((w >> bpack_shift(e)) & 0xFu) - 8) * sc);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = DT::from_f(0.f);
+      }
+      *(u32x4*)(wl + (size_t)r * Kp + p0) = *(const u32x4*)v;
+    }
+    __syncthreads();
+    // one output chunk of RB rows: positions from the register cache (t < PW_CH) or the table
+    auto chunk = [&](int c, const uint32_t* pc) {
+      const int j0 = 8 * c;
+      if (j0 < a.Kq) {
+        for (int r = 0; r < RB; ++r) {
+          const T* row = wl + (size_t)r * Kp;
+          uint16_t u[8];
+#pragma unroll
+          for (int h = 0; h < 4; ++h) {
+            const uint32_t pl = pc[h] & 0xFFFFu, ph = pc[h] >> 16;
+            u[2 * h] = pl != 0xFFFFu ? __builtin_bit_cast(uint16_t, row[pl]) : (uint16_t)0;
+            u[2 * h + 1] = ph != 0xFFFFu ? __builtin_bit_cast(uint16_t, row[ph]) : (uint16_t)0;
+          }
+          *(u32x4*)(wp + (size_t)(nb0 + r) * W + j0) = *(const u32x4*)u;
+        }
+      } else {
+        for (int r = 0; r < RB; ++r) {
+          const int n = nb0 + r;
+          u32x4 v = u32x4{0u, 0u, 0u, 0u};
+          if (n < a.N) v = *(const u32x4*)(wsal + (size_t)n * a.S_pad + (j0 - a.Kq));
+          *(u32x4*)(wp + (size_t)n * W + j0) = v;
+        }
+      }
+    };
+#pragma unroll
+    for (int t = 0; t < PW_CH; ++t)
+      if (tid + nt * t < nch) chunk(tid + nt * t, pos[t]);
+    for (int c = tid + nt * PW_CH; c < nch; c += nt) {  // rows wider than the cache
+      uint32_t pc[4];
+      load_pos(c, pc);
+      chunk(c, pc);
+    }
+    __syncthreads();  // the batch buffer is rewritten by the next batch
   }
 }
 
@@ -645,7 +689,7 @@ int launch_quant_lc(int dtype, int mode, const void* x, int M, int K, int q_max,
 }
 
 static int pw_rows(int Kp) {
-  // rows per permutation workgroup: 16 KiB of dequantized rows; Np % 256 == 0, so RB | Np
+  // rows per permutation batch: 16 KiB of dequantized rows; Np % 256 == 0, so RB | Np
   static const int env = [] {
     const char* e = getenv("SQMP_PW_RB");
     return e ? atoi(e) : 0;
@@ -654,21 +698,34 @@ static int pw_rows(int Kp) {
   return rb >= 8 ? 8 : rb >= 4 ? 4 : rb >= 2 ? 2 : 1;
 }
 
+// rows per permutation workgroup (batches of pw_rows): 8 batches of table reuse, a multiple
+// of RB dividing Np (Np % 256 == 0)
+static int pw_wg_rows(int RB) {
+  static const int env = [] {
+    const char* e = getenv("SQMP_PW_RW");
+    return e ? atoi(e) : 0;
+  }();
+  int rw = env > 0 ? env : 8 * RB;
+  rw = rw < RB ? RB : (rw > 256 ? 256 : rw);
+  return rw / RB * RB;
+}
+
 int launch_perm_weight_c4(int dtype, const uint32_t* lctab, const void* codes,
                           const void* wscale, const void* wsal, int N, int Kp, int Gw, int ngw,
                           int Kn, int S_pad, void* wp, hipStream_t s) {
-  const int Np = pad_n(N), RB = pw_rows(Kp);
-  PermArgs pa{(const uint32_t*)codes, wscale, wsal, wp, N, Np, Kp, Gw, ngw, Kn,
-              (int)round_up(Kn, 64), S_pad, RB};
+  const int Np = pad_n(N), RB = pw_rows(Kp), RW = pw_wg_rows(RB);
+  const int Kq = (int)round_up(Kn, 64);
+  PermArgs pa{(const uint32_t*)codes, wscale, wsal, wp, N, Np, Kp, Gw, ngw, Kn, Kq, S_pad, RB, RW};
   const size_t lds = (size_t)RB * Kp * 2;
+  const dim3 grid((unsigned)cdiv(Np, RW));
   if (dtype == SQMP_F16) {
     SQMP_HIP_CHECK(hipFuncSetAttribute((const void*)perm_weight_kernel<F16>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    perm_weight_kernel<F16><<<dim3(Np / RB), dim3(256), lds, s>>>(pa, lctab);
+    perm_weight_kernel<F16><<<grid, dim3(256), lds, s>>>(pa, lctab);
   } else if (dtype == SQMP_BF16) {
     SQMP_HIP_CHECK(hipFuncSetAttribute((const void*)perm_weight_kernel<BF16>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    perm_weight_kernel<BF16><<<dim3(Np / RB), dim3(256), lds, s>>>(pa, lctab);
+    perm_weight_kernel<BF16><<<grid, dim3(256), lds, s>>>(pa, lctab);
   } else {
     return SQMP_EUNSUPPORTED;
   }
@@ -698,9 +755,9 @@ int launch_quant_lc_c4(int dtype, const void* x, int M, int K, int q_max, int G,
   }
   // fused: the quantizer's grid (as quant_lc_launch) + Np / RB permutation workgroups
   const int nw = lc_waves(K, Kn);
-  const int Np = pad_n(cw->N), RB = pw_rows(cw->Kp);
+  const int Np = pad_n(cw->N), RB = pw_rows(cw->Kp), RW = pw_wg_rows(RB);
   PermArgs pa{(const uint32_t*)cw->codes, cw->wscale, cw->wsal, cw->wp, cw->N, Np, cw->Kp,
-              cw->Gw, cw->ngw, Kn, Kq, S_pad, RB};
+              cw->Gw, cw->ngw, Kn, Kq, S_pad, RB, RW};
   const size_t lq = sizeof(uint32_t) * (size_t)(P + S_pad + 8), lp = (size_t)RB * cw->Kp * 2;
   const size_t lds = lq > lp ? lq : lp;
   int per_cu = (int)((150 * 1024) / lds);
@@ -716,7 +773,7 @@ int launch_quant_lc_c4(int dtype, const void* x, int M, int K, int q_max, int G,
   int nq = 256 * (qpc < per_cu ? qpc : per_cu);
   const int npair = (M + 1) / 2;
   if (nq > npair) nq = npair;
-  const dim3 grid(nq + Np / RB), block(64 * nw);
+  const dim3 grid(nq + cdiv(Np, RW)), block(64 * nw);
   if (dtype == SQMP_F16) {
     SQMP_HIP_CHECK(hipFuncSetAttribute((const void*)quant_c4_fused_kernel<F16>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));

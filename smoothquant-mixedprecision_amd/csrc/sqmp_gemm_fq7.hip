@@ -600,9 +600,7 @@ static int dispatch_tr(const void* wp, const void* codes_t, const void* scale_t,
     case 3: SQMP_TR(3); break;
     case 4: SQMP_TR(4); break;
     case 5: SQMP_TR(5); break;
-    case 6: SQMP_TR(6); break;
-    case 7: SQMP_TR(7); break;
-    default: SQMP_TR(0); break;
+    default: SQMP_TR(0); break;  // 6, 7 (split + PF = 3) spill with the colmax epilogue
   }
 #undef SQMP_TR
   SQMP_LAUNCH_CHECK();
