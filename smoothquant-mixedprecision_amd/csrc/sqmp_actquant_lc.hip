@@ -690,10 +690,8 @@ int launch_quant_lc(int dtype, int mode, const void* x, int M, int K, int q_max,
 
 static int pw_rows(int Kp) {
   // rows per permutation batch: 16 KiB of dequantized rows; Np % 256 == 0, so RB | Np
-  static const int env = [] {
-    const char* e = getenv("SQMP_PW_RB");
-    return e ? atoi(e) : 0;
-  }();
+  const char* e = getenv("SQMP_PW_RB");  // tuning only, read per launch
+  const int env = e ? atoi(e) : 0;
   int rb = env > 0 ? env : 16384 / (Kp * 2);
   return rb >= 8 ? 8 : rb >= 4 ? 4 : rb >= 2 ? 2 : 1;
 }
@@ -701,10 +699,8 @@ static int pw_rows(int Kp) {
 // rows per permutation workgroup (batches of pw_rows): 8 batches of table reuse, a multiple
 // of RB dividing Np (Np % 256 == 0)
 static int pw_wg_rows(int RB) {
-  static const int env = [] {
-    const char* e = getenv("SQMP_PW_RW");
-    return e ? atoi(e) : 0;
-  }();
+  const char* e = getenv("SQMP_PW_RW");  // tuning only, read per launch
+  const int env = e ? atoi(e) : 0;
   int rw = env > 0 ? env : 8 * RB;
   rw = rw < RB ? RB : (rw > 256 ? 256 : rw);
   return rw / RB * RB;
@@ -765,10 +761,8 @@ int launch_quant_lc_c4(int dtype, const void* x, int M, int K, int q_max, int G,
   per_cu = per_cu < 1 ? 1 : (per_cu > by_waves ? by_waves : per_cu);
   // quantizer workgroups per CU: leave two slots of every CU to the permutation
   // workgroups (issued after them), so the two run side by side
-  static const int q_env = [] {
-    const char* e = getenv("SQMP_C4_QPERCU");
-    return e ? atoi(e) : 0;
-  }();
+  const char* qe = getenv("SQMP_C4_QPERCU");  // tuning only, read per launch
+  const int q_env = qe ? atoi(qe) : 0;
   const int qpc = q_env > 0 ? q_env : (per_cu > 2 ? per_cu - 2 : 1);
   int nq = 256 * (qpc < per_cu ? qpc : per_cu);
   const int npair = (M + 1) / 2;

@@ -3,8 +3,12 @@ HIP-event timing): the fused quant_act_c4 (column max + rank table + C4 quantize
 weight permutation in one launch), then the quantizer alone (sqmp_quant_act_v2 OUT_C4) and
 the permutation alone (sqmp_perm_weight_c4), each ITERS times.
 
-    python tools/prepass_split.py [ITERS]
+    python tools/prepass_split.py [ITERS] [VAR=v1/v2/...,VAR=...]
+
+The optional second argument sweeps the permutation's per-launch tuning variables
+(SQMP_PW_RB, SQMP_PW_RW, SQMP_C4_QPERCU): every combination is timed (fused and perm alone).
 """
+import itertools
 import ctypes
 import os
 import sys
@@ -77,3 +81,17 @@ tp = t_us(perm_only)
 print(f"fused quant_act_c4 (colmax + rank + quant|perm): {tf:7.1f} us")
 print(f"quant_act_v2 OUT_C4 (colmax + rank + quant):     {tq:7.1f} us   quant bytes {qbytes/1e6:.1f} MB")
 print(f"perm_weight_c4 alone:                             {tp:7.1f} us   {pbytes/1e6:.1f} MB = {pbytes/tp/1e3:.0f} GB/s")
+
+if len(sys.argv) > 2:
+    axes = [(kv.split("=")[0], kv.split("=")[1].split("/")) for kv in sys.argv[2].split(",")]
+    for combo in itertools.product(*[v for _, v in axes]):
+        for (k, _), v in zip(axes, combo):
+            os.environ[k] = v
+        wp.zero_()
+        perm_only()
+        torch.cuda.synchronize()
+        ok = torch.equal(wp.view(torch.int16), wp_ref.view(torch.int16))
+        tf, tp = t_us(fused), t_us(perm_only)
+        tag = " ".join(f"{k}={v}" for (k, _), v in zip(axes, combo))
+        print(f"{tag:40s} fused {tf:7.1f} us  perm {tp:7.1f} us ({pbytes/tp/1e3:.0f} GB/s)"
+              f"{'' if ok else '  MISMATCH'}")
