@@ -70,13 +70,25 @@ struct PairScale {
   uint32_t sd;    // both scales as D bit patterns
 };
 
+// s = D(fl32(D(clamp(absmax, 1e-5)) / q_max)) and r = fl32(1 / s) without IEEE divisions:
+// the quotient by Markstein's correction with rq = fl32(1 / q_max) and the reciprocal by
+// one Newton step from v_rcp_f32 -- both equal to the correctly rounded results for every
+// D operand (exhaustive proof: tests/test_lc_arith_cpu.py)
 template <class DT>
-__device__ inline PairScale pair_scale(uint32_t mx, int q_max) {
+__device__ inline PairScale pair_scale(uint32_t mx, float qm, float rq) {
   PairScale c;
-  c.s[0] = group_scale<DT>(half_lo<DT>(mx), q_max);
-  c.s[1] = group_scale<DT>(half_hi<DT>(mx), q_max);
-  c.r[0] = 1.0f / c.s[0];
-  c.r[1] = 1.0f / c.s[1];
+  const float lo = rd<DT>(1e-5f);
+  f32x2 a = {half_lo<DT>(mx), half_hi<DT>(mx)};
+  a[0] = a[0] < lo ? lo : a[0];
+  a[1] = a[1] < lo ? lo : a[1];
+  const f32x2 q0 = a * rq;
+  const f32x2 e = __builtin_elementwise_fma(-q0, (f32x2){qm, qm}, a);
+  const f32x2 s = __builtin_elementwise_fma(e, (f32x2){rq, rq}, q0);
+  c.s[0] = rd<DT>(s[0]);
+  c.s[1] = rd<DT>(s[1]);
+  const f32x2 y = {__builtin_amdgcn_rcpf(c.s[0]), __builtin_amdgcn_rcpf(c.s[1])};
+  const f32x2 ey = __builtin_elementwise_fma(-c.s, y, (f32x2){1.f, 1.f});
+  c.r = __builtin_elementwise_fma(ey, y, y);
   c.sd = (uint32_t)__builtin_bit_cast(uint16_t, DT::from_f(c.s[0])) |
          ((uint32_t)__builtin_bit_cast(uint16_t, DT::from_f(c.s[1])) << 16);
   return c;
@@ -144,6 +156,39 @@ __device__ inline f32x2 code_pair<BF16>(uint32_t v, const PairScale& c) {
   return __builtin_elementwise_roundeven(d);
 }
 
+// The two rows' 4-bit codes + 8 (the same D(x/s) and round-half-even as code_pair) in
+// bytes 0 (row m0) and 2 (row m0 + 1), the other bytes unspecified: the low byte of D(q) + 1544
+// (fp16, one ulp = 1 from 1024) / fl32(D(q) + 2^23 + 8) (bf16) is code + 8 (exhaustive
+// check: tests/test_lc_arith_cpu.py)
+template <class DT>
+__device__ inline uint32_t nib_pair(uint32_t v, const PairScale& c);
+
+template <>
+__device__ inline uint32_t nib_pair<F16>(uint32_t v, const PairScale& c) {
+  const f32x2 t = __builtin_convertvector(__builtin_bit_cast(h16x2, v), f32x2);
+  const f32x2 q0 = t * c.r;
+  const f32x2 e = __builtin_elementwise_fma(-q0, c.s, t);
+  const f32x2 q = __builtin_elementwise_fma(e, c.r, q0);
+  const h16x2 magic = {(_Float16)1544.0f, (_Float16)1544.0f};
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(q, h16x2) + magic);
+}
+
+template <>
+__device__ inline uint32_t nib_pair<BF16>(uint32_t v, const PairScale& c) {
+  f32x2 t;
+  t[0] = __uint_as_float(v << 16);
+  t[1] = __uint_as_float(v & 0xFFFF0000u);
+  const f32x2 q0 = t * c.r;
+  const f32x2 e = __builtin_elementwise_fma(-q0, c.s, t);
+  const f32x2 q = __builtin_elementwise_fma(e, c.r, q0);
+  const uint32_t db = __builtin_bit_cast(uint32_t, __builtin_convertvector(q, b16x2));
+  f32x2 dq;
+  dq[0] = __uint_as_float(db << 16);
+  dq[1] = __uint_as_float(db & 0xFFFF0000u);
+  const f32x2 m = dq + (f32x2){8388616.0f, 8388616.0f};
+  return __builtin_amdgcn_perm(__float_as_uint(m[1]), __float_as_uint(m[0]), 0x0c040c00u);
+}
+
 // F8 output: the codes as OCP e4m3 bytes, row m0 in byte 0, row m0 + 1 in byte 2 -- exact
 // for |code| <= 15, so every 4-bit code.
 template <class DT>
@@ -187,6 +232,7 @@ __device__ __forceinline__ void quant_lc_body(
   const int nchk = K / 8;           // 16-B input chunks per row
   const int ochk = W / 8;           // 16-B output chunks per row
   const int rb = RPL * tid;         // this thread's first rank
+  const float qmf = (float)q_max, rqf = 1.0f / qmf;  // pair_scale's divisor, reciprocal
 
   // the first row pair's loads go out before the prologue (their latency covers it)
   const int npair = (M + 1) / 2;
@@ -251,7 +297,7 @@ __device__ __forceinline__ void quant_lc_body(
     m = 0.f;
     for (int w = 0; w < NW; ++w) m = fmaxf(m, lc_red[0][w]);
     const uint32_t mb = (uint32_t)__builtin_bit_cast(uint16_t, DT::from_f(m));
-    tens = pair_scale<DT>(mb | (mb << 16), q_max);
+    tens = pair_scale<DT>(mb | (mb << 16), qmf, rqf);
   }
   __syncthreads();
 
@@ -301,7 +347,7 @@ __device__ __forceinline__ void quant_lc_body(
         uint32_t mx = 0u;
 #pragma unroll
         for (int i = g * GS; i < (g + 1) * GS; ++i) mx = pk_absmax(mx, v[i]);
-        const PairScale c = pair_scale<DT>(mx, q_max);
+        const PairScale c = pair_scale<DT>(mx, qmf, rqf);
 #pragma unroll
         for (int i = g * GS; i < (g + 1) * GS; ++i) lc_buf[tab[i] >> 16] = quant_pair<DT>(v[i], c);
       }
@@ -330,7 +376,7 @@ __device__ __forceinline__ void quant_lc_body(
           mx = (uint32_t)__builtin_bit_cast(uint16_t, DT::from_f(m0f)) |
                ((uint32_t)__builtin_bit_cast(uint16_t, DT::from_f(m1f)) << 16);
         }
-        c = pair_scale<DT>(mx, q_max);
+        c = pair_scale<DT>(mx, qmf, rqf);
       } else {
         __syncthreads();
       }
@@ -338,14 +384,18 @@ __device__ __forceinline__ void quant_lc_body(
         // ranks rb .. rb + 15 = positions 16 u .. 16 u + 15 of bpack block rb / 64: dwords u
         // (elements 0-7) and 4 + u (8-15); element e at nibble e / 2 (even e) or 4 + e / 2
         if (rb < Kq) {
+          // elements 2p, 2p + 1 of a dword: one v_perm_b32 per row puts their code bytes at
+          // bits 0 and 16, shifted to nibbles p and 4 + p
           uint32_t d0[2] = {0u, 0u}, d1[2] = {0u, 0u};
 #pragma unroll
-          for (int i = 0; i < RPL; ++i) {
-            const f32x2 code = code_pair<DT>(v[i], c);
-            const int e = i & 7, sh = (e & 1) ? 16 + 4 * (e >> 1) : 4 * (e >> 1);
-            d0[i >> 3] |= (uint32_t)((int)code[0] + 8) << sh;
-            d1[i >> 3] |= (uint32_t)((int)code[1] + 8) << sh;
-          }
+          for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int p = 0; p < 4; ++p) {
+              const uint32_t lo = nib_pair<DT>(v[8 * h + 2 * p], c);
+              const uint32_t hi = nib_pair<DT>(v[8 * h + 2 * p + 1], c);
+              d0[h] |= __builtin_amdgcn_perm(hi, lo, 0x0c040c00u) << (4 * p);
+              d1[h] |= __builtin_amdgcn_perm(hi, lo, 0x0c060c02u) << (4 * p);
+            }
           const int u = (rb >> 4) & 3;
           if (ldsc < 0) {
             // Bt[nb][kb][lane][j][s]: dword d of the row's block kb at lane 16 (d / 2) + r16,

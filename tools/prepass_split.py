@@ -3,9 +3,9 @@ HIP-event timing): the fused quant_act_c4 (column max + rank table + C4 quantize
 weight permutation in one launch), then the quantizer alone (sqmp_quant_act_v2 OUT_C4) and
 the permutation alone (sqmp_perm_weight_c4), each ITERS times.
 
-    python tools/prepass_split.py [ITERS] [VAR=v1/v2/...,VAR=...]
+    python tools/prepass_split.py [ITERS] [VAR=v1/v2/... [VAR=...]]
 
-The optional second argument sweeps the permutation's per-launch tuning variables
+The optional further arguments sweep the permutation's per-launch tuning variables
 (SQMP_PW_RB, SQMP_PW_RW, SQMP_C4_QPERCU): every combination is timed (fused and perm alone).
 """
 import itertools
@@ -83,7 +83,7 @@ print(f"quant_act_v2 OUT_C4 (colmax + rank + quant):     {tq:7.1f} us   quant by
 print(f"perm_weight_c4 alone:                             {tp:7.1f} us   {pbytes/1e6:.1f} MB = {pbytes/tp/1e3:.0f} GB/s")
 
 if len(sys.argv) > 2:
-    axes = [(kv.split("=")[0], kv.split("=")[1].split("/")) for kv in sys.argv[2].split(",")]
+    axes = [(kv.split("=")[0], kv.split("=")[1].split("/")) for kv in sys.argv[2:]]
     for combo in itertools.product(*[v for _, v in axes]):
         for (k, _), v in zip(axes, combo):
             os.environ[k] = v
