@@ -543,22 +543,18 @@ __global__ __launch_bounds__(1024) void quant_lc_kernel(
 
 // ---- the activation-order weight operand (sqmp_gemm_fqt): wp[n][j] = W_hat[n][pos_j],
 // pos_j = lctab[j] >> 16 (the weight-packed position of the column of activation rank j),
-// 0 past Kn, then wsal[n][:].  Workgroup `bid` owns RW consecutive rows and walks them in
-// batches of RB: each batch is dequantized into LDS in packed order (one bpack dword -> 8 D
-// values D(code * scale), one 16-B LDS write), then gathered in rank order and stored as
-// 16-B chunks.  A thread's table entries (the packed positions of its output chunks) are
-// read once per workgroup and kept in registers for every batch: with one batch per
-// workgroup the table reads (4 B per element and batch) matched the output bytes.  It runs
-// in the same launch as the C4 quantizer (quant_c4_fused_kernel), on workgroups of its own.
+// 0 past Kn, then wsal[n][:].  Workgroup `bid` dequantizes its RB codes rows into LDS in
+// packed order (one bpack dword -> 8 D values D(code * scale), one 16-B LDS write), then
+// gathers them in rank order (an output chunk's table entries are read once for all RB
+// rows) and stores 16-B chunks.  Latency-bound rather than byte-bound, so it runs in the
+// same launch as the C4 quantizer (quant_c4_fused_kernel), on workgroups of its own.
 struct PermArgs {
   const uint32_t* codes;  // bpack [Np][Kp/2]
   const void* wscale;     // D [ngw][Np]
   const void* wsal;       // D [N][S_pad]
   void* wp;               // D [Np][Kq + S_pad]
-  int N, Np, Kp, Gw, ngw, Kn, Kq, S_pad, RB, RW;
+  int N, Np, Kp, Gw, ngw, Kn, Kq, S_pad, RB;
 };
-
-constexpr int PW_CH = 4;  // output chunks per thread whose table entries stay in registers
 
 template <class DT>
 __device__ __forceinline__ void perm_weight_body(const PermArgs& a, const uint32_t* __restrict__ lctab,
@@ -569,79 +565,47 @@ __device__ __forceinline__ void perm_weight_body(const PermArgs& a, const uint32
   const T* wscale = (const T*)a.wscale;
   const T* wsal = (const T*)a.wsal;
   T* wp = (T*)a.wp;
-  const int RB = a.RB, Kp = a.Kp, tid = threadIdx.x, nt = blockDim.x;
+  const int RB = a.RB, Kp = a.Kp, n0 = bid * RB, tid = threadIdx.x;
   const int dw = Kp / 8;  // bpack dwords per codes row
-  const int W = a.Kq + a.S_pad, nch = W / 8;
-  // the packed positions of output chunk c (two 16-bit positions per word; 0xFFFF: zero)
-  auto load_pos = [&](int c, uint32_t* pc) {
-    const int j0 = 8 * c;
-#pragma unroll
-    for (int h = 0; h < 4; ++h) {
-      uint32_t v = 0xFFFFFFFFu;
-      if (j0 < a.Kq) {
-        const uint32_t lo = j0 + 2 * h < a.Kn ? lctab[j0 + 2 * h] >> 16 : 0xFFFFu;
-        const uint32_t hi = j0 + 2 * h + 1 < a.Kn ? lctab[j0 + 2 * h + 1] >> 16 : 0xFFFFu;
-        v = lo | (hi << 16);
-      }
-      pc[h] = v;
-    }
-  };
-  // this thread's first PW_CH output chunks c = tid + nt * t, positions cached in registers
-  uint32_t pos[PW_CH][4];
-#pragma unroll
-  for (int t = 0; t < PW_CH; ++t) load_pos(tid + nt * t, pos[t]);
-  for (int nb0 = bid * a.RW; nb0 < min((bid + 1) * a.RW, a.Np); nb0 += RB) {
 #pragma unroll 4
-    for (int i = tid; i < RB * dw; i += nt) {
-      const int r = i / dw, d = i - r * dw, n = nb0 + r;
-      const int p0 = bpack_pos(d, 0);  // its 8 positions p0 .. p0 + 7 (one group: Gw % 8 == 0)
-      T v[8];
-      if (n < a.N) {
-        const uint32_t w = a.codes[(size_t)n * dw + d];
-        const float sc = DT::to_f(wscale[(size_t)min(p0 / a.Gw, a.ngw - 1) * a.Np + n]);
+  for (int i = tid; i < RB * dw; i += blockDim.x) {
+    const int r = i / dw, d = i - r * dw, n = n0 + r;
+    const int p0 = bpack_pos(d, 0);  // its 8 positions p0 .. p0 + 7 (one group: Gw % 8 == 0)
+    T v[8];
+    if (n < a.N) {
+      const uint32_t w = a.codes[(size_t)n * dw + d];
+      const float sc = DT::to_f(wscale[(size_t)min(p0 / a.Gw, a.ngw - 1) * a.Np + n]);
 #pragma unroll
-        for (int e = 0; e < 8; ++e)
-          v[e] = DT::from_f((float)((int)((w >> bpack_shift(e)) & 0xFu) - 8) * sc);
-      } else {
+      for (int e = 0; e < 8; ++e)
+        v[e] = DT::from_f((float)((int)((w >> bpack_shift(e)) & 0xFu) - 8) * sc);
+    } else {
 #pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = DT::from_f(0.f);
-      }
-      *(u32x4*)(wl + (size_t)r * Kp + p0) = *(const u32x4*)v;
+      for (int e = 0; e < 8; ++e) v[e] = DT::from_f(0.f);
     }
-    __syncthreads();
-    // one output chunk of RB rows: positions from the register cache (t < PW_CH) or the table
-    auto chunk = [&](int c, const uint32_t* pc) {
-      const int j0 = 8 * c;
-      if (j0 < a.Kq) {
-        for (int r = 0; r < RB; ++r) {
-          const T* row = wl + (size_t)r * Kp;
-          uint16_t u[8];
+    *(u32x4*)(wl + (size_t)r * Kp + p0) = *(const u32x4*)v;
+  }
+  __syncthreads();
+  const int W = a.Kq + a.S_pad, nch = W / 8;
+  for (int c = tid; c < nch; c += blockDim.x) {
+    const int j0 = 8 * c;
+    if (j0 < a.Kq) {
+      int pos[8];
 #pragma unroll
-          for (int h = 0; h < 4; ++h) {
-            const uint32_t pl = pc[h] & 0xFFFFu, ph = pc[h] >> 16;
-            u[2 * h] = pl != 0xFFFFu ? __builtin_bit_cast(uint16_t, row[pl]) : (uint16_t)0;
-            u[2 * h + 1] = ph != 0xFFFFu ? __builtin_bit_cast(uint16_t, row[ph]) : (uint16_t)0;
-          }
-          *(u32x4*)(wp + (size_t)(nb0 + r) * W + j0) = *(const u32x4*)u;
-        }
-      } else {
-        for (int r = 0; r < RB; ++r) {
-          const int n = nb0 + r;
-          u32x4 v = u32x4{0u, 0u, 0u, 0u};
-          if (n < a.N) v = *(const u32x4*)(wsal + (size_t)n * a.S_pad + (j0 - a.Kq));
-          *(u32x4*)(wp + (size_t)n * W + j0) = v;
-        }
+      for (int e = 0; e < 8; ++e) pos[e] = j0 + e < a.Kn ? (int)(lctab[j0 + e] >> 16) : -1;
+      for (int r = 0; r < RB; ++r) {
+        T v[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = pos[e] >= 0 ? wl[(size_t)r * Kp + pos[e]] : DT::from_f(0.f);
+        *(u32x4*)(wp + (size_t)(n0 + r) * W + j0) = *(const u32x4*)v;
       }
-    };
-#pragma unroll
-    for (int t = 0; t < PW_CH; ++t)
-      if (tid + nt * t < nch) chunk(tid + nt * t, pos[t]);
-    for (int c = tid + nt * PW_CH; c < nch; c += nt) {  // rows wider than the cache
-      uint32_t pc[4];
-      load_pos(c, pc);
-      chunk(c, pc);
+    } else {
+      for (int r = 0; r < RB; ++r) {
+        const int n = n0 + r;
+        u32x4 v = u32x4{0u, 0u, 0u, 0u};
+        if (n < a.N) v = *(const u32x4*)(wsal + (size_t)n * a.S_pad + (j0 - a.Kq));
+        *(u32x4*)(wp + (size_t)n * W + j0) = v;
+      }
     }
-    __syncthreads();  // the batch buffer is rewritten by the next batch
   }
 }
 
@@ -746,24 +710,14 @@ static int pw_rows(int Kp) {
   return rb >= 8 ? 8 : rb >= 4 ? 4 : rb >= 2 ? 2 : 1;
 }
 
-// rows per permutation workgroup (batches of pw_rows): 8 batches of table reuse, a multiple
-// of RB dividing Np (Np % 256 == 0)
-static int pw_wg_rows(int RB) {
-  const char* e = getenv("SQMP_PW_RW");  // tuning only, read per launch
-  const int env = e ? atoi(e) : 0;
-  int rw = env > 0 ? env : 8 * RB;
-  rw = rw < RB ? RB : (rw > 256 ? 256 : rw);
-  return rw / RB * RB;
-}
-
 int launch_perm_weight_c4(int dtype, const uint32_t* lctab, const void* codes,
                           const void* wscale, const void* wsal, int N, int Kp, int Gw, int ngw,
                           int Kn, int S_pad, void* wp, hipStream_t s) {
-  const int Np = pad_n(N), RB = pw_rows(Kp), RW = pw_wg_rows(RB);
+  const int Np = pad_n(N), RB = pw_rows(Kp);
   const int Kq = (int)round_up(Kn, 64);
-  PermArgs pa{(const uint32_t*)codes, wscale, wsal, wp, N, Np, Kp, Gw, ngw, Kn, Kq, S_pad, RB, RW};
+  PermArgs pa{(const uint32_t*)codes, wscale, wsal, wp, N, Np, Kp, Gw, ngw, Kn, Kq, S_pad, RB};
   const size_t lds = (size_t)RB * Kp * 2;
-  const dim3 grid((unsigned)cdiv(Np, RW));
+  const dim3 grid((unsigned)(Np / RB));
   if (dtype == SQMP_F16) {
     SQMP_HIP_CHECK(hipFuncSetAttribute((const void*)perm_weight_kernel<F16>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
@@ -801,9 +755,9 @@ int launch_quant_lc_c4(int dtype, const void* x, int M, int K, int q_max, int G,
   }
   // fused: the quantizer's grid (as quant_lc_launch) + Np / RB permutation workgroups
   const int nw = lc_waves(K, Kn);
-  const int Np = pad_n(cw->N), RB = pw_rows(cw->Kp), RW = pw_wg_rows(RB);
+  const int Np = pad_n(cw->N), RB = pw_rows(cw->Kp);
   PermArgs pa{(const uint32_t*)cw->codes, cw->wscale, cw->wsal, cw->wp, cw->N, Np, cw->Kp,
-              cw->Gw, cw->ngw, Kn, Kq, S_pad, RB, RW};
+              cw->Gw, cw->ngw, Kn, Kq, S_pad, RB};
   const size_t lq = sizeof(uint32_t) * (size_t)(P + S_pad + 8), lp = (size_t)RB * cw->Kp * 2;
   const size_t lds = lq > lp ? lq : lp;
   int per_cu = (int)((150 * 1024) / lds);
@@ -817,7 +771,7 @@ int launch_quant_lc_c4(int dtype, const void* x, int M, int K, int q_max, int G,
   int nq = 256 * (qpc < per_cu ? qpc : per_cu);
   const int npair = (M + 1) / 2;
   if (nq > npair) nq = npair;
-  const dim3 grid(nq + cdiv(Np, RW)), block(64 * nw);
+  const dim3 grid(nq + Np / RB), block(64 * nw);
   if (dtype == SQMP_F16) {
     SQMP_HIP_CHECK(hipFuncSetAttribute((const void*)quant_c4_fused_kernel<F16>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));

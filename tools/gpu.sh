@@ -18,6 +18,7 @@
 #   sweep            bench_sweep.py (config 5)
 #   layer            bench_llama.py (config 4 end to end)
 #   py:SCRIPT[:ARGS] python SCRIPT ARGS (comma-separated args)
+#   profpy:SCRIPT[:ARGS]  the same under rocprofv3 --kernel-trace --stats
 # TAG (env, default "run") names the output directory.
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -84,6 +85,14 @@ step() {
     layer)
       timeout -k 10 400 python bench_llama.py > "$O/layer.json" 2> "$O/layer.err" || fail layer "$O/layer.err"
       cat "$O/layer.json" ;;
+    profpy:*)
+      local rest=${s#profpy:}; local script=${rest%%:*}; local args=""
+      [ "$rest" != "$script" ] && args=$(echo "${rest#*:}" | tr ',' ' ')
+      local name=$(basename "$script" .py)
+      (cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof_$name" -o run \
+        -- python "$R/$script" $args > "$O/prof_$name.log" 2>&1) || fail "$s" "$O/prof_$name.log"
+      f=$(ls "$O"/prof_$name/*/run_kernel_stats.csv "$O"/prof_$name/run_kernel_stats.csv 2>/dev/null | head -1)
+      [ -n "$f" ] && cp "$f" "$O/kernel_stats_$name.csv" && cut -d, -f1-4 "$O/kernel_stats_$name.csv" | cut -c1-150 ;;
     py:*)
       local rest=${s#py:}; local script=${rest%%:*}; local args=""
       [ "$rest" != "$script" ] && args=$(echo "${rest#*:}" | tr ',' ' ')

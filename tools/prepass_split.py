@@ -6,7 +6,7 @@ the permutation alone (sqmp_perm_weight_c4), each ITERS times.
     python tools/prepass_split.py [ITERS] [VAR=v1/v2/... [VAR=...]]
 
 The optional further arguments sweep the permutation's per-launch tuning variables
-(SQMP_PW_RB, SQMP_PW_RW, SQMP_C4_QPERCU): every combination is timed (fused and perm alone).
+(SQMP_PW_RB, SQMP_C4_QPERCU): every combination is timed (fused and perm alone).
 """
 import itertools
 import ctypes
