@@ -34,7 +34,7 @@ namespace sqmp {
 namespace {
 
 constexpr int LC_MODE_TOKEN = 0, LC_MODE_TENSOR = 1, LC_MODE_GROUP = 2;
-constexpr int LC_CH = 4;    // 16-B input chunks per thread per row
+constexpr int LC_CH = 2;    // 16-B input chunks per thread per row
 constexpr int LC_MAXW = 16;  // waves per workgroup (1024 threads)
 
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
@@ -589,9 +589,13 @@ __device__ __forceinline__ void perm_weight_body(const PermArgs& a, const uint32
   for (int c = tid; c < nch; c += blockDim.x) {
     const int j0 = 8 * c;
     if (j0 < a.Kq) {
+      // the 8 table entries as two 16-B loads (lctab is padded with (zero, sink) entries to
+      // whole rounds of the quantizer, >= Kq)
       int pos[8];
+      const u32x4 t0 = ((const u32x4*)(lctab + j0))[0], t1 = ((const u32x4*)(lctab + j0))[1];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) pos[e] = j0 + e < a.Kn ? (int)(lctab[j0 + e] >> 16) : -1;
+      for (int e = 0; e < 8; ++e)
+        pos[e] = j0 + e < a.Kn ? (int)((e < 4 ? t0[e] : t1[e - 4]) >> 16) : -1;
       for (int r = 0; r < RB; ++r) {
         T v[8];
 #pragma unroll
@@ -634,6 +638,22 @@ __global__ __launch_bounds__(1024) void quant_c4_fused_kernel(
 
 constexpr int LC_RPL = 16;
 
+// Workgroups of `block` threads and `lds` dynamic LDS bytes a CU holds at once for kernel f
+// (registers included: the C4 quantizer's 70 VGPRs allow 7 four-wave workgroups, not the 8
+// its LDS would), cached per (kernel, block, lds)
+static int occ_per_cu(const void* f, int block, size_t lds) {
+  struct E { const void* f; int block; size_t lds; int n; };
+  static thread_local E cache[16];
+  static thread_local int next = 0;
+  for (const E& e : cache)
+    if (e.f == f && e.block == block && e.lds == lds) return e.n;
+  int n = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, f, block, lds) != hipSuccess || n < 1) n = 1;
+  cache[next] = E{f, block, lds, n};
+  next = (next + 1) % 16;
+  return n;
+}
+
 static int lc_waves(int K, int Kn) {
   const int a = Kn > 0 ? cdiv(Kn, 64 * LC_RPL) : 1;
   const int b = cdiv(K / 8, 64 * LC_CH);
@@ -651,9 +671,7 @@ static int quant_lc_launch(const void* x, int M, int K, int q_max, int G, const 
   const size_t lds = sizeof(uint32_t) * (size_t)(P + S_pad + 8);
   SQMP_HIP_CHECK(hipFuncSetAttribute((const void*)quant_lc_kernel<DT, MODE, LC_RPL, GS, F8>,
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  int per_cu = (int)((150 * 1024) / lds);
-  const int by_waves = 32 / nw;
-  per_cu = per_cu < 1 ? 1 : (per_cu > by_waves ? by_waves : per_cu);
+  int per_cu = occ_per_cu((const void*)quant_lc_kernel<DT, MODE, LC_RPL, GS, F8>, 64 * nw, lds);
   if (const char* e = getenv("SQMP_LC_PERCU")) per_cu = atoi(e);  // tuning only
   int grid = 256 * per_cu;
   const int npair = (M + 1) / 2;
@@ -760,10 +778,10 @@ int launch_quant_lc_c4(int dtype, const void* x, int M, int K, int q_max, int G,
               cw->Gw, cw->ngw, Kn, Kq, S_pad, RB};
   const size_t lq = sizeof(uint32_t) * (size_t)(P + S_pad + 8), lp = (size_t)RB * cw->Kp * 2;
   const size_t lds = lq > lp ? lq : lp;
-  int per_cu = (int)((150 * 1024) / lds);
-  const int by_waves = 32 / nw;
-  per_cu = per_cu < 1 ? 1 : (per_cu > by_waves ? by_waves : per_cu);
-  // quantizer workgroups per CU: leave two slots of every CU to the permutation
+  const void* kf = dtype == SQMP_BF16 ? (const void*)quant_c4_fused_kernel<BF16>
+                                       : (const void*)quant_c4_fused_kernel<F16>;
+  const int per_cu = occ_per_cu(kf, 64 * nw, lds);
+  // quantizer workgroups per CU: the rest of every CU's slots go to the permutation
   // workgroups (issued after them), so the two run side by side
   const char* qe = getenv("SQMP_C4_QPERCU");  // tuning only, read per launch
   const int q_env = qe ? atoi(qe) : 0;
