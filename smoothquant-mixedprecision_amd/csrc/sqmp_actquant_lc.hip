@@ -257,9 +257,9 @@ __device__ __forceinline__ void quant_lc_body(
   // partial-line writes merge there instead of leaving eight XCDs as masked writes.
   const int xcd = bid & 7, per = nblk >> 3, rem = nblk & 7;
   const int wg = (xcd < rem ? xcd * (per + 1) : rem * (per + 1) + (xcd - rem) * per) + (bid >> 3);
-  const int run = (npair + nblk - 1) / nblk;
-  const int rp_end = min(npair, (wg + 1) * run);
-  int rp = wg * run;
+  // (runs of floor or ceil(npair / nblk) pairs: every XCD gets an eighth of the rows)
+  const int rp_end = (int)((long)(wg + 1) * npair / nblk);
+  int rp = (int)((long)wg * npair / nblk);
   if (rp < rp_end) load_pair(rp);
 
   // ---- once per workgroup: salient-position mask, zeroed buffer (+ two spare words: W =
