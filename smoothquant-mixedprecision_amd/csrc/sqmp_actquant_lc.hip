@@ -660,6 +660,15 @@ static int lc_waves(int K, int Kn) {
   return a > b ? a : b;
 }
 
+// Quantizer workgroups for npair row pairs with `slots` workgroups per CU: runs of a power
+// of two pairs (config 2, 8192 pairs at 7 slots: 1024 workgroups of 8 pairs 71 us, 2048 of 4
+// 70.5 us, 1792 of 4-5 pairs 76.6 us; tools/prepass_split.py)
+static int lc_grid(int npair, int slots) {
+  int ppw = 1;
+  while (ppw < cdiv(npair, 256L * slots)) ppw <<= 1;
+  return cdiv(npair, ppw);
+}
+
 template <class DT, int MODE, int GS, int F8>
 static int quant_lc_launch(const void* x, int M, int K, int q_max, int G, const uint32_t* lctab,
                            int Kn, const int32_t* amap, int P, const int32_t* sal, int S,
@@ -673,9 +682,7 @@ static int quant_lc_launch(const void* x, int M, int K, int q_max, int G, const 
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   int per_cu = occ_per_cu((const void*)quant_lc_kernel<DT, MODE, LC_RPL, GS, F8>, 64 * nw, lds);
   if (const char* e = getenv("SQMP_LC_PERCU")) per_cu = atoi(e);  // tuning only
-  int grid = 256 * per_cu;
-  const int npair = (M + 1) / 2;
-  if (grid > npair) grid = npair;
+  const int grid = lc_grid((M + 1) / 2, per_cu);
   quant_lc_kernel<DT, MODE, LC_RPL, GS, F8><<<dim3(grid), dim3(64 * nw), lds, s>>>(
       (const T*)x, M, K, q_max, G, lctab, Kn, amap, P, sal, S, S_pad, cmax, nonsal, (T*)out,
       key_clear, clear_words, out_scale, (T*)out_xs, Kq, ldsc);
@@ -786,9 +793,7 @@ int launch_quant_lc_c4(int dtype, const void* x, int M, int K, int q_max, int G,
   const char* qe = getenv("SQMP_C4_QPERCU");  // tuning only, read per launch
   const int q_env = qe ? atoi(qe) : 0;
   const int qpc = q_env > 0 ? q_env : (per_cu > 2 ? per_cu - 2 : 1);
-  int nq = 256 * (qpc < per_cu ? qpc : per_cu);
-  const int npair = (M + 1) / 2;
-  if (nq > npair) nq = npair;
+  const int nq = lc_grid((M + 1) / 2, qpc < per_cu ? qpc : per_cu);
   const dim3 grid(nq + Np / RB), block(64 * nw);
   if (dtype == SQMP_F16) {
     SQMP_HIP_CHECK(hipFuncSetAttribute((const void*)quant_c4_fused_kernel<F16>,

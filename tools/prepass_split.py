@@ -6,7 +6,7 @@ the permutation alone (sqmp_perm_weight_c4), each ITERS times.
     python tools/prepass_split.py [ITERS] [VAR=v1/v2/... [VAR=...]]
 
 The optional further arguments sweep the permutation's per-launch tuning variables
-(SQMP_PW_RB, SQMP_C4_QPERCU): every combination is timed (fused and perm alone).
+(SQMP_PW_RB, SQMP_C4_QPERCU, SQMP_LC_PERCU): every combination is timed (fused and perm alone).
 """
 import itertools
 import ctypes
@@ -91,7 +91,7 @@ if len(sys.argv) > 2:
         perm_only()
         torch.cuda.synchronize()
         ok = torch.equal(wp.view(torch.int16), wp_ref.view(torch.int16))
-        tf, tp = t_us(fused), t_us(perm_only)
+        tf, tq, tp = t_us(fused), t_us(quant_only), t_us(perm_only)
         tag = " ".join(f"{k}={v}" for (k, _), v in zip(axes, combo))
-        print(f"{tag:40s} fused {tf:7.1f} us  perm {tp:7.1f} us ({pbytes/tp/1e3:.0f} GB/s)"
+        print(f"{tag:40s} fused {tf:7.1f} us  quant {tq:7.1f} us  perm {tp:7.1f} us ({pbytes/tp/1e3:.0f} GB/s)"
               f"{'' if ok else '  MISMATCH'}")
