@@ -1,5 +1,6 @@
 """Run only the W4A4 GEMM (and optionally the prepass) of BASELINE config 2 -- a target
-for rocprofv3 counter passes.  python tools/gemm_only.py [fq|fqt|i8|f8|h2] [iters] [per_group|per_token] [prepass]"""
+for rocprofv3 counter passes.  python tools/gemm_only.py [fq|fqt|i8|f8|h2|c4] [iters] [per_group|per_token] [prepass]
+(c4: the activation-order prepass alone -- column max, rank table, fused quantizer + permutation)"""
 import os
 import sys
 
@@ -15,7 +16,7 @@ iters = int(sys.argv[2]) if len(sys.argv) > 2 else 10
 extra = sys.argv[3:]
 prepass = "prepass" in extra
 dev = torch.device("cuda")
-act = next((a for a in extra if a.startswith("per_")), "per_group" if kind in ("fq", "fqt") else "per_token")
+act = next((a for a in extra if a.startswith("per_")), "per_group" if kind in ("fq", "fqt", "c4") else "per_token")
 q, x, lin = bench.make_layer(dev, act, seed=1,
                              dtype=torch.float32 if kind == "h2" else torch.float16)
 if kind == "h2":
@@ -33,6 +34,9 @@ elif kind == "fqt":
         if prepass:
             ops.quant_act_c4(x, pw, act, 4, bench.G)
         ops.gemm_fqt(*c4, pw, lin.bias, bench.G)
+elif kind == "c4":
+    for _ in range(iters):
+        ops.quant_act_c4(x, pw, act, 4, bench.G)
 elif kind == "f8":
     a8, sa, xs = ops.quant_act_f8(x, pw, act, 4)
     for _ in range(iters):

@@ -2,7 +2,7 @@
 run_counter_collection.csv) into one JSON per GEMM kind with the derived figures DESIGN.md
 quotes, so every fraction can be recomputed from profiles/ alone.
 
-    python tools/pmc_summary.py <pmc dir> <kind> <avg kernel us> <algorithmic bytes> <mfma cycles per inst> [out.json]
+    python tools/pmc_summary.py <pmc dir> <kind> <avg kernel us> <algorithmic bytes> <mfma cycles per inst> [out.json] [kernel-name substring, default gemm]
 
 Derivations (MI355X_MICROARCH.md: HBM / rocprofv3 sections):
   hbm_bytes      = 2 * FETCH_SIZE * 1024 + WRITE_SIZE * 1024   (gfx950 FETCH_SIZE reads 1/2
@@ -20,21 +20,22 @@ import sys
 from collections import defaultdict
 
 
-def load(d):
+def load(d, match):
     vals = defaultdict(list)
-    for f in glob.glob(os.path.join(d, "*counter_collection.csv")):
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            if "gemm" in r.get("Kernel_Name", ""):
+            if match in r.get("Kernel_Name", ""):
                 vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
     return {k: sum(v) / len(v) for k, v in vals.items()}
 
 
 def main():
     root, kind, us, alg_bytes, cyc = sys.argv[1], sys.argv[2], float(sys.argv[3]), float(sys.argv[4]), float(sys.argv[5])
+    match = sys.argv[7] if len(sys.argv) > 7 else "gemm"
     c = {}
     for d in sorted(glob.glob(os.path.join(root, f"{kind}_*"))):
         if os.path.isdir(d):
-            c.update(load(d))
+            c.update(load(d, match))
     t = us * 1e-6
     xcd_cycles = c["GRBM_GUI_ACTIVE"] / 8
     out = {
@@ -45,7 +46,9 @@ def main():
         "clock_GHz_profiled": xcd_cycles / t / 1e9,
         "mfma_busy": c["SQ_VALU_MFMA_BUSY_CYCLES"] / (1024 * xcd_cycles),
         "mfma_busy_from_inst_count": c["SQ_INSTS_MFMA"] * cyc / (1024 * xcd_cycles),
-        "valu_insts_per_mfma": c["SQ_INSTS_VALU"] / c["SQ_INSTS_MFMA"],
+        "valu_insts_per_mfma": c["SQ_INSTS_VALU"] / max(c["SQ_INSTS_MFMA"], 1),
+        # VALU issue share: wave-instructions x 4 cycles over the SIMD-cycles of the launch
+        "valu_issue_frac": c["SQ_INSTS_VALU"] * 4 / (1024 * xcd_cycles),
         "lds_bank_conflict_frac_of_lds_insts": c.get("SQ_LDS_BANK_CONFLICT", 0) / max(c.get("SQ_INSTS_LDS", 1), 1),
         "l2_hit_rate": c["TCC_HIT_sum"] / (c["TCC_HIT_sum"] + c["TCC_MISS_sum"]),
         "wave_cycles_wait_any_frac": c["SQ_WAIT_ANY"] / c["SQ_WAVE_CYCLES"],
