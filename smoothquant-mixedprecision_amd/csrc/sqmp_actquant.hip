@@ -594,25 +594,37 @@ static bool rank_table_fits(int L) {
 static int launch_rank_table(const uint32_t* key, const int32_t* nonsal, int L,
                              const int32_t* posmap, int32_t* colsorted, uint32_t* lctab,
                              int lc_len, uint32_t lc_none, hipStream_t s) {
-  // about 128-256 competitors per lane (SQMP_RT_TPO=16/32 overrides, tuning only)
-  static const int tpo_env = getenv("SQMP_RT_TPO") ? atoi(getenv("SQMP_RT_TPO")) : 0;
-  const int tpo = tpo_env == 16 || tpo_env == 32 ? tpo_env : (L <= 2048 ? 16 : 32);
+  // about 128-256 competitors per lane (SQMP_RT_TPO = 4 / 8 / 16 / 32 overrides, tuning
+  // only, read per launch)
+  const char* te = getenv("SQMP_RT_TPO");
+  const int tpo_env = te ? atoi(te) : 0;
+  const int tpo = tpo_env == 4 || tpo_env == 8 || tpo_env == 16 || tpo_env == 32
+                      ? tpo_env
+                      : (L <= 2048 ? 16 : 32);
   const int grid = cdiv((long)L * tpo, 256);
   const size_t lds = sizeof(uint32_t) * (size_t)round_up(L, 4 * tpo);
   static bool attr_set = false;  // up to 64 KiB of keys: raise the dynamic-LDS limit once
   if (!attr_set) {
+    SQMP_HIP_CHECK(hipFuncSetAttribute((const void*)rank_table_kernel<4>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, 4 * RT_MAX));
+    SQMP_HIP_CHECK(hipFuncSetAttribute((const void*)rank_table_kernel<8>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, 4 * RT_MAX));
     SQMP_HIP_CHECK(hipFuncSetAttribute((const void*)rank_table_kernel<16>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, 4 * RT_MAX));
     SQMP_HIP_CHECK(hipFuncSetAttribute((const void*)rank_table_kernel<32>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, 4 * RT_MAX));
     attr_set = true;
   }
-  if (tpo == 16)
-    rank_table_kernel<16><<<dim3(grid), dim3(256), lds, s>>>(key, nonsal, L, posmap, colsorted,
-                                                              lctab, lc_len, lc_none);
-  else
-    rank_table_kernel<32><<<dim3(grid), dim3(256), lds, s>>>(key, nonsal, L, posmap, colsorted,
-                                                              lctab, lc_len, lc_none);
+#define SQMP_RT(T)                                                                          \
+  rank_table_kernel<T><<<dim3(grid), dim3(256), lds, s>>>(key, nonsal, L, posmap, colsorted, \
+                                                         lctab, lc_len, lc_none)
+  switch (tpo) {
+    case 4: SQMP_RT(4); break;
+    case 8: SQMP_RT(8); break;
+    case 16: SQMP_RT(16); break;
+    default: SQMP_RT(32); break;
+  }
+#undef SQMP_RT
   SQMP_LAUNCH_CHECK();
   return SQMP_OK;
 }

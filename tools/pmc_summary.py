@@ -3,6 +3,7 @@ run_counter_collection.csv) into one JSON per GEMM kind with the derived figures
 quotes, so every fraction can be recomputed from profiles/ alone.
 
     python tools/pmc_summary.py <pmc dir> <kind> <avg kernel us> <algorithmic bytes> <mfma cycles per inst> [out.json] [kernel-name substring, default gemm]
+(avg kernel us <= 0: the median duration of the profiled dispatches)
 
 Derivations (MI355X_MICROARCH.md: HBM / rocprofv3 sections):
   hbm_bytes      = 2 * FETCH_SIZE * 1024 + WRITE_SIZE * 1024   (gfx950 FETCH_SIZE reads 1/2
@@ -20,12 +21,14 @@ import sys
 from collections import defaultdict
 
 
-def load(d, match):
+def load(d, match, durs=None):
     vals = defaultdict(list)
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
             if match in r.get("Kernel_Name", ""):
                 vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
+                if durs is not None and "End_Timestamp" in r:
+                    durs[r["Dispatch_Id"] + d] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
     return {k: sum(v) / len(v) for k, v in vals.items()}
 
 
@@ -33,9 +36,12 @@ def main():
     root, kind, us, alg_bytes, cyc = sys.argv[1], sys.argv[2], float(sys.argv[3]), float(sys.argv[4]), float(sys.argv[5])
     match = sys.argv[7] if len(sys.argv) > 7 else "gemm"
     c = {}
+    durs = {}
     for d in sorted(glob.glob(os.path.join(root, f"{kind}_*"))):
         if os.path.isdir(d):
-            c.update(load(d, match))
+            c.update(load(d, match, durs))
+    if us <= 0:  # the profiled dispatches' own mean duration (reads long against unprofiled runs)
+        us = sorted(durs.values())[len(durs) // 2]
     t = us * 1e-6
     xcd_cycles = c["GRBM_GUI_ACTIVE"] / 8
     out = {
