@@ -520,17 +520,21 @@ __global__ __launch_bounds__(256) void lc_table_kernel(
 
 // ---------------------------------------------------------------- rank + table, one launch
 // For lists up to RT_MAX entries: every workgroup stages all L keys key[nonsal[j]] in LDS
-// and ranks 256 / TPO owners, TPO lanes per owner splitting the competitors (16-B LDS
-// reads, interleaved so the TPO lanes hit consecutive chunks), then reduces the TPO
-// partial counts by lane shuffles.  The stable rank of owner i is
+// and ranks R * 256 / TPO owners, TPO lanes per group of R owners splitting the competitors
+// (16-B LDS reads, interleaved so the TPO lanes hit consecutive chunks; each chunk read is
+// compared against all R owners), then reduces the TPO partial counts by lane shuffles.  The
+// stable rank of owner i is
 //   #{j : key_j < key_i} + #{j < i : key_j == key_i}
 // (the reference's stable argsort, fake_quant.py:113), counted as key_j < thr with
 // thr = key_i + 1 on 4-entry chunks wholly below i, key_i elsewhere, plus the equal keys
 // of i's own chunk below i.  Writes colsorted[r] and lctab[r] = col | posmap[col] << 16,
 // and the (zero, sink) entries of ranks [L, lc_len).  The keys are NOT cleared here (other
 // workgroups may still read them): the quantizer launched next clears them.
+// The staging gathers up to RT_SB entries per thread in one batch (all index loads, then
+// all key loads: two dependent round trips for the whole list up to 256 * RT_SB entries).
 constexpr int RT_MAX = 16384;  // 64 KiB of keys in LDS
-template <int TPO>
+constexpr int RT_SB = 24;
+template <int TPO, int R>
 __global__ __launch_bounds__(256) void rank_table_kernel(
     const uint32_t* __restrict__ key, const int32_t* __restrict__ nonsal, int L,
     const int32_t* __restrict__ posmap, int32_t* __restrict__ colsorted,
@@ -538,20 +542,18 @@ __global__ __launch_bounds__(256) void rank_table_kernel(
   extern __shared__ __attribute__((aligned(16))) uint32_t rt_kv[];  // roundup(L, 4 TPO)
   const int tid = threadIdx.x;
   const int L4 = (int)round_up_dev(L, 4 * TPO) >> 2;
-  // gathers in batches of 16 per thread (all index loads, then all key loads): two
-  // dependent round trips per batch instead of two per element
-  for (int j0 = tid; j0 < 4 * L4; j0 += 256 * 16) {
-    int idx[16];
-    uint32_t kv[16];
+  for (int j0 = tid; j0 < 4 * L4; j0 += 256 * RT_SB) {
+    int idx[RT_SB];
+    uint32_t kv[RT_SB];
 #pragma unroll
-    for (int u = 0; u < 16; ++u) {
+    for (int u = 0; u < RT_SB; ++u) {
       const int j = j0 + 256 * u;
       idx[u] = j < L ? nonsal[j] : -1;
     }
 #pragma unroll
-    for (int u = 0; u < 16; ++u) kv[u] = idx[u] >= 0 ? key[idx[u]] : 0xFFFFFFFFu;
+    for (int u = 0; u < RT_SB; ++u) kv[u] = idx[u] >= 0 ? key[idx[u]] : 0xFFFFFFFFu;
 #pragma unroll
-    for (int u = 0; u < 16; ++u) {
+    for (int u = 0; u < RT_SB; ++u) {
       const int j = j0 + 256 * u;
       if (j < 4 * L4) rt_kv[j] = kv[u];
     }
@@ -560,28 +562,39 @@ __global__ __launch_bounds__(256) void rank_table_kernel(
   for (int r = L + blockIdx.x * 256 + tid; r < lc_len; r += nt) lctab[r] = lc_none;
   __syncthreads();
   const int sub = tid % TPO;
-  const int owner = blockIdx.x * (256 / TPO) + tid / TPO;
-  const int oi = owner < L ? owner : L - 1;
-  const uint32_t mine = rt_kv[oi];
-  const int ochunk = oi >> 2;
-  uint32_t c0 = 0, c1 = 0;
+  const int g0 = (blockIdx.x * (256 / TPO) + tid / TPO) * R;  // this lane group's first owner
+  uint32_t mine[R], cnt[R];
+  int ochunk[R];
+#pragma unroll
+  for (int o = 0; o < R; ++o) {
+    const int oi = g0 + o < L ? g0 + o : L - 1;
+    mine[o] = rt_kv[oi];
+    ochunk[o] = oi >> 2;
+    cnt[o] = 0u;
+  }
   const u32x4* kv4 = (const u32x4*)rt_kv;
-#pragma unroll 4
+#pragma unroll 2
   for (int j4 = sub; j4 < L4; j4 += TPO) {
     const u32x4 k = kv4[j4];
-    const uint32_t thr = j4 < ochunk ? mine + 1u : mine;  // keys never reach 0xFFFFFFFF
-    c0 += (k[0] < thr ? 1u : 0u) + (k[1] < thr ? 1u : 0u);
-    c1 += (k[2] < thr ? 1u : 0u) + (k[3] < thr ? 1u : 0u);
-  }
-  uint32_t cnt = c0 + c1;
-  if (sub == (ochunk % TPO))
-    for (int e = 0; e < (oi & 3); ++e) cnt += rt_kv[4 * ochunk + e] == mine ? 1u : 0u;
 #pragma unroll
-  for (int o = 1; o < TPO; o <<= 1) cnt += (uint32_t)__shfl_xor((int)cnt, o, 64);
-  if (sub == 0 && owner < L) {
-    const int col = nonsal[owner];
-    colsorted[cnt] = col;
-    lctab[cnt] = (uint32_t)col | ((uint32_t)(posmap ? posmap[col] : col) << 16);
+    for (int o = 0; o < R; ++o) {
+      const uint32_t thr = j4 < ochunk[o] ? mine[o] + 1u : mine[o];  // keys never reach 0xFFFFFFFF
+      cnt[o] += (k[0] < thr ? 1u : 0u) + (k[1] < thr ? 1u : 0u) + (k[2] < thr ? 1u : 0u) +
+                (k[3] < thr ? 1u : 0u);
+    }
+  }
+#pragma unroll
+  for (int o = 0; o < R; ++o) {
+    const int oi = g0 + o < L ? g0 + o : L - 1;
+    if (sub == (ochunk[o] % TPO))
+      for (int e = 0; e < (oi & 3); ++e) cnt[o] += rt_kv[4 * ochunk[o] + e] == mine[o] ? 1u : 0u;
+#pragma unroll
+    for (int w = 1; w < TPO; w <<= 1) cnt[o] += (uint32_t)__shfl_xor((int)cnt[o], w, 64);
+    if (sub == 0 && g0 + o < L) {
+      const int col = nonsal[g0 + o];
+      colsorted[cnt[o]] = col;
+      lctab[cnt[o]] = (uint32_t)col | ((uint32_t)(posmap ? posmap[col] : col) << 16);
+    }
   }
 }
 
@@ -594,36 +607,40 @@ static bool rank_table_fits(int L) {
 static int launch_rank_table(const uint32_t* key, const int32_t* nonsal, int L,
                              const int32_t* posmap, int32_t* colsorted, uint32_t* lctab,
                              int lc_len, uint32_t lc_none, hipStream_t s) {
-  // about 128-256 competitors per lane (SQMP_RT_TPO = 4 / 8 / 16 / 32 overrides, tuning
-  // only, read per launch)
+  // TPO lanes per group of R owners (SQMP_RT_TPO = 8 / 16 / 32 and SQMP_RT_R = 1 / 2 / 4
+  // override, tuning only, read per launch)
   const char* te = getenv("SQMP_RT_TPO");
-  const int tpo_env = te ? atoi(te) : 0;
-  const int tpo = tpo_env == 4 || tpo_env == 8 || tpo_env == 16 || tpo_env == 32
-                      ? tpo_env
-                      : (L <= 2048 ? 16 : 32);
-  const int grid = cdiv((long)L * tpo, 256);
+  const char* re = getenv("SQMP_RT_R");
+  int tpo = L <= 2048 ? 16 : 32, r = 1;
+  if (te && (atoi(te) == 8 || atoi(te) == 16 || atoi(te) == 32)) tpo = atoi(te);
+  if (re && (atoi(re) == 1 || atoi(re) == 2 || atoi(re) == 4)) r = atoi(re);
+  const int grid = cdiv((long)L * tpo, 256L * r);
   const size_t lds = sizeof(uint32_t) * (size_t)round_up(L, 4 * tpo);
-  static bool attr_set = false;  // up to 64 KiB of keys: raise the dynamic-LDS limit once
-  if (!attr_set) {
-    SQMP_HIP_CHECK(hipFuncSetAttribute((const void*)rank_table_kernel<4>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, 4 * RT_MAX));
-    SQMP_HIP_CHECK(hipFuncSetAttribute((const void*)rank_table_kernel<8>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, 4 * RT_MAX));
-    SQMP_HIP_CHECK(hipFuncSetAttribute((const void*)rank_table_kernel<16>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, 4 * RT_MAX));
-    SQMP_HIP_CHECK(hipFuncSetAttribute((const void*)rank_table_kernel<32>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, 4 * RT_MAX));
-    attr_set = true;
+#define SQMP_RT(T, RR)                                                                       \
+  do {                                                                                      \
+    static bool attr = false; /* up to 64 KiB of keys: raise the dynamic-LDS limit once */ \
+    if (!attr) {                                                                            \
+      SQMP_HIP_CHECK(hipFuncSetAttribute((const void*)rank_table_kernel<T, RR>,             \
+                                         hipFuncAttributeMaxDynamicSharedMemorySize,        \
+                                         4 * RT_MAX));                                      \
+      attr = true;                                                                          \
+    }                                                                                       \
+    rank_table_kernel<T, RR><<<dim3(grid), dim3(256), lds, s>>>(key, nonsal, L, posmap,     \
+                                                               colsorted, lctab, lc_len,    \
+                                                               lc_none);                    \
+  } while (0)
+#define SQMP_RT_T(T)            \
+  switch (r) {                  \
+    case 2: SQMP_RT(T, 2); break; \
+    case 4: SQMP_RT(T, 4); break; \
+    default: SQMP_RT(T, 1); break; \
   }
-#define SQMP_RT(T)                                                                          \
-  rank_table_kernel<T><<<dim3(grid), dim3(256), lds, s>>>(key, nonsal, L, posmap, colsorted, \
-                                                         lctab, lc_len, lc_none)
   switch (tpo) {
-    case 4: SQMP_RT(4); break;
-    case 8: SQMP_RT(8); break;
-    case 16: SQMP_RT(16); break;
-    default: SQMP_RT(32); break;
+    case 8: SQMP_RT_T(8); break;
+    case 16: SQMP_RT_T(16); break;
+    default: SQMP_RT_T(32); break;
   }
+#undef SQMP_RT_T
 #undef SQMP_RT
   SQMP_LAUNCH_CHECK();
   return SQMP_OK;
