@@ -14,7 +14,7 @@
 //     thread's values lie in one group (G / RPL lanes per group, combined by lane
 //     shuffles; groups never straddle waves) and for G < RPL a thread holds RPL / G whole
 //     groups: the group absmax needs no LDS atomics.
-//   * Per row pair: 16-B global loads (prefetched one row pair ahead) -> interleave into
+//   * Per row pair: 16-B global loads (the next pair's issued after the interleave) -> interleave into
 //     LDS -> gather the thread's RPL column pairs (ds_read_b32) -> group absmax on the
 //     packed magnitudes (v_pk_max_u16) -> scales -> quantize both rows at once with packed
 //     math -> scatter to the packed positions in the same LDS buffer (ds_write_b32) ->
@@ -331,6 +331,9 @@ __device__ __forceinline__ void quant_lc_body(
         ((u32x4*)lc_buf)[2 * c + 1] = w1;
       }
     }
+    // prefetch the next pair: its registers are free once interleaved, and its latency now
+    // overlaps this pair's gather, quantization and stores (same VGPR count)
+    if (rp + 1 < rp_end) load_pair(rp + 1);
     __syncthreads();
 
     // ---- gather; exact salient columns into the tail (>= K)
@@ -450,7 +453,6 @@ __device__ __forceinline__ void quant_lc_body(
     // salient columns' own packed positions hold 0 (their weight codes are 0 too)
     if (F8 != 3)
       for (uint64_t zm = zmask; zm; zm &= zm - 1) lc_buf[zp0 + __builtin_ctzll(zm)] = 0u;
-    if (rp + 1 < rp_end) load_pair(rp + 1);  // prefetch the next pair
     __syncthreads();
 
     if (F8 == 1) {
