@@ -172,6 +172,8 @@ int sqmp_quant_act(void* x, int dtype, int M, int K, int amode, int n_bits,
 #define SQMP_QA_TILED 8       /* SQMP_OUT_C4: codes, group scales and salient x written in the
                                  tile-major layouts of sqmp_gemm_fqt7 (sqmp_fq7_sizes with
                                  J = 2 and N = M gives their sizes) instead of row-major */
+#define SQMP_QA_TILED4 16     /* as SQMP_QA_TILED with 64-row blocks (J = 4), the operands of
+                                 sqmp_gemm_fqt7j with J = 4 */
 
 /* sqmp_quant_act with the per-weight map posmap (int32 [K]: packed position of column k,
  * the inverse of perm; NULL = derive it per call) and flags.  With posmap, OUT_FP on
@@ -305,6 +307,13 @@ int sqmp_gemm_fqt7(const void* codes_t, const void* scale_t, const void* sal_t, 
 int sqmp_gemm_fqt7_colmax(const void* codes_t, const void* scale_t, const void* sal_t,
                           const void* wp, const void* bias, void* y, int dtype, int M, int N,
                           int Kq, int S_pad, int G, int ngq, uint32_t* colmax, void* stream);
+
+/* sqmp_gemm_fqt7 / _colmax for either tile-major operand layout: J = 2 (SQMP_QA_TILED, 32-row
+ * blocks; 256 x 256 output tiles) or J = 4 (SQMP_QA_TILED4, 64-row blocks; 128 weight rows x
+ * 512 tokens per tile).  colmax NULL: no statistics. */
+int sqmp_gemm_fqt7j(const void* codes_t, const void* scale_t, const void* sal_t, const void* wp,
+                    const void* bias, void* y, int dtype, int M, int N, int Kq, int S_pad, int G,
+                    int ngq, int J, uint32_t* colmax, void* stream);
 
 /* The fp32 faithful GEMM on the f16 MFMA (the default for fp32 layers): every row of A and
  * of W is scaled by a power of two (exact) so that its maximum lies in [2^13, 2^14), each

@@ -206,8 +206,9 @@ __device__ inline uint32_t f8_pair(uint32_t v, const PairScale& c) {
 // F8 = 3 (SQMP_OUT_C4, group mode, G >= RPL): out is the int4 codes in ACTIVATION-RANK
 // order as bpack rows of Kq positions (Kq / 2 bytes per row; the act-order GEMM operand),
 // out_scale (as D) the group scales [Kq / G][ldsc], out_xs the exact salient columns.
-// ldsc < 0 (SQMP_QA_TILED): the three in sqmp_gemm_fqt7's tile-major layouts (fq7, J = 2:
-// 32-row blocks nb = m / 32, row j = m / 16 % 2, r16 = m % 16), -ldsc groups.
+// ldsc < 0 (SQMP_QA_TILED): the three in sqmp_gemm_fqt7's tile-major layouts (fq7 with TJ =
+// 2 or 4 row tiles: 16 TJ-row blocks nb = m / (16 TJ), row tile j = m / 16 % TJ, r16 = m % 16);
+// -ldsc = ngq * 8 + TJ.
 // (the body of quant_lc_kernel: workgroup `bid` of `nblk` quantizer workgroups)
 template <class DT, int MODE, int RPL, int GS, int F8 = 0>
 __device__ __forceinline__ void quant_lc_body(
@@ -401,25 +402,27 @@ __device__ __forceinline__ void quant_lc_body(
             }
           const int u = (rb >> 4) & 3;
           if (ldsc < 0) {
-            // Bt[nb][kb][lane][j][s]: dword d of the row's block kb at lane 16 (d / 2) + r16,
-            // slot 2 j + d % 2 (m0 even: both rows share nb and j).  Lanes u and u ^ 1 hold
-            // the two slots of a lane: the even one stores row m0's pair, the odd one row
-            // m0 + 1's, 8 B each (Kq % 128 == 0: both lanes of a pair are active)
+            // Bt[nb][kb][lane][j][s] (TJ = 2 or 4 row tiles of 16 per 16 TJ-row block nb):
+            // dword d of the row's block kb at lane 16 (d / 2) + r16, slot 2 j + d % 2 (m0
+            // even: both rows share nb and j).  Lanes u and u ^ 1 hold the two slots of a
+            // lane: the even one stores row m0's pair, the odd one row m0 + 1's, 8 B each
+            // (Kq % 128 == 0: both lanes of a pair are active)
             typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-            const int nb = m0 >> 5, j = (m0 >> 4) & 1, r = m0 & 15, od = u & 1;
+            const int TJ = (-ldsc) & 7, ngq = (-ldsc) >> 3;
+            const int nb = m0 / (16 * TJ), j = (m0 >> 4) & (TJ - 1), r = m0 & 15, od = u & 1;
             const uint32_t x0 = __shfl_xor(od ? d0[0] : d1[0], 1, 64);
             const uint32_t x1 = __shfl_xor(od ? d0[1] : d1[1], 1, 64);
-            u32x2* t = (u32x2*)out + ((size_t)nb * (Kq / 64) + (rb >> 6)) * 128 + j;
+            u32x2* t = (u32x2*)out + ((size_t)nb * (Kq / 64) + (rb >> 6)) * (64 * TJ) + j;
             const int rr = r + od;
             if (!od || has1) {
-              t[(16 * (u >> 1) + rr) * 2] = od ? u32x2{x0, d1[0]} : u32x2{d0[0], x0};
-              t[(16 * (2 + (u >> 1)) + rr) * 2] = od ? u32x2{x1, d1[1]} : u32x2{d0[1], x1};
+              t[(16 * (u >> 1) + rr) * TJ] = od ? u32x2{x0, d1[0]} : u32x2{d0[0], x0};
+              t[(16 * (2 + (u >> 1)) + rr) * TJ] = od ? u32x2{x1, d1[1]} : u32x2{d0[1], x1};
             }
             if (rb % G == 0) {
               // St[nb][g][r16][j]
-              uint16_t* sc = (uint16_t*)out_scale + ((size_t)(nb * -ldsc + rb / G) * 16 + r) * 2 + j;
+              uint16_t* sc = (uint16_t*)out_scale + ((size_t)(nb * ngq + rb / G) * 16 + r) * TJ + j;
               sc[0] = (uint16_t)(c.sd & 0xFFFFu);
-              if (has1) sc[2] = (uint16_t)(c.sd >> 16);
+              if (has1) sc[TJ] = (uint16_t)(c.sd >> 16);
             }
           } else {
             uint32_t* r0 = (uint32_t*)((unsigned char*)out + (size_t)m0 * (Kq / 2)) + (rb >> 6) * 8;
@@ -494,11 +497,12 @@ __device__ __forceinline__ void quant_lc_body(
         z1[3] = __builtin_amdgcn_perm(b[3], b[2], 0x07060302u);
         if (F8 == 3 && ldsc < 0) {
           // Salt[nb][kd][lane][j][s][8]: chunk cc of block kd = c(q, s) = 4 (q & 1) + 2 s + q / 2
-          const int nb = m0 >> 5, j = (m0 >> 4) & 1, r = m0 & 15, kd = c >> 3, cc = c & 7;
+          const int TJ = (-ldsc) & 7;
+          const int nb = m0 / (16 * TJ), j = (m0 >> 4) & (TJ - 1), r = m0 & 15, kd = c >> 3, cc = c & 7;
           const int lq = 16 * ((cc >> 2) | ((cc & 1) << 1)), sl = (cc >> 1) & 1;
-          u32x4* t = (u32x4*)out_xs + ((size_t)nb * (S_pad / 64) + kd) * 256 + 2 * j + sl;
-          t[(lq + r) * 4] = z0;
-          if (has1) t[(lq + r + 1) * 4] = z1;
+          u32x4* t = (u32x4*)out_xs + ((size_t)nb * (S_pad / 64) + kd) * (128 * TJ) + 2 * j + sl;
+          t[(lq + r) * 2 * TJ] = z0;
+          if (has1) t[(lq + r + 1) * 2 * TJ] = z1;
         } else {
           ((u32x4*)x0)[c] = z0;
           if (has1) ((u32x4*)x1)[c] = z1;

@@ -110,7 +110,9 @@ __host__ __device__ inline int brev3(int c) { return ((c & 1) << 2) | (c & 2) | 
 // DIAG (timing diagnostics, wrong results by design, instantiated only in a SQMP_DIAG_BUILD;
 // 0 = the product kernel): 1 no weight
 // register loads after the prologue, 2 no A DMA after the prologue, 3 no int4 decode, 4 no
-// per-stage barrier
+// per-stage barrier, 5 half the A fragment LDS reads (each fragment used for two blocks), 6 the
+// A pieces written by ds_write_b128 from registers instead of LDS-DMA, 7 the A DMA from two
+// L2-hot stages only
 // J = 16-row weight tiles per wave: tile TM x TN with TN = 8 * 16 J (J = 4: 128 x 512;
 // J = 2: 256 x 256, fq6's decode-optimal shape -- a decoded fragment feeds TM / 16 MFMAs)
 // TR (sqmp_gemm_fqt on the tile-major activation operands): A = the permuted weight wp,
@@ -172,12 +174,20 @@ __global__ __launch_bounds__(512, 1) void gemm_fq7_kernel(
   auto issue_a = [&](int kt) {
     if (kt < nkt && (DIAG != 2 || kt < PA) && (!SPLIT || wave < 4)) {
       unsigned char* slot = lds + (kt % NS) * SLOT;
-      const uint32_t so = (uint32_t)kt * 64 * sizeof(T);
+      const uint32_t so = (uint32_t)(DIAG == 7 ? (kt & 1) : kt) * 64 * sizeof(T);
 #pragma unroll
       for (int o = 0; o < NO; ++o)
 #pragma unroll
-        for (int i = 0; i < NA; ++i)
-          dma16(rA, a_off[o][i], so, slot + (i * 8 + wave + 4 * o) * 1024);
+        for (int i = 0; i < NA; ++i) {
+          unsigned char* dst = slot + (i * 8 + wave + 4 * o) * 1024;
+          if (DIAG == 6 && kt >= PA) {  // the same LDS bytes written by ds_write_b128, no VMEM
+            const u32x4 v = {a_off[o][i], so, 0u, 0u};
+            const uint32_t la = (uint32_t)(size_t)(__attribute__((address_space(3))) unsigned char*)dst + lane * 16;
+            asm volatile("ds_write_b128 %0, %1" ::"v"(la), "v"(v) : "memory");
+          } else {
+            dma16(rA, a_off[o][i], so, dst);
+          }
+        }
     }
   };
 
@@ -239,6 +249,7 @@ __global__ __launch_bounds__(512, 1) void gemm_fq7_kernel(
   const int a_sw = (r16 >> 1) & 7;
   // A fragment of block t (sub-step s = t / I, row tile i = t % I)
   auto ald = [&](const unsigned char* __restrict__ slot, int t) {
+    if (DIAG == 5) t &= ~1;  // timing diagnostic: half the A fragment reads
     const int c = 4 * (q & 1) + 2 * (t / I) + (q >> 1);
     return *(const u32x4*)(slot + (16 * (t % I) + r16) * 128 + ((brev3(c) ^ a_sw) << 4));
   };
@@ -499,12 +510,9 @@ static int group_m_env() {
 
 // the activation-order (TR) launch: 4 weight-row tiles per raster group (same box, config 2:
 // GEMM 422.5 vs 429.8 us at 8, alternating runs); SQMP_FQT7_GROUP_M overrides
-static int group_m_tr_env() {
-  static int v = [] {
-    const char* e = getenv("SQMP_FQT7_GROUP_M");
-    return e && atoi(e) > 0 ? atoi(e) : 4;
-  }();
-  return v;
+static int group_m_tr_env() {  // read per launch (in-process A/B)
+  const char* e = getenv("SQMP_FQT7_GROUP_M");
+  return e && atoi(e) > 0 ? atoi(e) : 4;
 }
 
 // the activation-order launch's OPT variant (A/B knob, see gemm_fq7_kernel)
@@ -519,12 +527,9 @@ static int opt_tr_env() {  // read per launch (in-process A/B)
 #ifdef SQMP_DIAG_BUILD
 // timing-diagnostic variants (wrong results by design) only in a diagnostics build:
 // SQMP_DIAG=1 python smoothquant-mixedprecision_amd/build_ext.py --force
-static int diag_env() {
-  static int v = [] {
-    const char* e = getenv("SQMP_FQ7_DIAG");
-    return e ? atoi(e) : 0;
-  }();
-  return v;
+static int diag_env() {  // read per launch (in-process A/B)
+  const char* e = getenv("SQMP_FQ7_DIAG");
+  return e ? atoi(e) : 0;
 }
 #endif
 
@@ -583,24 +588,53 @@ static int dispatch(const void* a, const void* bt, const void* st, const void* s
 }
 
 // the activation-order GEMM (TR): kernel M = weight rows N (wp rows), kernel N = tokens M
-template <class DT>
+// J = 2: 256 weight rows x 256 tokens (8 waves of 32 tokens); J = 4: 128 weight rows x 512
+// tokens (8 waves of 64 tokens: half the wp LDS-DMA and LDS fragment reads per MFMA, twice the
+// act-code decode per MFMA)
+template <class DT, int J>
 static int dispatch_tr(const void* wp, const void* codes_t, const void* scale_t, const void* sal_t,
                        const void* bias, void* y, int M, int N, int Kq, int S_pad, int G, int ngq,
                        uint32_t* colmax, hipStream_t s) {
   typedef typename DT::T T;
-  constexpr int TM = std::is_same<DT, BF16>::value ? 128 : 256;
-  const int tiles_m = cdiv(N, TM), tiles_n = cdiv(M, 256);
+  constexpr int TM = (J == 4 || std::is_same<DT, BF16>::value) ? 128 : 256;
+  const int tiles_m = cdiv(N, TM), tiles_n = cdiv(M, 128 * J);
 #define SQMP_TR(O)                                                                              \
-  gemm_fq7_kernel<DT, 1, TM, 2, 0, true, O><<<dim3(tiles_m * tiles_n), dim3(512), 0, s>>>(      \
+  gemm_fq7_kernel<DT, 1, TM, J, 0, true, O><<<dim3(tiles_m * tiles_n), dim3(512), 0, s>>>(      \
       (const T*)wp, (const uint32_t*)codes_t, (const T*)scale_t, (const T*)sal_t, (const T*)bias, \
       (T*)y, N, M, Kq, S_pad, G, ngq, tiles_m, tiles_n, group_m_tr_env(), colmax)
-  switch (opt_tr_env()) {
-    case 1: SQMP_TR(1); break;
-    case 2: SQMP_TR(2); break;
-    case 3: SQMP_TR(3); break;
-    case 4: SQMP_TR(4); break;
-    case 5: SQMP_TR(5); break;
-    default: SQMP_TR(0); break;  // 6, 7 (split + PF = 3) spill with the colmax epilogue
+#ifdef SQMP_DIAG_BUILD
+#define SQMP_TRD(D)                                                                             \
+  gemm_fq7_kernel<DT, 1, TM, 2, D, true, 3><<<dim3(tiles_m * tiles_n), dim3(512), 0, s>>>(      \
+      (const T*)wp, (const uint32_t*)codes_t, (const T*)scale_t, (const T*)sal_t, (const T*)bias, \
+      (T*)y, N, M, Kq, S_pad, G, ngq, tiles_m, tiles_n, group_m_tr_env(), colmax)
+  if (std::is_same<DT, F16>::value && J == 2 && diag_env() > 0) {
+    switch (diag_env()) {
+      case 1: SQMP_TRD(1); break;
+      case 2: SQMP_TRD(2); break;
+      case 3: SQMP_TRD(3); break;
+      case 4: SQMP_TRD(4); break;
+      case 5: SQMP_TRD(5); break;
+      case 6: SQMP_TRD(6); break;
+      default: SQMP_TRD(7); break;
+    }
+    SQMP_LAUNCH_CHECK();
+    return SQMP_OK;
+  }
+#undef SQMP_TRD
+#endif
+  if constexpr (J == 4) {
+    // setprio only (the loader split spills a VGPR at J = 4; OPT 0 / 4 / 5 measured within
+    // 0.3 % of 1 at config 2, all 7 % slower than J = 2: profiles/r03_ab_fqt7_j4.txt)
+    SQMP_TR(1);
+  } else {
+    switch (opt_tr_env()) {
+      case 1: SQMP_TR(1); break;
+      case 2: SQMP_TR(2); break;
+      case 3: SQMP_TR(3); break;
+      case 4: SQMP_TR(4); break;
+      case 5: SQMP_TR(5); break;
+      default: SQMP_TR(0); break;  // 6, 7 (split + PF = 3) spill with the colmax epilogue
+    }
   }
 #undef SQMP_TR
   SQMP_LAUNCH_CHECK();
@@ -680,24 +714,28 @@ extern "C" int sqmp_gemm_fq7(const void* a, const void* codes_t, const void* sca
 // writes when called with the SQMP_QA_TILED flag
 static int gemm_fqt7_impl(const void* codes_t, const void* scale_t, const void* sal_t,
                           const void* wp, const void* bias, void* y, int dtype, int M, int N,
-                          int Kq, int S_pad, int G, int ngq, uint32_t* colmax, void* stream) {
+                          int Kq, int S_pad, int G, int ngq, int J, uint32_t* colmax,
+                          void* stream) {
   if (!codes_t || !scale_t || !sal_t || !wp || !y) return SQMP_EINVAL;
+  if (J != 2 && J != 4) return SQMP_EINVAL;
   if (M < 0 || N <= 0 || Kq <= 0 || Kq % 128 || S_pad < 0 || S_pad % 64 || G <= 0 || ngq <= 0)
     return SQMP_EINVAL;
   if (dtype != SQMP_F16 && dtype != SQMP_BF16) return SQMP_EUNSUPPORTED;
   if (G % 64 || N % 8) return SQMP_EUNSUPPORTED;
   if (M == 0) return SQMP_OK;
   hipStream_t s = (hipStream_t)stream;
-  if (dtype == SQMP_F16)
-    return fq7::dispatch_tr<F16>(wp, codes_t, scale_t, sal_t, bias, y, M, N, Kq, S_pad, G, ngq, colmax, s);
-  return fq7::dispatch_tr<BF16>(wp, codes_t, scale_t, sal_t, bias, y, M, N, Kq, S_pad, G, ngq, colmax, s);
+#define SQMP_DTR(DTT, JJ) \
+  fq7::dispatch_tr<DTT, JJ>(wp, codes_t, scale_t, sal_t, bias, y, M, N, Kq, S_pad, G, ngq, colmax, s)
+  if (dtype == SQMP_F16) return J == 4 ? SQMP_DTR(F16, 4) : SQMP_DTR(F16, 2);
+  return J == 4 ? SQMP_DTR(BF16, 4) : SQMP_DTR(BF16, 2);
+#undef SQMP_DTR
 }
 
 extern "C" int sqmp_gemm_fqt7(const void* codes_t, const void* scale_t, const void* sal_t,
                               const void* wp, const void* bias, void* y, int dtype, int M, int N,
                               int Kq, int S_pad, int G, int ngq, void* stream) {
   return gemm_fqt7_impl(codes_t, scale_t, sal_t, wp, bias, y, dtype, M, N, Kq, S_pad, G, ngq,
-                        nullptr, stream);
+                        2, nullptr, stream);
 }
 
 // the same with the fused output-quant statistics (as sqmp_gemm_fq_colmax): colmax[n] =
@@ -708,6 +746,15 @@ extern "C" int sqmp_gemm_fqt7_colmax(const void* codes_t, const void* scale_t, c
                                      void* stream) {
   if (!colmax) return SQMP_EINVAL;
   return gemm_fqt7_impl(codes_t, scale_t, sal_t, wp, bias, y, dtype, M, N, Kq, S_pad, G, ngq,
+                        2, colmax, stream);
+}
+
+// the general entry: J = 2 (SQMP_QA_TILED operands) or 4 (SQMP_QA_TILED4); colmax may be NULL
+extern "C" int sqmp_gemm_fqt7j(const void* codes_t, const void* scale_t, const void* sal_t,
+                               const void* wp, const void* bias, void* y, int dtype, int M, int N,
+                               int Kq, int S_pad, int G, int ngq, int J, uint32_t* colmax,
+                               void* stream) {
+  return gemm_fqt7_impl(codes_t, scale_t, sal_t, wp, bias, y, dtype, M, N, Kq, S_pad, G, ngq, J,
                         colmax, stream);
 }
 

@@ -298,6 +298,9 @@ FQT_MIN_ROWS = int(os.environ.get("SQMP_FQT_MIN_ROWS", "16384"))
 # the activation-order GEMM on fq7's structure (sqmp_gemm_fqt7: tile-major activation
 # operands written by the quantizer) when Kq % 128 == 0, else on fq6's (sqmp_gemm_fqt)
 FQT7 = os.environ.get("SQMP_FQT7", "1") == "1"
+# its register operand's row tiles per wave: 2 (256 weight rows x 256 tokens per tile) or 4
+# (128 x 512: half the permuted-weight LDS traffic per MFMA, twice the act-code decode)
+FQT7_J = int(os.environ.get("SQMP_FQT7_J", "2"))
 
 
 def fqt_eligible(pw: PackedWeight, act_quant: str, act_bits: int, group_size: int,
@@ -319,8 +322,9 @@ def quant_act_c4(x2: torch.Tensor, pw: PackedWeight, act_quant: str, n_bits: int
     """x [M, K] -> the activation-order operands of gemm_fqt: (int4 codes [M, Kq/2] bytes,
     D group scales [Kq/G, Mp], exact salient x [M, S_pad], permuted weight [Np, Kq + S_pad])
     with Kq = roundup(K - S, 64).  With FQT7 and Kq % 128 == 0 the first three are in
-    sqmp_gemm_fqt7's tile-major layouts (SQMP_QA_TILED): codes [R, Kq/2], scales
-    [R/32, Kq/G, 32] (3-d marks the layout), xs [R, S_pad][:M], R = roundup(M, 256).
+    sqmp_gemm_fqt7's tile-major layouts (SQMP_QA_TILED / _TILED4 for FQT7_J = 2 / 4): codes
+    [R, Kq/2], scales [R/(16 J), Kq/G, 16 J] (3-d marks the layout), xs [R, S_pad][:M],
+    R = roundup(M, 128 J).
     Statistics reuse as quant_act_fp."""
     _require_gpu(x2, "quant_act")
     M, K = x2.shape
@@ -330,10 +334,12 @@ def quant_act_c4(x2: torch.Tensor, pw: PackedWeight, act_quant: str, n_bits: int
     ngq = (Kn + group_size - 1) // group_size
     dev = x2.device
     tiled = FQT7 and Kq % 128 == 0
+    tj = FQT7_J if FQT7_J in (2, 4) else 2
     if tiled:
-        codes = torch.empty((Mp, Kq // 2), dtype=torch.uint8, device=dev)
-        scales = torch.empty((Mp // 32, ngq, 32), dtype=x2.dtype, device=dev)
-        xs = torch.empty((Mp, max(pw.S_pad, 64)), dtype=x2.dtype, device=dev)[:M]
+        R = max(128 * tj, (M + 128 * tj - 1) // (128 * tj) * (128 * tj))
+        codes = torch.empty((R, Kq // 2), dtype=torch.uint8, device=dev)
+        scales = torch.empty((R // (16 * tj), ngq, 16 * tj), dtype=x2.dtype, device=dev)
+        xs = torch.empty((R, max(pw.S_pad, 64)), dtype=x2.dtype, device=dev)[:M]
     else:
         codes = torch.empty((Mp, Kq // 2), dtype=torch.uint8, device=dev)[:M]
         scales = torch.empty((ngq, Mp), dtype=x2.dtype, device=dev)
@@ -342,7 +348,7 @@ def quant_act_c4(x2: torch.Tensor, pw: PackedWeight, act_quant: str, n_bits: int
     nb = _ws_bytes(M, K, pw.Kp)
     stream = torch.cuda.current_stream(dev).cuda_stream
     e = _act_ws(dev, stream, K, pw.Kp, nb)
-    flags = _lib.QA_CLEAN_WS | (_lib.QA_TILED if tiled else 0)
+    flags = _lib.QA_CLEAN_WS | ((_lib.QA_TILED4 if tj == 4 else _lib.QA_TILED) if tiled else 0)
     src = x2 if stats_of is None else stats_of
     skey = (src.data_ptr(), tuple(src.shape), src.dtype, src._version, pw.sal_key, act_quant,
             M, K)
@@ -377,13 +383,11 @@ def gemm_fqt(codes: torch.Tensor, scales: torch.Tensor, xs: torch.Tensor, wp: to
     M = xs.shape[0]
     y = torch.empty((M, pw.N), dtype=pw.dtype, device=codes.device)
     Kq = codes.shape[1] * 2
-    if scales.dim() == 3:   # tile-major (SQMP_QA_TILED)
-        args = (_p(codes), _p(scales), _p(xs), _p(wp), _p(bias), _p(y), _dtype_code(pw.dtype), M,
-                pw.N, Kq, pw.S_pad, group_size, scales.shape[1])
-        if colmax is None:
-            check(load().sqmp_gemm_fqt7(*args, _stream(codes)), "gemm_fqt7")
-        else:
-            check(load().sqmp_gemm_fqt7_colmax(*args, _p(colmax), _stream(codes)), "gemm_fqt7")
+    if scales.dim() == 3:   # tile-major (SQMP_QA_TILED: 32-row blocks, TILED4: 64-row)
+        check(load().sqmp_gemm_fqt7j(_p(codes), _p(scales), _p(xs), _p(wp), _p(bias), _p(y),
+                                     _dtype_code(pw.dtype), M, pw.N, Kq, pw.S_pad, group_size,
+                                     scales.shape[1], scales.shape[2] // 16, _p(colmax),
+                                     _stream(codes)), "gemm_fqt7")
         return y
     if colmax is not None:
         raise ValueError("gemm_fqt: fused column statistics need the tile-major operands")

@@ -14,8 +14,9 @@ weight permutation, sqmp_gemm_fqt / sqmp_gemm_fqt7) against the ORACLE
     fqt7): sampled rows of y against the fp64 product of the PyTorch-CPU restatement's q_x
     (oracle/torch_cpu.py, batch-wide sort over all 16384 rows) and W_hat.
 
-Both operand layouts: row-major (sqmp_gemm_fqt on fq6's structure) and tile-major
-(SQMP_QA_TILED + sqmp_gemm_fqt7, untiled here before the same checks).
+Every operand layout: row-major (sqmp_gemm_fqt on fq6's structure) and tile-major with 32-
+or 64-row blocks (SQMP_QA_TILED / SQMP_QA_TILED4 + sqmp_gemm_fqt7j with J = 2 / 4, untiled
+here before the same checks).
 """
 import numpy as np
 import pytest
@@ -71,21 +72,23 @@ def decode_c4(codes, scales, Kq, G, dt):
 
 
 def untile_c4(codes_t, scales_t, xs_t, M, Kq, S_pad):
-    """The tile-major operands (sqmp_pack_fq7 layouts, J = 2) -> row-major codes [M, Kq/2],
-    scales [ngq, R], xs [M, S_pad]."""
+    """The tile-major operands (sqmp_pack_fq7 layouts, J = 2 or 4 row tiles per 16 J-row
+    block) -> row-major codes [M, Kq/2], scales [ngq, R], xs [M, S_pad]."""
     R = codes_t.shape[0]
     KB = Kq // 64
-    w = codes_t.contiguous().view(torch.int32).reshape(R // 32, KB, 4, 16, 2, 2)  # nb kb q r j s
+    J = scales_t.shape[2] // 16
+    B = 16 * J
+    w = codes_t.contiguous().view(torch.int32).reshape(R // B, KB, 4, 16, J, 2)  # nb kb q r j s
     codes = w.permute(0, 4, 3, 1, 2, 5).reshape(R, KB * 8).contiguous().view(torch.uint8)[:M]
     ngq = scales_t.shape[1]
-    scales = scales_t.reshape(R // 32, ngq, 16, 2).permute(1, 0, 3, 2).reshape(ngq, R)
+    scales = scales_t.reshape(R // B, ngq, 16, J).permute(1, 0, 3, 2).reshape(ngq, R)
     xs = None
     if S_pad:
         W = xs_t.stride(0)
         flat = torch.as_strided(xs_t, (R * W,), (1,))[: R * S_pad]
-        t = flat.reshape(R // 32, S_pad // 64, 4, 16, 2, 2, 8)         # nb kd q r j s e
+        t = flat.reshape(R // B, S_pad // 64, 4, 16, J, 2, 8)          # nb kd q r j s e
         xs = torch.empty((R, S_pad), dtype=xs_t.dtype, device=xs_t.device)
-        v = xs.view(R // 32, 2, 16, S_pad // 64, 8, 8)                 # nb j r kd c e
+        v = xs.view(R // B, J, 16, S_pad // 64, 8, 8)                  # nb j r kd c e
         for q in range(4):
             for sl in range(2):
                 c = 4 * (q & 1) + 2 * sl + (q >> 1)
@@ -141,7 +144,7 @@ def same_values(a, b):
     return bool(ok.all())
 
 
-@pytest.mark.parametrize("tiled", [False, True], ids=["rowmajor", "tiled"])
+@pytest.mark.parametrize("tiled", [0, 2, 4], ids=["rowmajor", "tiled", "tiled4"])
 @pytest.mark.parametrize("M,K,N,Gs,p,dt,aq", CASES)
 def test_fqt_operands_exact_and_y(M, K, N, Gs, p, dt, aq, tiled):
     """Column for column against the ORACLE (oracle/fake_quant_oracle.py, pinned to the
@@ -158,13 +161,15 @@ def test_fqt_operands_exact_and_y(M, K, N, Gs, p, dt, aq, tiled):
     if tiled and Kq % 128:
         pytest.skip("tile-major operands need Kq % 128 == 0 (the dispatcher then takes "
                     "the row-major layout, covered by the rowmajor case)")
-    fqt7 = ops.FQT7
-    ops.FQT7 = tiled
+    fqt7, fqt7_j = ops.FQT7, ops.FQT7_J
+    ops.FQT7, ops.FQT7_J = tiled > 0, tiled or 2
     try:
         codes, scales, xs, wp = ops.quant_act_c4(x, pw, aq, 4, Gs)
     finally:
-        ops.FQT7 = fqt7
-    assert (scales.dim() == 3) == tiled
+        ops.FQT7, ops.FQT7_J = fqt7, fqt7_j
+    assert (scales.dim() == 3) == (tiled > 0)
+    if tiled:
+        assert scales.shape[2] == 16 * tiled
     y = ops.gemm_fqt(codes, scales, xs, wp, pw, lin.bias, Gs)
     if tiled:
         codes, scales, xs = untile_c4(codes, scales, xs, M, Kq, pw.S_pad)

@@ -1,6 +1,10 @@
 """In-process A/B of the activation-order GEMM's variants at config 2 (sqmp_gemm_fqt7,
 SQMP_FQT7_OPT read per launch): interleaved rounds, HIP events, y bit-identical across
-variants.  python tools/ab_fqt7.py [variants, comma-separated] [rounds] [iters]"""
+variants.  python tools/ab_fqt7.py [variants, "+"- or comma-separated] [rounds] [iters] [ENV]
+ENV (default SQMP_FQT7_OPT) names the per-launch variable; SQMP_FQ7_DIAG selects the timing
+diagnostics of a SQMP_DIAG=1 build (wrong results by design: no equality check then).  A
+variant "J4:3" runs the 64-row-block operands (ops.FQT7_J = 4) with value 3; "P..." times the
+prepass (quant_act_c4) of that variant instead of the GEMM."""
 import os
 import sys
 
@@ -11,33 +15,63 @@ import torch  # noqa: E402
 import bench  # noqa: E402
 from smoothquant import ops  # noqa: E402
 
-variants = (sys.argv[1] if len(sys.argv) > 1 else "0,1,2,3,4,5").split(",")
+variants = (sys.argv[1] if len(sys.argv) > 1 else "0+1+2+3+4+5").replace(",", "+").split("+")
 rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 4
 iters = int(sys.argv[3]) if len(sys.argv) > 3 else 200
+ENV = sys.argv[4] if len(sys.argv) > 4 else "SQMP_FQT7_OPT"
 dev = torch.device("cuda")
 q, x, lin = bench.make_layer(dev, "per_group", seed=1)
 pw = q.packed()
-c4 = ops.quant_act_c4(x, pw, "per_group", 4, bench.G)
 stream = torch.cuda.current_stream(dev)
-run = lambda: ops.gemm_fqt(*c4, pw, lin.bias, bench.G)  # noqa: E731
+
+
+def parse(v):
+    pre = v.startswith("P")
+    v = v[1:] if pre else v
+    j, val = (int(v[1:v.index(":")]), v[v.index(":") + 1:]) if v.startswith("J") else (2, v)
+    return pre, j, val
+
+
+ops_c4 = {}
+for v in variants:
+    _, j, _ = parse(v)
+    if j not in ops_c4:
+        ops.FQT7_J = j
+        ops_c4[j] = ops.quant_act_c4(x, pw, "per_group", 4, bench.G)
+
+
+def runner(v):
+    pre, j, _ = parse(v)
+    if pre:
+        def f():
+            ops.FQT7_J = j
+            return ops.quant_act_c4(x, pw, "per_group", 4, bench.G)[0]
+        return f
+    return lambda: ops.gemm_fqt(*ops_c4[j], pw, lin.bias, bench.G)
+
+
 ref = None
 for v in variants:
-    os.environ["SQMP_FQT7_OPT"] = v
+    os.environ[ENV] = parse(v)[2]
+    run = runner(v)
     y = run()
+    if parse(v)[0]:
+        continue
     torch.cuda.synchronize()
     if ref is None:
         ref = y.clone()
-    assert torch.equal(y.view(torch.int16), ref.view(torch.int16)), f"variant {v} changed y"
+    assert ENV != "SQMP_FQT7_OPT" or torch.equal(y.view(torch.int16), ref.view(torch.int16)), f"variant {v} changed y"
 t_end = __import__("time").perf_counter() + 2.0
 while __import__("time").perf_counter() < t_end:
     for _ in range(10):
-        run()
+        runner(variants[0])()
     torch.cuda.synchronize()
 res = {v: [] for v in variants}
 flops = 2.0 * bench.M * bench.N * bench.K
 for r in range(rounds):
     for v in variants:
-        os.environ["SQMP_FQT7_OPT"] = v
+        os.environ[ENV] = parse(v)[2]
+        run = runner(v)
         for _ in range(10):
             run()
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -49,5 +83,5 @@ for r in range(rounds):
         res[v].append(a.elapsed_time(b) / iters * 1e3)
 for v in variants:
     t = sorted(res[v])
-    print(f"OPT={v}: median {t[len(t) // 2]:7.1f} us  min {t[0]:7.1f} us  "
+    print(f"{ENV}={v}: median {t[len(t) // 2]:7.1f} us  min {t[0]:7.1f} us  "
           f"({flops / t[len(t) // 2] / 1e6:7.1f} TFLOP/s)  all {[round(u, 1) for u in res[v]]}")
