@@ -26,9 +26,11 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I", INCLUDE,
           "-Wno-unused-result"]
 # SQMP_DIAG=1: also instantiate the timing-diagnostic kernel variants (wrong results by
-# design; never in the product build)
+# design; never in the product build), into libsqmp_w4a4_diag.so (loaded by SQMP_DIAG_LIB=1)
 if os.environ.get("SQMP_DIAG") == "1":
     CFLAGS.append("-DSQMP_DIAG_BUILD")
+    OBJ = os.path.join(CSRC, "_obj_diag")
+    LIB = os.path.join(HERE, "smoothquant", "libsqmp_w4a4_diag.so")
 
 
 def _headers():

@@ -112,7 +112,7 @@ __host__ __device__ inline int brev3(int c) { return ((c & 1) << 2) | (c & 2) | 
 // register loads after the prologue, 2 no A DMA after the prologue, 3 no int4 decode, 4 no
 // per-stage barrier, 5 half the A fragment LDS reads (each fragment used for two blocks), 6 the
 // A pieces written by ds_write_b128 from registers instead of LDS-DMA, 7 the A DMA from two
-// L2-hot stages only
+// L2-hot stages only, 8 the A loads into a scratch register (VMEM issue without the LDS write)
 // J = 16-row weight tiles per wave: tile TM x TN with TN = 8 * 16 J (J = 4: 128 x 512;
 // J = 2: 256 x 256, fq6's decode-optimal shape -- a decoded fragment feeds TM / 16 MFMAs)
 // TR (sqmp_gemm_fqt on the tile-major activation operands): A = the permuted weight wp,
@@ -180,7 +180,12 @@ __global__ __launch_bounds__(512, 1) void gemm_fq7_kernel(
 #pragma unroll
         for (int i = 0; i < NA; ++i) {
           unsigned char* dst = slot + (i * 8 + wave + 4 * o) * 1024;
-          if (DIAG == 6 && kt >= PA) {  // the same LDS bytes written by ds_write_b128, no VMEM
+          if (DIAG == 8 && kt >= PA) {  // the same VMEM loads into a scratch register, no LDS write
+            u32x4 sink;
+            asm volatile("buffer_load_dwordx4 %0, %1, %2, %3 offen" : "=v"(sink)
+                         : "v"(a_off[o][i]), "s"(rA), "s"(so));
+            asm volatile("" ::"v"(sink));
+          } else if (DIAG == 6 && kt >= PA) {  // the same LDS bytes written by ds_write_b128, no VMEM
             const u32x4 v = {a_off[o][i], so, 0u, 0u};
             const uint32_t la = (uint32_t)(size_t)(__attribute__((address_space(3))) unsigned char*)dst + lane * 16;
             asm volatile("ds_write_b128 %0, %1" ::"v"(la), "v"(v) : "memory");
@@ -615,7 +620,8 @@ static int dispatch_tr(const void* wp, const void* codes_t, const void* scale_t,
       case 4: SQMP_TRD(4); break;
       case 5: SQMP_TRD(5); break;
       case 6: SQMP_TRD(6); break;
-      default: SQMP_TRD(7); break;
+      case 7: SQMP_TRD(7); break;
+      default: SQMP_TRD(8); break;
     }
     SQMP_LAUNCH_CHECK();
     return SQMP_OK;

@@ -10,7 +10,12 @@ import ctypes
 import os
 import threading
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libsqmp_w4a4.so")
+# SQMP_DIAG_LIB=1 loads the timing-diagnostics build (libsqmp_w4a4_diag.so, made by
+# `SQMP_DIAG=1 python build_ext.py`: extra kernel variants selected by SQMP_*_DIAG, wrong
+# results by design) -- tools only, never the product path
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                        "libsqmp_w4a4_diag.so" if os.environ.get("SQMP_DIAG_LIB") == "1"
+                        else "libsqmp_w4a4.so")
 
 SQMP_OK, SQMP_EINVAL, SQMP_EUNSUPPORTED, SQMP_EHIP, SQMP_EWORKSPACE = 0, -1, -2, -3, -4
 
