@@ -611,7 +611,9 @@ static int launch_rank_table(const uint32_t* key, const int32_t* nonsal, int L,
   // override, tuning only, read per launch)
   const char* te = getenv("SQMP_RT_TPO");
   const char* re = getenv("SQMP_RT_R");
-  int tpo = L <= 2048 ? 16 : 32, r = 1;
+  // two owners per lane group above 8192 entries (half the workgroups staging the whole key
+  // list: Llama down_proj's 10458-column prepass 61 -> 55.6 us; profiles/r03_prepass_sweep.txt)
+  int tpo = L <= 2048 ? 16 : 32, r = L > 8192 ? 2 : 1;
   if (te && (atoi(te) == 8 || atoi(te) == 16 || atoi(te) == 32)) tpo = atoi(te);
   if (re && (atoi(re) == 1 || atoi(re) == 2 || atoi(re) == 4)) r = atoi(re);
   const int grid = cdiv((long)L * tpo, 256L * r);

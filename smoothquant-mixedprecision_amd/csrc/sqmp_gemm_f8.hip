@@ -297,7 +297,7 @@ __global__ __launch_bounds__(512, 1) void gemm_f8v2_kernel(
     const float* __restrict__ ws32, const typename DT::T* __restrict__ wsal,
     const typename DT::T* __restrict__ bias, typename DT::T* __restrict__ Y, int M, int N,
     int Kp, int S_pad, int Gw, int ngw, int tiles_m, int tiles_n, int group_m,
-    uint32_t* __restrict__ colmax) {
+    uint32_t* __restrict__ colmax, int nt) {
   typedef typename DT::T T;
   __shared__ __attribute__((aligned(16))) unsigned char lds[V2_NSLOT * V2_SLOT];
 
@@ -518,7 +518,13 @@ __global__ __launch_bounds__(512, 1) void gemm_f8v2_kernel(
     for (int k = 0; k < 16; ++k) {
       const int ml = 16 * k + (tid >> 5);
       const u32x4 val = *(const u32x4*)(lds + ml * 512 + ((c ^ (ml & 31)) << 4));
-      if (m0 + ml < M) *(u32x4*)(Y + (size_t)(m0 + ml) * N + n0 + c * 8) = val;
+      if (m0 + ml < M) {
+        u32x4* dst = (u32x4*)(Y + (size_t)(m0 + ml) * N + n0 + c * 8);
+        if (nt)  // streaming stores of a large output (nt_output)
+          store16_nt(dst, val);
+        else
+          *dst = val;
+      }
     }
     return;
   }
@@ -626,11 +632,12 @@ static int gemm_f8_impl(const void* a8, const float* ascale, const void* xs, con
     const char* e = getenv("SQMP_GROUP_M");
     return e && atoi(e) > 0 ? atoi(e) : 4;
   }();
+  const bool nt = nt_output((size_t)M * N * (dtype == SQMP_F32 ? 4 : 2));
 #define SQMP_F8L(DTT)                                                                        \
   if (v2) gemm_f8v2_kernel<DTT><<<grid, block, 0, s>>>(                                      \
       (const unsigned char*)a8, ascale, (const DTT::T*)xs, (const unsigned char*)w8, ws32,   \
       (const DTT::T*)wsal, (const DTT::T*)bias, (DTT::T*)y, M, N, Kp, S_pad, Gw, ngw, tiles_m, \
-      tiles_n, group_m, colmax);                                                             \
+      tiles_n, group_m, colmax, nt ? 1 : 0);                                                 \
   else gemm_f8_kernel<DTT><<<grid, block, 0, s>>>(                                           \
       (const unsigned char*)a8, ascale, (const DTT::T*)xs, (const unsigned char*)w8, ws32,   \
       (const DTT::T*)wsal, (const DTT::T*)bias, (DTT::T*)y, M, N, Kp, S_pad, Gw, ngw, tiles_m, \

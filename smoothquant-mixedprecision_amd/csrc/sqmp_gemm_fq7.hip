@@ -130,7 +130,7 @@ __global__ __launch_bounds__(512, 1) void gemm_fq7_kernel(
     const typename DT::T* __restrict__ St, const typename DT::T* __restrict__ Salt,
     const typename DT::T* __restrict__ bias, typename DT::T* __restrict__ Y, int M, int N,
     int Kp, int S_pad, int Gw, int ngw, int tiles_m, int tiles_n, int group_m,
-    uint32_t* __restrict__ colmax) {
+    uint32_t* __restrict__ colmax, int nt) {
   typedef typename DT::T T;
   constexpr int I = TM / 16;            // 16 x 16 tiles per wave: TM rows x 16 J weight rows
   constexpr int TN = 128 * J, WR = 16 * J;  // tile width, weight rows per wave
@@ -406,7 +406,13 @@ __global__ __launch_bounds__(512, 1) void gemm_fq7_kernel(
       const int nl = k / CPR, c = k % CPR;
       const int gn = n0 + nl, gm = m0 + c * 8;
       if (gn < N && gm < M)  // M % 8 == 0 (launcher)
-        *(u32x4*)(Y + (size_t)gn * M + gm) = *(const u32x4*)(lds + nl * RS + c * 16);
+      {
+        const u32x4 v = *(const u32x4*)(lds + nl * RS + c * 16);
+        if (nt)  // streaming stores of a large output (nt_output)
+          store16_nt(Y + (size_t)gn * M + gm, v);
+        else
+          *(u32x4*)(Y + (size_t)gn * M + gm) = v;
+      }
     }
     return;
   }
@@ -456,7 +462,13 @@ __global__ __launch_bounds__(512, 1) void gemm_fq7_kernel(
     const int ml = RPP * k + tid / CPR;
     const int gm = m0 + ml;
     const u32x4 val = *(const u32x4*)(lds + ml * (TN * 2) + ((c ^ (ml & 15)) << 4));
-    if (gm < M && cok) *(u32x4*)(Y + (size_t)gm * N + n0 + c * 8) = val;
+    if (gm < M && cok) {
+      u32x4* dst = (u32x4*)(Y + (size_t)gm * N + n0 + c * 8);
+      if (nt)  // streaming stores of a large output (nt_output)
+        store16_nt(dst, val);
+      else
+        *dst = val;
+    }
   }
 }
 
@@ -546,7 +558,8 @@ static int launch_k(const void* a, const void* bt, const void* st, const void* s
   const int tiles_m = cdiv(M, TM), tiles_n = cdiv(N, 128 * J);
   gemm_fq7_kernel<DT, GB, TM, J, DIAG><<<dim3(tiles_m * tiles_n), dim3(512), 0, s>>>(
       (const T*)a, (const uint32_t*)bt, (const T*)st, (const T*)salt, (const T*)bias, (T*)y, M,
-      N, Kp, S_pad, Gw, ngw, tiles_m, tiles_n, group_m_env(), colmax);
+      N, Kp, S_pad, Gw, ngw, tiles_m, tiles_n, group_m_env(), colmax,
+      nt_output((size_t)M * N * sizeof(T)) ? 1 : 0);
   SQMP_LAUNCH_CHECK();
   return SQMP_OK;
 }
@@ -606,12 +619,13 @@ static int dispatch_tr(const void* wp, const void* codes_t, const void* scale_t,
 #define SQMP_TR(O)                                                                              \
   gemm_fq7_kernel<DT, 1, TM, J, 0, true, O><<<dim3(tiles_m * tiles_n), dim3(512), 0, s>>>(      \
       (const T*)wp, (const uint32_t*)codes_t, (const T*)scale_t, (const T*)sal_t, (const T*)bias, \
-      (T*)y, N, M, Kq, S_pad, G, ngq, tiles_m, tiles_n, group_m_tr_env(), colmax)
+      (T*)y, N, M, Kq, S_pad, G, ngq, tiles_m, tiles_n, group_m_tr_env(), colmax, nt)
+  const int nt = nt_output((size_t)M * N * sizeof(T)) ? 1 : 0;
 #ifdef SQMP_DIAG_BUILD
 #define SQMP_TRD(D)                                                                             \
   gemm_fq7_kernel<DT, 1, TM, 2, D, true, 3><<<dim3(tiles_m * tiles_n), dim3(512), 0, s>>>(      \
       (const T*)wp, (const uint32_t*)codes_t, (const T*)scale_t, (const T*)sal_t, (const T*)bias, \
-      (T*)y, N, M, Kq, S_pad, G, ngq, tiles_m, tiles_n, group_m_tr_env(), colmax)
+      (T*)y, N, M, Kq, S_pad, G, ngq, tiles_m, tiles_n, group_m_tr_env(), colmax, nt)
   if (std::is_same<DT, F16>::value && J == 2 && diag_env() > 0) {
     switch (diag_env()) {
       case 1: SQMP_TRD(1); break;

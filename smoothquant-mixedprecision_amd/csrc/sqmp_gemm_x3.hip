@@ -89,7 +89,8 @@ template <bool COLMAX, int WN, bool H = false, int BN = 128, int BK = 32>
 __global__ __launch_bounds__(128 * WN, 4 / WN) void gemm_x3_kernel(
     const float* __restrict__ A, const uint16_t* __restrict__ B3, const float* __restrict__ bias,
     float* __restrict__ Y, int M, int N, int L, int Np, int tiles_m, int tiles_n,
-    uint32_t* __restrict__ colmax, const int* __restrict__ aexp, const int* __restrict__ bexp) {
+    uint32_t* __restrict__ colmax, const int* __restrict__ aexp, const int* __restrict__ bexp,
+    int nt) {
   constexpr int NPL = H ? 2 : 3;  // pieces per operand
   // A planes (NPL x 128 rows) then B planes (NPL x BN rows), rows of BK 16-bit values
   constexpr int APL = X3_BM * BK * 2;  // one A plane
@@ -233,7 +234,10 @@ __global__ __launch_bounds__(128 * WN, 4 / WN) void gemm_x3_kernel(
         v[r] = (H ? __builtin_ldexpf(acc[i][j][r], -(aei + be[r])) : acc[i][j][r]) + bv[r];
       if (gm < M) {
         if (nb + 4 <= N && (N & 3) == 0) {
-          *(f32x4*)(Y + (size_t)gm * N + nb) = v;
+          if (nt)  // streaming stores of a large output (nt_output)
+            store16_nt(Y + (size_t)gm * N + nb, __builtin_bit_cast(u32x4, v));
+          else
+            *(f32x4*)(Y + (size_t)gm * N + nb) = v;
         } else {
 #pragma unroll
           for (int r = 0; r < 4; ++r)
@@ -346,11 +350,12 @@ extern "C" int sqmp_gemm_h2(const float* a, const int* aexp, const void* b2, con
     return !e || atoi(e) != 0;
   }();
   const bool k64 = bk64 && L % 64 == 0;
+  const int nt = nt_output((size_t)M * N * sizeof(float)) ? 1 : 0;
 #define SQMP_H2(CM, WN, BNV, TN)                                                                 \
   (k64 ? gemm_x3_kernel<CM, WN, true, BNV, 64><<<tiles_m * TN, 128 * WN, 0, (hipStream_t)stream>>>( \
-             a, (const uint16_t*)b2, bias, y, M, N, L, Np, tiles_m, TN, colmax, aexp, bexp)      \
+             a, (const uint16_t*)b2, bias, y, M, N, L, Np, tiles_m, TN, colmax, aexp, bexp, nt) \
        : gemm_x3_kernel<CM, WN, true, BNV, 32><<<tiles_m * TN, 128 * WN, 0, (hipStream_t)stream>>>( \
-             a, (const uint16_t*)b2, bias, y, M, N, L, Np, tiles_m, TN, colmax, aexp, bexp))
+             a, (const uint16_t*)b2, bias, y, M, N, L, Np, tiles_m, TN, colmax, aexp, bexp, nt))
   if (colmax) {
     if (wide) SQMP_H2(true, 4, 256, tiles_n2); else if (small) SQMP_H2(true, 4, 128, tiles_n); else SQMP_H2(true, 2, 128, tiles_n);
   } else {

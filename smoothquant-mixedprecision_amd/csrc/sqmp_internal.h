@@ -1,8 +1,22 @@
 // Internal (non-ABI) launchers shared between the translation units of libsqmp_w4a4.so.
 #pragma once
+#include <stdlib.h>
+
 #include "sqmp_common.h"
 
 namespace sqmp {
+
+// Whether a GEMM stores its output with non-temporal (streaming) stores.  An output larger
+// than a quarter of the 256-MiB Infinity Cache left dirty there is written back to HBM during
+// the kernels that follow -- at config 2 the next forward's prepass, which then shares HBM
+// with 134 MB of write-back.  Same-box step A/B (GEMM time unchanged;
+// profiles/r03_step_ab_nt.txt): per_group 523.1 -> 502.3 us, per_token 359.9 -> 351.2 us,
+// fp32 2068 -> 2044 us.  Smaller outputs stay cached for their consumer.
+// SQMP_NT_STORES = 0 / 1 forces it off / on (read per launch).
+inline bool nt_output(size_t bytes) {
+  if (const char* e = getenv("SQMP_NT_STORES")) return atoi(e) != 0;
+  return bytes >= ((size_t)64 << 20);
+}
 
 // cmax[c] = bits(max_r |x[r][c]|) over a contiguous D matrix [R][C] (fp32 bits of the
 // D value; non-negative floats order like their bit patterns).  Zeroes cmax first.

@@ -122,6 +122,12 @@ __device__ inline void unpack_i8(uint32_t w, uint32_t& lo, uint32_t& hi) {
   hi = (((w >> 4) & 0x0F0F0F0Fu) + 0x78787878u) ^ 0x80808080u;
 }
 
+// 16-B non-temporal (streaming) global store.  From inline asm: hipcc merges the two arms of
+// `if (nt) __builtin_nontemporal_store(v, p); else *p = v;` into one plain store.
+__device__ inline void store16_nt(void* p, const u32x4& v) {
+  asm volatile("global_store_dwordx4 %0, %1, off nt" ::"v"(p), "v"(v) : "memory");
+}
+
 __device__ inline void glds16(const void* src, unsigned char* lds_dst) {
   __builtin_amdgcn_global_load_lds(src, (lds_void_ptr)lds_dst, 16, 0, 0);
 }

@@ -68,8 +68,10 @@ static void colmax_launch(const void* x, int R, int C, uint32_t* cmax, hipStream
   const bool vec_ok = ((C * sizeof(T)) % 16 == 0) && (((uintptr_t)x) % 16 == 0);
   int rows_per_block = 128;
   const int cblocks_v = cdiv(C, 64 * VEC);
-  // keep >= ~1024 blocks in flight when R is large, fewer row passes when R is small
-  while (rows_per_block > 16 && (long)cblocks_v * cdiv(R, rows_per_block) < 1024)
+  // keep >= ~1024 blocks in flight when R is large, fewer row passes when R is small (at
+  // least 32 rows per block: 2048-row Llama inputs 25.7 -> 24.1 us for the whole prepass,
+  // fewer atomics per column; profiles/r03_prepass_sweep.txt)
+  while (rows_per_block > 32 && (long)cblocks_v * cdiv(R, rows_per_block) < 1024)
     rows_per_block >>= 1;
   if (const char* e = getenv("SQMP_COLMAX_RPB")) rows_per_block = atoi(e);
   dim3 block(256);
