@@ -36,6 +36,7 @@ The timed region is still exactly K steps between barriers.
 from __future__ import annotations
 
 import argparse
+import glob
 import json
 import os
 import statistics
@@ -454,11 +455,14 @@ def main(argv=None):
     prepass_bytes = reads * xbytes + wbytes
 
     traffic = None
-    prof = os.path.join(ROOT, "profiles", "r02_pmc_gemm_f8v2_per_token.json" if kdt == "f8"
-                        else "r02_pmc_gemm_h2_fp32.json" if fp32
-                        else "r02_pmc_gemm_fqt7_per_group.json" if use_fqt and "fqt7" in kname
-                        else "r02_pmc_gemm_fqt_per_group.json" if use_fqt
-                        else f"r02_pmc_gemm_fq6_{args.act}.json")
+    pname = ("pmc_gemm_f8v2_per_token.json" if kdt == "f8"
+             else "pmc_gemm_h2_fp32.json" if fp32
+             else "pmc_gemm_fqt7_per_group.json" if use_fqt and "fqt7" in kname
+             else "pmc_gemm_fqt_per_group.json" if use_fqt
+             else f"pmc_gemm_fq6_{args.act}.json")
+    # the newest committed counter profile of this kernel (profiles/r0N[_final]_pmc_*.json)
+    cands = sorted(glob.glob(os.path.join(ROOT, "profiles", "r0*_" + pname)))
+    prof = cands[-1] if cands else ""
     if os.path.exists(prof):
         try:
             with open(prof) as f:
@@ -526,6 +530,10 @@ def main(argv=None):
             "algorithmic_bytes": prepass_bytes,
             "GB_per_s": round(prepass_bytes / (quant_ms * 1e-3) / 1e9, 1),
             "hbm_peak_GB_per_s": HBM_PEAK_GBS,
+            "in_step_ms": round(ms_per_step - gemm_ms, 4),
+            "note": "avg_ms: the prepass kernels timed back to back on their own (x stays in the "
+                    "Infinity Cache); in_step_ms = step time - GEMM time (the prepass inside the "
+                    "forward, plus launch gaps)",
         },
     }
     if not fp32 and not args.no_layer:
