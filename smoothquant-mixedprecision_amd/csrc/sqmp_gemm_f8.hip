@@ -290,7 +290,10 @@ __device__ inline i32x8b cat8(const u32x4& a, const u32x4& b) {
 }
 }  // namespace
 
-template <class DT>
+// OPT (A/B knob SQMP_F8_OPT, read per launch): bit 0 -- waves 4-7 at s_setprio 1 through the
+// K loop; bit 1 -- loader split: waves 0-3 issue every DMA piece of a stage (their own and
+// those of waves 4-7), waves 4-7 only wait, read and multiply
+template <class DT, int OPT = 0>
 __global__ __launch_bounds__(512, 1) void gemm_f8v2_kernel(
     const unsigned char* __restrict__ A8, const float* __restrict__ ascale,
     const typename DT::T* __restrict__ XS, const unsigned char* __restrict__ W8,
@@ -311,12 +314,9 @@ __global__ __launch_bounds__(512, 1) void gemm_f8v2_kernel(
   const int nk8 = Kp / 128, nkt = nk8 + S_pad / 64;
   const int Np = pad_n(N);
 
-  // ---- DMA geometry: piece p = 4 wave + j moves rows 8p .. 8p + 7 of a 256 x 128 B image;
+  // ---- DMA geometry: piece p = 4 w + j moves rows 8p .. 8p + 7 of a 256 x 128 B image;
   // lane L writes row 8p + (L >> 3), physical chunk L & 7 = logical chunk (L & 7) ^ v2_sw
   // (offsets recomputed per stage: a few VALU ops instead of 12 live VGPRs)
-  const int drow0 = 32 * wave + (lane >> 3);
-  auto drow = [&](int j) { return drow0 + 8 * j; };
-  auto dchunk16 = [&](int j) { return (uint32_t)(((lane & 7) ^ v2_sw(drow(j))) << 4); };
   const i32x4b rA = rsrc_of(A8 + (size_t)m0 * Kp, 0xFFFFFFFFu);
   const i32x4b rW = rsrc_of(W8 + (size_t)n0 * Kp, 0xFFFFFFFFu);
   const i32x4b rX = rsrc_of(XS + (size_t)m0 * S_pad, 0xFFFFFFFFu);
@@ -324,30 +324,42 @@ __global__ __launch_bounds__(512, 1) void gemm_f8v2_kernel(
   const i32x4b rS = rsrc_of(ws32 + n0, 0xFFFFFFFFu);
   const i32x4b rR = rsrc_of(ascale + m0, (uint32_t)(M - m0) * 4u);  // rows >= M read 0
 
+  constexpr bool SPLIT = (OPT & 2) != 0;
   auto issue = [&](int kt) {
+    if (SPLIT && wave >= 4) return;
     unsigned char* slot = lds + (kt & 1) * V2_SLOT;
-    if (kt < nk8) {
-      const uint32_t so = (uint32_t)kt * 128;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const uint32_t v = (uint32_t)drow(j) * Kp + dchunk16(j);
-        dma16(rA, v, so, slot + V2_A + (4 * wave + j) * 1024);
-        dma16(rW, v, so, slot + V2_B + (4 * wave + j) * 1024);
+    for (int o = 0; o < (SPLIT ? 2 : 1); ++o) {
+      const int w = wave + 4 * o;  // the (virtual) wave whose pieces these are
+      const int r0 = 32 * w + (lane >> 3);
+      auto row = [&](int j) { return r0 + 8 * j; };
+      auto ch = [&](int j) { return (uint32_t)(((lane & 7) ^ v2_sw(row(j))) << 4); };
+      if (kt < nk8) {
+        const uint32_t so = (uint32_t)kt * 128;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint32_t v = (uint32_t)row(j) * Kp + ch(j);
+          dma16(rA, v, so, slot + V2_A + (4 * w + j) * 1024);
+          dma16(rW, v, so, slot + V2_B + (4 * w + j) * 1024);
+        }
+      } else {
+        const uint32_t so = (uint32_t)(kt - nk8) * 64 * sizeof(T);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint32_t c = ch(j);
+          dma16(rX, (uint32_t)row(j) * S_pad * sizeof(T) + c, so, slot + V2_A + (4 * w + j) * 1024);
+          dma16(rL, (uint32_t)min(n0 + row(j), N - 1) * S_pad * sizeof(T) + c, so,
+                slot + V2_B + (4 * w + j) * 1024);
+        }
       }
-      if (wave == 0) {
+    }
+    if (wave == 0) {
+      if (kt < nk8) {
         const int g = min((kt * 128) / Gw, ngw - 1);
         dma16(rS, (uint32_t)lane * 16, (uint32_t)g * Np * 4, slot + V2_S);
+      } else if (kt == nk8) {
+        dma16(rR, (uint32_t)lane * 16, 0u, slot + V2_S);
       }
-    } else {
-      const uint32_t so = (uint32_t)(kt - nk8) * 64 * sizeof(T);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const uint32_t c = dchunk16(j);
-        dma16(rX, (uint32_t)drow(j) * S_pad * sizeof(T) + c, so, slot + V2_A + (4 * wave + j) * 1024);
-        dma16(rL, (uint32_t)min(n0 + drow(j), N - 1) * S_pad * sizeof(T) + c, so,
-              slot + V2_B + (4 * wave + j) * 1024);
-      }
-      if (wave == 0 && kt == nk8) dma16(rR, (uint32_t)lane * 16, 0u, slot + V2_S);
     }
   };
 
@@ -433,6 +445,7 @@ __global__ __launch_bounds__(512, 1) void gemm_f8v2_kernel(
     return (const unsigned char*)(lds + (kt & 1) * V2_SLOT);
   };
   issue(0);
+  if ((OPT & 1) && wave >= 4) __builtin_amdgcn_s_setprio(1);
   int kt = 0;
   for (; kt + 1 < nk8; ++kt) {
     const unsigned char* slot = top(kt);
@@ -633,11 +646,24 @@ static int gemm_f8_impl(const void* a8, const float* ascale, const void* xs, con
     return e && atoi(e) > 0 ? atoi(e) : 4;
   }();
   const bool nt = nt_output((size_t)M * N * (dtype == SQMP_F32 ? 4 : 2));
-#define SQMP_F8L(DTT)                                                                        \
-  if (v2) gemm_f8v2_kernel<DTT><<<grid, block, 0, s>>>(                                      \
+  // default 2 (loader split): same-box config-2 per_token step 334.5 -> 324.0 us; setprio for
+  // waves 4-7 +-0 (profiles/r03_ab_f8_opt.txt).  SQMP_F8_OPT: A/B knob, read per launch
+  const char* oe = getenv("SQMP_F8_OPT");
+  const int opt = oe ? atoi(oe) & 3 : 2;
+#define SQMP_F8V2(DTT, O)                                                                    \
+  gemm_f8v2_kernel<DTT, O><<<grid, block, 0, s>>>(                                           \
       (const unsigned char*)a8, ascale, (const DTT::T*)xs, (const unsigned char*)w8, ws32,   \
       (const DTT::T*)wsal, (const DTT::T*)bias, (DTT::T*)y, M, N, Kp, S_pad, Gw, ngw, tiles_m, \
-      tiles_n, group_m, colmax, nt ? 1 : 0);                                                 \
+      tiles_n, group_m, colmax, nt ? 1 : 0)
+#define SQMP_F8L(DTT)                                                                        \
+  if (v2) {                                                                                  \
+    switch (opt) {                                                                           \
+      case 1: SQMP_F8V2(DTT, 1); break;                                                      \
+      case 2: SQMP_F8V2(DTT, 2); break;                                                      \
+      case 3: SQMP_F8V2(DTT, 3); break;                                                      \
+      default: SQMP_F8V2(DTT, 0); break;                                                     \
+    }                                                                                        \
+  }                                                                                          \
   else gemm_f8_kernel<DTT><<<grid, block, 0, s>>>(                                           \
       (const unsigned char*)a8, ascale, (const DTT::T*)xs, (const unsigned char*)w8, ws32,   \
       (const DTT::T*)wsal, (const DTT::T*)bias, (DTT::T*)y, M, N, Kp, S_pad, Gw, ngw, tiles_m, \
@@ -648,6 +674,7 @@ static int gemm_f8_impl(const void* a8, const float* ascale, const void* xs, con
     SQMP_F8L(BF16);
   }
 #undef SQMP_F8L
+#undef SQMP_F8V2
   SQMP_LAUNCH_CHECK();
   return SQMP_OK;
 }
