@@ -532,6 +532,14 @@ static int group_m_tr_env() {  // read per launch (in-process A/B)
   return e && atoi(e) > 0 ? atoi(e) : 4;
 }
 
+// the packed-order launch's OPT variant (A/B knob, see gemm_fq7_kernel): default 3, same box
+// (profiles/r03_ab_fq7_opt.txt): 2048 x 4096 -> 4096 67.2 -> 65.6 us, -> 11008 182.4 -> 181.9,
+// 11008 -> 4096 164.5 -> 163.9, config 2 in packed order 461.2 -> 448.3
+static int opt_pk_env() {  // read per launch (in-process A/B)
+  const char* e = getenv("SQMP_FQ7_OPT");
+  return e ? atoi(e) : 3;
+}
+
 // the activation-order launch's OPT variant (A/B knob, see gemm_fq7_kernel)
 // default 3 (setprio + loader split): same box, interleaved rounds at config 2, 421.6 us
 // against 431.4 us for 0 (either bit alone +-0.3 %, PF = 3 +-0.1 %; tools/ab_fqt7.py,
@@ -556,10 +564,24 @@ static int launch_k(const void* a, const void* bt, const void* st, const void* s
                   uint32_t* colmax, hipStream_t s) {
   typedef typename DT::T T;
   const int tiles_m = cdiv(M, TM), tiles_n = cdiv(N, 128 * J);
-  gemm_fq7_kernel<DT, GB, TM, J, DIAG><<<dim3(tiles_m * tiles_n), dim3(512), 0, s>>>(
-      (const T*)a, (const uint32_t*)bt, (const T*)st, (const T*)salt, (const T*)bias, (T*)y, M,
-      N, Kp, S_pad, Gw, ngw, tiles_m, tiles_n, group_m_env(), colmax,
-      nt_output((size_t)M * N * sizeof(T)) ? 1 : 0);
+  const int nt = nt_output((size_t)M * N * sizeof(T)) ? 1 : 0;
+#define SQMP_PK(O)                                                                              \
+  gemm_fq7_kernel<DT, GB, TM, J, DIAG, false, O><<<dim3(tiles_m * tiles_n), dim3(512), 0, s>>>( \
+      (const T*)a, (const uint32_t*)bt, (const T*)st, (const T*)salt, (const T*)bias, (T*)y, M,  \
+      N, Kp, S_pad, Gw, ngw, tiles_m, tiles_n, group_m_env(), colmax, nt)
+  // OPT variants (setprio for waves 4-7, loader split) for the fp16 J = 2 kernels, the
+  // 2048-token Llama GEMMs (A/B knob SQMP_FQ7_OPT, read per launch)
+  if constexpr (std::is_same<DT, F16>::value && J == 2 && GB == 1 && DIAG == 0) {
+    switch (opt_pk_env()) {
+      case 1: SQMP_PK(1); break;
+      case 2: SQMP_PK(2); break;
+      case 3: SQMP_PK(3); break;
+      default: SQMP_PK(0); break;
+    }
+  } else {
+    SQMP_PK(0);
+  }
+#undef SQMP_PK
   SQMP_LAUNCH_CHECK();
   return SQMP_OK;
 }
