@@ -315,6 +315,16 @@ int sqmp_gemm_fqt7j(const void* codes_t, const void* scale_t, const void* sal_t,
                     const void* bias, void* y, int dtype, int M, int N, int Kq, int S_pad, int G,
                     int ngq, int J, uint32_t* colmax, void* stream);
 
+/* Sibling operand reuse: dst = the SQMP_OUT_FP operand of a layer whose weight shares the
+ * quantized input, the salient set and the act mode with the layer that produced src (q/k/v,
+ * gate/up), rebuilt by moving positions instead of quantizing again: dst[m][p] =
+ * map[p] >= 0 ? src[m][map[p]] : 0 for p < P, dst[m][P + j] = src[m][P + j] (the salient tail)
+ * -- bit-exact.  map[p] = the source layer's packed position of the destination layer's
+ * column at p (-1 at its salient / padding positions).  fp16 / bf16; P + S_pad <= 8192; src,
+ * dst 16-B aligned with rows of P + S_pad elements. */
+int sqmp_permute_act(const void* src, void* dst, const int32_t* map, int dtype, int M, int P,
+                     int S_pad, void* stream);
+
 /* The fp32 faithful GEMM on the f16 MFMA (the default for fp32 layers): every row of A and
  * of W is scaled by a power of two (exact) so that its maximum lies in [2^13, 2^14), each
  * scaled value v is split as v = h + l + r with h = f16(v), l = f16(v - h) (|r| <= 2^-22 |v|,

@@ -62,6 +62,7 @@ SIGNATURES = {
     "sqmp_perm_weight_c4": (_i, [_vp, _i, _i, _i, _i, _vp, _vp, _vp, _i, _i, _i, _i, _vp, _vp]),
     "sqmp_gemm_fqt": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _vp]),
     "sqmp_gemm_fqt7": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _vp]),
+    "sqmp_permute_act": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _vp]),
     "sqmp_gemm_fqt7j": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _vp,
                              _vp]),
     "sqmp_gemm_fqt7_colmax": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i,

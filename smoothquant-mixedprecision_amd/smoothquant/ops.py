@@ -93,6 +93,7 @@ class PackedWeight:
     ws32: Optional[torch.Tensor] = field(default=None)   # fp32 [ngw, Np] scales (f8 GEMM)
     fq7: Optional[tuple] = field(default=None)           # (codes_t, scale_t, sal_t, J) of gemm_fq7
     h2: Optional[tuple] = field(default=None)            # (f16 [2, Np, L], int32 [Np]) (gemm_h2)
+    sib_maps: Optional[dict] = field(default=None)       # sibling position maps (sqmp_permute_act)
 
     @property
     def gemm_operand(self):
@@ -241,6 +242,36 @@ def _act_ws(device, stream_ptr: int, K: int, Kp: int, nbytes: int, tag: str = "i
     return e
 
 
+# Sibling operand reuse (sqmp_permute_act): a layer that quantizes the same input as the
+# previous call, with the same salient set, act mode, bits and group size (q/k/v, gate/up),
+# gets the previous operand with its positions moved into its own packed order instead of a
+# table build + quantizer pass.  Operands up to SIB_MAX_BYTES are kept for this.
+SIB_REUSE = os.environ.get("SQMP_SIB_REUSE", "1") == "1"
+SIB_MAX_BYTES = 64 << 20
+
+
+def _sibling_map(src: PackedWeight, dst: PackedWeight) -> torch.Tensor:
+    """int32 [Kp]: the packed position in `src` of the column at each packed position of
+    `dst` (-1 at dst's salient / padding positions), cached on dst."""
+    key = src.codes.data_ptr()
+    if dst.sib_maps is None:
+        dst.sib_maps = {}
+    m = dst.sib_maps.get(key)
+    if m is None:
+        if src.posmap is None:
+            src.posmap = build_posmap(src.perm, src.K)
+        col = dst.amap.long()
+        m = torch.where(col >= 0, src.posmap.long()[col.clamp(min=0)], -1).to(torch.int32)
+        dst.sib_maps = {key: m}  # one source per layer (its sibling leader)
+    return m
+
+
+def _sibling_ok(src: PackedWeight, dst: PackedWeight) -> bool:
+    return (src is not dst and src.K == dst.K and src.S == dst.S and src.Kp == dst.Kp
+            and src.S_pad == dst.S_pad and src.sal_key == dst.sal_key and src.dtype == dst.dtype
+            and dst.dtype in (torch.float16, torch.bfloat16) and (dst.Kp + dst.S_pad) <= 8192)
+
+
 def quant_act_fp(x2: torch.Tensor, pw: PackedWeight, act_quant: str, n_bits: int,
                  group_size: int, stats_of: Optional[torch.Tensor] = None) -> torch.Tensor:
     """x [M, K] -> A [M, Kp + S_pad] in D: x_hat in packed order + exact salient tail.
@@ -264,6 +295,14 @@ def quant_act_fp(x2: torch.Tensor, pw: PackedWeight, act_quant: str, n_bits: int
         src = x2 if stats_of is None else stats_of
         skey = (src.data_ptr(), tuple(src.shape), src.dtype, src._version, pw.sal_key,
                 act_quant, M, K)
+        la = e.get("last_a")
+        if (SIB_REUSE and la is not None and la[0]() is src and la[1] == skey + (n_bits, group_size)
+                and la[2]() is not None and _sibling_ok(la[2](), pw)):
+            # a sibling of the layer that produced la[3] on this same input
+            check(lib.sqmp_permute_act(_p(la[3]), _p(a), _p(_sibling_map(la[2](), pw)),
+                                       _dtype_code(x2.dtype), M, pw.Kp, pw.S_pad,
+                                       ctypes.c_void_p(stream)), "permute_act")
+            return a
         st = e["stats"]
         # only a DIFFERENT layer on the same input reuses them: calling one layer again
         # (e.g. a benchmark loop) always recomputes its statistics
@@ -283,6 +322,10 @@ def quant_act_fp(x2: torch.Tensor, pw: PackedWeight, act_quant: str, n_bits: int
     if skey is not None:
         e["stats"] = (weakref.ref(stats_of if stats_of is not None else x2), skey,
                       pw.codes.data_ptr())
+        e["last_a"] = None
+        if SIB_REUSE and a.numel() * a.element_size() <= SIB_MAX_BYTES:
+            e["last_a"] = (weakref.ref(stats_of if stats_of is not None else x2),
+                           skey + (n_bits, group_size), weakref.ref(pw), a)
     return a
 
 
