@@ -105,6 +105,15 @@ __device__ inline void fence(V& v) {
   asm volatile("" : "+v"(v));
 }
 
+// the lane index computed again where it is used (volatile: never merged with the kernel-entry
+// value), so that lane-derived offsets of the salient tail and the epilogue are not live
+// through the codes loop (OPT bit 3, 128 VGPRs)
+__device__ inline int lane_now() {
+  uint32_t l;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+  return (int)l;
+}
+
 __host__ __device__ inline int brev3(int c) { return ((c & 1) << 2) | (c & 2) | ((c >> 2) & 1); }
 
 // DIAG (timing diagnostics, wrong results by design, instantiated only in a SQMP_DIAG_BUILD;
@@ -123,9 +132,12 @@ __host__ __device__ inline int brev3(int c) { return ((c & 1) << 2) | (c & 2) | 
 // s_setprio 1 through the K loop (MI355X_MICROARCH.md "Two waves per SIMD" item 4); bit 1 --
 // loader split: waves 0-3 issue every LDS-DMA piece of a stage (their own and those of
 // waves 4-7), waves 4-7 only wait, read and multiply (gemm_fq6's split); bit 2 -- A fragments
-// read 3 blocks ahead instead of 2
+// read 3 blocks ahead instead of 2; bit 3 -- two workgroups per CU (128 VGPRs: DMA pieces
+// i > 0 addressed through the scalar offset, the two fragment offsets kept instead of the lane
+// index, which the salient tail and the epilogue compute again; spill-free at TM = 128 only,
+// checked by tests/test_fq7_build_cpu.py)
 template <class DT, int GB, int TM, int J, int DIAG = 0, bool TR = false, int OPT = 0>
-__global__ __launch_bounds__(512, 1) void gemm_fq7_kernel(
+__global__ __launch_bounds__(512, (OPT & 8) ? 4 : 1) void gemm_fq7_kernel(
     const typename DT::T* __restrict__ A, const uint32_t* __restrict__ Bt,
     const typename DT::T* __restrict__ St, const typename DT::T* __restrict__ Salt,
     const typename DT::T* __restrict__ bias, typename DT::T* __restrict__ Y, int M, int N,
@@ -160,12 +172,14 @@ __global__ __launch_bounds__(512, 1) void gemm_fq7_kernel(
   constexpr bool SPLIT = (OPT & 2) != 0;
   constexpr int NO = SPLIT ? 2 : 1;       // waves whose pieces this wave issues
   const rsrc_t rA = make_rsrc(A + (size_t)m0 * lda);
-  uint32_t a_off[NO][NA];
+  // (OPT bit 3: piece i > 0 is piece 0 moved by 64 i rows, through the scalar offset)
+  constexpr int NAV = (OPT & 8) ? 1 : NA;
+  uint32_t a_off[NO][NAV];
 #pragma unroll
   for (int o = 0; o < NO; ++o) {
     const int arow = 8 * (wave + 4 * o) + (lane >> 3);
 #pragma unroll
-    for (int i = 0; i < NA; ++i)
+    for (int i = 0; i < NAV; ++i)
       a_off[o][i] = (uint32_t)((size_t)(arow + 64 * i) * lda * sizeof(T)) +
                     (uint32_t)(brev3((lane & 7) ^ ((arow >> 1) & 7)) << 4);
   }
@@ -190,7 +204,10 @@ __global__ __launch_bounds__(512, 1) void gemm_fq7_kernel(
             const uint32_t la = (uint32_t)(size_t)(__attribute__((address_space(3))) unsigned char*)dst + lane * 16;
             asm volatile("ds_write_b128 %0, %1" ::"v"(la), "v"(v) : "memory");
           } else {
-            dma16(rA, a_off[o][i], so, dst);
+            if constexpr ((OPT & 8) != 0)
+              dma16(rA, a_off[o][0], so + (uint32_t)(i * 64 * lda * (int)sizeof(T)), dst);
+            else
+              dma16(rA, a_off[o][i], so, dst);
           }
         }
     }
@@ -231,11 +248,12 @@ __global__ __launch_bounds__(512, 1) void gemm_fq7_kernel(
   auto issue_dense = [&](int kd, Dense& d, auto sc) {
     constexpr int S = decltype(sc)::value;
     const uint32_t so = (uint32_t)kd * (2048u * J);
-    ld16<16 * S>(d.w[S], rD, vD, so);
-    ld16<32 + 16 * S>(d.w[2 + S], rD, vD, so);
+    const uint32_t v = (OPT & 8) ? (uint32_t)lane_now() * (32u * J) : vD;
+    ld16<16 * S>(d.w[S], rD, v, so);
+    ld16<32 + 16 * S>(d.w[2 + S], rD, v, so);
     if (J == 4) {
-      ld16<64 + 16 * S>(d.w[(4 + S) % (2 * J)], rD, vD, so);
-      ld16<96 + 16 * S>(d.w[(6 + S) % (2 * J)], rD, vD, so);
+      ld16<64 + 16 * S>(d.w[(4 + S) % (2 * J)], rD, v, so);
+      ld16<96 + 16 * S>(d.w[(6 + S) % (2 * J)], rD, v, so);
     }
   };
   auto fence_codes = [&](Codes& d) {
@@ -253,17 +271,23 @@ __global__ __launch_bounds__(512, 1) void gemm_fq7_kernel(
   const DecK dk = make_deck();
   const int a_sw = (r16 >> 1) & 7;
   // A fragment of block t (sub-step s = t / I, row tile i = t % I)
+  // (OPT bit 3: the lane's two sub-step offsets kept instead of the lane index)
+  uint32_t a_lo[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+    a_lo[s] = (uint32_t)(r16 * 128 + ((brev3(4 * (q & 1) + 2 * s + (q >> 1)) ^ a_sw) << 4));
   auto ald = [&](const unsigned char* __restrict__ slot, int t) {
     if (DIAG == 5) t &= ~1;  // timing diagnostic: half the A fragment reads
+    if constexpr ((OPT & 8) != 0) return *(const u32x4*)(slot + 16 * (t % I) * 128 + a_lo[t / I]);
     const int c = 4 * (q & 1) + 2 * (t / I) + (q >> 1);
     return *(const u32x4*)(slot + (16 * (t % I) + r16) * 128 + ((brev3(c) ^ a_sw) << 4));
   };
-#define SQMP_FQ7_BLOCKS(BF, ...)                                               \
+#define SQMP_FQ7_BLOCKS(BF, LD, ...)                                           \
   {                                                                            \
     u32x4 a[PF + 1];                                                           \
-    _Pragma("unroll") for (int t = 0; t < PF; ++t) a[t] = ald(slot, t);        \
+    _Pragma("unroll") for (int t = 0; t < PF; ++t) a[t] = LD(slot, t);         \
     _Pragma("unroll") for (int t = 0; t < 2 * I; ++t) {                        \
-      if (t + PF < 2 * I) a[(t + PF) % (PF + 1)] = ald(slot, t + PF);          \
+      if (t + PF < 2 * I) a[(t + PF) % (PF + 1)] = LD(slot, t + PF);           \
       _Pragma("unroll") for (int j = 0; j < J; ++j)                            \
           Mfma<DT>::run(acc[t % I][j], BF(t / I, j), a[t % (PF + 1)]);         \
       __VA_ARGS__;                                                             \
@@ -287,7 +311,7 @@ __global__ __launch_bounds__(512, 1) void gemm_fq7_kernel(
       bf[0][j] = DIAG == 3 ? u32x4{cd.w[j >> 1][(j & 1) * 2], sp[j], sp[j], sp[j]}
                            : Dec<DT>::run(cd.w[j >> 1][(j & 1) * 2], sp[j], dk);
 #define SQMP_BF7(s, j) bf[s][j]
-    SQMP_FQ7_BLOCKS(SQMP_BF7,
+    SQMP_FQ7_BLOCKS(SQMP_BF7, ald,
                     if (t < J) bf[1][t] = DIAG == 3 ? u32x4{cd.w[t >> 1][(t & 1) * 2 + 1], sp[t], sp[t], sp[t]}
                                                     : Dec<DT>::run(cd.w[t >> 1][(t & 1) * 2 + 1], sp[t], dk));
 #undef SQMP_BF7
@@ -295,7 +319,7 @@ __global__ __launch_bounds__(512, 1) void gemm_fq7_kernel(
   // hook(t) runs after the MFMAs of block t (the mid-stage wait / issue at t = I - 1)
   auto compute_dense = [&](const unsigned char* __restrict__ slot, Dense& dd, auto hook) {
 #define SQMP_BD7(s, j) dd.w[2 * (j) + (s)]
-    SQMP_FQ7_BLOCKS(SQMP_BD7, hook(t));
+    SQMP_FQ7_BLOCKS(SQMP_BD7, ald, hook(t));
 #undef SQMP_BD7
   };
 #undef SQMP_FQ7_BLOCKS
@@ -416,17 +440,20 @@ __global__ __launch_bounds__(512, 1) void gemm_fq7_kernel(
     }
     return;
   }
+  // (OPT bit 3: the lane index computed again here rather than kept live from the entry)
+  const int el = (OPT & 8) ? lane_now() : lane;
+  const int etid = wave * 64 + el, er16 = el & 15, eq = el >> 4;
   float cmx[J][4] = {};
 #pragma unroll
   for (int j = 0; j < J; ++j) {
-    const int nl = WR * wave + 16 * j + 4 * q;  // first of the lane's 4 columns
+    const int nl = WR * wave + 16 * j + 4 * eq;  // first of the lane's 4 columns
     float bv[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r)
       bv[r] = bias && n0 + nl + r < N ? DT::to_f(bias[n0 + nl + r]) : 0.f;
 #pragma unroll
     for (int i = 0; i < I; ++i) {
-      const int ml = 16 * i + r16;
+      const int ml = 16 * i + er16;
       T v[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) v[r] = DT::from_f(acc[i][j][r] + bv[r]);
@@ -448,18 +475,18 @@ __global__ __launch_bounds__(512, 1) void gemm_fq7_kernel(
         v = fmaxf(v, __shfl_xor(v, 2, 64));
         v = fmaxf(v, __shfl_xor(v, 4, 64));
         v = fmaxf(v, __shfl_xor(v, 8, 64));
-        const int n = n0 + WR * wave + 16 * j + 4 * q + r;
-        if (r16 == 0 && n < N) atomicMax(colmax + n, __float_as_uint(v));
+        const int n = n0 + WR * wave + 16 * j + 4 * eq + r;
+        if (er16 == 0 && n < N) atomicMax(colmax + n, __float_as_uint(v));
       }
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   barrier();
   constexpr int CPR = TN / 8, RPP = 512 / CPR;  // 16-B chunks per row, rows per pass
-  const int c = tid % CPR;
+  const int c = etid % CPR;
   const bool cok = n0 + c * 8 < N;  // N % 8 == 0 (launcher)
 #pragma unroll
   for (int k = 0; k < TM / RPP; ++k) {
-    const int ml = RPP * k + tid / CPR;
+    const int ml = RPP * k + etid / CPR;
     const int gm = m0 + ml;
     const u32x4 val = *(const u32x4*)(lds + ml * (TN * 2) + ((c ^ (ml & 15)) << 4));
     if (gm < M && cok) {
@@ -535,9 +562,12 @@ static int group_m_tr_env() {  // read per launch (in-process A/B)
 // the packed-order launch's OPT variant (A/B knob, see gemm_fq7_kernel): default 3, same box
 // (profiles/r03_ab_fq7_opt.txt): 2048 x 4096 -> 4096 67.2 -> 65.6 us, -> 11008 182.4 -> 181.9,
 // 11008 -> 4096 164.5 -> 163.9, config 2 in packed order 461.2 -> 448.3
-static int opt_pk_env() {  // read per launch (in-process A/B)
+// 128-row tiles with more than one tile per CU: 8 (two workgroups per CU, 128 VGPRs), same
+// box (profiles/r03_ab_fq7_two_wg_per_cu.txt): 2048 x 4096 -> 11008 179.5 -> 159.6 us; at one
+// tile per CU (2048 x 4096 -> 4096, 2048 x 11008 -> 4096) within +-1 % of 3
+static int opt_pk_env(int tm, long tiles) {  // read per launch (in-process A/B)
   const char* e = getenv("SQMP_FQ7_OPT");
-  return e ? atoi(e) : 3;
+  return e ? atoi(e) : (tm == 128 && tiles > 256 ? 8 : 3);
 }
 
 // the activation-order launch's OPT variant (A/B knob, see gemm_fq7_kernel)
@@ -572,10 +602,12 @@ static int launch_k(const void* a, const void* bt, const void* st, const void* s
   // OPT variants (setprio for waves 4-7, loader split) for the fp16 J = 2 kernels, the
   // 2048-token Llama GEMMs (A/B knob SQMP_FQ7_OPT, read per launch)
   if constexpr (std::is_same<DT, F16>::value && J == 2 && GB == 1 && DIAG == 0) {
-    switch (opt_pk_env()) {
+    switch (opt_pk_env(TM, (long)tiles_m * tiles_n)) {
       case 1: SQMP_PK(1); break;
       case 2: SQMP_PK(2); break;
       case 3: SQMP_PK(3); break;
+      case 8: if constexpr (TM == 128) { SQMP_PK(8); } else { SQMP_PK(0); } break;
+      case 9: if constexpr (TM == 128) { SQMP_PK(9); } else { SQMP_PK(3); } break;
       default: SQMP_PK(0); break;
     }
   } else {
@@ -675,6 +707,14 @@ static int dispatch_tr(const void* wp, const void* codes_t, const void* scale_t,
       case 3: SQMP_TR(3); break;
       case 4: SQMP_TR(4); break;
       case 5: SQMP_TR(5); break;
+#define SQMP_TR128(O)                                                                           \
+  gemm_fq7_kernel<DT, 1, 128, 2, 0, true, O><<<dim3(cdiv(N, 128) * tiles_n), dim3(512), 0, s>>>( \
+      (const T*)wp, (const uint32_t*)codes_t, (const T*)scale_t, (const T*)sal_t, (const T*)bias, \
+      (T*)y, N, M, Kq, S_pad, G, ngq, cdiv(N, 128), tiles_n, group_m_tr_env(), colmax, nt)
+      // 128-row tiles at two workgroups per CU (OPT bit 3; 8, 9 spill at 128 VGPRs)
+      case 10: if constexpr (TM == 256) { SQMP_TR128(10); } else { SQMP_TR(0); } break;
+      case 11: if constexpr (TM == 256) { SQMP_TR128(11); } else { SQMP_TR(0); } break;
+#undef SQMP_TR128
       default: SQMP_TR(0); break;  // 6, 7 (split + PF = 3) spill with the colmax epilogue
     }
   }
