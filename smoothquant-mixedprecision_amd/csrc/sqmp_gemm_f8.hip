@@ -641,10 +641,9 @@ static int gemm_f8_impl(const void* a8, const float* ascale, const void* xs, con
   }();
   const bool v2 = Gw % 128 == 0 && !v1_only;
   if (colmax && !v2) return SQMP_EUNSUPPORTED;  // fused statistics: the 16x16x128 kernel only
-  static const int group_m = [] {  // M-tiles per raster group (SQMP_GROUP_M: A/B knob)
-    const char* e = getenv("SQMP_GROUP_M");
-    return e && atoi(e) > 0 ? atoi(e) : 4;
-  }();
+  // M-tiles per raster group (SQMP_GROUP_M: A/B knob, read per launch)
+  const char* ge = getenv("SQMP_GROUP_M");
+  const int group_m = ge && atoi(ge) > 0 ? atoi(ge) : 4;
   const bool nt = nt_output((size_t)M * N * (dtype == SQMP_F32 ? 4 : 2));
   // default 2 (loader split): same-box config-2 per_token step 334.5 -> 324.0 us; setprio for
   // waves 4-7 +-0 (profiles/r03_ab_f8_opt.txt).  SQMP_F8_OPT: A/B knob, read per launch

@@ -544,12 +544,13 @@ __global__ void pack_sal_kernel(const T* __restrict__ wsal, T* __restrict__ Salt
   Salt[idx] = n < N ? wsal[n * S_pad + kd * 64 + 8 * c + e] : (T)0.f;
 }
 
-static int group_m_env() {
-  static int v = [] {
-    const char* e = getenv("SQMP_FQ7_GROUP_M");
-    return e && atoi(e) > 0 ? atoi(e) : 8;
-  }();
-  return v;
+// the packed-order launch: 4 row tiles per raster group (same box, 8 / 2 / 4 / 16 at
+// 2048 x 4096 -> 4096 69.9 / 68.7 / 68.2 / 69.1 us, -> 11008 170.8 / 171.6 / 169.8 / 172.1,
+// 2048 x 11008 -> 4096 173.3 / 172.8 / 171.6 / 176.7, config 2 in packed order 467.3 / 463.1
+// / 459.6 / 473.6; profiles/r03_ab_group_m.txt); SQMP_FQ7_GROUP_M overrides
+static int group_m_env() {  // read per launch (in-process A/B)
+  const char* e = getenv("SQMP_FQ7_GROUP_M");
+  return e && atoi(e) > 0 ? atoi(e) : 4;
 }
 
 // the activation-order (TR) launch: 4 weight-row tiles per raster group (same box, config 2:

@@ -90,7 +90,7 @@ __global__ __launch_bounds__(128 * WN, 4 / WN) void gemm_x3_kernel(
     const float* __restrict__ A, const uint16_t* __restrict__ B3, const float* __restrict__ bias,
     float* __restrict__ Y, int M, int N, int L, int Np, int tiles_m, int tiles_n,
     uint32_t* __restrict__ colmax, const int* __restrict__ aexp, const int* __restrict__ bexp,
-    int nt) {
+    int nt, int group_m) {
   constexpr int NPL = H ? 2 : 3;  // pieces per operand
   // A planes (NPL x 128 rows) then B planes (NPL x BN rows), rows of BK 16-bit values
   constexpr int APL = X3_BM * BK * 2;  // one A plane
@@ -100,7 +100,7 @@ __global__ __launch_bounds__(128 * WN, 4 / WN) void gemm_x3_kernel(
   __shared__ __attribute__((aligned(16))) unsigned char lds[NPL * (APL + BPL)];
   unsigned char* const ldsb = lds + NPL * APL;
   int tm, tn;
-  tile_coords(tiles_m, tiles_n, 8, tm, tn);
+  tile_coords(tiles_m, tiles_n, group_m, tm, tn);
   const int m0 = tm * X3_BM, n0 = tn * BN;
   constexpr int NT = 128 * WN, CW = BN / WN, J = CW / 16;
   constexpr int BSH = (BN == 256 ? 8 : 7) + CSH;  // log2(16-B chunks per B plane)
@@ -351,11 +351,16 @@ extern "C" int sqmp_gemm_h2(const float* a, const int* aexp, const void* b2, con
   }();
   const bool k64 = bk64 && L % 64 == 0;
   const int nt = nt_output((size_t)M * N * sizeof(float)) ? 1 : 0;
+  // row tiles per raster group: 4 (same box, config-2 fp32 step: 1 / 2 / 4 / 8 / 16 / 32 ->
+  // 2078.7 / 2074.1 / 2002.3 / 2037.9 / 2146.8 / 2178.6 us, profiles/r03_ab_h2_group_m.txt);
+  // SQMP_H2_GROUP_M: A/B knob, read per launch
+  const char* ge = getenv("SQMP_H2_GROUP_M");
+  const int gm = ge && atoi(ge) > 0 ? atoi(ge) : 4;
 #define SQMP_H2(CM, WN, BNV, TN)                                                                 \
   (k64 ? gemm_x3_kernel<CM, WN, true, BNV, 64><<<tiles_m * TN, 128 * WN, 0, (hipStream_t)stream>>>( \
-             a, (const uint16_t*)b2, bias, y, M, N, L, Np, tiles_m, TN, colmax, aexp, bexp, nt) \
+             a, (const uint16_t*)b2, bias, y, M, N, L, Np, tiles_m, TN, colmax, aexp, bexp, nt, gm) \
        : gemm_x3_kernel<CM, WN, true, BNV, 32><<<tiles_m * TN, 128 * WN, 0, (hipStream_t)stream>>>( \
-             a, (const uint16_t*)b2, bias, y, M, N, L, Np, tiles_m, TN, colmax, aexp, bexp, nt))
+             a, (const uint16_t*)b2, bias, y, M, N, L, Np, tiles_m, TN, colmax, aexp, bexp, nt, gm))
   if (colmax) {
     if (wide) SQMP_H2(true, 4, 256, tiles_n2); else if (small) SQMP_H2(true, 4, 128, tiles_n); else SQMP_H2(true, 2, 128, tiles_n);
   } else {
