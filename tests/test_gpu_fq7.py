@@ -137,3 +137,36 @@ def test_fq7_full_size_config2():
     finally:
         ops.FQ7_AUTO = fq7
     assert rel(y7, y6) < 1e-3
+
+
+@pytest.mark.parametrize("env,vals", [
+    ("SQMP_FQ7_OPT", ("3", "8", "0")),      # two workgroups per CU (8) vs one (3, 0)
+    ("SQMP_FQ7_GROUP_M", ("4", "1", "8")),  # raster group sizes
+])
+@pytest.mark.parametrize("M,K,N", [(2048, 4096, 11008), (2048, 4096, 4096), (700, 2048, 1032)])
+def test_fq7_variants_bit_identical(env, vals, M, K, N):
+    """The launch variants only reorder work: y (and the fused column maxima) bit-identical.
+    2048 x 4096 -> 11008 has 688 tiles of 128 x 256 (the two-per-CU default), -> 4096 256."""
+    import os
+    dev = _dev()
+    from smoothquant import ops
+    q, lin, x = _layer(dev, M, K, N, 64, 0.05, torch.float16)
+    pw = q.packed()
+    a = ops.quant_act_fp(x, pw, "per_group", 4, 64)
+    old = os.environ.get(env)
+    outs = []
+    try:
+        for v in vals:
+            os.environ[env] = v
+            cm = torch.zeros(pw.N + 8, dtype=torch.int32, device=dev)
+            outs.append((ops.gemm_fq7(a, pw, lin.bias, cm), cm))
+    finally:
+        if old is None:
+            os.environ.pop(env, None)
+        else:
+            os.environ[env] = old
+    y0, c0 = outs[0]
+    assert rel(y0, _ref(a, pw, lin.bias)) < TOL[torch.float16]
+    for y, c in outs[1:]:
+        assert torch.equal(y.view(torch.int16), y0.view(torch.int16))
+        assert torch.equal(c, c0)

@@ -153,3 +153,32 @@ def test_h2_full_size_config2_fp32():
         ref = a.double() @ ops._w_full(pw).double().t() + q.bias.detach().reshape(-1).double()
     e = rel(y.double().cpu().numpy(), ref.cpu().numpy())
     assert e <= 2e-6, e
+
+
+@pytest.mark.parametrize("M,N", [(4096, 4096), (300, 520)])
+def test_h2_raster_groups_bit_identical(M, N):
+    """SQMP_H2_GROUP_M only reorders the tiles: y bit-identical for every group size."""
+    import os
+    from smoothquant import ops
+    dev = _dev()
+    rng = np.random.default_rng(5)
+    K = 1024
+    W = (rng.standard_normal((N, K)) * 0.02).astype(np.float32)
+    x = rng.standard_normal((M, K)).astype(np.float32)
+    q = make_layer(W, None, "fp32", dev, weight_quant="per_group", act_quant="per_group",
+                   importance=torch.from_numpy(np.abs(x).mean(0)), salient_prop=0.05, group_size=128)
+    pw = q.packed()
+    a = ops.quant_act_fp(torch.from_numpy(x).to(dev), pw, "per_group", 4, 128)
+    old = os.environ.get("SQMP_H2_GROUP_M")
+    ys = []
+    try:
+        for g in ("4", "1", "8", "32"):
+            os.environ["SQMP_H2_GROUP_M"] = g
+            ys.append(ops.gemm_h2(a, pw, None))
+    finally:
+        if old is None:
+            os.environ.pop("SQMP_H2_GROUP_M", None)
+        else:
+            os.environ["SQMP_H2_GROUP_M"] = old
+    for y in ys[1:]:
+        assert torch.equal(y.view(torch.int32), ys[0].view(torch.int32))
