@@ -687,7 +687,8 @@ static int quant_lc_launch(const void* x, int M, int K, int q_max, int G, const 
   SQMP_HIP_CHECK(hipFuncSetAttribute((const void*)quant_lc_kernel<DT, MODE, LC_RPL, GS, F8>,
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   int per_cu = occ_per_cu((const void*)quant_lc_kernel<DT, MODE, LC_RPL, GS, F8>, 64 * nw, lds);
-  if (const char* e = getenv("SQMP_LC_PERCU")) per_cu = atoi(e);  // tuning only
+  if (const char* e = getenv("SQMP_LC_PERCU"))  // tuning only (0 / unparsable: the default)
+    if (atoi(e) > 0) per_cu = atoi(e);
   const int grid = lc_grid((M + 1) / 2, per_cu);
   quant_lc_kernel<DT, MODE, LC_RPL, GS, F8><<<dim3(grid), dim3(64 * nw), lds, s>>>(
       (const T*)x, M, K, q_max, G, lctab, Kn, amap, P, sal, S, S_pad, cmax, nonsal, (T*)out,
