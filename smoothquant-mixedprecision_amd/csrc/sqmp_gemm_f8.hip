@@ -293,7 +293,10 @@ __device__ inline i32x8b cat8(const u32x4& a, const u32x4& b) {
 // OPT (A/B knob SQMP_F8_OPT, read per launch): bit 0 -- waves 4-7 at s_setprio 1 through the
 // K loop; bit 1 -- loader split: waves 0-3 issue every DMA piece of a stage (their own and
 // those of waves 4-7), waves 4-7 only wait, read and multiply
-template <class DT, int OPT = 0>
+// DIAG (timing diagnostics, wrong results by design, only in a SQMP_DIAG_BUILD): 1 the code
+// stages' DMA from two L2-hot stages, 2 no code-stage DMA after the first two stages, 3 no
+// per-group fold (the MFMA accumulates straight into the totals)
+template <class DT, int OPT = 0, int DIAG = 0>
 __global__ __launch_bounds__(512, 1) void gemm_f8v2_kernel(
     const unsigned char* __restrict__ A8, const float* __restrict__ ascale,
     const typename DT::T* __restrict__ XS, const unsigned char* __restrict__ W8,
@@ -335,7 +338,8 @@ __global__ __launch_bounds__(512, 1) void gemm_f8v2_kernel(
       auto row = [&](int j) { return r0 + 8 * j; };
       auto ch = [&](int j) { return (uint32_t)(((lane & 7) ^ v2_sw(row(j))) << 4); };
       if (kt < nk8) {
-        const uint32_t so = (uint32_t)kt * 128;
+        if (DIAG == 2 && kt >= 2) continue;
+        const uint32_t so = (uint32_t)(DIAG == 1 && kt >= 2 ? (kt & 1) : kt) * 128;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const uint32_t v = (uint32_t)row(j) * Kp + ch(j);
@@ -395,6 +399,13 @@ __global__ __launch_bounds__(512, 1) void gemm_f8v2_kernel(
     for (int i = 0; i < 8; ++i) {
       const i32x8b cur = ax;
       if (i + 1 < 8) ax = ald(i + 1);
+      if constexpr (DIAG == 3) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          tot[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(bw[j], cur, tot[i][j], 0, 0, 0, 127, 0, 127);
+        __builtin_amdgcn_sched_barrier(0);
+        continue;
+      }
       f32x4 t0 = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(bw[0], cur, zero, 0, 0, 0, 127, 0, 127);
       f32x4 t1 = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(bw[1], cur, zero, 0, 0, 0, 127, 0, 127);
 #pragma unroll
@@ -654,6 +665,21 @@ static int gemm_f8_impl(const void* a8, const float* ascale, const void* xs, con
       (const unsigned char*)a8, ascale, (const DTT::T*)xs, (const unsigned char*)w8, ws32,   \
       (const DTT::T*)wsal, (const DTT::T*)bias, (DTT::T*)y, M, N, Kp, S_pad, Gw, ngw, tiles_m, \
       tiles_n, group_m, colmax, nt ? 1 : 0)
+#ifdef SQMP_DIAG_BUILD
+  const char* de = getenv("SQMP_F8_DIAG");  // read per launch
+  const int diag = de ? atoi(de) : 0;
+#define SQMP_F8D(DTT, D)                                                                     \
+  gemm_f8v2_kernel<DTT, 2, D><<<grid, block, 0, s>>>(                                        \
+      (const unsigned char*)a8, ascale, (const DTT::T*)xs, (const unsigned char*)w8, ws32,   \
+      (const DTT::T*)wsal, (const DTT::T*)bias, (DTT::T*)y, M, N, Kp, S_pad, Gw, ngw, tiles_m, \
+      tiles_n, group_m, colmax, nt ? 1 : 0)
+  if (v2 && dtype == SQMP_F16 && diag > 0) {
+    if (diag == 1) SQMP_F8D(F16, 1); else if (diag == 2) SQMP_F8D(F16, 2); else SQMP_F8D(F16, 3);
+    SQMP_LAUNCH_CHECK();
+    return SQMP_OK;
+  }
+#undef SQMP_F8D
+#endif
 #define SQMP_F8L(DTT)                                                                        \
   if (v2) {                                                                                  \
     switch (opt) {                                                                           \
