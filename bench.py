@@ -239,7 +239,7 @@ LLAMA_T, LLAMA_G, LLAMA_P = 2048, 64, 0.05
 def llama_layer(dev, iters=40):
     """Per-linear and whole-layer time of the W4A4 layer against the same 7 unquantized fp16
     F.linear calls (hipBLASLt), HIP events on the launch stream."""
-    from smoothquant.fake_quant import W4A4Linear
+    from smoothquant.fake_quant import W4A4Linear, link_siblings
     gen = torch.Generator(device=dev).manual_seed(7)
     dt = torch.float16
     xs = {}
@@ -256,6 +256,9 @@ def llama_layer(dev, iters=40):
         q = W4A4Linear.from_float(lin, weight_quant="per_group", act_quant="per_group",
                                   importance=imp, salient_prop=LLAMA_P, group_size=LLAMA_G)
         layers.append((name, q, lin.weight.detach(), xs[src]))
+    # the sibling groups quantize_llama_like links (q/k/v, gate/up: fake_quant.SiblingGroup)
+    link_siblings(*[layers[i][1] for i in (0, 1, 2)])
+    link_siblings(*[layers[i][1] for i in (4, 5)])
     stream = torch.cuda.current_stream(dev)
 
     def run(fp16, ev=None):
@@ -295,9 +298,10 @@ def llama_layer(dev, iters=40):
         "per_linear": {name: {"w4a4_ms": round(a, 4), "fp16_ms": round(b, 4),
                               "fp16_over_w4a4": round(b / a, 3)}
                        for (name, _, _, _), a, b in zip(LLAMA_LINEARS, pw4, pf16)},
-        "note": "median of 40 layer passes, best of 2 interleaved rounds; per-linear times "
-                "include each layer's own prepass (column max / rank only on the first "
-                "sibling)",
+        "note": "median of 40 layer passes, best of 2 interleaved rounds; q/k/v and gate/up are "
+                "linked sibling groups (as quantize_llama_like links them): the first member's "
+                "time covers the group's one quantizer pass and one GEMM launch, the others "
+                "return the outputs it computed",
     }
 
 

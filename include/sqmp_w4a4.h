@@ -325,6 +325,40 @@ int sqmp_gemm_fqt7j(const void* codes_t, const void* scale_t, const void* sal_t,
 int sqmp_permute_act(const void* src, void* dst, const int32_t* map, int dtype, int M, int P,
                      int S_pad, void* stream);
 
+/* Sibling layers (q/k/v, gate/up: W4A4Linear modules that the model calls on the SAME input
+ * with the same salient set and sorted per_group act mode; fake_quant.py:479-561 swaps them
+ * one by one and each forward repeats :291-304 on that input).  One call quantizes x once for
+ * `nout` (1..3) packed weights: amaps[o] / posmaps[o] are weight o's amap and posmap (its
+ * packed order), outs[o] its SQMP_OUT_FP operand D [roundup(M, 256) rows][Kp + S_pad].  Every
+ * outs[o] equals what sqmp_quant_act_v2(..., SQMP_OUT_FP, ...) writes for weight o, bit for
+ * bit.  The weights share K, Kp, S_pad and the salient set.  fp16 / bf16, act mode PER_GROUP
+ * or PER_GROUP_MEAN3STD, group_size a power of two in [16, 1024], K - S <= 16384, flags ==
+ * SQMP_QA_CLEAN_WS.  amaps, posmaps and outs are HOST arrays of device pointers. */
+int sqmp_quant_act_group(void* x, int dtype, int M, int K, int amode, int n_bits,
+                         int group_size, int nout, const int32_t* const* amaps,
+                         const int32_t* const* posmaps, int Kp, const int32_t* nonsal,
+                         const int32_t* salient, int S, int S_pad, int flags, void* const* outs,
+                         void* workspace, size_t ws_bytes, void* stream);
+
+/* One launch of sqmp_gemm_fq7 over `nprob` (1..4) problems that share M, Kp, S_pad, Gw, ngw
+ * and J (the sibling layers above: each problem its own A operand, packed weight, bias,
+ * output and colmax); problem p computes exactly what sqmp_gemm_fq7 computes for it, bit for
+ * bit.  The tiles of all problems are scheduled together (no launch gap between siblings, and
+ * the last partial round of one problem's tiles is filled by the next problem's).  `probs`
+ * is a HOST array. */
+typedef struct sqmp_fq7_problem {
+  const void* a;        /* SQMP_OUT_FP operand, roundup(M, 256) rows allocated */
+  const void* codes_t;  /* sqmp_pack_fq7 operands of the problem's weight */
+  const void* scale_t;
+  const void* sal_t;
+  const void* bias;     /* D [N] or NULL */
+  void* y;              /* D [M][N] */
+  uint32_t* colmax;     /* NULL or as sqmp_gemm_fq_colmax */
+  int N;                /* output features, N % 8 == 0 */
+} sqmp_fq7_problem;
+int sqmp_gemm_fq7_group(const sqmp_fq7_problem* probs, int nprob, int dtype, int M, int Kp,
+                        int S_pad, int Gw, int ngw, int J, void* stream);
+
 /* The fp32 faithful GEMM on the f16 MFMA (the default for fp32 layers): every row of A and
  * of W is scaled by a power of two (exact) so that its maximum lies in [2^13, 2^14), each
  * scaled value v is split as v = h + l + r with h = f16(v), l = f16(v - h) (|r| <= 2^-22 |v|,

@@ -534,15 +534,11 @@ __global__ __launch_bounds__(256) void lc_table_kernel(
 // all key loads: two dependent round trips for the whole list up to 256 * RT_SB entries).
 constexpr int RT_MAX = 16384;  // 64 KiB of keys in LDS
 constexpr int RT_SB = 24;
-template <int TPO, int R>
-__global__ __launch_bounds__(256) void rank_table_kernel(
-    const uint32_t* __restrict__ key, const int32_t* __restrict__ nonsal, int L,
-    const int32_t* __restrict__ posmap, int32_t* __restrict__ colsorted,
-    uint32_t* __restrict__ lctab, int lc_len, uint32_t lc_none) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t rt_kv[];  // roundup(L, 4 TPO)
-  const int tid = threadIdx.x;
-  const int L4 = (int)round_up_dev(L, 4 * TPO) >> 2;
-  for (int j0 = tid; j0 < 4 * L4; j0 += 256 * RT_SB) {
+
+// stage the L keys key[nonsal[j]] (padded with 0xFFFFFFFF to 4 L4 entries) into LDS
+__device__ inline void rank_stage_keys(const uint32_t* key, const int32_t* __restrict__ nonsal,
+                                       int L, int L4, uint32_t* rt_kv) {
+  for (int j0 = threadIdx.x; j0 < 4 * L4; j0 += 256 * RT_SB) {
     int idx[RT_SB];
     uint32_t kv[RT_SB];
 #pragma unroll
@@ -558,11 +554,16 @@ __global__ __launch_bounds__(256) void rank_table_kernel(
       if (j < 4 * L4) rt_kv[j] = kv[u];
     }
   }
-  const int nt = gridDim.x * 256;
-  for (int r = L + blockIdx.x * 256 + tid; r < lc_len; r += nt) lctab[r] = lc_none;
-  __syncthreads();
-  const int sub = tid % TPO;
-  const int g0 = (blockIdx.x * (256 / TPO) + tid / TPO) * R;  // this lane group's first owner
+}
+
+// Rank the R owners g0 .. g0 + R - 1 of this lane group (TPO lanes, `sub` = this lane's index
+// in it) against the L staged keys, then write their table entries (see rank_table_kernel).
+template <int TPO, int R>
+__device__ inline void rank_owner_group(const uint32_t* rt_kv, int L, int L4, int g0, int sub,
+                                        const int32_t* __restrict__ nonsal,
+                                        const int32_t* __restrict__ posmap,
+                                        int32_t* __restrict__ colsorted,
+                                        uint32_t* __restrict__ lctab, const SibTables& sib) {
   uint32_t mine[R], cnt[R];
   int ochunk[R];
 #pragma unroll
@@ -594,6 +595,138 @@ __global__ __launch_bounds__(256) void rank_table_kernel(
       const int col = nonsal[g0 + o];
       colsorted[cnt[o]] = col;
       lctab[cnt[o]] = (uint32_t)col | ((uint32_t)(posmap ? posmap[col] : col) << 16);
+      for (int t = 0; t < sib.n; ++t)
+        sib.lctab[t][cnt[o]] = (uint32_t)col | ((uint32_t)sib.posmap[t][col] << 16);
+    }
+  }
+}
+
+template <int TPO, int R>
+__global__ __launch_bounds__(256) void rank_table_kernel(
+    const uint32_t* __restrict__ key, const int32_t* __restrict__ nonsal, int L,
+    const int32_t* __restrict__ posmap, int32_t* __restrict__ colsorted,
+    uint32_t* __restrict__ lctab, int lc_len, uint32_t lc_none, SibTables sib) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t rt_kv[];  // roundup(L, 4 TPO)
+  const int tid = threadIdx.x;
+  const int L4 = (int)round_up_dev(L, 4 * TPO) >> 2;
+  rank_stage_keys(key, nonsal, L, L4, rt_kv);
+  const int nt = gridDim.x * 256;
+  for (int r = L + blockIdx.x * 256 + tid; r < lc_len; r += nt) {
+    lctab[r] = lc_none;
+    for (int o = 0; o < sib.n; ++o) sib.lctab[o][r] = lc_none;
+  }
+  __syncthreads();
+  const int g0 = (blockIdx.x * (256 / TPO) + tid / TPO) * R;  // this lane group's first owner
+  rank_owner_group<TPO, R>(rt_kv, L, L4, g0, tid % TPO, nonsal, posmap, colsorted, lctab, sib);
+}
+
+// ---------------------------------------------------------------- column max + rank, one launch
+// The column maxima of x [M][K] (colmax_kernel's blocks: VEC consecutive columns per lane, the
+// block's rows split over its four waves, one atomicMax per column and block into the clean
+// cmax) followed by the rank table (rank_table_kernel) in the SAME launch: every block takes a
+// ticket after its maxima are published (each wave drains its atomics, then the block's lane 0
+// releases at agent scope and adds to the counter); the last NR blocks to arrive become the
+// rankers, wait until every block has arrived (relaxed poll of the counter, one agent-scope
+// acquire: MI355X_MICROARCH.md, "Workgroup dispatch ... visibility"), stage the keys and rank
+// their share of the owners.  The last ranker to finish returns both counters to zero.
+// Saves the rank launch and its ramp (Llama prefill: the 2048-row inputs' statistics).
+// ctr[0] = arrivals, ctr[1] = finished rankers (zero on entry; the clean-workspace words).
+struct RankArgs {
+  const int32_t* nonsal;
+  const int32_t* posmap;
+  int32_t* colsorted;
+  uint32_t* lctab;
+  int L, lc_len;
+  uint32_t lc_none;
+  int NR;  // rankers
+};
+template <class DT, int VEC, int TPO, int R>
+__global__ __launch_bounds__(256) void colmax_rank_kernel(const typename DT::T* __restrict__ x,
+                                                          int Mr, int C, int rows_per_block,
+                                                          uint32_t* cmax, uint32_t* ctr,
+                                                          RankArgs ra, SibTables sib) {
+  typedef typename DT::T T;
+  extern __shared__ __attribute__((aligned(16))) uint32_t cr_lds[];  // max(4 x 64 VEC floats, keys)
+  __shared__ int cr_ticket;
+  float* red = (float*)cr_lds;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int c0 = (blockIdx.x * 64 + lane) * VEC;
+  const int r0 = blockIdx.y * rows_per_block;
+  const int r1 = min(Mr, r0 + rows_per_block);
+  float m[VEC];
+#pragma unroll
+  for (int i = 0; i < VEC; ++i) m[i] = 0.f;
+  if (c0 + VEC <= C) {
+    int r = r0 + wid;
+    for (; r + 28 < r1; r += 32) {
+      u32x4 raw[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) raw[u] = *(const u32x4*)(x + (size_t)(r + 4 * u) * C + c0);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const T* v = (const T*)&raw[u];
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) m[i] = fmaxf(m[i], fabsf(DT::to_f(v[i])));
+      }
+    }
+    for (; r < r1; r += 4) {
+      const u32x4 raw = *(const u32x4*)(x + (size_t)r * C + c0);
+      const T* v = (const T*)&raw;
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) m[i] = fmaxf(m[i], fabsf(DT::to_f(v[i])));
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < VEC; ++i) red[wid * 64 * VEC + lane * VEC + i] = m[i];
+  __syncthreads();
+  for (int t = tid; t < 64 * VEC; t += 256) {
+    const float v = fmaxf(fmaxf(red[t], red[64 * VEC + t]), fmaxf(red[2 * 64 * VEC + t], red[3 * 64 * VEC + t]));
+    const int c = blockIdx.x * 64 * VEC + t;
+    if (c < C && v > 0.f) atomicMax(&cmax[c], __float_as_uint(v));
+  }
+  // publish: every wave's atomics performed, then one release + ticket per block
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  const unsigned nblk = gridDim.x * gridDim.y;
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    cr_ticket = (int)__hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  const int ranker = cr_ticket - (int)(nblk - (unsigned)ra.NR);
+  if (ranker < 0) return;
+  // ---- a ranker: wait for every block's maxima (bounded spin), acquire, rank
+  if (tid == 0) {
+    for (unsigned spin = 0; spin < (1u << 20); ++spin) {
+      if (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= nblk) break;
+      __builtin_amdgcn_s_sleep(2);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  const int L = ra.L;
+  const int L4 = (int)round_up_dev(L, 4 * TPO) >> 2;
+  rank_stage_keys(cmax, ra.nonsal, L, L4, cr_lds);
+  for (int r = L + ranker * 256 + tid; r < ra.lc_len; r += ra.NR * 256) {
+    ra.lctab[r] = ra.lc_none;
+    for (int o = 0; o < sib.n; ++o) sib.lctab[o][r] = ra.lc_none;
+  }
+  __syncthreads();
+  for (int g0 = (ranker * (256 / TPO) + tid / TPO) * R; g0 < L + 0; g0 += ra.NR * (256 / TPO) * R) {
+    rank_owner_group<TPO, R>(cr_lds, L, L4, g0, tid % TPO, ra.nonsal, ra.posmap, ra.colsorted,
+                             ra.lctab, sib);
+    // (every lane of a TPO group takes the same trip count: g0 is uniform over the group)
+  }
+  // the last ranker returns the counters to zero (every ranker is past its poll)
+  __syncthreads();
+  if (tid == 0) {
+    const unsigned done =
+        __hip_atomic_fetch_add(ctr + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (done == (unsigned)ra.NR - 1) {
+      __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(ctr + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
 }
@@ -606,7 +739,8 @@ static bool rank_table_fits(int L) {
 
 static int launch_rank_table(const uint32_t* key, const int32_t* nonsal, int L,
                              const int32_t* posmap, int32_t* colsorted, uint32_t* lctab,
-                             int lc_len, uint32_t lc_none, hipStream_t s) {
+                             int lc_len, uint32_t lc_none, hipStream_t s,
+                             const SibTables& sib = SibTables{}) {
   // TPO lanes per group of R owners (SQMP_RT_TPO = 8 / 16 / 32 and SQMP_RT_R = 1 / 2 / 4
   // override, tuning only, read per launch)
   const char* te = getenv("SQMP_RT_TPO");
@@ -629,7 +763,7 @@ static int launch_rank_table(const uint32_t* key, const int32_t* nonsal, int L,
     }                                                                                       \
     rank_table_kernel<T, RR><<<dim3(grid), dim3(256), lds, s>>>(key, nonsal, L, posmap,     \
                                                                colsorted, lctab, lc_len,    \
-                                                               lc_none);                    \
+                                                               lc_none, sib);               \
   } while (0)
 #define SQMP_RT_T(T)            \
   switch (r) {                  \
@@ -644,6 +778,60 @@ static int launch_rank_table(const uint32_t* key, const int32_t* nonsal, int L,
   }
 #undef SQMP_RT_T
 #undef SQMP_RT
+  SQMP_LAUNCH_CHECK();
+  return SQMP_OK;
+}
+
+// Column max + rank table in one launch (colmax_rank_kernel) for fp16 / bf16 rows whose 16-B
+// chunks are aligned, L <= RT_MAX.  ctr: two zero words (left zero).  SQMP_COLMAX_RANK=0 keeps
+// the two launches (A/B knob, read per call).  Returns SQMP_EUNSUPPORTED where not covered.
+static int launch_colmax_rank(const void* x, int dtype, int M, int K, uint32_t* cmax,
+                              uint32_t* ctr, const int32_t* nonsal, int L, const int32_t* posmap,
+                              int32_t* colsorted, uint32_t* lctab, int lc_len, uint32_t lc_none,
+                              hipStream_t s, const SibTables& sib = SibTables{}) {
+  if (const char* e = getenv("SQMP_COLMAX_RANK"))
+    if (atoi(e) == 0) return SQMP_EUNSUPPORTED;
+  if ((dtype != SQMP_F16 && dtype != SQMP_BF16) || L <= 0 || L > RT_MAX || M <= 0) return SQMP_EUNSUPPORTED;
+  if ((K * 2) % 16 != 0 || ((uintptr_t)x) % 16 != 0) return SQMP_EUNSUPPORTED;
+  constexpr int VEC = 8;
+  // colmax geometry as colmax_launch (>= 32 rows per block, ~1024 blocks)
+  int rpb = 128;
+  const int cb = cdiv(K, 64 * VEC);
+  while (rpb > 32 && (long)cb * cdiv(M, rpb) < 1024) rpb >>= 1;
+  const dim3 grid(cb, cdiv(M, rpb));
+  const int nblk = (int)(grid.x * grid.y);
+  // rankers: TPO lanes per owner, L TPO / 256 rankers (per-lane compares L / TPO), at most one
+  // per CU: waiting rankers never hold every slot a block still to arrive needs
+  static int ncu = 0;
+  if (ncu == 0) {
+    int dev = 0;
+    SQMP_HIP_CHECK(hipGetDevice(&dev));
+    SQMP_HIP_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+  }
+  int tpo = 16;
+  while (tpo > 4 && cdiv((long)L * tpo, 256) > ncu) tpo >>= 1;
+  const int nr = cdiv((long)L * tpo, 256);
+  if (nr > nblk || nr > ncu) return SQMP_EUNSUPPORTED;  // (tiny inputs: the two-launch path)
+  RankArgs ra{nonsal, posmap, colsorted, lctab, L, lc_len, lc_none, nr};
+  const size_t lds_keys = sizeof(uint32_t) * (size_t)round_up(L, 4 * tpo);
+  const size_t lds = lds_keys > 4 * 64 * VEC * sizeof(float) ? lds_keys : 4 * 64 * VEC * sizeof(float);
+#define SQMP_CR(DTT, TPOV)                                                                          \
+  do {                                                                                          \
+    static bool attr = false;                                                                   \
+    if (!attr) {                                                                                \
+      SQMP_HIP_CHECK(hipFuncSetAttribute((const void*)colmax_rank_kernel<DTT, VEC, TPOV, 1>,    \
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, 4 * RT_MAX)); \
+      attr = true;                                                                              \
+    }                                                                                           \
+    colmax_rank_kernel<DTT, VEC, TPOV, 1><<<grid, dim3(256), lds, s>>>(                         \
+        (const typename DTT::T*)x, M, K, rpb, cmax, ctr, ra, sib);                              \
+  } while (0)
+  if (dtype == SQMP_F16) {
+    if (tpo == 16) SQMP_CR(F16, 16); else if (tpo == 8) SQMP_CR(F16, 8); else SQMP_CR(F16, 4);
+  } else {
+    if (tpo == 16) SQMP_CR(BF16, 16); else if (tpo == 8) SQMP_CR(BF16, 8); else SQMP_CR(BF16, 4);
+  }
+#undef SQMP_CR
   SQMP_LAUNCH_CHECK();
   return SQMP_OK;
 }
@@ -1132,9 +1320,17 @@ static size_t ws_u32_words(int K, int Kp) {
   return k64 * (4 + (size_t)rank_tiles(K)) + (size_t)round_up(Kp > K ? Kp : K, 64) +
          (size_t)round_up(K > 0 ? K : 1, 4096);
 }
+// + the two sibling tables of sqmp_quant_act_group (round_up(K, 4096) words each) at the end
+static size_t ws_sib_offset(int K, int Kp) {
+  return sizeof(uint32_t) * ws_u32_words(K, Kp) + 2 * sizeof(double) * ws_k64(K);
+}
+// + four words for colmax_rank_kernel's counters (zero between calls)
+static size_t ws_ctr_offset(int K, int Kp) {
+  return ws_sib_offset(K, Kp) + 2 * sizeof(uint32_t) * (size_t)round_up(K > 0 ? K : 1, 4096);
+}
 extern "C" size_t sqmp_act_workspace_bytes(int M, int K, int Kp) {
   (void)M;
-  return sizeof(uint32_t) * ws_u32_words(K, Kp) + 2 * sizeof(double) * ws_k64(K);
+  return ws_ctr_offset(K, Kp) + 4 * sizeof(uint32_t);
 }
 
 static int quant_act_impl(void* x, int dtype, int M, int K, int amode, int n_bits,
@@ -1211,6 +1407,8 @@ static int quant_act_impl(void* x, int dtype, int M, int K, int amode, int n_bit
   int32_t* counts = (int32_t*)(lctab + round_up(K, 4096));
   int32_t* colsorted = counts + k64;
   double* sums = (double*)((uint32_t*)workspace + ws_u32_words(K, Kp));
+  uint32_t* ctr = (uint32_t*)((unsigned char*)workspace + ws_ctr_offset(K, Kp));
+  const SibTables sibt{};
   const int Kn = K - S;
   if (Kn == 0) {
     // every channel salient: the reference skips quantization entirely (:299)
@@ -1244,7 +1442,16 @@ static int quant_act_impl(void* x, int dtype, int M, int K, int amode, int n_bit
           if (stats_given) {
             st2 = SQMP_OK;
           } else {
-            if (!clean) SQMP_HIP_CHECK(hipMemsetAsync(cmax, 0, sizeof(uint32_t) * k64, s));
+            if (!clean) {
+              SQMP_HIP_CHECK(hipMemsetAsync(cmax, 0, sizeof(uint32_t) * k64, s));
+              SQMP_HIP_CHECK(hipMemsetAsync(ctr, 0, 4 * sizeof(uint32_t), s));
+            }
+            if (rank_table_fits(Kn) &&
+                launch_colmax_rank(x, dtype, M, K, cmax, ctr, nonsal, Kn, pm, colsorted, lctab,
+                                   lc_len, none, s, sibt) == SQMP_OK) {
+              key_clear = cmax;  // cleared by the quantizer, after every ranker's read
+              return SQMP_OK;
+            }
             st2 = launch_colmax(x, dtype, M, K, cmax, s, false);
           }
         } else {
@@ -1463,4 +1670,78 @@ extern "C" int sqmp_quant_act_c4(void* x, int dtype, int M, int K, int amode, in
   return quant_act_impl(x, dtype, M, K, amode, n_bits, group_size, amap, Kp, nonsal, salient, S,
                         S_pad, posmap, flags, SQMP_OUT_C4, acodes, ascale, xs, workspace,
                         ws_bytes, stream, &cw);
+}
+
+// ---------------------------------------------------------------- sibling layers (group)
+// One quantizer pass for a layer and up to two siblings that quantize the same input with the
+// same salient set and sorted per_group mode (q/k/v, gate/up): the statistics and the rank
+// once, the rank tables of every sibling from the same launch, and every sibling's OUT_FP
+// operand written from the same quantized values (each in its own packed order).  Every
+// output equals what sqmp_quant_act_v2(SQMP_OUT_FP) writes for that sibling, bit for bit.
+extern "C" int sqmp_quant_act_group(void* x, int dtype, int M, int K, int amode, int n_bits,
+                                    int group_size, int nout, const int32_t* const* amaps,
+                                    const int32_t* const* posmaps, int Kp, const int32_t* nonsal,
+                                    const int32_t* salient, int S, int S_pad, int flags,
+                                    void* const* outs, void* workspace, size_t ws_bytes,
+                                    void* stream) {
+  if (nout < 1 || nout > 3 || !amaps || !posmaps || !outs) return SQMP_EINVAL;
+  for (int o = 0; o < nout; ++o)
+    if (!amaps[o] || !posmaps[o] || !outs[o]) return SQMP_EINVAL;
+  if (nout == 1)
+    return sqmp_quant_act_v2(x, dtype, M, K, amode, n_bits, group_size, amaps[0], Kp, nonsal,
+                             salient, S, S_pad, posmaps[0], flags, SQMP_OUT_FP, outs[0], nullptr,
+                             nullptr, workspace, ws_bytes, stream);
+  if (dtype != SQMP_F16 && dtype != SQMP_BF16) return SQMP_EUNSUPPORTED;
+  if (amode != SQMP_ACT_PER_GROUP && amode != SQMP_ACT_PER_GROUP_MEAN3STD) return SQMP_EUNSUPPORTED;
+  if (flags != SQMP_QA_CLEAN_WS) return SQMP_EUNSUPPORTED;
+  if (M < 0 || K <= 0 || K > 65000 || S < 0 || S >= K || !x || !nonsal || (S > 0 && !salient))
+    return SQMP_EINVAL;
+  if (n_bits < 2 || n_bits > 8) return SQMP_EUNSUPPORTED;
+  if (Kp < K || Kp % 128 != 0 || S_pad < S || S_pad % 64 != 0) return SQMP_EINVAL;
+  const int Kn = K - S;
+  if (!rank_table_fits(Kn)) return SQMP_EUNSUPPORTED;
+  for (int o = 0; o < nout; ++o)
+    if (!quant_lc_supported(dtype, M, K, true, group_size, Kn, Kp, S_pad, x, outs[o]))
+      return SQMP_EUNSUPPORTED;
+  if (group_size < 16) return SQMP_EUNSUPPORTED;
+  if (M == 0) return SQMP_OK;
+  if (ws_bytes < sqmp_act_workspace_bytes(M, K, Kp) || !workspace) return SQMP_EWORKSPACE;
+  hipStream_t s = (hipStream_t)stream;
+  const size_t k64 = ws_k64(K);
+  uint32_t* cmax = (uint32_t*)workspace;
+  int32_t* rank = (int32_t*)(cmax + k64);
+  int32_t* part = rank + k64;
+  uint32_t* ent = (uint32_t*)(part + k64 * (size_t)rank_tiles(K));
+  uint32_t* lctab = ent + round_up(Kp > K ? Kp : K, 64);
+  int32_t* counts = (int32_t*)(lctab + round_up(K, 4096));
+  int32_t* colsorted = counts + k64;
+  double* sums = (double*)((uint32_t*)workspace + ws_u32_words(K, Kp));
+  uint32_t* sibtab = (uint32_t*)((unsigned char*)workspace + ws_sib_offset(K, Kp));
+  const int lc_len = (int)round_up(K, 4096);
+  const uint32_t lc_none = (uint32_t)(Kp + S_pad) | ((uint32_t)(Kp + S_pad + 1) << 16);
+  SibTables st;
+  LcSib ls;
+  st.n = ls.n = nout - 1;
+  for (int o = 0; o + 1 < nout; ++o) {
+    st.posmap[o] = posmaps[o + 1];
+    st.lctab[o] = sibtab + (size_t)o * lc_len;
+    ls.tab[o] = st.lctab[o];
+    ls.amap[o] = amaps[o + 1];
+    ls.out[o] = outs[o + 1];
+  }
+  uint32_t* ctr = (uint32_t*)((unsigned char*)workspace + ws_ctr_offset(K, Kp));
+  int r = SQMP_EUNSUPPORTED;
+  if (amode == SQMP_ACT_PER_GROUP)
+    r = launch_colmax_rank(x, dtype, M, K, cmax, ctr, nonsal, Kn, posmaps[0], colsorted, lctab,
+                           lc_len, lc_none, s, st);
+  if (r != SQMP_OK) {
+    r = amode == SQMP_ACT_PER_GROUP ? launch_colmax(x, dtype, M, K, cmax, s, false)
+                                    : launch_colkey_mean3std(x, dtype, M, K, sums, cmax, s, true);
+    if (r) return r;
+    r = launch_rank_table(cmax, nonsal, Kn, posmaps[0], colsorted, lctab, lc_len, lc_none, s, st);
+    if (r) return r;
+  }
+  return launch_quant_lc_group(dtype, x, M, K, (1 << (n_bits - 1)) - 1, group_size, lctab, Kn,
+                               amaps[0], Kp, salient, S, S_pad, cmax, nonsal, outs[0], cmax,
+                               (int)k64, ls, s);
 }

@@ -210,15 +210,16 @@ __device__ inline uint32_t f8_pair(uint32_t v, const PairScale& c) {
 // 2 or 4 row tiles: 16 TJ-row blocks nb = m / (16 TJ), row tile j = m / 16 % TJ, r16 = m % 16);
 // -ldsc = ngq * 8 + TJ.
 // (the body of quant_lc_kernel: workgroup `bid` of `nblk` quantizer workgroups)
-template <class DT, int MODE, int RPL, int GS, int F8 = 0>
+template <class DT, int MODE, int RPL, int GS, int F8 = 0, int NOUT = 1>
 __device__ __forceinline__ void quant_lc_body(
     const typename DT::T* x, int M, int K, int q_max, int G,
     const uint32_t* __restrict__ lctab, int Kn, const int32_t* __restrict__ amap, int P,
     const int32_t* __restrict__ sal, int S, int S_pad, const uint32_t* __restrict__ cmax,
     const int32_t* __restrict__ nonsal, typename DT::T* out, uint32_t* __restrict__ key_clear,
     int clear_words, float* __restrict__ out_scale, typename DT::T* __restrict__ out_xs,
-    int Kq, int ldsc, const int bid, const int nblk) {
+    int Kq, int ldsc, const int bid, const int nblk, const LcSib& sib = LcSib{}) {
   static_assert(!F8 || F8 == 3 || MODE != LC_MODE_GROUP, "F8 codes need one scale per row");
+  static_assert(NOUT == 1 || (F8 == 0 && GS == 0), "sibling outputs: OUT_FP, groups >= RPL");
   static_assert(F8 != 3 || (MODE == LC_MODE_GROUP && GS == 0), "C4: groups of >= RPL ranks");
   // x and out alias for in-place output quantization (every row is read before it is
   // written: a workgroup stores a pair only after loading it)
@@ -266,22 +267,30 @@ __device__ __forceinline__ void quant_lc_body(
   // ---- once per workgroup: salient-position mask, zeroed buffer (+ two spare words: W =
   // a zero read by padding table entries, W + 1 = a write-only sink for their scatter)
   const int zp0 = 64 * tid;
-  uint64_t zmask = 0;
-  if (amap) {  // NULL: in-place output quantization, salient columns pass through
-    if (zp0 + 64 <= K && ((uintptr_t)amap & 15) == 0) {
+  auto zmask_of = [&](const int32_t* am) {
+    uint64_t zm = 0;
+    if (am) {  // NULL: in-place output quantization, salient columns pass through
+      if (zp0 + 64 <= K && ((uintptr_t)am & 15) == 0) {
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const u32x4 e = ((const u32x4*)(amap + zp0))[i];
+        for (int i = 0; i < 16; ++i) {
+          const u32x4 e = ((const u32x4*)(am + zp0))[i];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) zmask |= (uint64_t)(e[j] >> 31) << (4 * i + j);
-      }
-    } else {
-      for (int i = 0; i < 64; ++i) {
-        const int p = zp0 + i;
-        if (p < K && amap[p] < 0) zmask |= 1ull << i;
+          for (int j = 0; j < 4; ++j) zm |= (uint64_t)(e[j] >> 31) << (4 * i + j);
+        }
+      } else {
+        for (int i = 0; i < 64; ++i) {
+          const int p = zp0 + i;
+          if (p < K && am[p] < 0) zm |= 1ull << i;
+        }
       }
     }
-  }
+    return zm;
+  };
+  const uint64_t zmask = zmask_of(amap);
+  // the sibling outputs' salient / padding positions (their own packed orders)
+  uint64_t zmask_s[NOUT > 1 ? NOUT - 1 : 1];
+#pragma unroll
+  for (int o = 0; o + 1 < NOUT; ++o) zmask_s[o] = zmask_of(sib.amap[o]);
   for (int c = tid; c < W + 2; c += nthr) lc_buf[c] = 0u;
   // the column statistics of this call, read by the (completed) table kernel: restore the
   // clean-workspace zeros
@@ -315,6 +324,16 @@ __device__ __forceinline__ void quant_lc_body(
       const u32x4 e = ((const u32x4*)(lctab + toff))[i];
       tab[4 * i] = e[0]; tab[4 * i + 1] = e[1]; tab[4 * i + 2] = e[2]; tab[4 * i + 3] = e[3];
     }
+    // the siblings' tables (same ranks, their packed positions)
+    uint32_t tabs[NOUT > 1 ? NOUT - 1 : 1][RPL];
+#pragma unroll
+    for (int o = 0; o + 1 < NOUT; ++o)
+#pragma unroll
+      for (int i = 0; i < RPL / 4; ++i) {
+        const u32x4 e = ((const u32x4*)(sib.tab[o] + toff))[i];
+        tabs[o][4 * i] = e[0]; tabs[o][4 * i + 1] = e[1];
+        tabs[o][4 * i + 2] = e[2]; tabs[o][4 * i + 3] = e[3];
+      }
     // ---- interleave the two rows into LDS: word k = (x[m0][k], x[m0+1][k])
 #pragma unroll
     for (int i = 0; i < LC_CH; ++i) {
@@ -450,7 +469,10 @@ __device__ __forceinline__ void quant_lc_body(
         }
       } else {
 #pragma unroll
-        for (int i = 0; i < RPL; ++i) lc_buf[tab[i] >> 16] = quant_pair<DT>(v[i], c);
+        for (int i = 0; i < RPL; ++i) {
+          v[i] = quant_pair<DT>(v[i], c);  // kept for the sibling outputs
+          lc_buf[tab[i] >> 16] = v[i];
+        }
       }
     }
     // salient columns' own packed positions hold 0 (their weight codes are 0 too)
@@ -530,21 +552,50 @@ __device__ __forceinline__ void quant_lc_body(
       if (has1) ((u32x4*)o1)[c] = y1;
     }
     __syncthreads();  // the buffer is rewritten by the next pair
+    // ---- the sibling outputs: the same quantized pairs scattered to their packed positions
+    // (every position < P is rewritten: non-salient ones by the scatter, salient ones zeroed;
+    // the exact salient tail >= P is shared)
+#pragma unroll
+    for (int o = 0; o + 1 < NOUT; ++o) {
+#pragma unroll
+      for (int i = 0; i < RPL; ++i) lc_buf[tabs[o][i] >> 16] = v[i];
+      for (uint64_t zm = zmask_s[o]; zm; zm &= zm - 1) lc_buf[zp0 + __builtin_ctzll(zm)] = 0u;
+      __syncthreads();
+      T* s0 = (T*)sib.out[o] + (size_t)m0 * W;
+      T* s1 = (T*)sib.out[o] + (size_t)(m0 + 1) * W;
+      for (int c = tid; c < ochk; c += nthr) {
+        const u32x4 a = ((const u32x4*)lc_buf)[2 * c];
+        const u32x4 b = ((const u32x4*)lc_buf)[2 * c + 1];
+        u32x4 y0, y1;
+        y0[0] = __builtin_amdgcn_perm(a[1], a[0], 0x05040100u);
+        y0[1] = __builtin_amdgcn_perm(a[3], a[2], 0x05040100u);
+        y0[2] = __builtin_amdgcn_perm(b[1], b[0], 0x05040100u);
+        y0[3] = __builtin_amdgcn_perm(b[3], b[2], 0x05040100u);
+        y1[0] = __builtin_amdgcn_perm(a[1], a[0], 0x07060302u);
+        y1[1] = __builtin_amdgcn_perm(a[3], a[2], 0x07060302u);
+        y1[2] = __builtin_amdgcn_perm(b[1], b[0], 0x07060302u);
+        y1[3] = __builtin_amdgcn_perm(b[3], b[2], 0x07060302u);
+        ((u32x4*)s0)[c] = y0;
+        if (has1) ((u32x4*)s1)[c] = y1;
+      }
+      __syncthreads();
+    }
   }
 }
 
 
-template <class DT, int MODE, int RPL, int GS, int F8 = 0>
+template <class DT, int MODE, int RPL, int GS, int F8 = 0, int NOUT = 1>
 __global__ __launch_bounds__(1024) void quant_lc_kernel(
     const typename DT::T* x, int M, int K, int q_max, int G,
     const uint32_t* __restrict__ lctab, int Kn, const int32_t* __restrict__ amap, int P,
     const int32_t* __restrict__ sal, int S, int S_pad, const uint32_t* __restrict__ cmax,
     const int32_t* __restrict__ nonsal, typename DT::T* out, uint32_t* __restrict__ key_clear,
     int clear_words, float* __restrict__ out_scale, typename DT::T* __restrict__ out_xs,
-    int Kq, int ldsc) {
-  quant_lc_body<DT, MODE, RPL, GS, F8>(x, M, K, q_max, G, lctab, Kn, amap, P, sal, S, S_pad,
-                                       cmax, nonsal, out, key_clear, clear_words, out_scale,
-                                       out_xs, Kq, ldsc, blockIdx.x, gridDim.x);
+    int Kq, int ldsc, LcSib sib) {
+  quant_lc_body<DT, MODE, RPL, GS, F8, NOUT>(x, M, K, q_max, G, lctab, Kn, amap, P, sal, S,
+                                             S_pad, cmax, nonsal, out, key_clear, clear_words,
+                                             out_scale, out_xs, Kq, ldsc, blockIdx.x, gridDim.x,
+                                             sib);
 }
 
 // ---- the activation-order weight operand (sqmp_gemm_fqt): wp[n][j] = W_hat[n][pos_j],
@@ -675,24 +726,25 @@ static int lc_grid(int npair, int slots) {
   return cdiv(npair, ppw);
 }
 
-template <class DT, int MODE, int GS, int F8>
+template <class DT, int MODE, int GS, int F8, int NOUT = 1>
 static int quant_lc_launch(const void* x, int M, int K, int q_max, int G, const uint32_t* lctab,
                            int Kn, const int32_t* amap, int P, const int32_t* sal, int S,
                            int S_pad, const uint32_t* cmax, const int32_t* nonsal, void* out,
                            uint32_t* key_clear, int clear_words, float* out_scale,
-                           void* out_xs, hipStream_t s, int Kq = 0, int ldsc = 0) {
+                           void* out_xs, hipStream_t s, int Kq = 0, int ldsc = 0,
+                           const LcSib& sib = LcSib{}) {
   typedef typename DT::T T;
+  const void* kf = (const void*)quant_lc_kernel<DT, MODE, LC_RPL, GS, F8, NOUT>;
   const int nw = lc_waves(K, Kn);
   const size_t lds = sizeof(uint32_t) * (size_t)(P + S_pad + 8);
-  SQMP_HIP_CHECK(hipFuncSetAttribute((const void*)quant_lc_kernel<DT, MODE, LC_RPL, GS, F8>,
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  int per_cu = occ_per_cu((const void*)quant_lc_kernel<DT, MODE, LC_RPL, GS, F8>, 64 * nw, lds);
+  SQMP_HIP_CHECK(hipFuncSetAttribute(kf, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  int per_cu = occ_per_cu(kf, 64 * nw, lds);
   if (const char* e = getenv("SQMP_LC_PERCU"))  // tuning only (0 / unparsable: the default)
     if (atoi(e) > 0) per_cu = atoi(e);
   const int grid = lc_grid((M + 1) / 2, per_cu);
-  quant_lc_kernel<DT, MODE, LC_RPL, GS, F8><<<dim3(grid), dim3(64 * nw), lds, s>>>(
+  quant_lc_kernel<DT, MODE, LC_RPL, GS, F8, NOUT><<<dim3(grid), dim3(64 * nw), lds, s>>>(
       (const T*)x, M, K, q_max, G, lctab, Kn, amap, P, sal, S, S_pad, cmax, nonsal, (T*)out,
-      key_clear, clear_words, out_scale, (T*)out_xs, Kq, ldsc);
+      key_clear, clear_words, out_scale, (T*)out_xs, Kq, ldsc, sib);
   SQMP_LAUNCH_CHECK();
   return SQMP_OK;
 }
@@ -732,6 +784,26 @@ int launch_quant_lc(int dtype, int mode, const void* x, int M, int K, int q_max,
   return SQMP_EUNSUPPORTED;
 #undef SQMP_LC_MODE
 #undef SQMP_LC
+}
+
+// The OUT_FP quantizer for a layer and up to two siblings (sqmp_quant_act_group): group mode,
+// groups of >= LC_RPL ranks; out[0] in the packed order of lctab, sib.out[o] in sib.tab[o]'s.
+int launch_quant_lc_group(int dtype, const void* x, int M, int K, int q_max, int G,
+                          const uint32_t* lctab, int Kn, const int32_t* amap, int P,
+                          const int32_t* sal, int S, int S_pad, const uint32_t* cmax,
+                          const int32_t* nonsal, void* out, uint32_t* key_clear, int clear_words,
+                          const LcSib& sib, hipStream_t s) {
+  if (G < LC_RPL || sib.n < 0 || sib.n > 2) return SQMP_EUNSUPPORTED;
+#define SQMP_LCG(DTT, NO)                                                                     \
+  quant_lc_launch<DTT, LC_MODE_GROUP, 0, 0, NO>(x, M, K, q_max, G, lctab, Kn, amap, P, sal, S, \
+                                               S_pad, cmax, nonsal, out, key_clear,            \
+                                               clear_words, nullptr, nullptr, s, 0, 0, sib)
+#define SQMP_LCG_N(DTT) (sib.n == 0 ? SQMP_LCG(DTT, 1) : sib.n == 1 ? SQMP_LCG(DTT, 2) : SQMP_LCG(DTT, 3))
+  if (dtype == SQMP_F16) return SQMP_LCG_N(F16);
+  if (dtype == SQMP_BF16) return SQMP_LCG_N(BF16);
+  return SQMP_EUNSUPPORTED;
+#undef SQMP_LCG_N
+#undef SQMP_LCG
 }
 
 static int pw_rows(int Kp) {

@@ -116,6 +116,21 @@ __device__ inline int lane_now() {
 
 __host__ __device__ inline int brev3(int c) { return ((c & 1) << 2) | (c & 2) | ((c >> 2) & 1); }
 
+// Sibling problems of one grouped launch (sqmp_gemm_fq7_group): problem p owns the global
+// tiles [tile_end[p - 1], tile_end[p]) and its own operands; M, Kp, S_pad, Gw, ngw are shared.
+constexpr int FQ7_GRP_MAX = 4;
+struct Fq7Grp {
+  const void* A[FQ7_GRP_MAX];
+  const uint32_t* Bt[FQ7_GRP_MAX];
+  const void* St[FQ7_GRP_MAX];
+  const void* Salt[FQ7_GRP_MAX];
+  const void* bias[FQ7_GRP_MAX];
+  void* Y[FQ7_GRP_MAX];
+  uint32_t* colmax[FQ7_GRP_MAX];
+  int N[FQ7_GRP_MAX], tiles_n[FQ7_GRP_MAX], tile_end[FQ7_GRP_MAX];
+  int n;
+};
+
 // DIAG (timing diagnostics, wrong results by design, instantiated only in a SQMP_DIAG_BUILD;
 // 0 = the product kernel): 1 no weight
 // register loads after the prologue, 2 no A DMA after the prologue, 3 no int4 decode, 4 no
@@ -136,13 +151,16 @@ __host__ __device__ inline int brev3(int c) { return ((c & 1) << 2) | (c & 2) | 
 // i > 0 addressed through the scalar offset, the two fragment offsets kept instead of the lane
 // index, which the salient tail and the epilogue compute again; spill-free at TM = 128 only,
 // checked by tests/test_fq7_build_cpu.py)
-template <class DT, int GB, int TM, int J, int DIAG = 0, bool TR = false, int OPT = 0>
+// GRP: a grouped launch over the problems of `grp` (A, Bt, St, Salt, bias, Y, colmax, N and
+// tiles_n are taken from the block's problem; the other arguments are shared)
+template <class DT, int GB, int TM, int J, int DIAG = 0, bool TR = false, int OPT = 0,
+          bool GRP = false>
 __global__ __launch_bounds__(512, (OPT & 8) ? 4 : 1) void gemm_fq7_kernel(
     const typename DT::T* __restrict__ A, const uint32_t* __restrict__ Bt,
     const typename DT::T* __restrict__ St, const typename DT::T* __restrict__ Salt,
     const typename DT::T* __restrict__ bias, typename DT::T* __restrict__ Y, int M, int N,
     int Kp, int S_pad, int Gw, int ngw, int tiles_m, int tiles_n, int group_m,
-    uint32_t* __restrict__ colmax, int nt) {
+    uint32_t* __restrict__ colmax, int nt, const Fq7Grp grp) {
   typedef typename DT::T T;
   constexpr int I = TM / 16;            // 16 x 16 tiles per wave: TM rows x 16 J weight rows
   constexpr int TN = 128 * J, WR = 16 * J;  // tile width, weight rows per wave
@@ -158,7 +176,33 @@ __global__ __launch_bounds__(512, (OPT & 8) ? 4 : 1) void gemm_fq7_kernel(
   __shared__ __attribute__((aligned(16))) unsigned char lds[LDS_BYTES];
 
   int tm, tn;
-  tile_coords(tiles_m, tiles_n, group_m, tm, tn);
+  if constexpr (GRP) {
+    // XCD-aware bijective remap over every problem's tiles, then the problem and its own
+    // grouped raster (as tile_coords)
+    const int nwg = grp.tile_end[grp.n - 1];
+    const int bid = blockIdx.x, xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+    int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+    int p = 0;
+#pragma unroll
+    for (int i = 1; i < FQ7_GRP_MAX; ++i)
+      if (i < grp.n && wg >= grp.tile_end[i - 1]) p = i;
+    wg -= p > 0 ? grp.tile_end[p - 1] : 0;
+    A = (const T*)grp.A[p];
+    Bt = grp.Bt[p];
+    St = (const T*)grp.St[p];
+    Salt = (const T*)grp.Salt[p];
+    bias = (const T*)grp.bias[p];
+    Y = (T*)grp.Y[p];
+    colmax = grp.colmax[p];
+    N = grp.N[p];
+    tiles_n = grp.tiles_n[p];
+    const int per_group = group_m * tiles_n, gid = wg / per_group, first_m = gid * group_m;
+    const int gsz = min(tiles_m - first_m, group_m), in_g = wg - gid * per_group;
+    tm = first_m + in_g % gsz;
+    tn = in_g / gsz;
+  } else {
+    tile_coords(tiles_m, tiles_n, group_m, tm, tn);
+  }
   const int m0 = tm * TM, n0 = tn * TN;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -599,7 +643,7 @@ static int launch_k(const void* a, const void* bt, const void* st, const void* s
 #define SQMP_PK(O)                                                                              \
   gemm_fq7_kernel<DT, GB, TM, J, DIAG, false, O><<<dim3(tiles_m * tiles_n), dim3(512), 0, s>>>( \
       (const T*)a, (const uint32_t*)bt, (const T*)st, (const T*)salt, (const T*)bias, (T*)y, M,  \
-      N, Kp, S_pad, Gw, ngw, tiles_m, tiles_n, group_m_env(), colmax, nt)
+      N, Kp, S_pad, Gw, ngw, tiles_m, tiles_n, group_m_env(), colmax, nt, Fq7Grp{})
   // OPT variants (setprio for waves 4-7, loader split) for the fp16 J = 2 kernels, the
   // 2048-token Llama GEMMs (A/B knob SQMP_FQ7_OPT, read per launch)
   if constexpr (std::is_same<DT, F16>::value && J == 2 && GB == 1 && DIAG == 0) {
@@ -660,6 +704,42 @@ static int dispatch(const void* a, const void* bt, const void* st, const void* s
 #undef SQMP_FQ7
 }
 
+// The grouped packed-order launch (sqmp_gemm_fq7_group): J = 2, whole 64-blocks per weight
+// group.  Row tiles of 256 where the problems' 256 x 256 tiles fill two rounds of the CUs, else
+// of 128 (two workgroups per CU where that gives more than one tile per CU), as dispatch();
+// SQMP_FQ7G_TM = 128 / 256 overrides (A/B, read per launch).
+template <class DT>
+static int dispatch_group(Fq7Grp& g, int M, int Kp, int S_pad, int Gw, int ngw, int nt,
+                          hipStream_t s) {
+  typedef typename DT::T T;
+  long t256 = 0;
+  for (int p = 0; p < g.n; ++p) t256 += (long)cdiv(M, 256) * cdiv(g.N[p], 256);
+  int tm = t256 >= 512 ? 256 : 128;
+  if (const char* e = getenv("SQMP_FQ7G_TM")) tm = atoi(e) == 256 ? 256 : 128;
+  if (std::is_same<DT, BF16>::value) tm = 128;  // (bf16 at 256 x 256 puts an array in scratch)
+  const int tiles_m = cdiv(M, tm);
+  int end = 0;
+  for (int p = 0; p < g.n; ++p) {
+    g.tiles_n[p] = cdiv(g.N[p], 256);
+    end += tiles_m * g.tiles_n[p];
+    g.tile_end[p] = end;
+  }
+#define SQMP_G(TMV, O)                                                                          \
+  gemm_fq7_kernel<DT, 1, TMV, 2, 0, false, O, true><<<dim3(end), dim3(512), 0, s>>>(            \
+      (const T*)nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, M, 0, Kp, S_pad, Gw, ngw, \
+      tiles_m, 0, group_m_env(), nullptr, nt, g)
+  if (tm == 256) {
+    if constexpr (std::is_same<DT, F16>::value) SQMP_G(256, 3);
+  } else if (opt_pk_env(128, end) == 8) {
+    SQMP_G(128, 8);
+  } else {
+    SQMP_G(128, 3);
+  }
+#undef SQMP_G
+  SQMP_LAUNCH_CHECK();
+  return SQMP_OK;
+}
+
 // the activation-order GEMM (TR): kernel M = weight rows N (wp rows), kernel N = tokens M
 // J = 2: 256 weight rows x 256 tokens (8 waves of 32 tokens); J = 4: 128 weight rows x 512
 // tokens (8 waves of 64 tokens: half the wp LDS-DMA and LDS fragment reads per MFMA, twice the
@@ -674,13 +754,13 @@ static int dispatch_tr(const void* wp, const void* codes_t, const void* scale_t,
 #define SQMP_TR(O)                                                                              \
   gemm_fq7_kernel<DT, 1, TM, J, 0, true, O><<<dim3(tiles_m * tiles_n), dim3(512), 0, s>>>(      \
       (const T*)wp, (const uint32_t*)codes_t, (const T*)scale_t, (const T*)sal_t, (const T*)bias, \
-      (T*)y, N, M, Kq, S_pad, G, ngq, tiles_m, tiles_n, group_m_tr_env(), colmax, nt)
+      (T*)y, N, M, Kq, S_pad, G, ngq, tiles_m, tiles_n, group_m_tr_env(), colmax, nt, Fq7Grp{})
   const int nt = nt_output((size_t)M * N * sizeof(T)) ? 1 : 0;
 #ifdef SQMP_DIAG_BUILD
 #define SQMP_TRD(D)                                                                             \
   gemm_fq7_kernel<DT, 1, TM, 2, D, true, 3><<<dim3(tiles_m * tiles_n), dim3(512), 0, s>>>(      \
       (const T*)wp, (const uint32_t*)codes_t, (const T*)scale_t, (const T*)sal_t, (const T*)bias, \
-      (T*)y, N, M, Kq, S_pad, G, ngq, tiles_m, tiles_n, group_m_tr_env(), colmax, nt)
+      (T*)y, N, M, Kq, S_pad, G, ngq, tiles_m, tiles_n, group_m_tr_env(), colmax, nt, Fq7Grp{})
   if (std::is_same<DT, F16>::value && J == 2 && diag_env() > 0) {
     switch (diag_env()) {
       case 1: SQMP_TRD(1); break;
@@ -711,7 +791,7 @@ static int dispatch_tr(const void* wp, const void* codes_t, const void* scale_t,
 #define SQMP_TR128(O)                                                                           \
   gemm_fq7_kernel<DT, 1, 128, 2, 0, true, O><<<dim3(cdiv(N, 128) * tiles_n), dim3(512), 0, s>>>( \
       (const T*)wp, (const uint32_t*)codes_t, (const T*)scale_t, (const T*)sal_t, (const T*)bias, \
-      (T*)y, N, M, Kq, S_pad, G, ngq, cdiv(N, 128), tiles_n, group_m_tr_env(), colmax, nt)
+      (T*)y, N, M, Kq, S_pad, G, ngq, cdiv(N, 128), tiles_n, group_m_tr_env(), colmax, nt, Fq7Grp{})
       // 128-row tiles at two workgroups per CU (OPT bit 3; 8, 9 spill at 128 VGPRs)
       case 10: if constexpr (TM == 256) { SQMP_TR128(10); } else { SQMP_TR(0); } break;
       case 11: if constexpr (TM == 256) { SQMP_TR128(11); } else { SQMP_TR(0); } break;
@@ -790,6 +870,38 @@ extern "C" int sqmp_gemm_fq7(const void* a, const void* codes_t, const void* sca
   if (dtype == SQMP_F16)
     return fq7::dispatch<F16>(a, codes_t, scale_t, sal_t, bias, y, M, N, Kp, S_pad, Gw, ngw, J, colmax, s);
   return fq7::dispatch<BF16>(a, codes_t, scale_t, sal_t, bias, y, M, N, Kp, S_pad, Gw, ngw, J, colmax, s);
+}
+
+extern "C" int sqmp_gemm_fq7_group(const sqmp_fq7_problem* probs, int nprob, int dtype, int M,
+                                   int Kp, int S_pad, int Gw, int ngw, int J, void* stream) {
+  if (!probs || nprob < 1 || nprob > fq7::FQ7_GRP_MAX) return SQMP_EINVAL;
+  if (M < 0 || Kp <= 0 || Kp % 128 || S_pad < 0 || S_pad % 64 || Gw <= 0 || ngw <= 0)
+    return SQMP_EINVAL;
+  if (J != 2 || Gw % 64) return SQMP_EUNSUPPORTED;
+  if (dtype != SQMP_F16 && dtype != SQMP_BF16) return SQMP_EUNSUPPORTED;
+  fq7::Fq7Grp g{};
+  g.n = nprob;
+  size_t ybytes = 0;
+  for (int p = 0; p < nprob; ++p) {
+    const sqmp_fq7_problem& q = probs[p];
+    if (!q.a || !q.codes_t || !q.scale_t || !q.sal_t || !q.y || q.N <= 0) return SQMP_EINVAL;
+    if (q.N % 8) return SQMP_EUNSUPPORTED;  // whole 16-B output chunks
+    g.A[p] = q.a;
+    g.Bt[p] = (const uint32_t*)q.codes_t;
+    g.St[p] = q.scale_t;
+    g.Salt[p] = q.sal_t;
+    g.bias[p] = q.bias;
+    g.Y[p] = q.y;
+    g.colmax[p] = q.colmax;
+    g.N[p] = q.N;
+    const size_t yb = (size_t)M * q.N * 2;
+    ybytes = yb > ybytes ? yb : ybytes;
+  }
+  if (M == 0) return SQMP_OK;
+  const int nt = nt_output(ybytes) ? 1 : 0;
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == SQMP_F16) return fq7::dispatch_group<F16>(g, M, Kp, S_pad, Gw, ngw, nt, s);
+  return fq7::dispatch_group<BF16>(g, M, Kp, S_pad, Gw, ngw, nt, s);
 }
 
 // sqmp_gemm_fqt7: the activation-order GEMM (sqmp_gemm_fqt) on fq7's register-operand

@@ -49,6 +49,23 @@ int launch_build_maps(int K, int Kp, const int32_t* rank_by_col, const int32_t* 
                       int S, int32_t* perm, int32_t* amap, int32_t* amap_fq,
                       int32_t* nonsal, hipStream_t s);
 
+// Sibling layers of one input (q/k/v, gate/up: same K, salient set and act mode, each in its
+// own packed order): the rank-table kernel also writes their rank-ordered tables
+// lctab[o][r] = column | posmap[o][column] << 16 (padding ranks: the (zero, sink) entry).
+struct SibTables {
+  int n = 0;
+  const int32_t* posmap[2] = {nullptr, nullptr};
+  uint32_t* lctab[2] = {nullptr, nullptr};
+};
+// ... and the lane-contiguous quantizer writes their OUT_FP operands from the same pass:
+// out[o] in the packed order of table tab[o], zeros at the positions amap[o] marks < 0.
+struct LcSib {
+  int n = 0;
+  const uint32_t* tab[2] = {nullptr, nullptr};
+  const int32_t* amap[2] = {nullptr, nullptr};
+  void* out[2] = {nullptr, nullptr};
+};
+
 // Lane-contiguous OUT_FP quantizer (sqmp_actquant_lc.hip).  mode: 0 token, 1 tensor,
 // 2 group (any rank order: sorted / unsorted / mean3std -- lctab carries it).
 bool quant_lc_supported(int dtype, int M, int K, int amode_group, int G, int Kn, int P,
@@ -60,6 +77,12 @@ int launch_quant_lc(int dtype, int mode, const void* x, int M, int K, int q_max,
                     hipStream_t s, float* out_scale = nullptr, void* out_xs = nullptr);
 // key_clear: zeroed (clear_words % 4 == 0), may be NULL.  out_scale != NULL selects the
 // e4m3 code output (token / tensor modes): out = codes [M][P], out_xs = D [M][S_pad].
+// group mode with up to two sibling outputs (sib.n), fp16 / bf16, G >= 16
+int launch_quant_lc_group(int dtype, const void* x, int M, int K, int q_max, int G,
+                          const uint32_t* lctab, int Kn, const int32_t* amap, int P,
+                          const int32_t* sal, int S, int S_pad, const uint32_t* cmax,
+                          const int32_t* nonsal, void* out, uint32_t* key_clear, int clear_words,
+                          const LcSib& sib, hipStream_t s);
 
 // SQMP_OUT_C4 lane-contiguous quantizer (act-order int4 codes, group scales [Kq/G][ldsc],
 // exact salient columns); P = the table's packed length (Kp).  cw != NULL: the same launch

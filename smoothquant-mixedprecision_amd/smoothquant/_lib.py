@@ -30,6 +30,16 @@ QA_CLEAN_WS, QA_REUSE_STATS, QA_STATS_GIVEN, QA_TILED, QA_TILED4 = 1, 2, 4, 8, 1
 _vp, _i, _sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t
 _ip = ctypes.POINTER(ctypes.c_int)
 
+
+
+class Fq7Problem(ctypes.Structure):
+    """sqmp_fq7_problem (include/sqmp_w4a4.h): one problem of sqmp_gemm_fq7_group."""
+    _fields_ = [("a", ctypes.c_void_p), ("codes_t", ctypes.c_void_p),
+                ("scale_t", ctypes.c_void_p), ("sal_t", ctypes.c_void_p),
+                ("bias", ctypes.c_void_p), ("y", ctypes.c_void_p), ("colmax", ctypes.c_void_p),
+                ("N", ctypes.c_int)]
+
+
 # name -> (restype, argtypes); the authoritative list of exported symbols
 SIGNATURES = {
     "sqmp_version": (ctypes.c_char_p, []),
@@ -72,6 +82,10 @@ SIGNATURES = {
     "sqmp_pack_fq7": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp]),
     "sqmp_gemm_fq7": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _vp,
                            _vp]),
+    "sqmp_quant_act_group": (_i, [_vp, _i, _i, _i, _i, _i, _i, _i, _vp, _vp, _i, _vp, _vp, _i,
+                                  _i, _i, _vp, _vp, _sz, _vp]),
+    "sqmp_gemm_fq7_group": (_i, [ctypes.POINTER(Fq7Problem), _i, _i, _i, _i, _i, _i, _i, _i,
+                                 _vp]),
     "sqmp_split2_f16": (_i, [_vp, _i, _i, _i, _vp, _vp, _vp]),
     "sqmp_row_exp": (_i, [_vp, _i, _i, _vp, _vp]),
     "sqmp_gemm_h2": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _vp, _vp]),

@@ -17,6 +17,7 @@ Reference map (file:line in fake_quant.py):
 from __future__ import annotations
 
 import inspect
+import weakref
 from functools import partial
 from typing import Optional
 
@@ -486,6 +487,11 @@ class W4A4Linear(nn.Module):
         if x.device.type != "cuda":
             raise RuntimeError("W4A4Linear.forward runs on a ROCm GPU only (HIP kernels); "
                                f"got a tensor on {x.device}")
+        grp = self.__dict__.get("_sqmp_group")
+        if grp is not None:
+            y = grp.forward(self, x, x2)
+            if y is not None:
+                return y
         pw = self.packed()
         if x2.dtype != pw.dtype:
             raise RuntimeError(f"expected input dtype {pw.dtype}, got {x2.dtype}")
@@ -591,6 +597,92 @@ class W4A4Linear(nn.Module):
 
 
 # ----------------------------------------------------------------------------------------
+# sibling layers (q/k/v, gate/up)
+# ----------------------------------------------------------------------------------------
+class SiblingGroup:
+    """W4A4Linear layers that the model calls one after another on the SAME input tensor:
+    q/k/v of an attention block and gate/up of a gated MLP (fake_quant.py:479-561 swaps them
+    one by one; the reference then repeats the activation quantization of :291-304 for each).
+
+    The first member called computes every member's output: one quantizer pass for all of
+    them (ops.quant_act_fp_group: the column statistics, the rank and the quantized values
+    once, each member's operand in its own packed order) and one GEMM launch
+    (ops.gemm_fq7_group).  The other members' outputs are kept for their own call on the same
+    input object (identity, storage, shape and version must match -- an input changed in
+    place, or another tensor, is computed as usual) and handed out once.  Each output is
+    bit-identical to the member's own forward; layers that the grouped kernels do not cover
+    (other act modes, output quantization, the activation-order path, ...) compute alone."""
+
+    def __init__(self, members):
+        self.members = list(members)
+        self._stash = {}  # member index -> (weakref(x), key(x), y)
+
+    def __getstate__(self):  # (pickling a model: outputs kept for one input are not state)
+        return {"members": self.members, "_stash": {}}
+
+    @staticmethod
+    def _key(x):
+        return (x.data_ptr(), tuple(x.shape), tuple(x.stride()), x.dtype, x._version)
+
+    def _plan(self, x2):
+        """(packed weights, biases, (mode, bits, group_size)) when the grouped kernels cover
+        every member for this input, else None."""
+        spec, pws, biases = None, [], []
+        for m in self.members:
+            if m.kernel != "auto" or resolve_quantizer(m.output_quant) is not None:
+                return None
+            sp = resolve_quantizer(m.act_quant)
+            if spec is None:
+                spec = sp
+            elif sp != spec:
+                return None
+            pw = m.packed()
+            b = None if m.bias is None else m.bias.reshape(-1)
+            if x2.dtype != pw.dtype or (b is not None and (b.dtype != pw.dtype
+                                                            or b.device != x2.device)):
+                return None
+            pws.append(pw)
+            biases.append(b)
+        if spec is None or not ops.f8_input_ok(x2):
+            return None
+        if not ops.group_eligible(pws, spec[0], spec[1], spec[2], x2.shape[0]):
+            return None
+        return pws, biases, spec
+
+    def forward(self, member, x, x2):
+        """member's output for x, or None (the member then computes alone)."""
+        i = self.members.index(member)
+        key = self._key(x)
+        e = self._stash.pop(i, None)
+        if e is not None and e[0]() is x and e[1] == key:
+            return e[2]
+        plan = self._plan(x2)
+        if plan is None:
+            return None
+        pws, biases, (mode, bits, gs) = plan
+        a = ops.quant_act_fp_group(x2.contiguous(), pws, mode, bits, gs)
+        ys = ops.gemm_fq7_group(a, pws, biases)
+        if x.dim() == 3:
+            ys = [y.view(x.shape[0], x.shape[1], -1) for y in ys]
+        ref = weakref.ref(x)
+        self._stash = {j: (ref, key, y) for j, y in enumerate(ys) if j != i}
+        return ys[i]
+
+
+def link_siblings(*modules):
+    """Declare W4A4Linear layers that the model calls one after another on the same input
+    (see SiblingGroup); returns the group.  quantize_llama_like / quantize_mixtral link q/k/v
+    and gate/up (w1/w3) themselves; other members than W4A4Linear are ignored."""
+    mods = [m for m in modules if isinstance(m, W4A4Linear)]
+    if len(mods) < 2:
+        return None
+    g = SiblingGroup(mods)
+    for m in mods:
+        m.__dict__["_sqmp_group"] = g
+    return g
+
+
+# ----------------------------------------------------------------------------------------
 # model surgery (fake_quant.py:377-799)
 # ----------------------------------------------------------------------------------------
 def _importance(input_feat, key, guarded):
@@ -637,10 +729,12 @@ def quantize_llama_like(model, weight_quant="per_channel", act_quant="per_token"
         if isinstance(m, (LlamaMLP, MistralMLP)):
             for proj in ("gate_proj", "up_proj", "down_proj"):
                 _swap(m, proj, pre + proj, input_feat, True, **kw)
+            link_siblings(m.gate_proj, m.up_proj)      # both called on the MLP input
         elif isinstance(m, (LlamaAttention, MistralAttention)):
             for proj in ("q_proj", "k_proj", "v_proj"):
                 _swap(m, proj, pre + proj, input_feat, True, quantize_output=quantize_bmm_input, **kw)
             _swap(m, "o_proj", pre + "o_proj", input_feat, True, **kw)
+            link_siblings(m.q_proj, m.k_proj, m.v_proj)  # all three on the hidden states
     return model
 
 
@@ -658,10 +752,12 @@ def quantize_mixtral(model, weight_quant="per_channel", act_quant="per_token",
         if expert_cls is not None and isinstance(m, expert_cls):
             for proj in ("w1", "w2", "w3"):
                 _swap(m, proj, pre + proj, input_feat, True, **kw)
+            link_siblings(m.w1, m.w3)                  # w2(act(w1(x)) * w3(x))
         elif isinstance(m, mm.MixtralAttention):
             for proj in ("q_proj", "k_proj", "v_proj"):
                 _swap(m, proj, pre + proj, input_feat, True, quantize_output=quantize_bmm_input, **kw)
             _swap(m, "o_proj", pre + "o_proj", input_feat, True, **kw)
+            link_siblings(m.q_proj, m.k_proj, m.v_proj)
         elif isinstance(m, mm.MixtralSparseMoeBlock) and isinstance(getattr(m, "gate", None), nn.Linear):
             _swap(m, "gate", pre + "gate", input_feat, True, **kw)
     return model

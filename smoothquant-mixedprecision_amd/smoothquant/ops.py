@@ -329,6 +329,88 @@ def quant_act_fp(x2: torch.Tensor, pw: PackedWeight, act_quant: str, n_bits: int
     return a
 
 
+def quant_act_fp_group(x2: torch.Tensor, pws, act_quant: str, n_bits: int,
+                       group_size: int):
+    """x [M, K] -> [A_0, ..., A_{n-1}]: quant_act_fp's operand for each packed weight of
+    `pws` (sibling layers: same K, Kp, S_pad and salient set), from ONE quantizer pass
+    (sqmp_quant_act_group); every A_o is bit-identical to quant_act_fp(x2, pws[o], ...)."""
+    _require_gpu(x2, "quant_act_group")
+    M, K = x2.shape
+    p0 = pws[0]
+    outs = [torch.empty((_pad_rows(M), p0.Kp + p0.S_pad), dtype=x2.dtype, device=x2.device)[:M]
+            for _ in pws]
+    for pw in pws:
+        if pw.posmap is None:
+            pw.posmap = build_posmap(pw.perm, K)
+    n = len(pws)
+    vp = ctypes.c_void_p
+    amaps = (vp * n)(*[t.data_ptr() for t in (pw.amap for pw in pws)])
+    posmaps = (vp * n)(*[pw.posmap.data_ptr() for pw in pws])
+    optr = (vp * n)(*[t.data_ptr() for t in outs])
+    lib = load()
+    nb = _ws_bytes(M, K, p0.Kp)
+    stream = torch.cuda.current_stream(x2.device).cuda_stream
+    e = _act_ws(x2.device, stream, K, p0.Kp, nb)
+    status = lib.sqmp_quant_act_group(_p(x2), _dtype_code(x2.dtype), M, K, ACT_MODES[act_quant],
+                                      n_bits, group_size, n, amaps, posmaps, p0.Kp,
+                                      _p(p0.nonsal), _p(p0.salient), p0.S, p0.S_pad,
+                                      _lib.QA_CLEAN_WS, optr, _p(e["buf"]), e["buf"].numel(),
+                                      vp(stream))
+    if status != _lib.SQMP_OK:
+        _WS.pop((x2.device.index, stream, K, p0.Kp, "in"), None)  # it may be left dirty
+        check(status, "quant_act_group")
+    # the workspace's sorted column list now describes x2 (a later sibling call on x2 may
+    # reuse it); no operand is kept for sqmp_permute_act
+    e["stats"] = (weakref.ref(x2), (x2.data_ptr(), tuple(x2.shape), x2.dtype, x2._version,
+                                    p0.sal_key, act_quant, M, K), p0.codes.data_ptr())
+    e["last_a"] = None
+    return outs
+
+
+def gemm_fq7_group(As, pws, biases):
+    """[y_0, ..., y_{n-1}] with y_o = gemm_fq7(As[o], pws[o], biases[o]) bit for bit, in one
+    launch (sqmp_gemm_fq7_group)."""
+    M = As[0].shape[0]
+    p0 = pws[0]
+    n = len(pws)
+    probs = (_lib.Fq7Problem * n)()
+    ys = []
+    for o, (a, pw, b) in enumerate(zip(As, pws, biases)):
+        bt, st, salt, J = fq7_operands(pw)
+        y = torch.empty((M, pw.N), dtype=pw.dtype, device=a.device)
+        ys.append(y)
+        _require_gpu(a, "gemm_fq7_group")
+        probs[o] = _lib.Fq7Problem(a.data_ptr(), bt.data_ptr(), st.data_ptr(), salt.data_ptr(),
+                                   None if b is None else b.data_ptr(), y.data_ptr(), None,
+                                   pw.N)
+    check(load().sqmp_gemm_fq7_group(probs, n, _dtype_code(p0.dtype), M, p0.Kp, p0.S_pad, p0.Gw,
+                                     p0.ngw, FQ7_J, _stream(As[0])), "gemm_fq7_group")
+    return ys
+
+
+def group_eligible(pws, act_quant: str, act_bits: int, group_size: int, M: int) -> bool:
+    """Whether quant_act_fp_group + gemm_fq7_group compute these sibling layers: sorted
+    per_group activations of <= 8 bits in power-of-two groups of 16 .. 1024 on the
+    packed-order path (below FQT_MIN_ROWS rows), 4-bit fq7 weights in whole 64-blocks per
+    group, one K (<= 16384, % 8 == 0) / Kp / S_pad / group geometry / salient set / dtype
+    (fp16 / bf16) for all, 2 or 3 layers."""
+    if not 2 <= len(pws) <= 3 or act_quant not in _SORTED or act_bits > 8:
+        return False
+    if not 16 <= group_size <= 1024 or group_size & (group_size - 1):
+        return False
+    if pws[0].K > 16384 or pws[0].K % 8:
+        return False
+    if FQT_MODE == "1" or (FQT_MODE == "auto" and M >= FQT_MIN_ROWS):
+        return False
+    p0 = pws[0]
+    if not FQ7_AUTO or p0.dtype not in (torch.float16, torch.bfloat16) or p0.K - p0.S <= 0:
+        return False
+    return all(fq7_eligible(pw) and pw.Gw % 64 == 0 and pw.K == p0.K and pw.Kp == p0.Kp
+               and pw.S_pad == p0.S_pad and pw.S == p0.S and pw.Gw == p0.Gw
+               and pw.ngw == p0.ngw and pw.sal_key == p0.sal_key and pw.dtype == p0.dtype
+               for pw in pws)
+
+
 # Activation-order path (SQMP_OUT_C4 + sqmp_perm_weight_c4 + sqmp_gemm_fqt) for sorted
 # per_group activations: the GEMM runs over the K - S non-salient positions in activation
 # order instead of the Kp packed positions (which carry S zero salient positions), and the

@@ -19,6 +19,7 @@
 #   layer            bench_llama.py (config 4 end to end)
 #   py:SCRIPT[:ARGS] python SCRIPT ARGS (comma-separated args)
 #   profpy:SCRIPT[:ARGS]  the same under rocprofv3 --kernel-trace --stats
+#   trace:SCRIPT[:ARGS]   the same under rocprofv3 --kernel-trace (per-dispatch CSV)
 # TAG (env, default "run") names the output directory.
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -33,9 +34,9 @@ step() {
   local s=$1
   case "$s" in
     tests|tests:*)
-      local k=""; [ "$s" != tests ] && k="-k ${s#tests:}"
+      local k=(); [ "$s" != tests ] && k=(-k "${s#tests:}")
       timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 180 --timeout-method thread \
-        -p no:cacheprovider $k > "$O/pytest_gpu.log" 2>&1 || fail "$s" "$O/pytest_gpu.log"
+        -p no:cacheprovider "${k[@]}" > "$O/pytest_gpu.log" 2>&1 || fail "$s" "$O/pytest_gpu.log"
       tail -1 "$O/pytest_gpu.log" ;;
     smoke)
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1 \
@@ -93,6 +94,14 @@ step() {
         -- python "$R/$script" $args > "$O/prof_$name.log" 2>&1) || fail "$s" "$O/prof_$name.log"
       f=$(ls "$O"/prof_$name/*/run_kernel_stats.csv "$O"/prof_$name/run_kernel_stats.csv 2>/dev/null | head -1)
       [ -n "$f" ] && cp "$f" "$O/kernel_stats_$name.csv" && cut -d, -f1-4 "$O/kernel_stats_$name.csv" | cut -c1-150 ;;
+    trace:*)
+      local rest=${s#trace:}; local script=${rest%%:*}; local args=""
+      [ "$rest" != "$script" ] && args=$(echo "${rest#*:}" | tr ',' ' ')
+      local name=$(basename "$script" .py)
+      (cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --output-format csv -d "$O/trace_$name" -o run \
+        -- python "$R/$script" $args > "$O/trace_$name.log" 2>&1) || fail "$s" "$O/trace_$name.log"
+      f=$(ls "$O"/trace_$name/*/run_kernel_trace.csv "$O"/trace_$name/run_kernel_trace.csv 2>/dev/null | head -1)
+      [ -n "$f" ] && cp "$f" "$O/kernel_trace_$name.csv" && rm -rf "$O/trace_$name" && echo "trace $name ok" ;;
     py:*)
       local rest=${s#py:}; local script=${rest%%:*}; local args=""
       [ "$rest" != "$script" ] && args=$(echo "${rest#*:}" | tr ',' ' ')
