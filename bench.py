@@ -207,10 +207,20 @@ def cpu_baseline(act, rows=M, runs=3):
         layer(x)
         ts.append(time.perf_counter() - t0)
     dt = statistics.median(ts)
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = None
     return {
         "value": round(2.0 * rows * N * K / dt / 1e12, 4),
         "unit": "TFLOP/s",
         "cores": torch.get_num_threads(),
+        "host_cpu_count": os.cpu_count(),
+        "process_affinity_cpus": affinity,
+        "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS"),
+        "cores_note": ("cores = the torch intra-op threads used (OMP_NUM_THREADS, set by the GPU "
+                       "box to this job's CPU share); host_cpu_count / process_affinity_cpus are "
+                       "the machine's and the process's CPU counts"),
         "kind": "torch-cpu-fp32",
         "cpu_model": cpu_model(),
         "sample": (f"oracle/torch_cpu.py CPUFakeQuantLinear (the reference's fake_quant ops, "
@@ -218,6 +228,49 @@ def cpu_baseline(act, rows=M, runs=3):
                    f"{rows}x{K}->{N}, G={G}, p={P}; median of {runs} after 1 warm-up: "
                    f"{dt:.3f} s per forward (runs {', '.join(f'{t:.3f}' for t in ts)})"),
     }
+
+
+def lib_sha1() -> str:
+    """sha1 of the product library (tools/pmc_summary.py records it in each profile)."""
+    import hashlib
+    path = os.path.join(ROOT, "smoothquant-mixedprecision_amd", "smoothquant", "libsqmp_w4a4.so")
+    try:
+        with open(path, "rb") as f:
+            return hashlib.sha1(f.read()).hexdigest()
+    except OSError:
+        return ""
+
+
+def pick_traffic(pname: str, live_us: float, tol: float = 0.05):
+    """HBM bytes per launch of the timed kernel from a committed counter profile
+    (profiles/r0N*_<pname>, tools/pmc_summary.py): the newest one whose profiled average
+    kernel duration is within `tol` of the live HIP-event average -- a profile of the same
+    kernel as built now.  Returns (bytes or None, {file, avg_kernel_us, live, accepted})."""
+    cands = sorted(glob.glob(os.path.join(ROOT, "profiles", "r0*_" + pname)))
+    lib = lib_sha1()
+    info, rows = None, []
+    for prof in reversed(cands):
+        try:
+            with open(prof) as f:
+                j = json.load(f)
+        except (OSError, ValueError):
+            continue
+        us = j.get("avg_kernel_us")
+        ok = bool(us) and abs(us - live_us) <= tol * live_us
+        cur = {"file": os.path.relpath(prof, ROOT), "avg_kernel_us": us,
+               "live_avg_us": round(live_us, 2), "accepted": ok,
+               "same_library": bool(lib) and j.get("lib_sha1") == lib}
+        if info is None:
+            info = cur  # the newest, reported even when rejected
+        rows.append((cur, j))
+    # a profile of this very library build first, then the newest within the tolerance
+    for want_same in (True, False):
+        for cur, j in rows:
+            if cur["accepted"] and (cur["same_library"] or not want_same):
+                return j.get("hbm_bytes_per_launch"), cur
+    if info is not None:
+        info["note"] = f"no committed profile within {tol:.0%} of the live kernel time: traffic null"
+    return None, info
 
 
 # ------------------------------------------------------------------ Llama-2-7B layer
@@ -458,21 +511,12 @@ def main(argv=None):
         reads = 2 if args.act in ("per_group", "per_tensor") else 1
     prepass_bytes = reads * xbytes + wbytes
 
-    traffic = None
     pname = ("pmc_gemm_f8v2_per_token.json" if kdt == "f8"
              else "pmc_gemm_h2_fp32.json" if fp32
              else "pmc_gemm_fqt7_per_group.json" if use_fqt and "fqt7" in kname
              else "pmc_gemm_fqt_per_group.json" if use_fqt
              else f"pmc_gemm_fq6_{args.act}.json")
-    # the newest committed counter profile of this kernel (profiles/r0N[_final]_pmc_*.json)
-    cands = sorted(glob.glob(os.path.join(ROOT, "profiles", "r0*_" + pname)))
-    prof = cands[-1] if cands else ""
-    if os.path.exists(prof):
-        try:
-            with open(prof) as f:
-                traffic = json.load(f).get("hbm_bytes_per_launch")
-        except (OSError, ValueError):
-            traffic = None
+    traffic, traffic_prof = pick_traffic(pname, gemm_ms * 1e3)
 
     out = {
         "metric": "quantized-Linear TFLOP/s (W4A4Linear 4096x4096, G=128, 10% salient, bs*seq=16384)",
@@ -506,6 +550,7 @@ def main(argv=None):
             "unit": "TFLOP/s",
             "frac": round(achieved / PEAK_TFLOPS[kdt], 4),
             "traffic": traffic,
+            "traffic_profile": traffic_prof,
             "kernel": kname,
             "avg_ms": round(gemm_ms, 4),
             "algorithmic_flops_per_launch": flops,

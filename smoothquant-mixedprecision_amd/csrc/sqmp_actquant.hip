@@ -620,117 +620,6 @@ __global__ __launch_bounds__(256) void rank_table_kernel(
   rank_owner_group<TPO, R>(rt_kv, L, L4, g0, tid % TPO, nonsal, posmap, colsorted, lctab, sib);
 }
 
-// ---------------------------------------------------------------- column max + rank, one launch
-// The column maxima of x [M][K] (colmax_kernel's blocks: VEC consecutive columns per lane, the
-// block's rows split over its four waves, one atomicMax per column and block into the clean
-// cmax) followed by the rank table (rank_table_kernel) in the SAME launch: every block takes a
-// ticket after its maxima are published (each wave drains its atomics, then the block's lane 0
-// releases at agent scope and adds to the counter); the last NR blocks to arrive become the
-// rankers, wait until every block has arrived (relaxed poll of the counter, one agent-scope
-// acquire: MI355X_MICROARCH.md, "Workgroup dispatch ... visibility"), stage the keys and rank
-// their share of the owners.  The last ranker to finish returns both counters to zero.
-// Saves the rank launch and its ramp (Llama prefill: the 2048-row inputs' statistics).
-// ctr[0] = arrivals, ctr[1] = finished rankers (zero on entry; the clean-workspace words).
-struct RankArgs {
-  const int32_t* nonsal;
-  const int32_t* posmap;
-  int32_t* colsorted;
-  uint32_t* lctab;
-  int L, lc_len;
-  uint32_t lc_none;
-  int NR;  // rankers
-};
-template <class DT, int VEC, int TPO, int R>
-__global__ __launch_bounds__(256) void colmax_rank_kernel(const typename DT::T* __restrict__ x,
-                                                          int Mr, int C, int rows_per_block,
-                                                          uint32_t* cmax, uint32_t* ctr,
-                                                          RankArgs ra, SibTables sib) {
-  typedef typename DT::T T;
-  extern __shared__ __attribute__((aligned(16))) uint32_t cr_lds[];  // max(4 x 64 VEC floats, keys)
-  __shared__ int cr_ticket;
-  float* red = (float*)cr_lds;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int c0 = (blockIdx.x * 64 + lane) * VEC;
-  const int r0 = blockIdx.y * rows_per_block;
-  const int r1 = min(Mr, r0 + rows_per_block);
-  float m[VEC];
-#pragma unroll
-  for (int i = 0; i < VEC; ++i) m[i] = 0.f;
-  if (c0 + VEC <= C) {
-    int r = r0 + wid;
-    for (; r + 28 < r1; r += 32) {
-      u32x4 raw[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) raw[u] = *(const u32x4*)(x + (size_t)(r + 4 * u) * C + c0);
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const T* v = (const T*)&raw[u];
-#pragma unroll
-        for (int i = 0; i < VEC; ++i) m[i] = fmaxf(m[i], fabsf(DT::to_f(v[i])));
-      }
-    }
-    for (; r < r1; r += 4) {
-      const u32x4 raw = *(const u32x4*)(x + (size_t)r * C + c0);
-      const T* v = (const T*)&raw;
-#pragma unroll
-      for (int i = 0; i < VEC; ++i) m[i] = fmaxf(m[i], fabsf(DT::to_f(v[i])));
-    }
-  }
-#pragma unroll
-  for (int i = 0; i < VEC; ++i) red[wid * 64 * VEC + lane * VEC + i] = m[i];
-  __syncthreads();
-  for (int t = tid; t < 64 * VEC; t += 256) {
-    const float v = fmaxf(fmaxf(red[t], red[64 * VEC + t]), fmaxf(red[2 * 64 * VEC + t], red[3 * 64 * VEC + t]));
-    const int c = blockIdx.x * 64 * VEC + t;
-    if (c < C && v > 0.f) atomicMax(&cmax[c], __float_as_uint(v));
-  }
-  // publish: every wave's atomics performed, then one release + ticket per block
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  const unsigned nblk = gridDim.x * gridDim.y;
-  if (tid == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    cr_ticket = (int)__hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  __syncthreads();
-  const int ranker = cr_ticket - (int)(nblk - (unsigned)ra.NR);
-  if (ranker < 0) return;
-  // ---- a ranker: wait for every block's maxima (bounded spin), acquire, rank
-  if (tid == 0) {
-    for (unsigned spin = 0; spin < (1u << 20); ++spin) {
-      if (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= nblk) break;
-      __builtin_amdgcn_s_sleep(2);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __syncthreads();
-  const int L = ra.L;
-  const int L4 = (int)round_up_dev(L, 4 * TPO) >> 2;
-  rank_stage_keys(cmax, ra.nonsal, L, L4, cr_lds);
-  for (int r = L + ranker * 256 + tid; r < ra.lc_len; r += ra.NR * 256) {
-    ra.lctab[r] = ra.lc_none;
-    for (int o = 0; o < sib.n; ++o) sib.lctab[o][r] = ra.lc_none;
-  }
-  __syncthreads();
-  for (int g0 = (ranker * (256 / TPO) + tid / TPO) * R; g0 < L + 0; g0 += ra.NR * (256 / TPO) * R) {
-    rank_owner_group<TPO, R>(cr_lds, L, L4, g0, tid % TPO, ra.nonsal, ra.posmap, ra.colsorted,
-                             ra.lctab, sib);
-    // (every lane of a TPO group takes the same trip count: g0 is uniform over the group)
-  }
-  // the last ranker returns the counters to zero (every ranker is past its poll)
-  __syncthreads();
-  if (tid == 0) {
-    const unsigned done =
-        __hip_atomic_fetch_add(ctr + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (done == (unsigned)ra.NR - 1) {
-      __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(ctr + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-}
-
 // SQMP_RANK_TABLE_OFF=1 keeps rank_count + lc_table (A/B diagnostics).
 static bool rank_table_fits(int L) {
   static const bool off = getenv("SQMP_RANK_TABLE_OFF") != nullptr;
@@ -778,60 +667,6 @@ static int launch_rank_table(const uint32_t* key, const int32_t* nonsal, int L,
   }
 #undef SQMP_RT_T
 #undef SQMP_RT
-  SQMP_LAUNCH_CHECK();
-  return SQMP_OK;
-}
-
-// Column max + rank table in one launch (colmax_rank_kernel) for fp16 / bf16 rows whose 16-B
-// chunks are aligned, L <= RT_MAX.  ctr: two zero words (left zero).  SQMP_COLMAX_RANK=0 keeps
-// the two launches (A/B knob, read per call).  Returns SQMP_EUNSUPPORTED where not covered.
-static int launch_colmax_rank(const void* x, int dtype, int M, int K, uint32_t* cmax,
-                              uint32_t* ctr, const int32_t* nonsal, int L, const int32_t* posmap,
-                              int32_t* colsorted, uint32_t* lctab, int lc_len, uint32_t lc_none,
-                              hipStream_t s, const SibTables& sib = SibTables{}) {
-  if (const char* e = getenv("SQMP_COLMAX_RANK"))
-    if (atoi(e) == 0) return SQMP_EUNSUPPORTED;
-  if ((dtype != SQMP_F16 && dtype != SQMP_BF16) || L <= 0 || L > RT_MAX || M <= 0) return SQMP_EUNSUPPORTED;
-  if ((K * 2) % 16 != 0 || ((uintptr_t)x) % 16 != 0) return SQMP_EUNSUPPORTED;
-  constexpr int VEC = 8;
-  // colmax geometry as colmax_launch (>= 32 rows per block, ~1024 blocks)
-  int rpb = 128;
-  const int cb = cdiv(K, 64 * VEC);
-  while (rpb > 32 && (long)cb * cdiv(M, rpb) < 1024) rpb >>= 1;
-  const dim3 grid(cb, cdiv(M, rpb));
-  const int nblk = (int)(grid.x * grid.y);
-  // rankers: TPO lanes per owner, L TPO / 256 rankers (per-lane compares L / TPO), at most one
-  // per CU: waiting rankers never hold every slot a block still to arrive needs
-  static int ncu = 0;
-  if (ncu == 0) {
-    int dev = 0;
-    SQMP_HIP_CHECK(hipGetDevice(&dev));
-    SQMP_HIP_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
-  }
-  int tpo = 16;
-  while (tpo > 4 && cdiv((long)L * tpo, 256) > ncu) tpo >>= 1;
-  const int nr = cdiv((long)L * tpo, 256);
-  if (nr > nblk || nr > ncu) return SQMP_EUNSUPPORTED;  // (tiny inputs: the two-launch path)
-  RankArgs ra{nonsal, posmap, colsorted, lctab, L, lc_len, lc_none, nr};
-  const size_t lds_keys = sizeof(uint32_t) * (size_t)round_up(L, 4 * tpo);
-  const size_t lds = lds_keys > 4 * 64 * VEC * sizeof(float) ? lds_keys : 4 * 64 * VEC * sizeof(float);
-#define SQMP_CR(DTT, TPOV)                                                                          \
-  do {                                                                                          \
-    static bool attr = false;                                                                   \
-    if (!attr) {                                                                                \
-      SQMP_HIP_CHECK(hipFuncSetAttribute((const void*)colmax_rank_kernel<DTT, VEC, TPOV, 1>,    \
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, 4 * RT_MAX)); \
-      attr = true;                                                                              \
-    }                                                                                           \
-    colmax_rank_kernel<DTT, VEC, TPOV, 1><<<grid, dim3(256), lds, s>>>(                         \
-        (const typename DTT::T*)x, M, K, rpb, cmax, ctr, ra, sib);                              \
-  } while (0)
-  if (dtype == SQMP_F16) {
-    if (tpo == 16) SQMP_CR(F16, 16); else if (tpo == 8) SQMP_CR(F16, 8); else SQMP_CR(F16, 4);
-  } else {
-    if (tpo == 16) SQMP_CR(BF16, 16); else if (tpo == 8) SQMP_CR(BF16, 8); else SQMP_CR(BF16, 4);
-  }
-#undef SQMP_CR
   SQMP_LAUNCH_CHECK();
   return SQMP_OK;
 }
@@ -1324,13 +1159,9 @@ static size_t ws_u32_words(int K, int Kp) {
 static size_t ws_sib_offset(int K, int Kp) {
   return sizeof(uint32_t) * ws_u32_words(K, Kp) + 2 * sizeof(double) * ws_k64(K);
 }
-// + four words for colmax_rank_kernel's counters (zero between calls)
-static size_t ws_ctr_offset(int K, int Kp) {
-  return ws_sib_offset(K, Kp) + 2 * sizeof(uint32_t) * (size_t)round_up(K > 0 ? K : 1, 4096);
-}
 extern "C" size_t sqmp_act_workspace_bytes(int M, int K, int Kp) {
   (void)M;
-  return ws_ctr_offset(K, Kp) + 4 * sizeof(uint32_t);
+  return ws_sib_offset(K, Kp) + 2 * sizeof(uint32_t) * (size_t)round_up(K > 0 ? K : 1, 4096);
 }
 
 static int quant_act_impl(void* x, int dtype, int M, int K, int amode, int n_bits,
@@ -1407,8 +1238,6 @@ static int quant_act_impl(void* x, int dtype, int M, int K, int amode, int n_bit
   int32_t* counts = (int32_t*)(lctab + round_up(K, 4096));
   int32_t* colsorted = counts + k64;
   double* sums = (double*)((uint32_t*)workspace + ws_u32_words(K, Kp));
-  uint32_t* ctr = (uint32_t*)((unsigned char*)workspace + ws_ctr_offset(K, Kp));
-  const SibTables sibt{};
   const int Kn = K - S;
   if (Kn == 0) {
     // every channel salient: the reference skips quantization entirely (:299)
@@ -1442,16 +1271,7 @@ static int quant_act_impl(void* x, int dtype, int M, int K, int amode, int n_bit
           if (stats_given) {
             st2 = SQMP_OK;
           } else {
-            if (!clean) {
-              SQMP_HIP_CHECK(hipMemsetAsync(cmax, 0, sizeof(uint32_t) * k64, s));
-              SQMP_HIP_CHECK(hipMemsetAsync(ctr, 0, 4 * sizeof(uint32_t), s));
-            }
-            if (rank_table_fits(Kn) &&
-                launch_colmax_rank(x, dtype, M, K, cmax, ctr, nonsal, Kn, pm, colsorted, lctab,
-                                   lc_len, none, s, sibt) == SQMP_OK) {
-              key_clear = cmax;  // cleared by the quantizer, after every ranker's read
-              return SQMP_OK;
-            }
+            if (!clean) SQMP_HIP_CHECK(hipMemsetAsync(cmax, 0, sizeof(uint32_t) * k64, s));
             st2 = launch_colmax(x, dtype, M, K, cmax, s, false);
           }
         } else {
@@ -1729,18 +1549,11 @@ extern "C" int sqmp_quant_act_group(void* x, int dtype, int M, int K, int amode,
     ls.amap[o] = amaps[o + 1];
     ls.out[o] = outs[o + 1];
   }
-  uint32_t* ctr = (uint32_t*)((unsigned char*)workspace + ws_ctr_offset(K, Kp));
-  int r = SQMP_EUNSUPPORTED;
-  if (amode == SQMP_ACT_PER_GROUP)
-    r = launch_colmax_rank(x, dtype, M, K, cmax, ctr, nonsal, Kn, posmaps[0], colsorted, lctab,
-                           lc_len, lc_none, s, st);
-  if (r != SQMP_OK) {
-    r = amode == SQMP_ACT_PER_GROUP ? launch_colmax(x, dtype, M, K, cmax, s, false)
-                                    : launch_colkey_mean3std(x, dtype, M, K, sums, cmax, s, true);
-    if (r) return r;
-    r = launch_rank_table(cmax, nonsal, Kn, posmaps[0], colsorted, lctab, lc_len, lc_none, s, st);
-    if (r) return r;
-  }
+  int r = amode == SQMP_ACT_PER_GROUP ? launch_colmax(x, dtype, M, K, cmax, s, false)
+                                      : launch_colkey_mean3std(x, dtype, M, K, sums, cmax, s, true);
+  if (r) return r;
+  r = launch_rank_table(cmax, nonsal, Kn, posmaps[0], colsorted, lctab, lc_len, lc_none, s, st);
+  if (r) return r;
   return launch_quant_lc_group(dtype, x, M, K, (1 << (n_bits - 1)) - 1, group_size, lctab, Kn,
                                amaps[0], Kp, salient, S, S_pad, cmax, nonsal, outs[0], cmax,
                                (int)k64, ls, s);

@@ -133,14 +133,24 @@ extern "C" int sqmp_permute_act(const void* src, void* dst, const int32_t* map, 
   const int ppw = npair > 4096 ? cdiv(npair, 4096) : 1;
   const dim3 grid((unsigned)cdiv(npair, ppw));
   const size_t lds = sizeof(uint32_t) * (size_t)(P + S_pad);
+  // the dynamic-LDS limit raised once to the largest row this entry accepts (256 PR_CH chunks
+  // of 8 positions), not per launch
+  constexpr int kMaxLds = (int)sizeof(uint32_t) * 8 * 256 * PR_CH;
+  static bool attr_h = false, attr_b = false;
   if (dtype == SQMP_F16) {
-    SQMP_HIP_CHECK(hipFuncSetAttribute((const void*)permute_rows_kernel<_Float16>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    if (!attr_h) {
+      SQMP_HIP_CHECK(hipFuncSetAttribute((const void*)permute_rows_kernel<_Float16>,
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, kMaxLds));
+      attr_h = true;
+    }
     permute_rows_kernel<_Float16><<<grid, dim3(256), lds, s>>>(
         (const _Float16*)src, (_Float16*)dst, map, M, P, S_pad, ppw);
   } else {
-    SQMP_HIP_CHECK(hipFuncSetAttribute((const void*)permute_rows_kernel<__bf16>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    if (!attr_b) {
+      SQMP_HIP_CHECK(hipFuncSetAttribute((const void*)permute_rows_kernel<__bf16>,
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, kMaxLds));
+      attr_b = true;
+    }
     permute_rows_kernel<__bf16><<<grid, dim3(256), lds, s>>>(
         (const __bf16*)src, (__bf16*)dst, map, M, P, S_pad, ppw);
   }

@@ -537,7 +537,7 @@ class W4A4Linear(nn.Module):
         # y into the output quantizer's workspace, which then skips its statistics pass
         fuse = (ospec is not None and ospec[0] in ("per_group", "per_tensor") and _OQ_FUSE
                 and not use_i8
-                and (not use_f8 or pw.Gw % 128 == 0)           # the 16x16x128 FP8 kernel
+                and (not use_f8 or ops.f8_colmax_ok(pw))       # the 16x16x128 FP8 kernel
                 and (not use_fqt or c4[1].dim() == 3)          # the tile-major fqt7 GEMM
                 and (self.salient_indices is None or pw.K - pw.S > 0))
         colmax = ops.out_quant_workspace(x2.shape[0], pw.N, x2.device)["buf"] if fuse else None

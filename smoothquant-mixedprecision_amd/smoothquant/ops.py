@@ -93,7 +93,7 @@ class PackedWeight:
     ws32: Optional[torch.Tensor] = field(default=None)   # fp32 [ngw, Np] scales (f8 GEMM)
     fq7: Optional[tuple] = field(default=None)           # (codes_t, scale_t, sal_t, J) of gemm_fq7
     h2: Optional[tuple] = field(default=None)            # (f16 [2, Np, L], int32 [Np]) (gemm_h2)
-    sib_maps: Optional[dict] = field(default=None)       # sibling position maps (sqmp_permute_act)
+    sib_maps: Optional[tuple] = field(default=None)      # sibling position map (sqmp_permute_act)
 
     @property
     def gemm_operand(self):
@@ -252,17 +252,18 @@ SIB_MAX_BYTES = 64 << 20
 
 def _sibling_map(src: PackedWeight, dst: PackedWeight) -> torch.Tensor:
     """int32 [Kp]: the packed position in `src` of the column at each packed position of
-    `dst` (-1 at dst's salient / padding positions), cached on dst."""
-    key = src.codes.data_ptr()
-    if dst.sib_maps is None:
-        dst.sib_maps = {}
-    m = dst.sib_maps.get(key)
-    if m is None:
-        if src.posmap is None:
-            src.posmap = build_posmap(src.perm, src.K)
-        col = dst.amap.long()
-        m = torch.where(col >= 0, src.posmap.long()[col.clamp(min=0)], -1).to(torch.int32)
-        dst.sib_maps = {key: m}  # one source per layer (its sibling leader)
+    `dst` (-1 at dst's salient / padding positions), cached on dst for this exact `src`
+    object and the current contents of both orders (a PackedWeight is rebuilt whenever a
+    module's buffers change; the perm / amap versions catch in-place rewrites)."""
+    if src.posmap is None:
+        src.posmap = build_posmap(src.perm, src.K)
+    ver = (src.perm._version, src.posmap._version, dst.amap._version)
+    c = dst.sib_maps
+    if c is not None and c[0]() is src and c[1] == ver:
+        return c[2]
+    col = dst.amap.long()
+    m = torch.where(col >= 0, src.posmap.long()[col.clamp(min=0)], -1).to(torch.int32)
+    dst.sib_maps = (weakref.ref(src), ver, m)  # one source per layer (its sibling leader)
     return m
 
 
@@ -324,9 +325,19 @@ def quant_act_fp(x2: torch.Tensor, pw: PackedWeight, act_quant: str, n_bits: int
                       pw.codes.data_ptr())
         e["last_a"] = None
         if SIB_REUSE and a.numel() * a.element_size() <= SIB_MAX_BYTES:
-            e["last_a"] = (weakref.ref(stats_of if stats_of is not None else x2),
+            # held while the input lives: freeing the input drops the operand with it
+            e["last_a"] = (weakref.ref(stats_of if stats_of is not None else x2, _drop_last_a(e)),
                            skey + (n_bits, group_size), weakref.ref(pw), a)
     return a
+
+
+def _drop_last_a(e):
+    """weakref callback: the input a kept sibling operand belongs to was freed."""
+    def cb(ref):
+        la = e.get("last_a")
+        if la is not None and la[0] is ref:
+            e["last_a"] = None
+    return cb
 
 
 def quant_act_fp_group(x2: torch.Tensor, pws, act_quant: str, n_bits: int,
@@ -741,6 +752,13 @@ def quant_act_f8(x2: torch.Tensor, pw: PackedWeight, act_quant: str, n_bits: int
         _WS.pop((x2.device.index, stream, K, pw.Kp, "in"), None)
         check(status, "quant_act")
     return a8, sa, xs
+
+
+def f8_colmax_ok(pw: PackedWeight) -> bool:
+    """Whether gemm_f8 can fuse the output-quant column statistics: the 16x16x128 kernel
+    (Gw % 128 == 0) and not its SQMP_F8_V1=1 A/B variant (the 32x32x64 kernel has no fused
+    statistics; read per call like the library does)."""
+    return pw.Gw % 128 == 0 and os.environ.get("SQMP_F8_V1") != "1"
 
 
 def gemm_f8(a8: torch.Tensor, sa: torch.Tensor, xs: torch.Tensor, pw: PackedWeight,

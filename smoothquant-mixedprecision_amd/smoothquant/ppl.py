@@ -8,7 +8,8 @@ The split is joined with "\\n\\n" and tokenized once into a [1, T] id stream.  W
 ids[:, i*B:(i+1)*B]; its negative log-likelihood is B x the mean cross-entropy of the
 B-1 next-token predictions (fp32 logits) -- B = batch_size for every window, a short last
 window included, as the reference computes it -- and PPL = exp(sum of window NLLs / (n*B)).
-n_samples=None/0 means every full window.  Without hub access pass a dataset with a
+n_samples=None/0 means size // 2048 windows (the reference's count, whatever B is).
+Without hub access pass a dataset with a
 "text" column, or the token ids directly (`input_ids=`).  `last_tokens_per_s` is the
 throughput of the last evaluate() (windows x B tokens over its wall time).
 """
@@ -57,7 +58,9 @@ class Evaluator:
 
     def windows(self):
         B = self.batch_size
-        n = self.n_samples or self.dataset.shape[1] // B
+        # n_samples falsy: the reference counts 2048-token windows whatever batch_size is
+        # (run_experiments.py:103), then slices windows of batch_size
+        n = self.n_samples or self.dataset.shape[1] // 2048
         return [self.dataset[:, i * B:(i + 1) * B] for i in range(n)]
 
     @torch.no_grad()

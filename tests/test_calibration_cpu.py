@@ -84,10 +84,10 @@ def test_evaluator_formula():
     case = MG.cases()[0]
     model = build_model(case)
     ids = torch.from_numpy(MG.arr(case["key"], "ev").copy())
-    ev = Evaluator(None, None, "cpu", n_samples=None, batch_size=case["eval_window"], input_ids=ids)
+    B = case["eval_window"]
+    ev = Evaluator(None, None, "cpu", n_samples=ids.size(1) // B, batch_size=B, input_ids=ids)
     ppl = float(ev.evaluate(model))
     # restated: exp(mean over windows of the mean CE)
-    B = case["eval_window"]
     ces = []
     with torch.no_grad():
         for i in range(ids.size(1) // B):
@@ -118,4 +118,27 @@ def test_evaluator_short_last_window_scales_by_batch_size():
             ce = torch.nn.functional.cross_entropy(lg.reshape(-1, lg.size(-1)), b[:, 1:].reshape(-1))
             nlls.append(ce.float() * B)
     want = float(torch.exp(torch.stack(nlls).sum() / ((n_full + 1) * B)))
+    assert abs(ppl - want) <= 1e-4 * want
+
+
+def test_evaluator_default_window_count_is_per_2048_tokens():
+    """n_samples falsy: the reference evaluates dataset.size(1) // 2048 windows of batch_size
+    tokens (run_experiments.py:103), not size // batch_size."""
+    case = MG.cases()[0]
+    model = build_model(case)
+    base = torch.from_numpy(MG.arr(case["key"], "ev").copy())
+    ids = base.repeat(1, 4196 // base.size(1) + 1)[:, :4196]   # 2 x 2048 + 100 tokens
+    B = 256
+    ev = Evaluator(None, None, "cpu", n_samples=None, batch_size=B, input_ids=ids)
+    wins = ev.windows()
+    assert len(wins) == 2 and all(w.shape == (1, B) for w in wins)
+    assert torch.equal(wins[1], ids[:, B:2 * B])
+    ppl = float(ev.evaluate(model))
+    nlls = []
+    with torch.no_grad():
+        for w in wins:
+            lg = model(w).logits[:, :-1].float()
+            ce = torch.nn.functional.cross_entropy(lg.reshape(-1, lg.size(-1)), w[:, 1:].reshape(-1))
+            nlls.append(ce.float() * B)
+    want = float(torch.exp(torch.stack(nlls).sum() / (2 * B)))
     assert abs(ppl - want) <= 1e-4 * want

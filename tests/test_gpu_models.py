@@ -44,7 +44,8 @@ def test_tiny_model_matches_reference(case):
     want = MG.arr(key, "logits")
     rel = np.linalg.norm(logits - want) / np.linalg.norm(want)
     ev = torch.from_numpy(MG.arr(key, "ev").copy())
-    ppl = float(Evaluator(None, None, "cuda", n_samples=None, batch_size=case["eval_window"],
+    B = case["eval_window"]  # the golden evaluates every full window (gen_model_golden.py)
+    ppl = float(Evaluator(None, None, "cuda", n_samples=ev.size(1) // B, batch_size=B,
                           input_ids=ev).evaluate(q))
     print(f"{key}: logits rel {rel:.3e}, ppl {ppl:.4f} vs {case['ppl']:.4f}")
     assert rel <= TOL_LOGITS

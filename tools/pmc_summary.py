@@ -61,6 +61,11 @@ def main():
         "wave_cycles_wait_inst_any_frac": c["SQ_WAIT_INST_ANY"] / c["SQ_WAVE_CYCLES"],
     }
     out["traffic_over_algorithmic"] = out["hbm_bytes_per_launch"] / alg_bytes
+    # the library build the counters describe (bench.py's pick_traffic matches on it); set
+    # SQMP_PMC_LIB_SHA1 when summarising elsewhere than the tree that was profiled
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    out["lib_sha1"] = os.environ.get("SQMP_PMC_LIB_SHA1") or bench.lib_sha1()
     s = json.dumps(out, indent=1)
     if len(sys.argv) > 6:
         open(sys.argv[6], "w").write(s + "\n")
