@@ -11,8 +11,8 @@ GOLDEN = os.path.join(HERE, "golden", "model_golden.npz")
 
 
 class ModelGolden:
-    def __init__(self):
-        self.z = np.load(GOLDEN, allow_pickle=False)
+    def __init__(self, path=GOLDEN):
+        self.z = np.load(path, allow_pickle=False)
         self.meta = json.loads(bytes(self.z["meta_json"]).decode())
 
     def cases(self):
@@ -59,3 +59,17 @@ def cal_blocks(case):
         g = torch.Generator().manual_seed(s)
         out.append(torch.randint(0, 512, (1, case["cal_len"]), generator=g))
     return out
+
+
+FALCON_GOLDEN = os.path.join(HERE, "golden", "falcon_golden.npz")
+
+
+def build_falcon(case, archs):
+    """The seeded random-init tiny Falcon of tests/golden/gen_falcon_golden.py (CPU, fp32)."""
+    from transformers import FalconConfig, FalconForCausalLM
+    cfg = FalconConfig(vocab_size=512, hidden_size=64, num_hidden_layers=2, num_attention_heads=4,
+                       bias=False, alibi=False, attention_dropout=0.0, hidden_dropout=0.0,
+                       max_position_embeddings=256, attn_implementation="eager",
+                       **archs[case["arch"]])
+    torch.manual_seed(case["seed"])
+    return FalconForCausalLM(cfg).eval()

@@ -1,0 +1,61 @@
+"""Falcon on the GPU against the reference (tests/golden/gen_falcon_golden.py): the reference's
+quantize_falcon (/root/reference/smoothquant/fake_quant.py:671-731) after its smooth_lm Falcon
+branch (/root/reference/smoothquant/smooth.py:74-160: parallel-attention, new-decoder and
+sequential layouts), restated by this repo's quantize_falcon / smooth_lm on HIP W4A4Linear
+layers.  Every W4A4Linear's W_hat and salient_indices are bit-exact (sha256 of the fp32
+bytes); logits and the Evaluator perplexity within the model-test tolerances
+(test_gpu_models.py: GPU vs CPU fp32 ops around the quantized layers); the fused
+query_key_value with bmm-input quantization and salient channels raises the reference's
+IndexError (:311-314)."""
+import hashlib
+
+import numpy as np
+import pytest
+import torch
+
+from model_cases import FALCON_GOLDEN, ModelGolden, build_falcon
+
+pytestmark = pytest.mark.gpu
+FG = ModelGolden(FALCON_GOLDEN)
+TOL_LOGITS, TOL_PPL = 2e-2, 1e-2
+
+
+@pytest.mark.parametrize("case", FG.cases(), ids=[c["key"] for c in FG.cases()])
+def test_falcon_matches_reference(case):
+    if not torch.cuda.is_available():
+        pytest.skip("no ROCm device")
+    from smoothquant.fake_quant import W4A4Linear, quantize_falcon
+    from smoothquant.ppl import Evaluator
+    from smoothquant.smooth import smooth_lm
+    key = case["key"]
+    model = build_falcon(case, FG.meta["archs"])
+    if case["alpha"] is not None:
+        smooth_lm(model, FG.scales(key), case["alpha"])
+    model = model.to("cuda")
+    q = quantize_falcon(model, input_feat=FG.feat(key), **case["kwargs"])
+    got = {}
+    for n, m in q.named_modules():
+        if isinstance(m, W4A4Linear):
+            w = m.weight.detach().float().cpu().contiguous().numpy()
+            got[n] = hashlib.sha256(w.tobytes()).hexdigest()
+            si = m.salient_indices
+            got[n + "#salient"] = (None if si is None else
+                                   hashlib.sha256(si.cpu().to(torch.int64).numpy().tobytes()).hexdigest())
+    assert got == case["w_hat"]
+    x = torch.from_numpy(FG.arr(key, "x").copy()).cuda()
+    if "raises" in case:
+        with pytest.raises(IndexError, match="does not match the shape"):
+            with torch.no_grad():
+                q(x)
+        return
+    with torch.no_grad():
+        logits = q(x).logits.float().cpu().numpy()
+    want = FG.arr(key, "logits")
+    rel = np.linalg.norm(logits - want) / np.linalg.norm(want)
+    ev = torch.from_numpy(FG.arr(key, "ev").copy())
+    B = case["eval_window"]
+    ppl = float(Evaluator(None, None, "cuda", n_samples=ev.size(1) // B, batch_size=B,
+                          input_ids=ev).evaluate(q))
+    print(f"{key}: logits rel {rel:.3e}, ppl {ppl:.4f} vs {case['ppl']:.4f}")
+    assert rel <= TOL_LOGITS
+    assert abs(ppl - case["ppl"]) <= TOL_PPL * case["ppl"]
