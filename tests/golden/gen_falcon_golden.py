@@ -77,11 +77,13 @@ CASES = [
 
 
 def w_hat_digests(model):
-    """sha256 of each W4A4Linear's W_hat (fp32 bytes) and of its salient_indices (int64)."""
+    """sha256 of each W4A4Linear's W_hat (fp32 bytes, -0.0 folded to +0.0 as config_cases.
+    what_digest: the packed path dequantizes integer code 0 to +0.0) and of its
+    salient_indices (int64)."""
     out = {}
     for n, m in model.named_modules():
         if type(m).__name__ == "W4A4Linear":
-            w = m.weight.detach().float().contiguous().numpy()
+            w = (m.weight.detach().float().contiguous() + 0.0).numpy()
             out[n] = hashlib.sha256(w.tobytes()).hexdigest()
             si = m.salient_indices
             out[n + "#salient"] = (None if si is None else

@@ -36,7 +36,7 @@ def test_falcon_matches_reference(case):
     got = {}
     for n, m in q.named_modules():
         if isinstance(m, W4A4Linear):
-            w = m.weight.detach().float().cpu().contiguous().numpy()
+            w = (m.weight.detach().float().cpu().contiguous() + 0.0).numpy()
             got[n] = hashlib.sha256(w.tobytes()).hexdigest()
             si = m.salient_indices
             got[n + "#salient"] = (None if si is None else
