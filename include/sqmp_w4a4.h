@@ -315,6 +315,15 @@ int sqmp_gemm_fqt7j(const void* codes_t, const void* scale_t, const void* sal_t,
                     const void* bias, void* y, int dtype, int M, int N, int Kq, int S_pad, int G,
                     int ngq, int J, uint32_t* colmax, void* stream);
 
+/* sqmp_gemm_fqt7j(J = 4)'s operands (SQMP_QA_TILED4) and results at ONE wave per SIMD: 256
+ * weight rows x 256 tokens per tile, each wave 256 rows x 64 tokens with its 256 fp32
+ * accumulators in the accumulator registers -- half the LDS reads and act-code decode per MFMA
+ * of the two-wave kernels.  Kq % 128 == 0, S_pad % 64 == 0, G % 64 == 0, N % 8 == 0, fp16 /
+ * bf16; colmax NULL: no statistics. */
+int sqmp_gemm_fqt8(const void* codes_t, const void* scale_t, const void* sal_t, const void* wp,
+                   const void* bias, void* y, int dtype, int M, int N, int Kq, int S_pad, int G,
+                   int ngq, uint32_t* colmax, void* stream);
+
 /* Sibling operand reuse: dst = the SQMP_OUT_FP operand of a layer whose weight shares the
  * quantized input, the salient set and the act mode with the layer that produced src (q/k/v,
  * gate/up), rebuilt by moving positions instead of quantizing again: dst[m][p] =

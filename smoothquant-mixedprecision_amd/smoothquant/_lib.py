@@ -75,6 +75,7 @@ SIGNATURES = {
     "sqmp_permute_act": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _vp]),
     "sqmp_gemm_fqt7j": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _vp,
                              _vp]),
+    "sqmp_gemm_fqt8": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _vp, _vp]),
     "sqmp_gemm_fqt7_colmax": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i,
                                    _vp, _vp]),
     "sqmp_fq7_sizes": (_i, [_i, _i, _i, _i, _i, ctypes.POINTER(_sz), ctypes.POINTER(_sz),

@@ -437,6 +437,15 @@ FQT7 = os.environ.get("SQMP_FQT7", "1") == "1"
 # its register operand's row tiles per wave: 2 (256 weight rows x 256 tokens per tile) or 4
 # (128 x 512: half the permuted-weight LDS traffic per MFMA, twice the act-code decode)
 FQT7_J = int(os.environ.get("SQMP_FQT7_J", "2"))
+# the one-wave-per-SIMD activation-order GEMM (sqmp_gemm_fqt8) on the J = 4 operands
+FQT8 = os.environ.get("SQMP_FQT8", "0") == "1"
+
+
+def _fqt_j() -> int:
+    """Tile-major operand layout of the activation-order path: 4 under FQT8, else FQT7_J."""
+    if FQT8:
+        return 4
+    return FQT7_J if FQT7_J in (2, 4) else 2
 
 
 def fqt_eligible(pw: PackedWeight, act_quant: str, act_bits: int, group_size: int,
@@ -470,7 +479,7 @@ def quant_act_c4(x2: torch.Tensor, pw: PackedWeight, act_quant: str, n_bits: int
     ngq = (Kn + group_size - 1) // group_size
     dev = x2.device
     tiled = FQT7 and Kq % 128 == 0
-    tj = FQT7_J if FQT7_J in (2, 4) else 2
+    tj = _fqt_j()
     if tiled:
         R = max(128 * tj, (M + 128 * tj - 1) // (128 * tj) * (128 * tj))
         codes = torch.empty((R, Kq // 2), dtype=torch.uint8, device=dev)
@@ -519,6 +528,11 @@ def gemm_fqt(codes: torch.Tensor, scales: torch.Tensor, xs: torch.Tensor, wp: to
     M = xs.shape[0]
     y = torch.empty((M, pw.N), dtype=pw.dtype, device=codes.device)
     Kq = codes.shape[1] * 2
+    if scales.dim() == 3 and scales.shape[2] == 64 and FQT8:
+        check(load().sqmp_gemm_fqt8(_p(codes), _p(scales), _p(xs), _p(wp), _p(bias), _p(y),
+                                    _dtype_code(pw.dtype), M, pw.N, Kq, pw.S_pad, group_size,
+                                    scales.shape[1], _p(colmax), _stream(codes)), "gemm_fqt8")
+        return y
     if scales.dim() == 3:   # tile-major (SQMP_QA_TILED: 32-row blocks, TILED4: 64-row)
         check(load().sqmp_gemm_fqt7j(_p(codes), _p(scales), _p(xs), _p(wp), _p(bias), _p(y),
                                      _dtype_code(pw.dtype), M, pw.N, Kq, pw.S_pad, group_size,

@@ -108,7 +108,14 @@ def main():
             sc = act_scales(m, cal)
             for n, v in sc.items():
                 arrays[f"{key}__scale__{n}"] = v.numpy()
+            before = {n: t.detach().clone() for n, t in m.state_dict().items()}
             smooth.smooth_lm(m, sc, alpha)
+            # the smoothed tensors themselves: smooth_lm's fp32 pow is vectorised per CPU ISA
+            # (AVX2 here, maybe AVX-512 on the GPU box's host), so the GPU test checks its own
+            # smoothing against these to 1e-6 and then quantizes exactly these values
+            for n, t in m.state_dict().items():
+                if not torch.equal(t, before[n]):
+                    arrays[f"{key}__smoothed__{n}"] = t.detach().clone().numpy()  # not a view: quantize_falcon rewrites per_channel weights in place
         feat = None
         if with_feat:
             # quantize_falcon looks features up as "model." + name (it walks model.named_modules())

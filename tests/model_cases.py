@@ -31,6 +31,11 @@ class ModelGolden:
         pre = f"{key}__scale__"
         return {k[len(pre):]: torch.from_numpy(self.z[k].copy()) for k in self.z.files if k.startswith(pre)}
 
+    def smoothed(self, key):
+        """The reference's smoothed tensors (state_dict names) of a case, when stored."""
+        pre = f"{key}__smoothed__"
+        return {k[len(pre):]: torch.from_numpy(self.z[k].copy()) for k in self.z.files if k.startswith(pre)}
+
     def arr(self, key, name):
         return self.z[f"{key}__{name}"]
 

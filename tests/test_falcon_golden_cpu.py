@@ -27,6 +27,15 @@ def test_falcon_what_matches_reference(case):
     model = build_falcon(case, FG.meta["archs"])
     if case["alpha"] is not None:
         smooth_lm(model, FG.scales(key), case["alpha"])
+        # within 1e-6 of the reference's smoothed tensors (bit-exact on the AVX2 host that made
+        # the goldens; smooth_lm's fp32 pow rounds per host ISA), then exactly those
+        sd = model.state_dict()
+        ref_sm = FG.smoothed(key)
+        assert ref_sm
+        with torch.no_grad():
+            for n, t in ref_sm.items():
+                torch.testing.assert_close(sd[n], t, rtol=1e-6, atol=0)
+                sd[n].copy_(t)
     feat = FG.feat(key)
     mods = dict(model.named_modules())
     n_checked = 0

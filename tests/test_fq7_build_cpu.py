@@ -39,3 +39,39 @@ def test_fq7_kernels_do_not_spill(tmp_path):
         scratch = int(re.search(r"ScratchSize \[bytes/lane\]: (\d+)", b).group(1))
         assert spill == 0 and scratch == 0, f"{name}: {spill} VGPR spills, {scratch} B scratch"
     assert seen >= 14
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC) and shutil.which("hipcc") is None,
+                    reason="hipcc not available")
+def test_fqt8_accumulators_stay_in_agprs(tmp_path):
+    """sqmp_gemm_fqt8 names its 256 accumulators as literal a[0:255] in asm statements that
+    hipcc cannot see into: the compiler must neither spill nor emit a v_accvgpr_* of its own
+    (that would land in an accumulator it does not know is live), and the kernel must issue
+    exactly 2 stages x 128 MFMAs in its loop body."""
+    src = os.path.join(ROOT, "smoothquant-mixedprecision_amd", "csrc", "sqmp_gemm_fqt8.hip")
+    r = subprocess.run([HIPCC, "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-I",
+                        os.path.join(ROOT, "include"), "-c", src, "-o", str(tmp_path / "f8.o"),
+                        "-save-temps=obj", "-Rpass-analysis=kernel-resource-usage"],
+                       capture_output=True, text=True, timeout=600, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stderr[-2000:]
+    spills = [int(v) for v in re.findall(r"VGPRs Spill: (\d+)", r.stderr)]
+    scratch = [int(v) for v in re.findall(r"ScratchSize \[bytes/lane\]: (\d+)", r.stderr)]
+    assert len(spills) == 2 and not any(spills) and not any(scratch), r.stderr[-3000:]
+    asm = [f for f in os.listdir(tmp_path) if f.endswith(".s") and "gfx950" in f]
+    assert asm
+    text = open(tmp_path / asm[0]).read()
+    kernels = re.split(r"\n(?=_ZN4sqmp4fqt8\w+:)", text)[1:]
+    assert len(kernels) == 2
+    for k in kernels:
+        inasm, own, mfma = False, 0, 0
+        for line in k.split("\n"):
+            if ";;#ASMSTART" in line:
+                inasm = True
+            elif ";;#ASMEND" in line:
+                inasm = False
+            elif "accvgpr" in line and not inasm:
+                own += 1
+            elif "v_mfma" in line:
+                mfma += 1
+        assert own == 0, "compiler-emitted accumulator moves"
+        assert mfma == 256

@@ -275,3 +275,34 @@ def test_standalone_perm_matches_fused():
                                     ctypes.c_void_p(stream))
     assert st == 0
     assert torch.equal(wp.view(torch.int16), wp2.view(torch.int16))
+
+
+@pytest.mark.parametrize("M,K,N,Gs,p,dt,aq", CASES + [(4096, 4096, 4096, 128, 0.10, torch.float16, "per_group")])
+def test_fqt8_matches_fqt7j(M, K, N, Gs, p, dt, aq):
+    """sqmp_gemm_fqt8 (one wave per SIMD) on the SQMP_QA_TILED4 operands == sqmp_gemm_fqt7j
+    (J = 4) on the same operands, bit for bit (the same MFMA sequence per output), the fused
+    column statistics too; test_fqt_operands_exact_and_y pins fqt7j against the oracle."""
+    dev = _dev()
+    from smoothquant import ops
+    q, lin, x = _layer(dev, M, K, N, Gs, p, dt, aq=aq)
+    pw = q.packed()
+    Kq = (pw.K - pw.S + 63) // 64 * 64
+    if Kq % 128:
+        pytest.skip("tile-major operands need Kq % 128 == 0")
+    saved = ops.FQT7, ops.FQT7_J, ops.FQT8
+    ops.FQT7, ops.FQT7_J, ops.FQT8 = True, 4, False
+    try:
+        codes, scales, xs, wp = ops.quant_act_c4(x, pw, aq, 4, Gs)
+        assert scales.shape[2] == 64
+        c7 = torch.zeros(pw.N, dtype=torch.int32, device=dev)
+        y7 = ops.gemm_fqt(codes, scales, xs, wp, pw, lin.bias, Gs, colmax=c7)
+        ops.FQT8 = True
+        c8 = torch.zeros(pw.N, dtype=torch.int32, device=dev)
+        y8 = ops.gemm_fqt(codes, scales, xs, wp, pw, lin.bias, Gs, colmax=c8)
+        y8n = ops.gemm_fqt(codes, scales, xs, wp, pw, None, Gs)
+    finally:
+        ops.FQT7, ops.FQT7_J, ops.FQT8 = saved
+    assert torch.equal(y7.view(torch.int16), y8.view(torch.int16))
+    assert torch.equal(c7, c8)
+    b = lin.bias.detach().float() if lin.bias is not None else 0.0
+    assert rel(y8n.float() + b, y8.float()) < 2e-2

@@ -4,7 +4,8 @@ variants.  python tools/ab_fqt7.py [variants, "+"- or comma-separated] [rounds] 
 ENV (default SQMP_FQT7_OPT) names the per-launch variable; SQMP_FQ7_DIAG selects the timing
 diagnostics of a SQMP_DIAG=1 build (wrong results by design: no equality check then).  A
 variant "J4:3" runs the 64-row-block operands (ops.FQT7_J = 4) with value 3; "P..." times the
-prepass (quant_act_c4) of that variant instead of the GEMM."""
+prepass (quant_act_c4) of that variant instead of the GEMM; "F8:v" runs sqmp_gemm_fqt8 (one
+wave per SIMD) on the J = 4 operands."""
 import os
 import sys
 
@@ -28,15 +29,22 @@ stream = torch.cuda.current_stream(dev)
 def parse(v):
     pre = v.startswith("P")
     v = v[1:] if pre else v
+    if v.startswith("F8"):
+        return pre, 8, v[3:] or "0"
     j, val = (int(v[1:v.index(":")]), v[v.index(":") + 1:]) if v.startswith("J") else (2, v)
     return pre, j, val
+
+
+def use(j):
+    ops.FQT8 = j == 8
+    ops.FQT7_J = 4 if j == 8 else j
 
 
 ops_c4 = {}
 for v in variants:
     _, j, _ = parse(v)
     if j not in ops_c4:
-        ops.FQT7_J = j
+        use(j)
         ops_c4[j] = ops.quant_act_c4(x, pw, "per_group", 4, bench.G)
 
 
@@ -44,10 +52,13 @@ def runner(v):
     pre, j, _ = parse(v)
     if pre:
         def f():
-            ops.FQT7_J = j
+            use(j)
             return ops.quant_act_c4(x, pw, "per_group", 4, bench.G)[0]
         return f
-    return lambda: ops.gemm_fqt(*ops_c4[j], pw, lin.bias, bench.G)
+    def g():
+        use(j)
+        return ops.gemm_fqt(*ops_c4[j], pw, lin.bias, bench.G)
+    return g
 
 
 ref = None
