@@ -15,17 +15,24 @@
 // written out: per stage 32 blocks (block t = wp row tile t % 16 of sub-step t / 16), each one
 // LDS fragment read PF = 3 blocks ahead and 4 MFMAs (one per 16-token tile);
 //   blocks 4-7     decode the stage's sub-step-1 act fragments (4 x bpack dword -> 8 halves)
+//   block 8        issues stage kt + 2's act operand into the registers just decoded
 //   blocks 1..15   (odd) the 8 LDS-DMA pieces of stage kt + 2 (3-slot ring)
-//   block 19       the counted vmcnt that retires the next stage's act codes (and everything
-//                  older: this wave's pieces of stage kt + 1), then its scales prepared
+//   block 19       the counted vmcnt that retires stage kt + 1's act operand and DMA pieces,
+//                  then its scales prepared
 //   blocks 20-23   decode the NEXT stage's sub-step-0 fragments (so a stage opens on MFMAs)
-// and one s_barrier per stage.  The MFMAs are issued from inline asm with "+a" accumulators,
-// so the 256 accumulators stay in AGPRs (hipcc's own MFMA allocation shuffled them through
-// VGPRs at this register count: 1.25 v_accvgpr per MFMA).  hipcc pads no
-// hazard inside an asm statement: the fragments an MFMA reads are written >= 12 blocks
-// earlier (decode) or waited for by hipcc's own lgkmcnt (LDS reads, which it sees as
-// operands), accumulators chain MFMA -> MFMA only (0 states), and the epilogue reads them
-// after an explicit s_nop pad.
+// and one s_barrier per stage.  The code stages whose next two are code stages run with every
+// kind known at compile time (no branches in that loop); the last code stages and the salient
+// ones run the same stage with the kinds tested at run time.  The 256 accumulators are literal
+// AGPRs (below); hipcc pads no hazard inside an asm statement: the fragments an MFMA reads are
+// written >= 12 blocks earlier (decode) or waited for by hipcc's own lgkmcnt (LDS reads, which
+// it sees as operands), accumulators chain MFMA -> MFMA only (0 states), and the epilogue reads
+// them after an explicit s_nop pad.
+//
+// Measured (config 2): 443 us vs sqmp_gemm_fqt7's 417 us on the same
+// box -- bit-identical results, opt-in (SQMP_FQT8=1).  Its timing diagnostics put the MFMA-only
+// floor of this tiling at 292 us; the wp DMA (+47 us), the act decode (+58 us) and the LDS
+// fragment reads (+34 us) each overflow the 8 free issue cycles of a 16-cycle 16x16x32 MFMA gap
+// at one wave per SIMD, where fqt7's partner wave hides them.
 //
 // Operands: wp [roundup(N, 256)][Kq + S_pad] (sqmp_quant_act_c4's permuted weight) by
 // LDS-DMA; the act codes / group scales / salient x in the SQMP_QA_TILED4 tile-major layouts
@@ -90,8 +97,8 @@ __device__ inline void fence(V& v) {
 // wave-uniform count -> immediate (waiting for more than needed is always safe)
 __device__ inline void vmwait_dyn(int n) {
   switch (n) {
-    case 8: vmwait<8>(); break;
-    case 4: vmwait<4>(); break;
+    case 16: vmwait<16>(); break;
+    case 11: vmwait<11>(); break;
     default: vmwait<0>(); break;
   }
 }
@@ -152,7 +159,10 @@ constexpr int RS = 2 * TM + 16;    // epilogue: y^T row stride (bytes)
 constexpr int EPI = TN * RS;
 constexpr int LDS_BYTES = NS * SLOT > EPI ? NS * SLOT : EPI;
 
-template <class DT>
+// DIAG (timing diagnostics, wrong results by design, instantiated only in a SQMP_DIAG_BUILD,
+// selected by SQMP_FQT8_DIAG): 1 no wp DMA in the K loop, 2 no LDS fragment reads in it, 4 no
+// act decode / copy, 8 no barrier, 16 no act operand loads in it.
+template <class DT, int DIAG = 0>
 __global__ __launch_bounds__(256, 1) void gemm_kernel(
     const typename DT::T* __restrict__ A, const uint32_t* __restrict__ Ct,
     const typename DT::T* __restrict__ St, const typename DT::T* __restrict__ Xt,
@@ -244,19 +254,17 @@ __global__ __launch_bounds__(256, 1) void gemm_kernel(
   // branches): act fragments decoded from cs[P] (k < nkm) or taken from the exact salient x in
   // dd[P]; the next stage's operand loaded into cs[P ^ 1] / dd[P ^ 1] (or none after the last).
   // 32 blocks (sub-step t / 16, wp row tile t % 16), 4 MFMAs each, MFMAs always on bf.
-  auto stage = [&](int k, int slot_c, int slot_d, auto pp) {
+  auto stage = [&](int k, int slot_c, int slot_d, auto pp, auto steady) {
     constexpr int P = decltype(pp)::value, PN = P ^ 1;
-    const bool cur_codes = k < nkm;
-    const int nk = k + 1 < nkm ? 0 : (k + 1 < nkt ? 1 : 2);  // next: codes / salient / none
-    barrier();  // every wave's pieces of stage k landed (their vmcnt ran a stage earlier);
-                // every wave is done with slot_d (read in stage k - 1)
-    // the next stage's act operand goes out first: its wait at block 19 leaves only the DMA
-    // pieces issued after it in flight
-    if (nk == 0)
-      issue_codes(k + 1, cs[PN]);
-    else if (nk == 1)
-      issue_dense(k + 1 - nkm, dd[PN]);
-    const bool dma = k + 2 < nkt;
+    // steady: k, k + 1 and k + 2 all code stages (known at compile time: no branches)
+    constexpr bool ST = decltype(steady)::value;
+    const bool cur_codes = ST || k < nkm;
+    const int nk = ST ? 0 : (k + 1 < nkm ? 0 : (k + 1 < nkt ? 1 : 2));  // next: codes / salient / none
+    const int n2 = ST ? 0 : (k + 2 < nkm ? 0 : (k + 2 < nkt ? 1 : 2));  // the one after
+    if constexpr (!(DIAG & 8))
+      barrier();  // every wave's pieces of stage k landed (their vmcnt ran a stage earlier);
+                  // every wave is done with slot_d (read in stage k - 1)
+    const bool dma = !(DIAG & 1) && (ST || k + 2 < nkt);
     const unsigned char* __restrict__ slot = lds + slot_c * SLOT;
     const uint32_t dlds = lds_base + (uint32_t)slot_d * SLOT + (uint32_t)wave * 1024u;
     const uint32_t dso = (uint32_t)(k + 2) * 128u;
@@ -266,7 +274,7 @@ __global__ __launch_bounds__(256, 1) void gemm_kernel(
       a[t] = *(const u32x4*)(slot + 16 * (t % I) * 128 + a_lo[t / I]);
     sfor<0, 2 * I>([&](auto tc) {
       constexpr int t = decltype(tc)::value;
-      if constexpr (t + PF < 2 * I)
+      if constexpr (t + PF < 2 * I && !(DIAG & 2))
         a[(t + PF) % (PF + 1)] =
             *(const u32x4*)(slot + 16 * ((t + PF) % I) * 128 + a_lo[(t + PF) / I]);
       constexpr int s = t / I, i = t % I;
@@ -275,7 +283,7 @@ __global__ __launch_bounds__(256, 1) void gemm_kernel(
         MfmaA<DT, 4 * (J * i + j)>::run(bf[s][j], a[t % (PF + 1)]);
       });
       // this stage's sub-step-1 fragments (blocks 4-7: >= 8 MFMAs after their last read)
-      if constexpr (t >= 4 && t < 4 + J) {
+      if constexpr (t >= 4 && t < 4 + J && !(DIAG & 4)) {
         if (cur_codes)
           bf[1][t - 4] = dec(cs[P], sp[P], t - 4, 1);
         else
@@ -284,9 +292,21 @@ __global__ __launch_bounds__(256, 1) void gemm_kernel(
       if constexpr ((t & 1) && t < 16) {  // piece t / 2 of stage k + 2
         if (dma) dma16(rA, a_off, dso + (uint32_t)(t >> 1) * a_piece, dlds + (uint32_t)(t >> 1) * 4096u);
       }
+      // stage k + 2's act operand into the registers this stage finished decoding at block 7
+      // (two stages of latency: with one wave per SIMD nothing else hides it)
+      if constexpr (t == 8 && !(DIAG & 16)) {
+        if (n2 == 0)
+          issue_codes(k + 2, cs[P]);
+        else if (n2 == 1)
+          issue_dense(k + 2 - nkm, dd[P]);
+      }
       if constexpr (t == 19) {
         if (nk != 2) {
-          vmwait_dyn(dma ? 8 : 0);
+          // in flight after the wait: this stage's DMA pieces and operand (both for k + 2)
+          if constexpr ((DIAG & 17) != 0)
+            vmwait<0>();
+          else
+            vmwait_dyn(dma ? (n2 == 0 ? 11 : 16) : 0);
           if (nk == 0) {
             fence(cs[PN].w[0]);
             fence(cs[PN].w[1]);
@@ -299,7 +319,7 @@ __global__ __launch_bounds__(256, 1) void gemm_kernel(
         }
       }
       // the next stage's sub-step-0 fragments (its first MFMAs then wait on nothing)
-      if constexpr (t >= 20 && t < 20 + J) {
+      if constexpr (t >= 20 && t < 20 + J && !(DIAG & 4)) {
         if (nk == 0)
           bf[0][t - 20] = dec(cs[PN], sp[PN], t - 20, 0);
         else if (nk == 1)
@@ -312,16 +332,17 @@ __global__ __launch_bounds__(256, 1) void gemm_kernel(
   using Z = std::integral_constant<int, 0>;
   using O = std::integral_constant<int, 1>;
 
-  // ---- prologue: DMA(0), codes(0), DMA(1); wait for DMA(0) and codes(0) (nkm >= 2)
+  // ---- prologue: DMA(0), codes(0), codes(1), DMA(1); wait for DMA(0) and codes(0) (nkm >= 2)
 #pragma unroll
   for (int p = 0; p < 8; ++p)
     dma16(rA, a_off, (uint32_t)p * a_piece, lds_base + (uint32_t)(4 * p + wave) * 1024u);
   issue_codes(0, cs[0]);
+  issue_codes(1, cs[1]);
 #pragma unroll
   for (int p = 0; p < 8; ++p)
     dma16(rA, a_off, 128u + (uint32_t)p * a_piece,
           lds_base + (uint32_t)SLOT + (uint32_t)(4 * p + wave) * 1024u);
-  vmwait<8>();
+  vmwait<11>();
   fence(cs[0].w[0]);
   fence(cs[0].w[1]);
   fence(cs[0].s);
@@ -331,12 +352,22 @@ __global__ __launch_bounds__(256, 1) void gemm_kernel(
 
   // ---- every stage in ONE loop (one register allocation for all of them): pairs of stages
   // with compile-time register parity
-  int sc = 0;
-  for (int k = 0; k < nkt; k += 2) {
-    stage(k, sc, sc == 0 ? 2 : sc - 1, Z());
+  using Yes = std::true_type;
+  using No = std::false_type;
+  int sc = 0, k = 0;
+  // the code stages whose next two are code stages too: every kind known at compile time
+  for (; k + 3 < nkm; k += 2) {
+    stage(k, sc, sc == 0 ? 2 : sc - 1, Z(), Yes());
+    sc = sc == 2 ? 0 : sc + 1;
+    stage(k + 1, sc, sc == 0 ? 2 : sc - 1, O(), Yes());
+    sc = sc == 2 ? 0 : sc + 1;
+  }
+  // the rest (the last code stages and the salient ones): kinds at run time
+  for (; k < nkt; k += 2) {
+    stage(k, sc, sc == 0 ? 2 : sc - 1, Z(), No());
     sc = sc == 2 ? 0 : sc + 1;
     if (k + 1 < nkt) {
-      stage(k + 1, sc, sc == 0 ? 2 : sc - 1, O());
+      stage(k + 1, sc, sc == 0 ? 2 : sc - 1, O(), No());
       sc = sc == 2 ? 0 : sc + 1;
     }
   }
@@ -395,10 +426,32 @@ static int launch(const void* wp, const void* codes_t, const void* scale_t, cons
   // kernel M = weight rows (wp rows, N of the layer), kernel N = tokens (M of the layer)
   const int tiles_m = cdiv(N, TM), tiles_n = cdiv(M, TN);
   const int nt = nt_output((size_t)M * N * sizeof(T)) ? 1 : 0;
-  gemm_kernel<DT><<<dim3(tiles_m * tiles_n), dim3(256), 0, s>>>(
-      (const T*)wp, (const uint32_t*)codes_t, (const T*)scale_t, (const T*)sal_t,
-      (const T*)bias, (T*)y, N, M, Kq, S_pad, G, ngq, tiles_m, tiles_n, group_m_env(), colmax,
-      nt);
+  auto go = [&](auto kern) {
+    kern<<<dim3(tiles_m * tiles_n), dim3(256), 0, s>>>(
+        (const T*)wp, (const uint32_t*)codes_t, (const T*)scale_t, (const T*)sal_t,
+        (const T*)bias, (T*)y, N, M, Kq, S_pad, G, ngq, tiles_m, tiles_n, group_m_env(), colmax,
+        nt);
+  };
+#ifdef SQMP_DIAG_BUILD
+  const char* de = getenv("SQMP_FQT8_DIAG");
+  const int diag = de ? atoi(de) : 0;
+  if (std::is_same<DT, F16>::value && diag) {
+    switch (diag) {
+      case 1: go(gemm_kernel<DT, 1>); break;
+      case 2: go(gemm_kernel<DT, 2>); break;
+      case 4: go(gemm_kernel<DT, 4>); break;
+      case 8: go(gemm_kernel<DT, 8>); break;
+      case 16: go(gemm_kernel<DT, 16>); break;
+      case 7: go(gemm_kernel<DT, 7>); break;
+      case 20: go(gemm_kernel<DT, 20>); break;
+      case 31: go(gemm_kernel<DT, 31>); break;
+      default: return SQMP_EINVAL;
+    }
+    SQMP_LAUNCH_CHECK();
+    return SQMP_OK;
+  }
+#endif
+  go(gemm_kernel<DT>);
   SQMP_LAUNCH_CHECK();
   return SQMP_OK;
 }
