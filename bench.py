@@ -72,7 +72,7 @@ def parse(argv=None):
                          "runs on the f16 MFMA as sqmp_gemm_h2)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--no-layer", action="store_true",
-                    help="skip the Llama-2-7B decoder-layer line (llama_layer)")
+                    help="skip the secondary lines (per_token, llama_layer)")
     ap.add_argument("--rehearsal", action="store_true",
                     help="CPU/gloo rehearsal of the launcher and timing path (no GPU): the "
                          "step is the CPU fake-quant layer on a 64-row batch")
@@ -358,6 +358,52 @@ def llama_layer(dev, iters=40):
     }
 
 
+def per_token_leg(dev, iters=200):
+    """The per_token act mode of the same config-2 layer (BASELINE configs' per_token rows; the
+    reference's per_token path, fake_quant.py:64-90): W4A4Linear.forward on the auto kernel
+    (e4m3 codes on the block-scaled FP8 MFMA, sqmp_gemm_f8), step and GEMM timed with HIP
+    events on the launch stream; frac against the dense FP8 MFMA peak."""
+    from smoothquant import ops
+    q, x, lin = make_layer(dev, "per_token", seed=4321)
+    pw = q.packed()
+    stream = torch.cuda.current_stream(dev)
+    flops = 2.0 * M * N * K
+    use_f8 = ops.f8_auto(pw, "per_token", 4)
+    if use_f8:
+        a8, sa, xs = ops.quant_act_f8(x, pw, "per_token", 4)
+        gemm = lambda: ops.gemm_f8(a8, sa, xs, pw, lin.bias)  # noqa: E731
+        quant = lambda: ops.quant_act_f8(x, pw, "per_token", 4)  # noqa: E731
+        kdt = "f8"
+    else:
+        a = ops.quant_act_fp(x, pw, "per_token", 4, G)
+        gemm = lambda: ops.gemm_fq(a, pw, lin.bias)  # noqa: E731
+        quant = lambda: ops.quant_act_fp(x, pw, "per_token", 4, G)  # noqa: E731
+        kdt = "f16"
+    step = lambda: q(x)  # noqa: E731
+    for fn in (gemm, quant, step):
+        for _ in range(20):
+            fn()
+    gemm_ms = time_events(gemm, iters, stream)
+    quant_ms = time_events(quant, iters, stream)
+    step_ms = time_events(step, iters, stream)
+    achieved = flops / (gemm_ms * 1e-3) / 1e12
+    return {
+        "workload": "the config-2 layer with act per_token (4-bit, per-row absmax), weight "
+                    "per_group(sorted), 10% salient",
+        "kernel": ("sqmp_gemm_f8 (e4m3 codes, block-scaled FP8 MFMA) + fp16 salient tail"
+                   if use_f8 else "sqmp_gemm_fq (fp16 D values)"),
+        "ms_per_step": round(step_ms, 4),
+        "TFLOP_per_s": round(flops / (step_ms * 1e-3) / 1e12, 1),
+        "gemm_avg_ms": round(gemm_ms, 4),
+        "gemm_TFLOP_per_s": round(achieved, 1),
+        "peak": PEAK_TFLOPS[kdt],
+        "frac": round(achieved / PEAK_TFLOPS[kdt], 4),
+        "prepass_avg_ms": round(quant_ms, 4),
+        "note": "HIP events, 200 back-to-back calls each after 20 warm-up; frac = GEMM "
+                "achieved / dense peak of the kernel's MFMA dtype (FP8 5033 TFLOP/s)",
+    }
+
+
 # ------------------------------------------------------------------ rehearsal (CPU)
 def rehearsal(args, rank, world):
     """The launcher / barrier / max-over-ranks / report path on CPU with gloo: the step is
@@ -585,6 +631,8 @@ def main(argv=None):
                     "forward, plus launch gaps)",
         },
     }
+    if not fp32 and args.act == "per_group" and not args.no_layer:
+        out["per_token"] = per_token_leg(dev)
     if not fp32 and not args.no_layer:
         out["llama_layer"] = llama_layer(dev)
     if rank == 0 and world == 1 and not args.no_cpu:
