@@ -341,8 +341,10 @@ int sqmp_permute_act(const void* src, void* dst, const int32_t* map, int dtype, 
  * packed order), outs[o] its SQMP_OUT_FP operand D [roundup(M, 256) rows][Kp + S_pad].  Every
  * outs[o] equals what sqmp_quant_act_v2(..., SQMP_OUT_FP, ...) writes for weight o, bit for
  * bit.  The weights share K, Kp, S_pad and the salient set.  fp16 / bf16, act mode PER_GROUP
- * or PER_GROUP_MEAN3STD, group_size a power of two in [16, 1024], K - S <= 16384, flags ==
- * SQMP_QA_CLEAN_WS.  amaps, posmaps and outs are HOST arrays of device pointers. */
+ * or PER_GROUP_MEAN3STD, group_size a power of two in [16, 1024], K - S <= 16384,
+ * 4 (Kp + S_pad + 8) nout <= 150 KiB (one LDS region per output), flags == SQMP_QA_CLEAN_WS
+ * (else SQMP_EUNSUPPORTED before anything is launched).  amaps, posmaps and outs are HOST
+ * arrays of device pointers. */
 int sqmp_quant_act_group(void* x, int dtype, int M, int K, int amode, int n_bits,
                          int group_size, int nout, const int32_t* const* amaps,
                          const int32_t* const* posmaps, int Kp, const int32_t* nonsal,

@@ -224,7 +224,9 @@ __device__ __forceinline__ void quant_lc_body(
   // x and out alias for in-place output quantization (every row is read before it is
   // written: a workgroup stores a pair only after loading it)
   typedef typename DT::T T;
-  extern __shared__ __attribute__((aligned(16))) uint32_t lc_buf[];  // [W + 8] column pairs
+  // [NOUT][W + 8] column pairs: region 0 = the interleaved input, then output 0; region o =
+  // sibling output o - 1 (written by the scatter only, so its salient positions stay zero)
+  extern __shared__ __attribute__((aligned(16))) uint32_t lc_buf[];
   __shared__ float lc_red[2][LC_MAXW];
   const int nthr = blockDim.x;
   const int NW = nthr >> 6;
@@ -287,11 +289,8 @@ __device__ __forceinline__ void quant_lc_body(
     return zm;
   };
   const uint64_t zmask = zmask_of(amap);
-  // the sibling outputs' salient / padding positions (their own packed orders)
-  uint64_t zmask_s[NOUT > 1 ? NOUT - 1 : 1];
-#pragma unroll
-  for (int o = 0; o + 1 < NOUT; ++o) zmask_s[o] = zmask_of(sib.amap[o]);
-  for (int c = tid; c < W + 2; c += nthr) lc_buf[c] = 0u;
+  const int RW = W + 8;  // LDS region stride (words; a multiple of 8)
+  for (int c = tid; c < (NOUT > 1 ? NOUT * RW : W + 2); c += nthr) lc_buf[c] = 0u;
   // the column statistics of this call, read by the (completed) table kernel: restore the
   // clean-workspace zeros
   if (key_clear)
@@ -360,7 +359,12 @@ __device__ __forceinline__ void quant_lc_body(
     uint32_t v[RPL];
 #pragma unroll
     for (int i = 0; i < RPL; ++i) v[i] = lc_buf[tab[i] & 0xFFFFu];
-    for (int j = tid; j < S; j += nthr) lc_buf[P + j] = lc_buf[sal[j]];
+    for (int j = tid; j < S; j += nthr) {
+      const uint32_t xs = lc_buf[sal[j]];
+      lc_buf[P + j] = xs;
+#pragma unroll
+      for (int o = 1; o < NOUT; ++o) lc_buf[o * RW + P + j] = xs;  // the shared salient tail
+    }
 
     // ---- scales, then quantize + scatter
     if (MODE == LC_MODE_GROUP && GS > 0) {
@@ -470,8 +474,10 @@ __device__ __forceinline__ void quant_lc_body(
       } else {
 #pragma unroll
         for (int i = 0; i < RPL; ++i) {
-          v[i] = quant_pair<DT>(v[i], c);  // kept for the sibling outputs
-          lc_buf[tab[i] >> 16] = v[i];
+          const uint32_t y = quant_pair<DT>(v[i], c);
+          lc_buf[tab[i] >> 16] = y;
+#pragma unroll
+          for (int o = 1; o < NOUT; ++o) lc_buf[o * RW + (tabs[o - 1][i] >> 16)] = y;
         }
       }
     }
@@ -533,39 +539,12 @@ __device__ __forceinline__ void quant_lc_body(
       __syncthreads();  // the buffer is rewritten by the next pair
       continue;
     }
-    // ---- de-interleave 16-B chunks and store both rows
-    T* o0 = out + (size_t)m0 * W;
-    T* o1 = out + (size_t)(m0 + 1) * W;
+    // ---- de-interleave 16-B chunks and store both rows of every output
     for (int c = tid; c < ochk; c += nthr) {
-      const u32x4 a = ((const u32x4*)lc_buf)[2 * c];
-      const u32x4 b = ((const u32x4*)lc_buf)[2 * c + 1];
-      u32x4 y0, y1;
-      y0[0] = __builtin_amdgcn_perm(a[1], a[0], 0x05040100u);
-      y0[1] = __builtin_amdgcn_perm(a[3], a[2], 0x05040100u);
-      y0[2] = __builtin_amdgcn_perm(b[1], b[0], 0x05040100u);
-      y0[3] = __builtin_amdgcn_perm(b[3], b[2], 0x05040100u);
-      y1[0] = __builtin_amdgcn_perm(a[1], a[0], 0x07060302u);
-      y1[1] = __builtin_amdgcn_perm(a[3], a[2], 0x07060302u);
-      y1[2] = __builtin_amdgcn_perm(b[1], b[0], 0x07060302u);
-      y1[3] = __builtin_amdgcn_perm(b[3], b[2], 0x07060302u);
-      ((u32x4*)o0)[c] = y0;
-      if (has1) ((u32x4*)o1)[c] = y1;
-    }
-    __syncthreads();  // the buffer is rewritten by the next pair
-    // ---- the sibling outputs: the same quantized pairs scattered to their packed positions
-    // (every position < P is rewritten: non-salient ones by the scatter, salient ones zeroed;
-    // the exact salient tail >= P is shared)
 #pragma unroll
-    for (int o = 0; o + 1 < NOUT; ++o) {
-#pragma unroll
-      for (int i = 0; i < RPL; ++i) lc_buf[tabs[o][i] >> 16] = v[i];
-      for (uint64_t zm = zmask_s[o]; zm; zm &= zm - 1) lc_buf[zp0 + __builtin_ctzll(zm)] = 0u;
-      __syncthreads();
-      T* s0 = (T*)sib.out[o] + (size_t)m0 * W;
-      T* s1 = (T*)sib.out[o] + (size_t)(m0 + 1) * W;
-      for (int c = tid; c < ochk; c += nthr) {
-        const u32x4 a = ((const u32x4*)lc_buf)[2 * c];
-        const u32x4 b = ((const u32x4*)lc_buf)[2 * c + 1];
+      for (int o = 0; o < NOUT; ++o) {
+        const u32x4 a = ((const u32x4*)(lc_buf + o * RW))[2 * c];
+        const u32x4 b = ((const u32x4*)(lc_buf + o * RW))[2 * c + 1];
         u32x4 y0, y1;
         y0[0] = __builtin_amdgcn_perm(a[1], a[0], 0x05040100u);
         y0[1] = __builtin_amdgcn_perm(a[3], a[2], 0x05040100u);
@@ -575,11 +554,12 @@ __device__ __forceinline__ void quant_lc_body(
         y1[1] = __builtin_amdgcn_perm(a[3], a[2], 0x07060302u);
         y1[2] = __builtin_amdgcn_perm(b[1], b[0], 0x07060302u);
         y1[3] = __builtin_amdgcn_perm(b[3], b[2], 0x07060302u);
-        ((u32x4*)s0)[c] = y0;
-        if (has1) ((u32x4*)s1)[c] = y1;
+        T* ob = o == 0 ? out : (T*)sib.out[o - 1];
+        ((u32x4*)(ob + (size_t)m0 * W))[c] = y0;
+        if (has1) ((u32x4*)(ob + (size_t)(m0 + 1) * W))[c] = y1;
       }
-      __syncthreads();
     }
+    __syncthreads();  // the buffer is rewritten by the next pair
   }
 }
 
@@ -736,7 +716,7 @@ static int quant_lc_launch(const void* x, int M, int K, int q_max, int G, const 
   typedef typename DT::T T;
   const void* kf = (const void*)quant_lc_kernel<DT, MODE, LC_RPL, GS, F8, NOUT>;
   const int nw = lc_waves(K, Kn);
-  const size_t lds = sizeof(uint32_t) * (size_t)(P + S_pad + 8);
+  const size_t lds = sizeof(uint32_t) * (size_t)(P + S_pad + 8) * NOUT;
   SQMP_HIP_CHECK(hipFuncSetAttribute(kf, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   int per_cu = occ_per_cu(kf, 64 * nw, lds);
   if (const char* e = getenv("SQMP_LC_PERCU"))  // tuning only (0 / unparsable: the default)
@@ -794,6 +774,8 @@ int launch_quant_lc_group(int dtype, const void* x, int M, int K, int q_max, int
                           const int32_t* nonsal, void* out, uint32_t* key_clear, int clear_words,
                           const LcSib& sib, hipStream_t s) {
   if (G < LC_RPL || sib.n < 0 || sib.n > 2) return SQMP_EUNSUPPORTED;
+  // one LDS region of P + S_pad + 8 words per output
+  if ((size_t)4 * (P + S_pad + 8) * (sib.n + 1) > 150 * 1024) return SQMP_EUNSUPPORTED;
 #define SQMP_LCG(DTT, NO)                                                                     \
   quant_lc_launch<DTT, LC_MODE_GROUP, 0, 0, NO>(x, M, K, q_max, G, lctab, Kn, amap, P, sal, S, \
                                                S_pad, cmax, nonsal, out, key_clear,            \
