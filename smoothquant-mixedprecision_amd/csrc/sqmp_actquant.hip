@@ -520,37 +520,36 @@ __global__ __launch_bounds__(256) void lc_table_kernel(
 
 // ---------------------------------------------------------------- rank + table, one launch
 // For up to RT_MAX columns: every workgroup stages ALL K column keys in LDS (coalesced 16-B
-// loads, one round trip; the salient columns then overwritten by the 0xFFFFFFFF sentinel,
-// which never orders before a key: |x| maxima never set the sign bit) and ranks R * 256 / TPO
-// owner COLUMNS, TPO lanes per group of R owners splitting the competitors (16-B LDS reads,
-// interleaved so the TPO lanes hit consecutive chunks; each chunk read is compared against
-// all R owners), then reduces the TPO partial counts by lane shuffles.  The stable rank of
-// non-salient owner column i is
-//   #{c : key_c < key_i} + #{c < i : key_c == key_i}    (c over the non-salient columns)
-// -- the reference's stable argsort over the non-salient list (fake_quant.py:113; the list is
-// ascending in column, so list order and column order break ties alike) -- counted as
-// key_c < thr with thr = key_i + 1 on 4-column chunks wholly below i, key_i elsewhere, plus
-// the equal keys of i's own chunk below i.  Writes colsorted[r] and lctab[r] = col |
-// posmap[col] << 16, and the (zero, sink) entries of ranks [K - S, lc_len).  The keys are NOT
-// cleared here (other workgroups may still read them): the quantizer launched next clears
-// them.
+// loads issued first, one round trip), the columns that are not in the list (the salient
+// ones: `nonsal` is the ascending list of the others; the salient list itself may be absent,
+// as for the in-place output quantizer) replaced by the 0xFFFFFFFF sentinel, which never
+// orders before a key (|x| maxima never set the sign bit), through a K-bit LDS mask built
+// from the list; then ranks R * 256 / TPO owner COLUMNS, TPO lanes per group of R owners
+// splitting the competitors (16-B LDS reads, interleaved so the TPO lanes hit consecutive
+// chunks; each chunk read is compared against all R owners), and reduces the TPO partial
+// counts by lane shuffles.  The stable rank of listed owner column i is
+//   #{c : key_c < key_i} + #{c < i : key_c == key_i}    (c over the listed columns)
+// -- the reference's stable argsort over the list (fake_quant.py:113; the list is ascending
+// in column, so list order and column order break ties alike) -- counted as key_c < thr
+// with thr = key_i + 1 on 4-column chunks wholly below i, key_i elsewhere, plus the equal
+// keys of i's own chunk below i.  Writes colsorted[r] and lctab[r] = col | posmap[col] << 16,
+// and the (zero, sink) entries of ranks [L, lc_len).  The keys are NOT cleared here (other
+// workgroups may still read them): the quantizer launched next clears them.
 constexpr int RT_MAX = 16384;  // 64 KiB of keys in LDS
-constexpr int RT_SB = 8;       // 16-B key loads per thread per batch
-constexpr int RT_SS = 4;       // salient indices per thread per batch
+constexpr int RT_SB = RT_MAX / 1024;  // 16-B key chunks per thread: all of them in one batch
 
-// stage the K keys (padded with the sentinel to 4 K4 entries), then the salient sentinels
-__device__ inline void rank_stage_keys(const uint32_t* key, int K, const int32_t* __restrict__ sal,
-                                       int S, int K4, uint32_t* rt_kv) {
+__device__ inline int rank_mask_words(int K) { return (K + 31) >> 5; }
+
+// stage the K keys (padded with the sentinel to 4 K4 entries), unlisted columns as sentinels
+__device__ inline void rank_stage_keys(const uint32_t* key, int K, const int32_t* __restrict__ list,
+                                       int L, int K4, uint32_t* rt_kv, uint32_t* mask) {
   const int tid = threadIdx.x;
-  int si[RT_SS];
-#pragma unroll
-  for (int u = 0; u < RT_SS; ++u) si[u] = tid + 256 * u < S ? sal[tid + 256 * u] : -1;
   const bool kvec = (K & 3) == 0;
-  for (int c0 = tid; c0 < K4; c0 += 256 * RT_SB) {
-    u32x4 kv[RT_SB];
+  u32x4 kv[RT_SB];
 #pragma unroll
-    for (int u = 0; u < RT_SB; ++u) {
-      const int c = c0 + 256 * u;
+  for (int u = 0; u < RT_SB; ++u) {
+    const int c = tid + 256 * u;
+    if (c < K4) {
       if (kvec && 4 * c + 3 < K) {
         kv[u] = ((const u32x4*)key)[c];
       } else {
@@ -558,15 +557,31 @@ __device__ inline void rank_stage_keys(const uint32_t* key, int K, const int32_t
         for (int e = 0; e < 4; ++e) kv[u][e] = 4 * c + e < K ? key[4 * c + e] : 0xFFFFFFFFu;
       }
     }
-#pragma unroll
-    for (int u = 0; u < RT_SB; ++u)
-      if (c0 + 256 * u < K4) ((u32x4*)rt_kv)[c0 + 256 * u] = kv[u];
   }
-  __syncthreads();  // the sentinels overwrite staged keys
+  const bool all = L == K;  // every column listed: no mask
+  if (!all) {
+    for (int w = tid; w < rank_mask_words(K); w += 256) mask[w] = 0u;
+    __syncthreads();
+    for (int j = tid; j < L; j += 256) {
+      const int c = list[j];
+      atomicOr(&mask[c >> 5], 1u << (c & 31));
+    }
+    __syncthreads();
+  }
 #pragma unroll
-  for (int u = 0; u < RT_SS; ++u)
-    if (si[u] >= 0) rt_kv[si[u]] = 0xFFFFFFFFu;
-  for (int j = tid + 256 * RT_SS; j < S; j += 256) rt_kv[sal[j]] = 0xFFFFFFFFu;
+  for (int u = 0; u < RT_SB; ++u) {
+    const int c = tid + 256 * u;
+    if (c < K4) {
+      u32x4 v = kv[u];
+      if (!all) {
+        const uint32_t mw = 4 * c < K ? mask[(4 * c) >> 5] >> ((4 * c) & 31) : 0u;
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (!((mw >> e) & 1u)) v[e] = 0xFFFFFFFFu;
+      }
+      ((u32x4*)rt_kv)[c] = v;
+    }
+  }
 }
 
 // Rank the R owner columns g0 .. g0 + R - 1 of this lane group (TPO lanes, `sub` = this
@@ -616,15 +631,16 @@ __device__ inline void rank_owner_group(const uint32_t* rt_kv, int K, int K4, in
 
 template <int TPO, int R>
 __global__ __launch_bounds__(256) void rank_table_kernel(
-    const uint32_t* __restrict__ key, int K, const int32_t* __restrict__ sal, int S,
+    const uint32_t* __restrict__ key, int K, const int32_t* __restrict__ list, int L,
     const int32_t* __restrict__ posmap, int32_t* __restrict__ colsorted,
     uint32_t* __restrict__ lctab, int lc_len, uint32_t lc_none, SibTables sib) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t rt_kv[];  // roundup(K, 4 TPO)
+  // roundup(K, 4 TPO) keys, then the K-bit list mask
+  extern __shared__ __attribute__((aligned(16))) uint32_t rt_kv[];
   const int tid = threadIdx.x;
   const int K4 = (int)round_up_dev(K, 4 * TPO) >> 2;
-  rank_stage_keys(key, K, sal, S, K4, rt_kv);
+  rank_stage_keys(key, K, list, L, K4, rt_kv, rt_kv + 4 * K4);
   const int nt = gridDim.x * 256;
-  for (int r = K - S + blockIdx.x * 256 + tid; r < lc_len; r += nt) {
+  for (int r = L + blockIdx.x * 256 + tid; r < lc_len; r += nt) {
     lctab[r] = lc_none;
     for (int o = 0; o < sib.n; ++o) sib.lctab[o][r] = lc_none;
   }
@@ -639,8 +655,8 @@ static bool rank_table_fits(int K) {
   return !off && K > 0 && K <= RT_MAX;
 }
 
-// key [K] column keys, sal [S] the salient columns (the list is the other K - S, ascending)
-static int launch_rank_table(const uint32_t* key, int K, const int32_t* sal, int S,
+// key [K] column keys, list [L] the ranked columns (ascending; the others are salient)
+static int launch_rank_table(const uint32_t* key, int K, const int32_t* list, int L,
                              const int32_t* posmap, int32_t* colsorted, uint32_t* lctab,
                              int lc_len, uint32_t lc_none, hipStream_t s,
                              const SibTables& sib = SibTables{}) {
@@ -654,17 +670,17 @@ static int launch_rank_table(const uint32_t* key, int K, const int32_t* sal, int
   if (te && (atoi(te) == 8 || atoi(te) == 16 || atoi(te) == 32)) tpo = atoi(te);
   if (re && (atoi(re) == 1 || atoi(re) == 2 || atoi(re) == 4)) r = atoi(re);
   const int grid = cdiv((long)K * tpo, 256L * r);
-  const size_t lds = sizeof(uint32_t) * (size_t)round_up(K, 4 * tpo);
+  const size_t lds = sizeof(uint32_t) * ((size_t)round_up(K, 4 * tpo) + (size_t)((K + 31) >> 5));
 #define SQMP_RT(T, RR)                                                                       \
   do {                                                                                      \
     static bool attr = false; /* up to 64 KiB of keys: raise the dynamic-LDS limit once */ \
     if (!attr) {                                                                            \
       SQMP_HIP_CHECK(hipFuncSetAttribute((const void*)rank_table_kernel<T, RR>,             \
                                          hipFuncAttributeMaxDynamicSharedMemorySize,        \
-                                         4 * RT_MAX));                                      \
+                                         4 * RT_MAX + 4 * (RT_MAX / 32)));                  \
       attr = true;                                                                          \
     }                                                                                       \
-    rank_table_kernel<T, RR><<<dim3(grid), dim3(256), lds, s>>>(key, K, sal, S, posmap,      \
+    rank_table_kernel<T, RR><<<dim3(grid), dim3(256), lds, s>>>(key, K, list, L, posmap,     \
                                                                colsorted, lctab, lc_len,    \
                                                                lc_none, sib);               \
   } while (0)
@@ -1294,7 +1310,7 @@ static int quant_act_impl(void* x, int dtype, int M, int K, int amode, int n_bit
         if (st2) return st2;
         if (rank_table_fits(K)) {
           key_clear = cmax;  // cleared by the quantizer, after every rank_table read
-          return launch_rank_table(cmax, K, salient, S, pm, colsorted, lctab, lc_len, none, s);
+          return launch_rank_table(cmax, K, nonsal, Kn, pm, colsorted, lctab, lc_len, none, s);
         }
         if (!clean) SQMP_HIP_CHECK(hipMemsetAsync(counts, 0, sizeof(int32_t) * k64, s));
         st2 = launch_rank_count(cmax, nonsal, Kn, counts, s);
@@ -1569,7 +1585,7 @@ extern "C" int sqmp_quant_act_group(void* x, int dtype, int M, int K, int amode,
   int r = amode == SQMP_ACT_PER_GROUP ? launch_colmax(x, dtype, M, K, cmax, s, false)
                                       : launch_colkey_mean3std(x, dtype, M, K, sums, cmax, s, true);
   if (r) return r;
-  r = launch_rank_table(cmax, K, salient, S, posmaps[0], colsorted, lctab, lc_len, lc_none, s, st);
+  r = launch_rank_table(cmax, K, nonsal, Kn, posmaps[0], colsorted, lctab, lc_len, lc_none, s, st);
   if (r) return r;
   return launch_quant_lc_group(dtype, x, M, K, (1 << (n_bits - 1)) - 1, group_size, lctab, Kn,
                                amaps[0], Kp, salient, S, S_pad, cmax, nonsal, outs[0], cmax,
