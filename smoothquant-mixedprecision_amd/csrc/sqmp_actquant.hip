@@ -519,76 +519,49 @@ __global__ __launch_bounds__(256) void lc_table_kernel(
 }
 
 // ---------------------------------------------------------------- rank + table, one launch
-// For up to RT_MAX columns: every workgroup stages ALL K column keys in LDS (coalesced 16-B
-// loads issued first, one round trip), the columns that are not in the list (the salient
-// ones: `nonsal` is the ascending list of the others; the salient list itself may be absent,
-// as for the in-place output quantizer) replaced by the 0xFFFFFFFF sentinel, which never
-// orders before a key (|x| maxima never set the sign bit), through a K-bit LDS mask built
-// from the list; then ranks R * 256 / TPO owner COLUMNS, TPO lanes per group of R owners
-// splitting the competitors (16-B LDS reads, interleaved so the TPO lanes hit consecutive
-// chunks; each chunk read is compared against all R owners), and reduces the TPO partial
-// counts by lane shuffles.  The stable rank of listed owner column i is
-//   #{c : key_c < key_i} + #{c < i : key_c == key_i}    (c over the listed columns)
-// -- the reference's stable argsort over the list (fake_quant.py:113; the list is ascending
-// in column, so list order and column order break ties alike) -- counted as key_c < thr
-// with thr = key_i + 1 on 4-column chunks wholly below i, key_i elsewhere, plus the equal
-// keys of i's own chunk below i.  Writes colsorted[r] and lctab[r] = col | posmap[col] << 16,
+// For lists up to RT_MAX entries: every workgroup stages all L keys key[nonsal[j]] in LDS
+// and ranks R * 256 / TPO owners, TPO lanes per group of R owners splitting the competitors
+// (16-B LDS reads, interleaved so the TPO lanes hit consecutive chunks; each chunk read is
+// compared against all R owners), then reduces the TPO partial counts by lane shuffles.  The
+// stable rank of owner i is
+//   #{j : key_j < key_i} + #{j < i : key_j == key_i}
+// (the reference's stable argsort, fake_quant.py:113), counted as key_j < thr with
+// thr = key_i + 1 on 4-entry chunks wholly below i, key_i elsewhere, plus the equal keys
+// of i's own chunk below i.  Writes colsorted[r] and lctab[r] = col | posmap[col] << 16,
 // and the (zero, sink) entries of ranks [L, lc_len).  The keys are NOT cleared here (other
 // workgroups may still read them): the quantizer launched next clears them.
+// The staging gathers up to SB entries per thread in one batch (all index loads, then
+// all key loads: two dependent round trips for the whole list up to 256 * SB entries):
+// SB = 24 up to 6144 entries, 64 above (one batch up to RT_MAX; SQMP_RT_SB=24 / 64 overrides).
 constexpr int RT_MAX = 16384;  // 64 KiB of keys in LDS
-constexpr int RT_SB = RT_MAX / 1024;  // 16-B key chunks per thread: all of them in one batch
 
-__device__ inline int rank_mask_words(int K) { return (K + 31) >> 5; }
-
-// stage the K keys (padded with the sentinel to 4 K4 entries), unlisted columns as sentinels
-__device__ inline void rank_stage_keys(const uint32_t* key, int K, const int32_t* __restrict__ list,
-                                       int L, int K4, uint32_t* rt_kv, uint32_t* mask) {
-  const int tid = threadIdx.x;
-  const bool kvec = (K & 3) == 0;
-  u32x4 kv[RT_SB];
+// stage the L keys key[nonsal[j]] (padded with 0xFFFFFFFF to 4 L4 entries) into LDS
+template <int RT_SB>
+__device__ inline void rank_stage_keys(const uint32_t* key, const int32_t* __restrict__ nonsal,
+                                       int L, int L4, uint32_t* rt_kv) {
+  for (int j0 = threadIdx.x; j0 < 4 * L4; j0 += 256 * RT_SB) {
+    int idx[RT_SB];
+    uint32_t kv[RT_SB];
 #pragma unroll
-  for (int u = 0; u < RT_SB; ++u) {
-    const int c = tid + 256 * u;
-    if (c < K4) {
-      if (kvec && 4 * c + 3 < K) {
-        kv[u] = ((const u32x4*)key)[c];
-      } else {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) kv[u][e] = 4 * c + e < K ? key[4 * c + e] : 0xFFFFFFFFu;
-      }
+    for (int u = 0; u < RT_SB; ++u) {
+      const int j = j0 + 256 * u;
+      idx[u] = j < L ? nonsal[j] : -1;
     }
-  }
-  const bool all = L == K;  // every column listed: no mask
-  if (!all) {
-    for (int w = tid; w < rank_mask_words(K); w += 256) mask[w] = 0u;
-    __syncthreads();
-    for (int j = tid; j < L; j += 256) {
-      const int c = list[j];
-      atomicOr(&mask[c >> 5], 1u << (c & 31));
-    }
-    __syncthreads();
-  }
 #pragma unroll
-  for (int u = 0; u < RT_SB; ++u) {
-    const int c = tid + 256 * u;
-    if (c < K4) {
-      u32x4 v = kv[u];
-      if (!all) {
-        const uint32_t mw = 4 * c < K ? mask[(4 * c) >> 5] >> ((4 * c) & 31) : 0u;
+    for (int u = 0; u < RT_SB; ++u) kv[u] = idx[u] >= 0 ? key[idx[u]] : 0xFFFFFFFFu;
 #pragma unroll
-        for (int e = 0; e < 4; ++e)
-          if (!((mw >> e) & 1u)) v[e] = 0xFFFFFFFFu;
-      }
-      ((u32x4*)rt_kv)[c] = v;
+    for (int u = 0; u < RT_SB; ++u) {
+      const int j = j0 + 256 * u;
+      if (j < 4 * L4) rt_kv[j] = kv[u];
     }
   }
 }
 
-// Rank the R owner columns g0 .. g0 + R - 1 of this lane group (TPO lanes, `sub` = this
-// lane's index in it) against the K staged keys, then write the table entries of the
-// non-salient ones (see rank_table_kernel).
+// Rank the R owners g0 .. g0 + R - 1 of this lane group (TPO lanes, `sub` = this lane's index
+// in it) against the L staged keys, then write their table entries (see rank_table_kernel).
 template <int TPO, int R>
-__device__ inline void rank_owner_group(const uint32_t* rt_kv, int K, int K4, int g0, int sub,
+__device__ inline void rank_owner_group(const uint32_t* rt_kv, int L, int L4, int g0, int sub,
+                                        const int32_t* __restrict__ nonsal,
                                         const int32_t* __restrict__ posmap,
                                         int32_t* __restrict__ colsorted,
                                         uint32_t* __restrict__ lctab, const SibTables& sib) {
@@ -596,31 +569,31 @@ __device__ inline void rank_owner_group(const uint32_t* rt_kv, int K, int K4, in
   int ochunk[R];
 #pragma unroll
   for (int o = 0; o < R; ++o) {
-    const int oi = g0 + o < K ? g0 + o : K - 1;
+    const int oi = g0 + o < L ? g0 + o : L - 1;
     mine[o] = rt_kv[oi];
     ochunk[o] = oi >> 2;
     cnt[o] = 0u;
   }
   const u32x4* kv4 = (const u32x4*)rt_kv;
 #pragma unroll 2
-  for (int j4 = sub; j4 < K4; j4 += TPO) {
+  for (int j4 = sub; j4 < L4; j4 += TPO) {
     const u32x4 k = kv4[j4];
 #pragma unroll
     for (int o = 0; o < R; ++o) {
-      const uint32_t thr = j4 < ochunk[o] ? mine[o] + 1u : mine[o];  // keys never reach the sentinel
+      const uint32_t thr = j4 < ochunk[o] ? mine[o] + 1u : mine[o];  // keys never reach 0xFFFFFFFF
       cnt[o] += (k[0] < thr ? 1u : 0u) + (k[1] < thr ? 1u : 0u) + (k[2] < thr ? 1u : 0u) +
                 (k[3] < thr ? 1u : 0u);
     }
   }
 #pragma unroll
   for (int o = 0; o < R; ++o) {
-    const int oi = g0 + o < K ? g0 + o : K - 1;
+    const int oi = g0 + o < L ? g0 + o : L - 1;
     if (sub == (ochunk[o] % TPO))
       for (int e = 0; e < (oi & 3); ++e) cnt[o] += rt_kv[4 * ochunk[o] + e] == mine[o] ? 1u : 0u;
 #pragma unroll
     for (int w = 1; w < TPO; w <<= 1) cnt[o] += (uint32_t)__shfl_xor((int)cnt[o], w, 64);
-    if (sub == 0 && g0 + o < K && mine[o] != 0xFFFFFFFFu) {
-      const int col = g0 + o;
+    if (sub == 0 && g0 + o < L) {
+      const int col = nonsal[g0 + o];
       colsorted[cnt[o]] = col;
       lctab[cnt[o]] = (uint32_t)col | ((uint32_t)(posmap ? posmap[col] : col) << 16);
       for (int t = 0; t < sib.n; ++t)
@@ -629,16 +602,15 @@ __device__ inline void rank_owner_group(const uint32_t* rt_kv, int K, int K4, in
   }
 }
 
-template <int TPO, int R>
+template <int TPO, int R, int SB>
 __global__ __launch_bounds__(256) void rank_table_kernel(
-    const uint32_t* __restrict__ key, int K, const int32_t* __restrict__ list, int L,
+    const uint32_t* __restrict__ key, const int32_t* __restrict__ nonsal, int L,
     const int32_t* __restrict__ posmap, int32_t* __restrict__ colsorted,
     uint32_t* __restrict__ lctab, int lc_len, uint32_t lc_none, SibTables sib) {
-  // roundup(K, 4 TPO) keys, then the K-bit list mask
-  extern __shared__ __attribute__((aligned(16))) uint32_t rt_kv[];
+  extern __shared__ __attribute__((aligned(16))) uint32_t rt_kv[];  // roundup(L, 4 TPO)
   const int tid = threadIdx.x;
-  const int K4 = (int)round_up_dev(K, 4 * TPO) >> 2;
-  rank_stage_keys(key, K, list, L, K4, rt_kv, rt_kv + 4 * K4);
+  const int L4 = (int)round_up_dev(L, 4 * TPO) >> 2;
+  rank_stage_keys<SB>(key, nonsal, L, L4, rt_kv);
   const int nt = gridDim.x * 256;
   for (int r = L + blockIdx.x * 256 + tid; r < lc_len; r += nt) {
     lctab[r] = lc_none;
@@ -646,41 +618,29 @@ __global__ __launch_bounds__(256) void rank_table_kernel(
   }
   __syncthreads();
   const int g0 = (blockIdx.x * (256 / TPO) + tid / TPO) * R;  // this lane group's first owner
-  rank_owner_group<TPO, R>(rt_kv, K, K4, g0, tid % TPO, posmap, colsorted, lctab, sib);
+  rank_owner_group<TPO, R>(rt_kv, L, L4, g0, tid % TPO, nonsal, posmap, colsorted, lctab, sib);
 }
 
 // SQMP_RANK_TABLE_OFF=1 keeps rank_count + lc_table (A/B diagnostics).
-static bool rank_table_fits(int K) {
+static bool rank_table_fits(int L) {
   static const bool off = getenv("SQMP_RANK_TABLE_OFF") != nullptr;
-  return !off && K > 0 && K <= RT_MAX;
+  return !off && L > 0 && L <= RT_MAX;
 }
 
-// key [K] column keys, list [L] the ranked columns (ascending; the others are salient)
-static int launch_rank_table(const uint32_t* key, int K, const int32_t* list, int L,
-                             const int32_t* posmap, int32_t* colsorted, uint32_t* lctab,
-                             int lc_len, uint32_t lc_none, hipStream_t s,
-                             const SibTables& sib = SibTables{}) {
-  // TPO lanes per group of R owners (SQMP_RT_TPO = 8 / 16 / 32 and SQMP_RT_R = 1 / 2 / 4
-  // override, tuning only, read per launch)
-  const char* te = getenv("SQMP_RT_TPO");
-  const char* re = getenv("SQMP_RT_R");
-  // two owners per lane group above 8192 columns (half the workgroups staging the whole key
-  // list: Llama down_proj's 10458-column prepass 61 -> 55.6 us; profiles/r03_prepass_sweep.txt)
-  int tpo = K <= 2048 ? 16 : 32, r = K > 8192 ? 2 : 1;
-  if (te && (atoi(te) == 8 || atoi(te) == 16 || atoi(te) == 32)) tpo = atoi(te);
-  if (re && (atoi(re) == 1 || atoi(re) == 2 || atoi(re) == 4)) r = atoi(re);
-  const int grid = cdiv((long)K * tpo, 256L * r);
-  const size_t lds = sizeof(uint32_t) * ((size_t)round_up(K, 4 * tpo) + (size_t)((K + 31) >> 5));
+template <int SBV>
+static void rank_table_go(int tpo, int r, int grid, size_t lds, hipStream_t s,
+                          const uint32_t* key, const int32_t* nonsal, int L,
+                          const int32_t* posmap, int32_t* colsorted, uint32_t* lctab,
+                          int lc_len, uint32_t lc_none, const SibTables& sib) {
 #define SQMP_RT(T, RR)                                                                       \
   do {                                                                                      \
     static bool attr = false; /* up to 64 KiB of keys: raise the dynamic-LDS limit once */ \
     if (!attr) {                                                                            \
-      SQMP_HIP_CHECK(hipFuncSetAttribute((const void*)rank_table_kernel<T, RR>,             \
-                                         hipFuncAttributeMaxDynamicSharedMemorySize,        \
-                                         4 * RT_MAX + 4 * (RT_MAX / 32)));                  \
+      (void)hipFuncSetAttribute((const void*)rank_table_kernel<T, RR, SBV>,                 \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 4 * RT_MAX);    \
       attr = true;                                                                          \
     }                                                                                       \
-    rank_table_kernel<T, RR><<<dim3(grid), dim3(256), lds, s>>>(key, K, list, L, posmap,     \
+    rank_table_kernel<T, RR, SBV><<<dim3(grid), dim3(256), lds, s>>>(key, nonsal, L, posmap, \
                                                                colsorted, lctab, lc_len,    \
                                                                lc_none, sib);               \
   } while (0)
@@ -697,6 +657,31 @@ static int launch_rank_table(const uint32_t* key, int K, const int32_t* list, in
   }
 #undef SQMP_RT_T
 #undef SQMP_RT
+}
+
+static int launch_rank_table(const uint32_t* key, const int32_t* nonsal, int L,
+                             const int32_t* posmap, int32_t* colsorted, uint32_t* lctab,
+                             int lc_len, uint32_t lc_none, hipStream_t s,
+                             const SibTables& sib = SibTables{}) {
+  // TPO lanes per group of R owners (SQMP_RT_TPO = 8 / 16 / 32 and SQMP_RT_R = 1 / 2 / 4
+  // override, tuning only, read per launch)
+  const char* te = getenv("SQMP_RT_TPO");
+  const char* re = getenv("SQMP_RT_R");
+  const char* be = getenv("SQMP_RT_SB");
+  // two owners per lane group above 8192 entries (half the workgroups staging the whole key
+  // list: Llama down_proj's 10458-column prepass 61 -> 55.6 us; profiles/r03_prepass_sweep.txt)
+  int tpo = L <= 2048 ? 16 : 32, r = L > 8192 ? 2 : 1, sb = L <= 256 * 24 ? 24 : 64;
+  if (te && (atoi(te) == 8 || atoi(te) == 16 || atoi(te) == 32)) tpo = atoi(te);
+  if (re && (atoi(re) == 1 || atoi(re) == 2 || atoi(re) == 4)) r = atoi(re);
+  if (be && (atoi(be) == 24 || atoi(be) == 64)) sb = atoi(be);
+  const int grid = cdiv((long)L * tpo, 256L * r);
+  const size_t lds = sizeof(uint32_t) * (size_t)round_up(L, 4 * tpo);
+  if (sb == 64)
+    rank_table_go<64>(tpo, r, grid, lds, s, key, nonsal, L, posmap, colsorted, lctab, lc_len,
+                      lc_none, sib);
+  else
+    rank_table_go<24>(tpo, r, grid, lds, s, key, nonsal, L, posmap, colsorted, lctab, lc_len,
+                      lc_none, sib);
   SQMP_LAUNCH_CHECK();
   return SQMP_OK;
 }
@@ -1308,9 +1293,9 @@ static int quant_act_impl(void* x, int dtype, int M, int K, int amode, int n_bit
           st2 = launch_colkey_mean3std(x, dtype, M, K, sums, cmax, s, clean);
         }
         if (st2) return st2;
-        if (rank_table_fits(K)) {
+        if (rank_table_fits(Kn)) {
           key_clear = cmax;  // cleared by the quantizer, after every rank_table read
-          return launch_rank_table(cmax, K, nonsal, Kn, pm, colsorted, lctab, lc_len, none, s);
+          return launch_rank_table(cmax, nonsal, Kn, pm, colsorted, lctab, lc_len, none, s);
         }
         if (!clean) SQMP_HIP_CHECK(hipMemsetAsync(counts, 0, sizeof(int32_t) * k64, s));
         st2 = launch_rank_count(cmax, nonsal, Kn, counts, s);
@@ -1549,7 +1534,7 @@ extern "C" int sqmp_quant_act_group(void* x, int dtype, int M, int K, int amode,
   if (n_bits < 2 || n_bits > 8) return SQMP_EUNSUPPORTED;
   if (Kp < K || Kp % 128 != 0 || S_pad < S || S_pad % 64 != 0) return SQMP_EINVAL;
   const int Kn = K - S;
-  if (!rank_table_fits(K)) return SQMP_EUNSUPPORTED;
+  if (!rank_table_fits(Kn)) return SQMP_EUNSUPPORTED;
   for (int o = 0; o < nout; ++o)
     if (!quant_lc_supported(dtype, M, K, true, group_size, Kn, Kp, S_pad, x, outs[o]))
       return SQMP_EUNSUPPORTED;
@@ -1585,7 +1570,7 @@ extern "C" int sqmp_quant_act_group(void* x, int dtype, int M, int K, int amode,
   int r = amode == SQMP_ACT_PER_GROUP ? launch_colmax(x, dtype, M, K, cmax, s, false)
                                       : launch_colkey_mean3std(x, dtype, M, K, sums, cmax, s, true);
   if (r) return r;
-  r = launch_rank_table(cmax, K, nonsal, Kn, posmaps[0], colsorted, lctab, lc_len, lc_none, s, st);
+  r = launch_rank_table(cmax, nonsal, Kn, posmaps[0], colsorted, lctab, lc_len, lc_none, s, st);
   if (r) return r;
   return launch_quant_lc_group(dtype, x, M, K, (1 << (n_bits - 1)) - 1, group_size, lctab, Kn,
                                amaps[0], Kp, salient, S, S_pad, cmax, nonsal, outs[0], cmax,
