@@ -532,7 +532,8 @@ __global__ __launch_bounds__(256) void lc_table_kernel(
 // workgroups may still read them): the quantizer launched next clears them.
 // The staging gathers up to SB entries per thread in one batch (all index loads, then
 // all key loads: two dependent round trips for the whole list up to 256 * SB entries):
-// SB = 24 up to 6144 entries, 64 above (one batch up to RT_MAX; SQMP_RT_SB=24 / 64 overrides).
+// SB = 24 (SQMP_RT_SB = 8 / 16 / 24 A/B; 64 -- one batch up to RT_MAX -- measured 2.4-3.2x
+// slower at 4096 / 11008 columns: the registers cost occupancy, profiles/r04_rank_sb.txt).
 constexpr int RT_MAX = 16384;  // 64 KiB of keys in LDS
 
 // stage the L keys key[nonsal[j]] (padded with 0xFFFFFFFF to 4 L4 entries) into LDS
@@ -670,14 +671,17 @@ static int launch_rank_table(const uint32_t* key, const int32_t* nonsal, int L,
   const char* be = getenv("SQMP_RT_SB");
   // two owners per lane group above 8192 entries (half the workgroups staging the whole key
   // list: Llama down_proj's 10458-column prepass 61 -> 55.6 us; profiles/r03_prepass_sweep.txt)
-  int tpo = L <= 2048 ? 16 : 32, r = L > 8192 ? 2 : 1, sb = L <= 256 * 24 ? 24 : 64;
+  int tpo = L <= 2048 ? 16 : 32, r = L > 8192 ? 2 : 1, sb = 24;
   if (te && (atoi(te) == 8 || atoi(te) == 16 || atoi(te) == 32)) tpo = atoi(te);
   if (re && (atoi(re) == 1 || atoi(re) == 2 || atoi(re) == 4)) r = atoi(re);
-  if (be && (atoi(be) == 24 || atoi(be) == 64)) sb = atoi(be);
+  if (be && (atoi(be) == 8 || atoi(be) == 16 || atoi(be) == 24)) sb = atoi(be);
   const int grid = cdiv((long)L * tpo, 256L * r);
   const size_t lds = sizeof(uint32_t) * (size_t)round_up(L, 4 * tpo);
-  if (sb == 64)
-    rank_table_go<64>(tpo, r, grid, lds, s, key, nonsal, L, posmap, colsorted, lctab, lc_len,
+  if (sb == 8)
+    rank_table_go<8>(tpo, r, grid, lds, s, key, nonsal, L, posmap, colsorted, lctab, lc_len,
+                     lc_none, sib);
+  else if (sb == 16)
+    rank_table_go<16>(tpo, r, grid, lds, s, key, nonsal, L, posmap, colsorted, lctab, lc_len,
                       lc_none, sib);
   else
     rank_table_go<24>(tpo, r, grid, lds, s, key, nonsal, L, posmap, colsorted, lctab, lc_len,
