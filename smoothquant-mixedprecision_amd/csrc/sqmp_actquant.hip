@@ -560,10 +560,40 @@ __device__ inline void rank_stage_keys(const uint32_t* key, const int32_t* __res
 
 // Rank the R owners g0 .. g0 + R - 1 of this lane group (TPO lanes, `sub` = this lane's index
 // in it) against the L staged keys, then write their table entries (see rank_table_kernel).
+// An owner's table entries: its column and packed positions (this layer's and the
+// siblings'), loaded at kernel start so that their round trips overlap the key staging.
+template <int R>
+struct RankOwnerEnt {
+  uint32_t ent[R][3];  // col | pos << 16 for the table and up to two sibling tables
+  int col[R];
+};
+
+template <int R>
+__device__ inline RankOwnerEnt<R> rank_owner_ents(int g0, int sub, int L,
+                                                  const int32_t* __restrict__ nonsal,
+                                                  const int32_t* __restrict__ posmap,
+                                                  const SibTables& sib) {
+  RankOwnerEnt<R> e;
+  int pm[R][3];
+#pragma unroll
+  for (int o = 0; o < R; ++o) e.col[o] = sub == 0 && g0 + o < L ? nonsal[g0 + o] : -1;
+#pragma unroll
+  for (int o = 0; o < R; ++o) {
+    const int c = e.col[o] < 0 ? 0 : e.col[o];
+    pm[o][0] = e.col[o] >= 0 && posmap ? posmap[c] : c;
+    pm[o][1] = e.col[o] >= 0 && sib.n > 0 ? sib.posmap[0][c] : 0;
+    pm[o][2] = e.col[o] >= 0 && sib.n > 1 ? sib.posmap[1][c] : 0;
+  }
+#pragma unroll
+  for (int o = 0; o < R; ++o)
+#pragma unroll
+    for (int t = 0; t < 3; ++t) e.ent[o][t] = (uint32_t)e.col[o] | ((uint32_t)pm[o][t] << 16);
+  return e;
+}
+
 template <int TPO, int R>
 __device__ inline void rank_owner_group(const uint32_t* rt_kv, int L, int L4, int g0, int sub,
-                                        const int32_t* __restrict__ nonsal,
-                                        const int32_t* __restrict__ posmap,
+                                        const RankOwnerEnt<R>& oe,
                                         int32_t* __restrict__ colsorted,
                                         uint32_t* __restrict__ lctab, const SibTables& sib) {
   uint32_t mine[R], cnt[R];
@@ -594,11 +624,10 @@ __device__ inline void rank_owner_group(const uint32_t* rt_kv, int L, int L4, in
 #pragma unroll
     for (int w = 1; w < TPO; w <<= 1) cnt[o] += (uint32_t)__shfl_xor((int)cnt[o], w, 64);
     if (sub == 0 && g0 + o < L) {
-      const int col = nonsal[g0 + o];
-      colsorted[cnt[o]] = col;
-      lctab[cnt[o]] = (uint32_t)col | ((uint32_t)(posmap ? posmap[col] : col) << 16);
-      for (int t = 0; t < sib.n; ++t)
-        sib.lctab[t][cnt[o]] = (uint32_t)col | ((uint32_t)sib.posmap[t][col] << 16);
+      colsorted[cnt[o]] = oe.col[o];
+      lctab[cnt[o]] = oe.ent[o][0];
+      if (sib.n > 0) sib.lctab[0][cnt[o]] = oe.ent[o][1];
+      if (sib.n > 1) sib.lctab[1][cnt[o]] = oe.ent[o][2];
     }
   }
 }
@@ -611,6 +640,8 @@ __global__ __launch_bounds__(256) void rank_table_kernel(
   extern __shared__ __attribute__((aligned(16))) uint32_t rt_kv[];  // roundup(L, 4 TPO)
   const int tid = threadIdx.x;
   const int L4 = (int)round_up_dev(L, 4 * TPO) >> 2;
+  const int g0 = (blockIdx.x * (256 / TPO) + tid / TPO) * R;  // this lane group's first owner
+  const RankOwnerEnt<R> oe = rank_owner_ents<R>(g0, tid % TPO, L, nonsal, posmap, sib);
   rank_stage_keys<SB>(key, nonsal, L, L4, rt_kv);
   const int nt = gridDim.x * 256;
   for (int r = L + blockIdx.x * 256 + tid; r < lc_len; r += nt) {
@@ -618,8 +649,7 @@ __global__ __launch_bounds__(256) void rank_table_kernel(
     for (int o = 0; o < sib.n; ++o) sib.lctab[o][r] = lc_none;
   }
   __syncthreads();
-  const int g0 = (blockIdx.x * (256 / TPO) + tid / TPO) * R;  // this lane group's first owner
-  rank_owner_group<TPO, R>(rt_kv, L, L4, g0, tid % TPO, nonsal, posmap, colsorted, lctab, sib);
+  rank_owner_group<TPO, R>(rt_kv, L, L4, g0, tid % TPO, oe, colsorted, lctab, sib);
 }
 
 // SQMP_RANK_TABLE_OFF=1 keeps rank_count + lc_table (A/B diagnostics).
