@@ -652,6 +652,132 @@ __global__ __launch_bounds__(256) void rank_table_kernel(
   rank_owner_group<TPO, R>(rt_kv, L, L4, g0, tid % TPO, oe, colsorted, lctab, sib);
 }
 
+// ---------------------------------------------------------------- bucketed rank + table
+// The same stable ranks and table as rank_table_kernel with O(L * bucket) compares instead of
+// O(L^2): every workgroup stages the L keys (as above), counts them into 4096 buckets by the
+// key's position in the list's [min, max] key range (a monotone map, so every key of a lower
+// bucket is smaller), scans the counts and scatters the list
+// indices bucket by bucket (any order inside a bucket); an owner's rank is then the count of
+// the lower buckets plus, inside its own bucket,
+//   #{j : key_j < key_i} + #{j < i : key_j == key_i}
+// (the reference's stable argsort, fake_quant.py:113), split over TPO lanes.  A skewed key
+// distribution costs compares (a bucket holding every key degenerates to rank_table_kernel's
+// work per owner over TPO lanes), never correctness.
+constexpr int RB_BUCKETS = 4096;
+
+template <int TPO, int SB>
+__global__ __launch_bounds__(256) void rank_bucket_kernel(
+    const uint32_t* __restrict__ key, const int32_t* __restrict__ nonsal, int L,
+    const int32_t* __restrict__ posmap, int32_t* __restrict__ colsorted,
+    uint32_t* __restrict__ lctab, int lc_len, uint32_t lc_none, SibTables sib) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t rb_lds[];
+  const int tid = threadIdx.x;
+  const int L4 = (int)round_up_dev(L, 4) >> 2;
+  uint32_t* keys = rb_lds;                        // [4 L4]
+  uint32_t* start = keys + 4 * L4;                // [RB_BUCKETS + 1] bucket starts
+  uint32_t* fill = start + RB_BUCKETS + 4;        // [RB_BUCKETS] scatter cursors
+  uint16_t* bj = (uint16_t*)(fill + RB_BUCKETS);  // [L] list indices in bucket order
+  const int g0 = blockIdx.x * (256 / TPO) + tid / TPO;  // this lane group's owner
+  const RankOwnerEnt<1> oe = rank_owner_ents<1>(g0, tid % TPO, L, nonsal, posmap, sib);
+  for (int b = tid; b < RB_BUCKETS; b += 256) fill[b] = 0u;
+  rank_stage_keys<SB>(key, nonsal, L, L4, keys);
+  const int nt = gridDim.x * 256;
+  for (int r = L + blockIdx.x * 256 + tid; r < lc_len; r += nt) {
+    lctab[r] = lc_none;
+    for (int o = 0; o < sib.n; ++o) sib.lctab[o][r] = lc_none;
+  }
+  __syncthreads();
+  // ---- the key range (bucket = its position in [kmin, kmax], monotone in the key: column
+  // maxima cluster, so fixed exponent buckets would hold most keys in a few)
+  __shared__ uint32_t kmm[2][4];
+  uint32_t kmn = 0xFFFFFFFFu, kmx = 0u;
+  for (int j = tid; j < L; j += 256) {
+    const uint32_t k = keys[j];
+    kmn = k < kmn ? k : kmn;
+    kmx = k > kmx ? k : kmx;
+  }
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t a = (uint32_t)__shfl_xor((int)kmn, o, 64);
+    const uint32_t b = (uint32_t)__shfl_xor((int)kmx, o, 64);
+    kmn = a < kmn ? a : kmn;
+    kmx = b > kmx ? b : kmx;
+  }
+  if ((tid & 63) == 0) {
+    kmm[0][tid >> 6] = kmn;
+    kmm[1][tid >> 6] = kmx;
+  }
+  __syncthreads();
+  kmn = kmm[0][0];
+  kmx = kmm[1][0];
+#pragma unroll
+  for (int w = 1; w < 4; ++w) {
+    kmn = kmm[0][w] < kmn ? kmm[0][w] : kmn;
+    kmx = kmm[1][w] > kmx ? kmm[1][w] : kmx;
+  }
+  const float bscale = (float)RB_BUCKETS / ((float)(kmx - kmn) + 1.0f);
+  auto bucket = [&](uint32_t k) {
+    const int b = (int)((float)(k - kmn) * bscale);
+    return b < RB_BUCKETS - 1 ? b : RB_BUCKETS - 1;
+  };
+  // ---- bucket counts
+  for (int j = tid; j < L; j += 256) atomicAdd(&fill[bucket(keys[j])], 1u);
+  __syncthreads();
+  // ---- exclusive scan of the counts: 16 buckets per thread, then across the 256 threads
+  constexpr int PER = RB_BUCKETS / 256;
+  uint32_t c[PER], run = 0u;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    c[i] = fill[PER * tid + i];
+    run += c[i];
+  }
+  const int lane = tid & 63, wave = tid >> 6;
+  uint32_t inc = run;  // inclusive scan of the per-thread totals over the wave
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t v = (uint32_t)__shfl_up((int)inc, o, 64);
+    if (lane >= o) inc += v;
+  }
+  __shared__ uint32_t wtot[4];
+  if (lane == 63) wtot[wave] = inc;
+  __syncthreads();
+  uint32_t base = inc - run;
+  for (int w = 0; w < wave; ++w) base += wtot[w];
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    start[PER * tid + i] = base;
+    fill[PER * tid + i] = base;
+    base += c[i];
+  }
+  if (tid == 0) start[RB_BUCKETS] = (uint32_t)L;
+  __syncthreads();
+  // ---- list indices in bucket order
+  for (int j = tid; j < L; j += 256) bj[atomicAdd(&fill[bucket(keys[j])], 1u)] = (uint16_t)j;
+  __syncthreads();
+  // ---- ranks: the lower buckets, then the owner's own bucket over TPO lanes
+  {
+    const int oi = g0 < L ? g0 : L - 1;  // whole lane groups past the list compute and discard
+    const uint32_t mine = keys[oi];
+    const int b = bucket(mine);
+    const int lo = (int)start[b], hi = (int)start[b + 1];
+    uint32_t cnt = 0u;
+    for (int e = lo + tid % TPO; e < hi; e += TPO) {
+      const int jj = bj[e];
+      const uint32_t k = keys[jj];
+      cnt += (k < mine || (k == mine && jj < oi)) ? 1u : 0u;
+    }
+#pragma unroll
+    for (int w = 1; w < TPO; w <<= 1) cnt += (uint32_t)__shfl_xor((int)cnt, w, 64);
+    cnt += (uint32_t)lo;
+    if (tid % TPO == 0 && g0 < L) {
+      colsorted[cnt] = oe.col[0];
+      lctab[cnt] = oe.ent[0][0];
+      if (sib.n > 0) sib.lctab[0][cnt] = oe.ent[0][1];
+      if (sib.n > 1) sib.lctab[1][cnt] = oe.ent[0][2];
+    }
+  }
+}
+
 // SQMP_RANK_TABLE_OFF=1 keeps rank_count + lc_table (A/B diagnostics).
 static bool rank_table_fits(int L) {
   static const bool off = getenv("SQMP_RANK_TABLE_OFF") != nullptr;
@@ -705,6 +831,38 @@ static int launch_rank_table(const uint32_t* key, const int32_t* nonsal, int L,
   if (te && (atoi(te) == 8 || atoi(te) == 16 || atoi(te) == 32)) tpo = atoi(te);
   if (re && (atoi(re) == 1 || atoi(re) == 2 || atoi(re) == 4)) r = atoi(re);
   if (be && (atoi(be) == 8 || atoi(be) == 16 || atoi(be) == 24)) sb = atoi(be);
+  // SQMP_RT_BUCKET=1: the bucketed kernel (A/B), TPO lanes per owner (SQMP_RT_BTPO, 4)
+  const char* bk = getenv("SQMP_RT_BUCKET");
+  if (bk && atoi(bk) == 1 && L <= 65535) {
+    const char* bt = getenv("SQMP_RT_BTPO");
+    int btpo = bt ? atoi(bt) : 4;
+    if (btpo != 1 && btpo != 2 && btpo != 4 && btpo != 8 && btpo != 16) btpo = 4;
+    const int bgrid = cdiv((long)L * btpo, 256L);
+    const size_t blds = sizeof(uint32_t) * ((size_t)round_up(L, 4) + 2 * RB_BUCKETS + 4) +
+                        sizeof(uint16_t) * (size_t)round_up(L, 2);
+#define SQMP_RB(T)                                                                            \
+  do {                                                                                       \
+    static bool battr = false;                                                               \
+    if (!battr) {                                                                            \
+      (void)hipFuncSetAttribute((const void*)rank_bucket_kernel<T, 24>,                      \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);     \
+      battr = true;                                                                          \
+    }                                                                                        \
+    rank_bucket_kernel<T, 24><<<dim3(bgrid), dim3(256), blds, s>>>(key, nonsal, L, posmap,   \
+                                                                  colsorted, lctab, lc_len,  \
+                                                                  lc_none, sib);             \
+  } while (0)
+    switch (btpo) {
+      case 1: SQMP_RB(1); break;
+      case 2: SQMP_RB(2); break;
+      case 8: SQMP_RB(8); break;
+      case 16: SQMP_RB(16); break;
+      default: SQMP_RB(4); break;
+    }
+#undef SQMP_RB
+    SQMP_LAUNCH_CHECK();
+    return SQMP_OK;
+  }
   const int grid = cdiv((long)L * tpo, 256L * r);
   const size_t lds = sizeof(uint32_t) * (size_t)round_up(L, 4 * tpo);
   if (sb == 8)

@@ -1,0 +1,53 @@
+"""The bucketed rank kernel (rank_bucket_kernel, SQMP_RT_BUCKET=1) against the all-pairs rank
+table kernel: the sorted per_group quantizer's operand must be bit-identical whichever builds
+the rank table (the stable argsort of fake_quant.py:113, ties to the lower list index) --
+random keys, heavy ties (quantized inputs: few distinct column maxima), all columns equal,
+zero columns, and the Llama shapes, through the single-layer and the sibling-group
+quantizers, every owner lane count."""
+import os
+
+import pytest
+import torch
+
+from test_gpu_sibling import _dev, _siblings
+
+pytestmark = pytest.mark.gpu
+
+
+def _inputs(kind, x):
+    if kind == "ties":      # column maxima from a handful of values
+        return (x * 4).round() / 4
+    if kind == "equal":     # every column the same maximum
+        return torch.ones_like(x) * torch.where(torch.rand_like(x.float()) > 0.5, 1.0, -1.0).to(x.dtype)
+    if kind == "zeros":     # a third of the columns zero
+        y = x.clone()
+        y[:, ::3] = 0
+        return y
+    return x
+
+
+@pytest.mark.parametrize("btpo", ["1", "4", "16"])
+@pytest.mark.parametrize("kind", ["random", "ties", "equal", "zeros"])
+@pytest.mark.parametrize("M,K,Ns,G,p,dt", [
+    (256, 1024, (512,), 64, 0.05, torch.float16),
+    (2048, 4096, (4096, 4096, 4096), 64, 0.05, torch.float16),
+    (300, 11008, (4096,), 64, 0.05, torch.float16),
+    (129, 768, (768, 768), 128, 0.10, torch.bfloat16),
+])
+def test_bucketed_rank_bit_identical(M, K, Ns, G, p, dt, kind, btpo, monkeypatch):
+    dev = _dev()
+    from smoothquant import ops
+    layers, x = _siblings(dev, M, K, Ns, G, p, dt, seed=5)
+    x = _inputs(kind, x).contiguous()
+    pws = [q.packed() for q in layers]
+    monkeypatch.setenv("SQMP_RT_BTPO", btpo)
+    outs = {}
+    for on in ("0", "1"):
+        monkeypatch.setenv("SQMP_RT_BUCKET", on)
+        if len(pws) > 1:
+            outs[on] = [a.clone() for a in ops.quant_act_fp_group(x, pws, "per_group", 4, G)]
+        else:
+            outs[on] = [ops.quant_act_fp(x, pws[0], "per_group", 4, G).clone()]
+        torch.cuda.synchronize()
+    for a, b in zip(outs["0"], outs["1"]):
+        assert torch.equal(a.view(torch.int16), b.view(torch.int16))
