@@ -62,6 +62,12 @@ def _first(t):
     return t[0] if isinstance(t, tuple) else t
 
 
+def _is_linear_like(m: nn.Module) -> bool:
+    """nn.Linear, and the transformers-5 MoE router (MixtralTopKRouter: an [E, H] weight
+    applied by F.linear -- an nn.Linear named `gate` in the reference's transformers 4.x)."""
+    return isinstance(m, nn.Linear) or type(m).__name__ == "MixtralTopKRouter"
+
+
 class LinearInputStats:
     """Forward hooks on every nn.Linear of `model`; `fold(name, old, x, y)` returns the
     module's new statistic (old is None on its first call)."""
@@ -70,7 +76,7 @@ class LinearInputStats:
         self.stats: Dict[str, object] = {}
         self._fold = fold
         self._handles = [m.register_forward_hook(functools.partial(self._on_forward, name))
-                         for name, m in model.named_modules() if isinstance(m, nn.Linear)]
+                         for name, m in model.named_modules() if _is_linear_like(m)]
 
     def _on_forward(self, name, module, inputs, output):
         self.stats[name] = self._fold(name, self.stats.get(name), _first(inputs), _first(output))

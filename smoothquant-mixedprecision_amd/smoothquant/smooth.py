@@ -19,8 +19,20 @@ def _smoothing_scales(fcs, act_scales, alpha):
 
 def _check(ln, fcs, act_scales):
     for fc in fcs:
-        assert isinstance(fc, nn.Linear)
-        assert ln.weight.numel() == fc.in_features == act_scales.numel()
+        # nn.Linear as in the reference; also a transformers-5 MoE router (MixtralTopKRouter:
+        # a [E, H] weight applied by F.linear) and the fused experts' rows (_FusedRows)
+        assert isinstance(fc, nn.Linear) or fc.weight.dim() == 2
+        assert ln.weight.numel() == fc.weight.shape[-1] == act_scales.numel()
+
+
+class _FusedRows:
+    """The w1 / w3 rows of every expert of a transformers-5 fused MixtralExperts
+    (gate_up_proj [E, 2I, H]) as one [E * 2I, H] weight view: their column maxima and the
+    in-place column scaling are exactly those of the reference's per-expert w1 / w3 Linears
+    (smooth.py:142-156)."""
+
+    def __init__(self, gate_up_proj):
+        self.weight = gate_up_proj.data.view(-1, gate_up_proj.shape[-1])
 
 
 @torch.no_grad()
@@ -95,9 +107,17 @@ def smooth_lm(model, scales, alpha=0.5):
             attn = module.self_attn
             smooth_ln_fcs_llama_like(module.input_layernorm, [attn.q_proj, attn.k_proj, attn.v_proj],
                                      scales[name + ".self_attn.q_proj"], alpha)
-            moe = module.block_sparse_moe
+            # transformers 4.x: block_sparse_moe.gate (nn.Linear) + experts with w1 / w3
+            # Linears (the reference's layout); 5.x: mlp.gate (MixtralTopKRouter) + fused experts
+            moe = getattr(module, "block_sparse_moe", None)
+            key = name + ".block_sparse_moe.gate"
+            if moe is None:
+                moe, key = module.mlp, name + ".mlp.gate"
             fcs = [moe.gate]
-            for expert in getattr(moe, "experts", []):
-                fcs += [expert.w1, expert.w3]
-            smooth_ln_fcs_llama_like(module.post_attention_layernorm, fcs,
-                                     scales[name + ".block_sparse_moe.gate"], alpha)
+            experts = getattr(moe, "experts", [])
+            if isinstance(experts, nn.ModuleList):
+                for expert in experts:
+                    fcs += [expert.w1, expert.w3]
+            elif hasattr(experts, "gate_up_proj"):
+                fcs.append(_FusedRows(experts.gate_up_proj))
+            smooth_ln_fcs_llama_like(module.post_attention_layernorm, fcs, scales[key], alpha)
