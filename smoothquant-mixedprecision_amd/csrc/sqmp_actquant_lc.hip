@@ -28,7 +28,6 @@
 #include <stdlib.h>
 
 #include "sqmp_internal.h"
-#include "sqmp_mfma.h"
 
 namespace sqmp {
 
@@ -218,7 +217,7 @@ __device__ __forceinline__ void quant_lc_body(
     const int32_t* __restrict__ sal, int S, int S_pad, const uint32_t* __restrict__ cmax,
     const int32_t* __restrict__ nonsal, typename DT::T* out, uint32_t* __restrict__ key_clear,
     int clear_words, float* __restrict__ out_scale, typename DT::T* __restrict__ out_xs,
-    int Kq, int ldsc, const int bid, const int nblk, const LcSib& sib = LcSib{}, int nt = 0) {
+    int Kq, int ldsc, const int bid, const int nblk, const LcSib& sib = LcSib{}) {
   static_assert(!F8 || F8 == 3 || MODE != LC_MODE_GROUP, "F8 codes need one scale per row");
   static_assert(NOUT == 1 || (F8 == 0 && GS == 0), "sibling outputs: OUT_FP, groups >= RPL");
   static_assert(F8 != 3 || (MODE == LC_MODE_GROUP && GS == 0), "C4: groups of >= RPL ranks");
@@ -445,15 +444,8 @@ __device__ __forceinline__ void quant_lc_body(
             if (!od || has1) {
               const u32x2 va = od ? u32x2{x0, d1[0]} : u32x2{d0[0], x0};
               const u32x2 vb = od ? u32x2{x1, d1[1]} : u32x2{d0[1], x1};
-              u32x2* pa = t + (16 * (u >> 1) + rr) * TJ;
-              u32x2* pb = t + (16 * (2 + (u >> 1)) + rr) * TJ;
-              if (nt) {  // streaming: leave the Infinity Cache to x (read again by this pass)
-                asm volatile("global_store_dwordx2 %0, %1, off nt" ::"v"(pa), "v"(va) : "memory");
-                asm volatile("global_store_dwordx2 %0, %1, off nt" ::"v"(pb), "v"(vb) : "memory");
-              } else {
-                *pa = va;
-                *pb = vb;
-              }
+              t[(16 * (u >> 1) + rr) * TJ] = va;
+              t[(16 * (2 + (u >> 1)) + rr) * TJ] = vb;
             }
             if (rb % G == 0) {
               // St[nb][g][r16][j]
@@ -610,7 +602,6 @@ struct PermArgs {
   const void* wsal;       // D [N][S_pad]
   void* wp;               // D [Np][Kq + S_pad]
   int N, Np, Kp, Gw, ngw, Kn, Kq, S_pad, RB;
-  int nt;                 // streaming (non-temporal) stores of wp
 };
 
 template <class DT>
@@ -657,10 +648,7 @@ __device__ __forceinline__ void perm_weight_body(const PermArgs& a, const uint32
         T v[8];
 #pragma unroll
         for (int e = 0; e < 8; ++e) v[e] = pos[e] >= 0 ? wl[(size_t)r * Kp + pos[e]] : DT::from_f(0.f);
-        if (a.nt)
-          store16_nt(wp + (size_t)(n0 + r) * W + j0, *(const u32x4*)v);
-        else
-          *(u32x4*)(wp + (size_t)(n0 + r) * W + j0) = *(const u32x4*)v;
+        *(u32x4*)(wp + (size_t)(n0 + r) * W + j0) = *(const u32x4*)v;
       }
     } else {
       for (int r = 0; r < RB; ++r) {
@@ -691,7 +679,7 @@ __global__ __launch_bounds__(1024) void quant_c4_fused_kernel(
     quant_lc_body<DT, LC_MODE_GROUP, 16, 0, 3>(x, M, K, q_max, G, lctab, Kn, nullptr, P, sal, S,
                                                S_pad, cmax, nonsal, (typename DT::T*)codes,
                                                key_clear, clear_words, (float*)scales, xs, Kq,
-                                               ldsc, blockIdx.x, nq, LcSib{}, pa.nt);
+                                               ldsc, blockIdx.x, nq);
   else
     perm_weight_body<DT>(pa, lctab, blockIdx.x - nq);
 }
@@ -824,7 +812,7 @@ int launch_perm_weight_c4(int dtype, const uint32_t* lctab, const void* codes,
                           int Kn, int S_pad, void* wp, hipStream_t s) {
   const int Np = pad_n(N), RB = pw_rows(Kp);
   const int Kq = (int)round_up(Kn, 64);
-  PermArgs pa{(const uint32_t*)codes, wscale, wsal, wp, N, Np, Kp, Gw, ngw, Kn, Kq, S_pad, RB, 0};
+  PermArgs pa{(const uint32_t*)codes, wscale, wsal, wp, N, Np, Kp, Gw, ngw, Kn, Kq, S_pad, RB};
   const size_t lds = (size_t)RB * Kp * 2;
   const dim3 grid((unsigned)(Np / RB));
   if (dtype == SQMP_F16) {
@@ -865,11 +853,8 @@ int launch_quant_lc_c4(int dtype, const void* x, int M, int K, int q_max, int G,
   // fused: the quantizer's grid (as quant_lc_launch) + Np / RB permutation workgroups
   const int nw = lc_waves(K, Kn);
   const int Np = pad_n(cw->N), RB = pw_rows(cw->Kp);
-  // SQMP_C4_NT=1 (A/B, read per launch): streaming stores of the act codes and wp, so that
-  // the Infinity Cache keeps x between the column-max pass and this one
-  const char* ne = getenv("SQMP_C4_NT");
   PermArgs pa{(const uint32_t*)cw->codes, cw->wscale, cw->wsal, cw->wp, cw->N, Np, cw->Kp,
-              cw->Gw, cw->ngw, Kn, Kq, S_pad, RB, ne && atoi(ne) == 1 ? 1 : 0};
+              cw->Gw, cw->ngw, Kn, Kq, S_pad, RB};
   const size_t lq = sizeof(uint32_t) * (size_t)(P + S_pad + 8), lp = (size_t)RB * cw->Kp * 2;
   const size_t lds = lq > lp ? lq : lp;
   const void* kf = dtype == SQMP_BF16 ? (const void*)quant_c4_fused_kernel<BF16>
