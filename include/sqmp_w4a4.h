@@ -174,6 +174,12 @@ int sqmp_quant_act(void* x, int dtype, int M, int K, int amode, int n_bits,
                                  J = 2 and N = M gives their sizes) instead of row-major */
 #define SQMP_QA_TILED4 16     /* as SQMP_QA_TILED with 64-row blocks (J = 4), the operands of
                                  sqmp_gemm_fqt7j with J = 4 */
+#define SQMP_QA_TILED32 32    /* SQMP_OUT_C4: the operands of sqmp_gemm_fqt9 -- 64-row blocks of
+                                 two 32-row token tiles, lane 32 h + r of a block holding row
+                                 32 j + r at positions 16 s + 8 h .. + 7 of each 64-position
+                                 stage (codes [R][Kq/2] as [R/64][Kq/64][64][4][2] dwords,
+                                 scales [R/64][ngq][32][2], xs [R][S_pad] as
+                                 [R/64][S_pad/64][64][4][2][8]), R = roundup(M, 256) */
 
 /* sqmp_quant_act with the per-weight map posmap (int32 [K]: packed position of column k,
  * the inverse of perm; NULL = derive it per call) and flags.  With posmap, OUT_FP on
@@ -323,6 +329,15 @@ int sqmp_gemm_fqt7j(const void* codes_t, const void* scale_t, const void* sal_t,
 int sqmp_gemm_fqt8(const void* codes_t, const void* scale_t, const void* sal_t, const void* wp,
                    const void* bias, void* y, int dtype, int M, int N, int Kq, int S_pad, int G,
                    int ngq, uint32_t* colmax, void* stream);
+
+/* The activation-order GEMM on SQMP_QA_TILED32 operands at ONE wave per SIMD on the 32x32x16
+ * MFMA (256 weight rows x 256 tokens per tile, each wave 256 rows x 64 tokens with 256 fp32
+ * accumulators in the accumulator registers): the results of sqmp_gemm_fqt7 up to the
+ * accumulation order.  Kq % 128 == 0, S_pad % 64 == 0, G % 64 == 0, N % 8 == 0, fp16 / bf16;
+ * no fused column statistics. */
+int sqmp_gemm_fqt9(const void* codes_t, const void* scale_t, const void* sal_t, const void* wp,
+                   const void* bias, void* y, int dtype, int M, int N, int Kq, int S_pad, int G,
+                   int ngq, void* stream);
 
 /* Sibling operand reuse: dst = the SQMP_OUT_FP operand of a layer whose weight shares the
  * quantized input, the salient set and the act mode with the layer that produced src (q/k/v,

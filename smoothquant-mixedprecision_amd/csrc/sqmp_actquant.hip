@@ -1399,9 +1399,10 @@ static int quant_act_impl(void* x, int dtype, int M, int K, int amode, int n_bit
   if (n_bits < 2 || n_bits > 8) return SQMP_EUNSUPPORTED;
   if (S < 0 || S > K || !x || !amap || (K - S > 0 && !nonsal)) return SQMP_EINVAL;
   if (flags & ~(SQMP_QA_CLEAN_WS | SQMP_QA_REUSE_STATS | SQMP_QA_STATS_GIVEN | SQMP_QA_TILED |
-                SQMP_QA_TILED4))
+                SQMP_QA_TILED4 | SQMP_QA_TILED32))
     return SQMP_EINVAL;
-  if ((flags & (SQMP_QA_TILED | SQMP_QA_TILED4)) && out_kind != SQMP_OUT_C4) return SQMP_EINVAL;
+  if ((flags & (SQMP_QA_TILED | SQMP_QA_TILED4 | SQMP_QA_TILED32)) && out_kind != SQMP_OUT_C4)
+    return SQMP_EINVAL;
   // column maxima already in the workspace (written by sqmp_gemm_fq_colmax's epilogue)
   const bool stats_given = (flags & SQMP_QA_STATS_GIVEN) != 0;
   if (stats_given && (out_kind != SQMP_OUT_INPLACE ||
@@ -1538,7 +1539,8 @@ static int quant_act_impl(void* x, int dtype, int M, int K, int amode, int n_bit
     if (st) return st;
     return launch_quant_lc_c4(dtype, x, M, K, q_max, group_size, lctab, Kn, Kp, salient, S,
                               S_pad, cmax, nonsal, out, out_scale,
-                              (flags & SQMP_QA_TILED4) ? -(int)(cdiv(Kn, group_size) * 8 + 4)
+                              (flags & SQMP_QA_TILED32) ? -(int)(cdiv(Kn, group_size) * 8 + 1)
+                              : (flags & SQMP_QA_TILED4) ? -(int)(cdiv(Kn, group_size) * 8 + 4)
                               : (flags & SQMP_QA_TILED) ? -(int)(cdiv(Kn, group_size) * 8 + 2)
                                                         : (int)round_up(M, 256),
                               out_xs, kc, (int)k64, s, cw);

@@ -25,7 +25,7 @@ ACT_PER_GROUP_MEAN3STD = 4
 W_PER_CHANNEL, W_PER_TENSOR, W_PER_GROUP, W_PER_GROUP_UNSORTED, W_NONE = 0, 1, 2, 3, 4
 W_PER_GROUP_MEAN3STD = 5
 OUT_FP, OUT_I8, OUT_INPLACE, OUT_F8, OUT_C4 = 0, 1, 2, 3, 5
-QA_CLEAN_WS, QA_REUSE_STATS, QA_STATS_GIVEN, QA_TILED, QA_TILED4 = 1, 2, 4, 8, 16
+QA_CLEAN_WS, QA_REUSE_STATS, QA_STATS_GIVEN, QA_TILED, QA_TILED4, QA_TILED32 = 1, 2, 4, 8, 16, 32
 
 _vp, _i, _sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t
 _ip = ctypes.POINTER(ctypes.c_int)
@@ -76,6 +76,7 @@ SIGNATURES = {
     "sqmp_gemm_fqt7j": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _vp,
                              _vp]),
     "sqmp_gemm_fqt8": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _vp, _vp]),
+    "sqmp_gemm_fqt9": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _vp]),
     "sqmp_gemm_fqt7_colmax": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i,
                                    _vp, _vp]),
     "sqmp_fq7_sizes": (_i, [_i, _i, _i, _i, _i, ctypes.POINTER(_sz), ctypes.POINTER(_sz),

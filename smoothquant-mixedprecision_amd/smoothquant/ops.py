@@ -443,6 +443,9 @@ FQT7 = os.environ.get("SQMP_FQT7", "1") == "1"
 FQT7_J = int(os.environ.get("SQMP_FQT7_J", "2"))
 # the one-wave-per-SIMD activation-order GEMM (sqmp_gemm_fqt8) on the J = 4 operands
 FQT8 = os.environ.get("SQMP_FQT8", "0") == "1"
+# the one-wave-per-SIMD activation-order GEMM on the 32x32x16 MFMA (sqmp_gemm_fqt9) on the
+# SQMP_QA_TILED32 operands
+FQT9 = os.environ.get("SQMP_FQT9", "0") == "1"
 
 
 def _fqt_j() -> int:
@@ -484,7 +487,13 @@ def quant_act_c4(x2: torch.Tensor, pw: PackedWeight, act_quant: str, n_bits: int
     dev = x2.device
     tiled = FQT7 and Kq % 128 == 0
     tj = _fqt_j()
-    if tiled:
+    t32 = tiled and FQT9
+    if t32:
+        R = max(256, (M + 255) // 256 * 256)
+        codes = torch.empty((R, Kq // 2), dtype=torch.uint8, device=dev)
+        scales = torch.empty((R // 64, ngq, 32, 2), dtype=x2.dtype, device=dev)  # 4-d: TILED32
+        xs = torch.empty((R, max(pw.S_pad, 64)), dtype=x2.dtype, device=dev)[:M]
+    elif tiled:
         R = max(128 * tj, (M + 128 * tj - 1) // (128 * tj) * (128 * tj))
         codes = torch.empty((R, Kq // 2), dtype=torch.uint8, device=dev)
         scales = torch.empty((R // (16 * tj), ngq, 16 * tj), dtype=x2.dtype, device=dev)
@@ -497,7 +506,8 @@ def quant_act_c4(x2: torch.Tensor, pw: PackedWeight, act_quant: str, n_bits: int
     nb = _ws_bytes(M, K, pw.Kp)
     stream = torch.cuda.current_stream(dev).cuda_stream
     e = _act_ws(dev, stream, K, pw.Kp, nb)
-    flags = _lib.QA_CLEAN_WS | ((_lib.QA_TILED4 if tj == 4 else _lib.QA_TILED) if tiled else 0)
+    flags = _lib.QA_CLEAN_WS | (_lib.QA_TILED32 if t32 else
+                                ((_lib.QA_TILED4 if tj == 4 else _lib.QA_TILED) if tiled else 0))
     src = x2 if stats_of is None else stats_of
     skey = (src.data_ptr(), tuple(src.shape), src.dtype, src._version, pw.sal_key, act_quant,
             M, K)
@@ -532,6 +542,13 @@ def gemm_fqt(codes: torch.Tensor, scales: torch.Tensor, xs: torch.Tensor, wp: to
     M = xs.shape[0]
     y = torch.empty((M, pw.N), dtype=pw.dtype, device=codes.device)
     Kq = codes.shape[1] * 2
+    if scales.dim() == 4:   # SQMP_QA_TILED32
+        if colmax is not None:
+            raise ValueError("gemm_fqt: the TILED32 GEMM has no fused column statistics")
+        check(load().sqmp_gemm_fqt9(_p(codes), _p(scales), _p(xs), _p(wp), _p(bias), _p(y),
+                                    _dtype_code(pw.dtype), M, pw.N, Kq, pw.S_pad, group_size,
+                                    scales.shape[1], _stream(codes)), "gemm_fqt9")
+        return y
     if scales.dim() == 3 and scales.shape[2] == 64 and FQT8:
         check(load().sqmp_gemm_fqt8(_p(codes), _p(scales), _p(xs), _p(wp), _p(bias), _p(y),
                                     _dtype_code(pw.dtype), M, pw.N, Kq, pw.S_pad, group_size,

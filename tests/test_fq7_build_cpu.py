@@ -43,12 +43,14 @@ def test_fq7_kernels_do_not_spill(tmp_path):
 
 @pytest.mark.skipif(not os.path.exists(HIPCC) and shutil.which("hipcc") is None,
                     reason="hipcc not available")
-def test_fqt8_accumulators_stay_in_agprs(tmp_path):
-    """sqmp_gemm_fqt8 names its 256 accumulators as literal a[0:255] in asm statements that
-    hipcc cannot see into: the compiler must neither spill nor emit a v_accvgpr_* of its own
-    (that would land in an accumulator it does not know is live), and the kernel must issue
-    128 MFMAs per stage: 2 x 2 stages (the steady code-stage loop and the general one)."""
-    src = os.path.join(ROOT, "smoothquant-mixedprecision_amd", "csrc", "sqmp_gemm_fqt8.hip")
+@pytest.mark.parametrize("name,ns,mfma", [("fqt8", "fqt8", 512), ("fqt9", "fqt9", 256)])
+def test_one_wave_gemm_accumulators_stay_in_agprs(tmp_path, name, ns, mfma):
+    """sqmp_gemm_fqt8 / _fqt9 name their 256 accumulators as literal a[0:255] in asm
+    statements that hipcc cannot see into: the compiler must neither spill nor emit a
+    v_accvgpr_* of its own (that would land in an accumulator it does not know is live), and
+    the kernels must issue every MFMA of 2 x 2 stages (the steady code-stage loop and the
+    general one): 128 16x16x32 or 64 32x32x16 per stage."""
+    src = os.path.join(ROOT, "smoothquant-mixedprecision_amd", "csrc", f"sqmp_gemm_{name}.hip")
     r = subprocess.run([HIPCC, "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-I",
                         os.path.join(ROOT, "include"), "-c", src, "-o", str(tmp_path / "f8.o"),
                         "-save-temps=obj", "-Rpass-analysis=kernel-resource-usage"],
@@ -60,10 +62,10 @@ def test_fqt8_accumulators_stay_in_agprs(tmp_path):
     asm = [f for f in os.listdir(tmp_path) if f.endswith(".s") and "gfx950" in f]
     assert asm
     text = open(tmp_path / asm[0]).read()
-    kernels = re.split(r"\n(?=_ZN4sqmp4fqt8\w+:)", text)[1:]
+    kernels = re.split(r"\n(?=_ZN4sqmp4" + ns + r"\w+:)", text)[1:]
     assert len(kernels) == 2
     for k in kernels:
-        inasm, own, mfma = False, 0, 0
+        inasm, own, n_mfma = False, 0, 0
         for line in k.split("\n"):
             if ";;#ASMSTART" in line:
                 inasm = True
@@ -72,6 +74,6 @@ def test_fqt8_accumulators_stay_in_agprs(tmp_path):
             elif "accvgpr" in line and not inasm:
                 own += 1
             elif "v_mfma" in line:
-                mfma += 1
+                n_mfma += 1
         assert own == 0, "compiler-emitted accumulator moves"
-        assert mfma == 512
+        assert n_mfma == mfma
