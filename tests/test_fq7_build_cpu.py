@@ -58,12 +58,12 @@ def test_one_wave_gemm_accumulators_stay_in_agprs(tmp_path, name, ns, mfma):
     assert r.returncode == 0, r.stderr[-2000:]
     spills = [int(v) for v in re.findall(r"VGPRs Spill: (\d+)", r.stderr)]
     scratch = [int(v) for v in re.findall(r"ScratchSize \[bytes/lane\]: (\d+)", r.stderr)]
-    assert len(spills) == 2 and not any(spills) and not any(scratch), r.stderr[-3000:]
+    assert len(spills) >= 2 and not any(spills) and not any(scratch), r.stderr[-3000:]
     asm = [f for f in os.listdir(tmp_path) if f.endswith(".s") and "gfx950" in f]
     assert asm
     text = open(tmp_path / asm[0]).read()
     kernels = re.split(r"\n(?=_ZN4sqmp4" + ns + r"\w+:)", text)[1:]
-    assert len(kernels) == 2
+    assert len(kernels) >= 2
     for k in kernels:
         inasm, own, n_mfma = False, 0, 0
         for line in k.split("\n"):
