@@ -53,8 +53,9 @@ __device__ inline i32x4b rsrc_of(const void* base, uint32_t nrec) {
 // compiler's LDS wait analysis does not see a pending DMA (see sqmp_gemm_fast.hip).
 __device__ inline void dma16(const i32x4b& rsrc, uint32_t voff, uint32_t soff,
                              unsigned char* lds_dst) {
-  const uint32_t m0v = __builtin_amdgcn_readfirstlane(
-      (uint32_t)(size_t)(__attribute__((address_space(3))) unsigned char*)lds_dst);
+  // the low half of an LDS pointer's generic address is its LDS address (the aperture
+  // is the high half): no generic -> local cast, whose null check costs 4 SALU per piece
+  const uint32_t m0v = __builtin_amdgcn_readfirstlane((uint32_t)(size_t)lds_dst);
   // s_nop 0: M0 write -> LDS-DMA (hazard table, MI355X asm guide §4.1); soff is SALU
   // arithmetic ("s" rejects a VGPR value at compile time), the descriptor built long before
   asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
@@ -391,33 +392,38 @@ __global__ __launch_bounds__(512, 1) void gemm_f8v2_kernel(
                   *(const u32x4*)(slot + V2_A + v2_off(r, 2 * q + 1)));
     };
     const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
-    // per activation tile i: 4 MFMAs, the fold of MFMA j - 1 issued behind MFMA j (its
-    // result latency), the next tile's fragment read under them; one sched barrier per
-    // tile keeps the compiler from hoisting every fragment read (register pressure)
-    i32x8b ax = ald(0);
+    // the 32 MFMAs u = 4 i + j (activation tile i, weight tile j) in order, the fold of MFMA
+    // u - 2 issued behind MFMA u: two MFMAs (64 cycles) cover the result latency, so the
+    // folds need no s_nop padding (one MFMA between them did: 14-18 nop cycles per tile);
+    // tile i + 1's fragment read goes out with MFMA 4 i.  One sched barrier per MFMA keeps
+    // that order (and the fragment reads from being hoisted: register pressure).
+    i32x8b ax[2];
+    ax[0] = ald(0);
+    if constexpr (DIAG == 3) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const i32x8b cur = ax;
-      if (i + 1 < 8) ax = ald(i + 1);
-      if constexpr (DIAG == 3) {
+      for (int i = 0; i < 8; ++i) {
+        if (i + 1 < 8) ax[(i + 1) & 1] = ald(i + 1);
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-          tot[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(bw[j], cur, tot[i][j], 0, 0, 0, 127, 0, 127);
+          tot[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(bw[j], ax[i & 1], tot[i][j], 0, 0, 0, 127, 0, 127);
         __builtin_amdgcn_sched_barrier(0);
-        continue;
       }
-      f32x4 t0 = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(bw[0], cur, zero, 0, 0, 0, 127, 0, 127);
-      f32x4 t1 = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(bw[1], cur, zero, 0, 0, 0, 127, 0, 127);
+      return;
+    }
+    f32x4 t[3];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) tot[i][0][r] = __builtin_fmaf(t0[r], sv[0][r], tot[i][0][r]);
-      t0 = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(bw[2], cur, zero, 0, 0, 0, 127, 0, 127);
+    for (int u = 0; u < 34; ++u) {
+      const int i = u >> 2, j = u & 3;
+      if (u < 32) {
+        if (j == 0 && i + 1 < 8) ax[(i + 1) & 1] = ald(i + 1);
+        t[u % 3] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(bw[j], ax[i & 1], zero, 0, 0, 0, 127, 0, 127);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if (u >= 2) {
+        const int v = u - 2, vi = v >> 2, vj = v & 3;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) tot[i][1][r] = __builtin_fmaf(t1[r], sv[1][r], tot[i][1][r]);
-      t1 = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(bw[3], cur, zero, 0, 0, 0, 127, 0, 127);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) tot[i][2][r] = __builtin_fmaf(t0[r], sv[2][r], tot[i][2][r]);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) tot[i][3][r] = __builtin_fmaf(t1[r], sv[3][r], tot[i][3][r]);
+        for (int r = 0; r < 4; ++r) tot[vi][vj][r] = __builtin_fmaf(t[v % 3][r], sv[vj][r], tot[vi][vj][r]);
+      }
       __builtin_amdgcn_sched_barrier(0);
     }
   };

@@ -13,9 +13,10 @@ import threading
 # SQMP_DIAG_LIB=1 loads the timing-diagnostics build (libsqmp_w4a4_diag.so, made by
 # `SQMP_DIAG=1 python build_ext.py`: extra kernel variants selected by SQMP_*_DIAG, wrong
 # results by design) -- tools only, never the product path
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)),
-                        "libsqmp_w4a4_diag.so" if os.environ.get("SQMP_DIAG_LIB") == "1"
-                        else "libsqmp_w4a4.so")
+# SQMP_LIB_PATH: another build of the same C ABI (same-box A/B of two builds, tools only)
+LIB_PATH = os.environ.get("SQMP_LIB_PATH") or os.path.join(
+    os.path.dirname(os.path.abspath(__file__)),
+    "libsqmp_w4a4_diag.so" if os.environ.get("SQMP_DIAG_LIB") == "1" else "libsqmp_w4a4.so")
 
 SQMP_OK, SQMP_EINVAL, SQMP_EUNSUPPORTED, SQMP_EHIP, SQMP_EWORKSPACE = 0, -1, -2, -3, -4
 

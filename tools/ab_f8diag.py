@@ -1,7 +1,9 @@
 """Timing diagnostics of the FP8 per_token GEMM at config 2 (SQMP_F8_DIAG, diagnostics
 library only: SQMP_DIAG_LIB=1 after SQMP_DIAG=1 python smoothquant-mixedprecision_amd/build_ext.py).
 Wrong results by design for every value but 0: no equality check.
-    SQMP_DIAG_LIB=1 python tools/ab_f8diag.py [values, '+'-separated] [rounds] [iters]"""
+    SQMP_DIAG_LIB=1 python tools/ab_f8diag.py [values, '+'-separated] [rounds] [iters] [ENV]
+ENV (default SQMP_F8_DIAG) names the per-launch variable: SQMP_F8_OPT A/Bs the product
+variants on the product library (y checked equal across them)."""
 import os
 import sys
 
@@ -15,15 +17,25 @@ from smoothquant import ops  # noqa: E402
 vals = (sys.argv[1] if len(sys.argv) > 1 else "0+1+2+3").split("+")
 rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 4
 iters = int(sys.argv[3]) if len(sys.argv) > 3 else 100
+ENV = sys.argv[4] if len(sys.argv) > 4 else "SQMP_F8_DIAG"
 dev = torch.device("cuda")
 q, x, lin = bench.make_layer(dev, "per_token", seed=1)
 pw = q.packed()
 a8, sa, xs = ops.quant_act_f8(x, pw, "per_token", 4)
 stream = torch.cuda.current_stream(dev)
 res = {v: [] for v in vals}
+ref = None
+if ENV != "SQMP_F8_DIAG":  # product variants: identical outputs
+    for v in vals:
+        os.environ[ENV] = v
+        y = ops.gemm_f8(a8, sa, xs, pw, lin.bias)
+        torch.cuda.synchronize()
+        if ref is None:
+            ref = y.clone()
+        assert torch.equal(y, ref), f"{ENV}={v}: y differs"
 for _ in range(rounds):
     for v in vals:
-        os.environ["SQMP_F8_DIAG"] = v
+        os.environ[ENV] = v
         for _ in range(10):
             ops.gemm_f8(a8, sa, xs, pw, lin.bias)
         t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -35,4 +47,4 @@ for _ in range(rounds):
         res[v].append(t0.elapsed_time(t1) / iters * 1e3)
 for v in vals:
     r = sorted(res[v])
-    print(f"SQMP_F8_DIAG={v}: median {r[len(r) // 2]:7.1f} us  all {[round(t, 1) for t in res[v]]}", flush=True)
+    print(f"{ENV}={v}: median {r[len(r) // 2]:7.1f} us  all {[round(t, 1) for t in res[v]]}", flush=True)
