@@ -404,6 +404,17 @@ int sqmp_gemm_h2(const float* a, const int* aexp, const void* b2, const int* bex
                  const float* bias, float* y, int M, int N, int L, uint32_t* colmax,
                  void* stream);
 
+/* The same product on the LDS-DMA ring (the default where L % 64 == 0 and N % 4 == 0; bit-
+ * identical to sqmp_gemm_h2): a2 / aexp = sqmp_split2_f16 of the SQMP_OUT_FP operand with ldr
+ * >= roundup(M, 128) rows (the two activation planes [2][ldr][L]), wt = sqmp_pack_h2d of the
+ * sqmp_split2_f16 weight planes [2][Np][L] (once per layer: Wt[p][Np / 32][L / 64][64][2][2][8],
+ * the register fragments of 32-row weight blocks), bexp as for sqmp_gemm_h2.  Replaces the
+ * F.linear of fake_quant.py:306 for fp32 layers (run_experiments.py:146-156). */
+int sqmp_pack_h2d(const void* planes, int Np, int L, void* wt, void* stream);
+int sqmp_gemm_h2d(const void* a2, int ldr, const int* aexp, const void* wt, const int* bexp,
+                  const float* bias, float* y, int M, int N, int L, uint32_t* colmax,
+                  void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -284,25 +284,56 @@ __global__ __launch_bounds__(256) void row_exp_kernel(const float* __restrict__ 
 }
 
 // [R][L] fp32 -> two f16 planes [2][ldr][L] of the row-scaled values + exp[ldr] (rows >= R
-// zero, exponent 0); one block per row
+// zero, exponent 0).  One wave per row: the row maximum from 16-B loads, then a second pass
+// over the (L2-resident) row writing 16 B per plane per 8 values (L % 8 == 0; a scalar tail
+// otherwise)
 __global__ __launch_bounds__(256) void split2h_kernel(const float* __restrict__ src, int R, int L,
                                                       int ldr, uint16_t* __restrict__ dst,
                                                       int* __restrict__ exp_out) {
-  __shared__ float red[16];
-  const int r = blockIdx.x;
+  const int lane = threadIdx.x & 63;
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= ldr) return;
   const float* row = src + (size_t)r * L;
+  const bool vec = (L & 7) == 0;
   float mx = 0.f;
-  if (r < R)
-    for (int c = threadIdx.x; c < L; c += 256) mx = fmaxf(mx, fabsf(row[c]));
-  mx = block_max(mx, red);
+  if (r < R) {
+    if (vec) {
+      for (int c = lane; c < L / 4; c += 64) {
+        const f32x4 v = ((const f32x4*)row)[c];
+        mx = fmaxf(mx, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
+      }
+    } else {
+      for (int c = lane; c < L; c += 64) mx = fmaxf(mx, fabsf(row[c]));
+    }
+  }
+  mx = wave_max(mx);
   const int e = row_exp_of(mx);
-  if (threadIdx.x == 0) exp_out[r] = e;
-  const size_t n = (size_t)ldr * L;
-  for (int c = threadIdx.x; c < L; c += 256) {
-    uint32_t h, l;
-    split2h(r < R ? __builtin_ldexpf(row[c], e) : 0.f, h, l);
-    dst[(size_t)r * L + c] = (uint16_t)h;
-    dst[n + (size_t)r * L + c] = (uint16_t)l;
+  if (lane == 0) exp_out[r] = e;
+  uint16_t* dh = dst + (size_t)r * L;
+  uint16_t* dl = dst + (size_t)ldr * L + (size_t)r * L;
+  if (vec) {
+    for (int c = lane; c < L / 8; c += 64) {
+      f32x4 v0 = {0.f, 0.f, 0.f, 0.f}, v1 = v0;
+      if (r < R) {
+        v0 = ((const f32x4*)row)[2 * c];
+        v1 = ((const f32x4*)row)[2 * c + 1];
+      }
+      uint32_t h[8], l[8];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        split2h(__builtin_ldexpf(v0[k], e), h[k], l[k]);
+        split2h(__builtin_ldexpf(v1[k], e), h[4 + k], l[4 + k]);
+      }
+      ((u32x4*)dh)[c] = u32x4{h[0] | (h[1] << 16), h[2] | (h[3] << 16), h[4] | (h[5] << 16), h[6] | (h[7] << 16)};
+      ((u32x4*)dl)[c] = u32x4{l[0] | (l[1] << 16), l[2] | (l[3] << 16), l[4] | (l[5] << 16), l[6] | (l[7] << 16)};
+    }
+  } else {
+    for (int c = lane; c < L; c += 64) {
+      uint32_t h, l;
+      split2h(r < R ? __builtin_ldexpf(row[c], e) : 0.f, h, l);
+      dh[c] = (uint16_t)h;
+      dl[c] = (uint16_t)l;
+    }
   }
 }
 
@@ -315,7 +346,7 @@ using namespace sqmp;
 extern "C" int sqmp_split2_f16(const float* src, int R, int L, int ldr, void* dst, int* rexp,
                                void* stream) {
   if (!src || !dst || !rexp || R <= 0 || L <= 0 || ldr < R) return SQMP_EINVAL;
-  split2h_kernel<<<ldr, 256, 0, (hipStream_t)stream>>>(src, R, L, ldr, (uint16_t*)dst, rexp);
+  split2h_kernel<<<cdiv(ldr, 4), 256, 0, (hipStream_t)stream>>>(src, R, L, ldr, (uint16_t*)dst, rexp);
   SQMP_LAUNCH_CHECK();
   return SQMP_OK;
 }

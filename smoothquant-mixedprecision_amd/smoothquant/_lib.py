@@ -92,6 +92,8 @@ SIGNATURES = {
     "sqmp_split2_f16": (_i, [_vp, _i, _i, _i, _vp, _vp, _vp]),
     "sqmp_row_exp": (_i, [_vp, _i, _i, _vp, _vp]),
     "sqmp_gemm_h2": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _vp, _vp]),
+    "sqmp_pack_h2d": (_i, [_vp, _i, _i, _vp, _vp]),
+    "sqmp_gemm_h2d": (_i, [_vp, _i, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _vp, _vp]),
 }
 
 _lock = threading.Lock()

@@ -93,6 +93,7 @@ class PackedWeight:
     ws32: Optional[torch.Tensor] = field(default=None)   # fp32 [ngw, Np] scales (f8 GEMM)
     fq7: Optional[tuple] = field(default=None)           # (codes_t, scale_t, sal_t, J) of gemm_fq7
     h2: Optional[tuple] = field(default=None)            # (f16 [2, Np, L], int32 [Np]) (gemm_h2)
+    h2d: Optional[torch.Tensor] = field(default=None)    # f16 tile-major planes (gemm_h2d)
     sib_maps: Optional[tuple] = field(default=None)      # sibling position map (sqmp_permute_act)
 
     @property
@@ -693,16 +694,46 @@ def h2_operand(pw: PackedWeight):
     return pw.h2
 
 
+# the fp32 GEMM on the LDS-DMA ring (sqmp_gemm_h2d: pre-split activation planes, weight planes
+# in registers; bit-identical to sqmp_gemm_h2) wherever L % 64 == 0 and N % 4 == 0;
+# SQMP_H2D=0 keeps sqmp_gemm_h2 (A/B)
+H2D = os.environ.get("SQMP_H2D", "1") != "0"
+
+
+def h2d_operand(pw: PackedWeight) -> torch.Tensor:
+    """The weight planes of h2_operand in sqmp_gemm_h2d's tile-major register layout
+    (sqmp_pack_h2d), built once per packed fp32 weight."""
+    if pw.h2d is None:
+        planes, _ = h2_operand(pw)
+        wt = torch.empty_like(planes)
+        check(load().sqmp_pack_h2d(_p(planes), planes.shape[1], planes.shape[2], _p(wt),
+                                   _stream(planes)), "pack_h2d")
+        pw.h2d = wt
+    return pw.h2d
+
+
 def gemm_h2(a: torch.Tensor, pw: PackedWeight, bias: Optional[torch.Tensor],
             colmax: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """gemm_fq for fp32 layers on the f16 MFMA (include/sqmp_w4a4.h sqmp_gemm_h2)."""
+    """gemm_fq for fp32 layers on the f16 MFMA (include/sqmp_w4a4.h sqmp_gemm_h2d /
+    sqmp_gemm_h2)."""
     M = a.shape[0]
     L = pw.Kp + pw.S_pad
     if a.dtype != torch.float32 or a.shape[1] != L or a.stride(0) != L:
         raise ValueError("gemm_h2: A must be fp32 [M, Kp + S_pad] with row stride Kp + S_pad")
     planes, bexp = h2_operand(pw)
-    aexp = torch.empty(max(M, 1), dtype=torch.int32, device=a.device)
     lib = load()
+    if H2D and L % 64 == 0 and pw.N % 4 == 0 and M > 0:
+        wt = h2d_operand(pw)
+        ldr = (M + 127) // 128 * 128
+        a2 = torch.empty((2, ldr, L), dtype=torch.float16, device=a.device)
+        aexp = torch.empty(ldr, dtype=torch.int32, device=a.device)
+        check(lib.sqmp_split2_f16(_p(a), M, L, ldr, _p(a2), _p(aexp), _stream(a)), "split2_f16")
+        y = torch.empty((M, pw.N), dtype=torch.float32, device=a.device)
+        check(lib.sqmp_gemm_h2d(_p(a2), ldr, _p(aexp), _p(wt), _p(bexp), _p(bias), _p(y), M,
+                                pw.N, L, _p(colmax) if colmax is not None else None,
+                                _stream(a)), "gemm_h2d")
+        return y
+    aexp = torch.empty(max(M, 1), dtype=torch.int32, device=a.device)
     check(lib.sqmp_row_exp(_p(a), M, L, _p(aexp), _stream(a)), "row_exp")
     y = torch.empty((M, pw.N), dtype=torch.float32, device=a.device)
     check(lib.sqmp_gemm_h2(_p(a), _p(aexp), _p(planes), _p(bexp), _p(bias), _p(y), M, pw.N, L,

@@ -182,3 +182,45 @@ def test_h2_raster_groups_bit_identical(M, N):
             os.environ["SQMP_H2_GROUP_M"] = old
     for y in ys[1:]:
         assert torch.equal(y.view(torch.int32), ys[0].view(torch.int32))
+
+
+@pytest.mark.parametrize("M,K,N,p,has_bias", [
+    (512, 1024, 512, 0.10, True),       # whole tiles
+    (300, 2048, 200, 0.05, False),      # ragged M and N (N < one 256-row weight tile)
+    (1, 1024, 260, 0.10, True),         # one row; N % 256 != 0
+    (2048, 2048, 8192, 0.05, True),     # OPT-1.3B fc1
+    (2048, 8192, 2048, 0.05, False),    # OPT-1.3B fc2
+])
+def test_h2d_bit_identical_to_h2(M, K, N, p, has_bias):
+    """sqmp_gemm_h2d (pre-split activation planes by LDS-DMA, weight planes in registers)
+    computes exactly sqmp_gemm_h2's sums in the same order: y and the fused column maxima
+    bit-identical."""
+    from smoothquant import ops
+    dev = _dev()
+    rng = np.random.default_rng(21)
+    W = (rng.standard_normal((N, K)) * 0.02).astype(np.float32)
+    b = (rng.standard_normal(N) * 0.1).astype(np.float32) if has_bias else None
+    x = rng.standard_normal((M, K)).astype(np.float32)
+    x[:, rng.choice(K, max(1, K // 100), replace=False)] *= 30.0
+    q = make_layer(W, b, "fp32", dev, weight_quant="per_group", act_quant="per_group",
+                   importance=torch.from_numpy(np.abs(x).mean(0)), salient_prop=p, group_size=128)
+    pw = q.packed()
+    L = pw.Kp + pw.S_pad
+    assert L % 64 == 0 and N % 4 == 0
+    a = ops.quant_act_fp(torch.from_numpy(x).to(dev), pw, "per_group", 4, 128)
+    bias = None if q.bias is None else q.bias.detach().reshape(-1)
+    old = ops.H2D
+    try:
+        ops.H2D = False
+        c0 = torch.zeros(N, dtype=torch.int32, device=dev)
+        y0 = ops.gemm_h2(a, pw, bias, colmax=c0)
+        ops.H2D = True
+        c1 = torch.zeros(N, dtype=torch.int32, device=dev)
+        y1 = ops.gemm_h2(a, pw, bias, colmax=c1)
+        y2 = ops.gemm_h2(a, pw, bias)
+    finally:
+        ops.H2D = old
+    assert pw.h2d is not None
+    assert torch.equal(y1.view(torch.int32), y0.view(torch.int32))
+    assert torch.equal(y2.view(torch.int32), y0.view(torch.int32))
+    assert torch.equal(c1, c0)
