@@ -80,14 +80,11 @@ __device__ inline void fence(V& v) {
   asm volatile("" : "+v"(v));
 }
 
-constexpr int TM = 128, TN = 256, J = 2, WR = 16 * J, I = TM / 16;
+// TM = 128 token rows per tile, or 64 where 128-row tiles leave CUs idle (OPT-1.3B's N = 2048
+// layers at 2048 tokens: 128 tiles of 128 x 256, 256 of 64 x 256)
+constexpr int TN = 256, J = 2, WR = 16 * J;
 constexpr int PA = 3, NS = PA + 1;     // A stages in flight, ring slots
-constexpr int PLANE = TM * 128;        // one activation plane of a stage: TM rows x 128 B
-constexpr int SLOT = 2 * PLANE;        // 32 KiB
-constexpr int NA = TM / 64;            // DMA pieces per wave per plane and stage
 constexpr int PF = 2;                  // A fragment read-ahead (blocks)
-constexpr int EPI = TM * TN * 4;       // fp32 output tile staged in LDS: 128 KiB
-constexpr int LDS_BYTES = NS * SLOT > EPI ? NS * SLOT : EPI;
 
 // 128-B LDS rows: 16-B chunk c of row r at c ^ (r & 7) (conflict-free for the ds_read_b128
 // lane groups, as gemm_x3's K-64 layout)
@@ -100,12 +97,18 @@ struct Wreg {
   u32x4 w[2][J][2];
 };
 
-template <bool COLMAX>
+template <bool COLMAX, int TM>
 __global__ __launch_bounds__(512, 1) void gemm_h2d_kernel(
     const uint16_t* __restrict__ A2, size_t a_plane, const int* __restrict__ aexp,
     const uint16_t* __restrict__ Wt, const int* __restrict__ bexp, const float* __restrict__ bias,
     float* __restrict__ Y, int M, int N, int L, int tiles_m, int tiles_n, int group_m,
     uint32_t* __restrict__ colmax, int nt) {
+  constexpr int I = TM / 16;
+  constexpr int PLANE = TM * 128;   // one activation plane of a stage: TM rows x 128 B
+  constexpr int SLOT = 2 * PLANE;   // 32 KiB at TM = 128
+  constexpr int NA = TM / 64;       // DMA pieces per wave per plane and stage
+  constexpr int EPI = TM * TN * 4;  // fp32 output tile staged in LDS: 128 KiB at TM = 128
+  constexpr int LDS_BYTES = NS * SLOT > EPI ? NS * SLOT : EPI;
   __shared__ __attribute__((aligned(16))) unsigned char lds[LDS_BYTES];
   const uint32_t lds32 = (uint32_t)(size_t)(__attribute__((address_space(3))) unsigned char*)lds;
 
@@ -337,9 +340,11 @@ extern "C" int sqmp_gemm_h2d(const void* a2, int ldr, const int* aexp, const voi
                              const int* bexp, const float* bias, float* y, int M, int N, int L,
                              uint32_t* colmax, void* stream) {
   if (!a2 || !aexp || !wt || !bexp || !y || M < 0 || N <= 0 || L <= 0) return SQMP_EINVAL;
-  if (L % 64 != 0 || N % 4 != 0 || ldr < h2d::TM * cdiv(M, h2d::TM)) return SQMP_EINVAL;
+  if (L % 64 != 0 || N % 4 != 0 || ldr < 128 * cdiv(M, 128)) return SQMP_EINVAL;
   if (M == 0) return SQMP_OK;
-  const int tiles_m = cdiv(M, h2d::TM), tiles_n = cdiv(N, h2d::TN);
+  const int tiles_n = cdiv(N, h2d::TN);
+  const int tm = (long)cdiv(M, 128) * tiles_n >= 256 ? 128 : 64;
+  const int tiles_m = cdiv(M, tm);
   const int nt = nt_output((size_t)M * N * sizeof(float)) ? 1 : 0;
   const char* ge = getenv("SQMP_H2D_GROUP_M");  // A/B knob, read per launch
   const int gm = ge && atoi(ge) > 0 ? atoi(ge) : 4;
@@ -347,7 +352,9 @@ extern "C" int sqmp_gemm_h2d(const void* a2, int ldr, const int* aexp, const voi
   // (32-bit buffer offsets: both planes of the tile rows within 4 GiB)
   if ((size_t)2 * a_plane * 2 >= (1ull << 32)) return SQMP_EINVAL;
 #define SQMP_H2D(CM)                                                                            \
-  h2d::gemm_h2d_kernel<CM><<<dim3(tiles_m * tiles_n), dim3(512), 0, (hipStream_t)stream>>>(      \
+  if (tm == 128) SQMP_H2D_TM(CM, 128); else SQMP_H2D_TM(CM, 64)
+#define SQMP_H2D_TM(CM, TMV)                                                                    \
+  h2d::gemm_h2d_kernel<CM, TMV><<<dim3(tiles_m * tiles_n), dim3(512), 0, (hipStream_t)stream>>>(      \
       (const uint16_t*)a2, a_plane, aexp, (const uint16_t*)wt, bexp, bias, y, M, N, L, tiles_m, \
       tiles_n, gm, colmax, nt)
   if (colmax) {
@@ -356,6 +363,7 @@ extern "C" int sqmp_gemm_h2d(const void* a2, int ldr, const int* aexp, const voi
     SQMP_H2D(false);
   }
 #undef SQMP_H2D
+#undef SQMP_H2D_TM
   SQMP_LAUNCH_CHECK();
   return SQMP_OK;
 }
