@@ -501,6 +501,14 @@ def main(argv=None):
         kname = ("sqmp::fq7::gemm_fq7_kernel<F16,1,256,2,0,true,3> (activation order, sqmp_gemm_fqt7)"
                  if c4[1].dim() == 3 else
                  "sqmp::gemm_fq6_kernel<F16,1,256,true> (activation order, sqmp_gemm_fqt)")
+    elif fp32 and ops.h2_planes_ok(pw, args.act):
+        # the forward's fp32 path: the quantizer writes the two f16 planes, sqmp_gemm_h2d
+        a2 = ops.quant_act_fp(x, pw, args.act, 4, G, h2=True)
+        gemm = lambda: ops.gemm_h2_planes(a2, pw, lin.bias)  # noqa: E731
+        quant = lambda: ops.quant_act_fp(x, pw, args.act, 4, G, h2=True)  # noqa: E731
+        kdt = "f32"
+        kname = ("sqmp::h2d::gemm_h2d_kernel<false,128> (sqmp_gemm_h2d: row-scaled two-piece "
+                 "fp16 planes by LDS-DMA, 3 f16 MFMAs per product)")
     else:
         a = ops.quant_act_fp(x, pw, args.act, 4, G)
         gemm = lambda: ops.gemm_fq(a, pw, lin.bias)  # noqa: E731
@@ -561,6 +569,7 @@ def main(argv=None):
     prepass_bytes = reads * xbytes + wbytes
 
     pname = ("pmc_gemm_f8v2_per_token.json" if kdt == "f8"
+             else "pmc_gemm_h2d_fp32.json" if fp32 and "h2d" in kname
              else "pmc_gemm_h2_fp32.json" if fp32
              else "pmc_gemm_fqt7_per_group.json" if use_fqt and "fqt7" in kname
              else "pmc_gemm_fqt_per_group.json" if use_fqt

@@ -97,13 +97,19 @@ enum sqmp_act_out {
                            [M] (the D scale); out_xs: D [M][S_pad] exact salient x
                            (operands of sqmp_gemm_f8) */
   /* 4: reserved (the removed FP6 code output) */
-  SQMP_OUT_C4 = 5       /* per_group activations in ACTIVATION order (operands of
+  SQMP_OUT_C4 = 5,      /* per_group activations in ACTIVATION order (operands of
                            sqmp_gemm_fqt): out = int4 codes [roundup(M, 256)][Kq / 2] bytes,
                            Kq = roundup(K - S, 64), bpack rows whose position j is the
                            column of activation rank j (zeros past K - S); out_scale = the D
                            group scales [Kq / group_size][roundup(M, 256)]; out_xs = the
                            exact salient columns [M][S_pad].  4-bit, group_size % 64 == 0,
                            fp16/bf16, posmap required. */
+  SQMP_OUT_H2 = 6       /* fp32 layers: the SQMP_OUT_FP values as the two f16 planes of
+                           sqmp_gemm_h2d -- out = f16 [2][roundup(M, 128)][Kp + S_pad] (rows
+                           scaled by 2^aexp[m], split h + l), out_scale = int32 aexp [M];
+                           bit-identical to SQMP_OUT_FP + sqmp_split2_f16.  The fp32 wave
+                           quantizers only (act per_token / per_group, K % 8 == 0, posmap):
+                           SQMP_EUNSUPPORTED elsewhere. */
 };
 
 /* Library identity. */

@@ -884,12 +884,19 @@ static int launch_rank_table(const uint32_t* key, const int32_t* nonsal, int L,
 // into registers while this one is quantized).  RCH = 16-B row chunks per lane
 // (K * esize <= RCH * 1 KiB), VCH = 8-position output chunks per lane (P <= VCH * 512).
 // The block (4 waves) shares the entry table and the salient column list.
-template <class DT, int MODE, int RCH, int VCH>
+// H2 (fp32, SQMP_OUT_H2): the row is written as the two f16 planes of sqmp_gemm_h2d's
+// operand (out: planes [2][ldr][P + S_pad], hplane = ldr (P + S_pad) halves) with its exponent
+// in aexp[m]; the exponent needs max |x_hat| of the row before any value is stored, and that
+// is known from the statistics: |code * s| is monotone in |t| within a scale group, so the
+// group's largest output is fast_code(gmax, s) * s (the row's: that of the row maximum), and
+// the salient tail adds its own maximum.
+template <class DT, int MODE, int RCH, int VCH, bool H2 = false>
 __global__ __launch_bounds__(256) void quant_fp_wave_kernel(
     const typename DT::T* __restrict__ x, int M, int K, int q_max, int nga,
     const u32x4* __restrict__ ent_g, int P, const int32_t* __restrict__ nonsal, int Kn,
     const int32_t* __restrict__ sal, int S, int S_pad, const uint32_t* __restrict__ cmax,
-    typename DT::T* __restrict__ out) {
+    typename DT::T* __restrict__ out, int* __restrict__ aexp = nullptr, size_t hplane = 0) {
+  static_assert(!H2 || DT::id == SQMP_F32, "the two-plane output is of fp32 rows");
   typedef typename DT::T T;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_w[];
   const int NCH = P / 8;
@@ -968,21 +975,35 @@ __global__ __launch_bounds__(256) void quant_fp_wave_kernel(
       }
     }
     float s_row = s_all, r_row = r_all;
+    float ym = 0.f;  // H2: max |x_hat| of the row
     if (MODE == MODE_TOKEN) {
-      s_row = group_scale<DT>(wave_max(lmax), q_max);
+      const float rm = wave_max(lmax);
+      s_row = group_scale<DT>(rm, q_max);
       r_row = 1.0f / s_row;
+      if (H2) ym = fast_code<DT>(rm, s_row, r_row) * s_row;
     } else if (MODE == MODE_GROUP) {
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
       for (int g = lane; g < nga; g += 64) {
-        const float sg = group_scale<DT>(__uint_as_float(gmax[g]), q_max);
+        const float gm = __uint_as_float(gmax[g]);
+        const float sg = group_scale<DT>(gm, q_max);
         scr[g] = make_float2(sg, 1.0f / sg);
+        if (H2) ym = fmaxf(ym, fast_code<DT>(gm, sg, 1.0f / sg) * sg);
       }
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    } else if (H2) {
+      ym = fast_code<DT>(wave_max(lmax), s_row, r_row) * s_row;
+    }
+    int eh = 0;
+    if constexpr (H2) {
+      for (int j = lane; j < S; j += 64) ym = fmaxf(ym, fabsf(DT::to_f(row[salc[j]])));
+      eh = row_exp_of(wave_max(ym));
+      if (lane == 0) aexp[m] = eh;
     }
     // ---- quantize from registers, 16-B stores
     T* o = out + (size_t)m * W;
+    uint16_t* oh = (uint16_t*)out + (size_t)m * W;
 #pragma unroll
     for (int i = 0; i < VCH; ++i) {
       const int c = lane + 64 * i;
@@ -1002,8 +1023,12 @@ __global__ __launch_bounds__(256) void quant_fp_wave_kernel(
           }
           r[j] = DT::from_f(y);
         }
+        if constexpr (H2) {
+          store_h2x8(oh + 8 * c, hplane, (const float*)r, eh);
+        } else {
 #pragma unroll
-        for (int h = 0; h < 8 / EPC; ++h) ((u32x4*)o)[(8 / EPC) * c + h] = ((const u32x4*)r)[h];
+          for (int h = 0; h < 8 / EPC; ++h) ((u32x4*)o)[(8 / EPC) * c + h] = ((const u32x4*)r)[h];
+        }
       }
     }
     for (int c = NCH + lane; c < WCH; c += 64) {
@@ -1013,8 +1038,12 @@ __global__ __launch_bounds__(256) void quant_fp_wave_kernel(
         const uint32_t k = salc[(c - NCH) * 8 + j];
         r[j] = k != 0xFFFFu ? row[k] : DT::from_f(0.f);
       }
+      if constexpr (H2) {
+        store_h2x8(oh + 8 * c, hplane, (const float*)r, eh);
+      } else {
 #pragma unroll
-      for (int h = 0; h < 8 / EPC; ++h) ((u32x4*)o)[(8 / EPC) * c + h] = ((const u32x4*)r)[h];
+        for (int h = 0; h < 8 / EPC; ++h) ((u32x4*)o)[(8 / EPC) * c + h] = ((const u32x4*)r)[h];
+      }
     }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");  // row / gmax reuse
@@ -1029,11 +1058,14 @@ __global__ __launch_bounds__(256) void quant_fp_wave_kernel(
 // rows of any length that fits LDS run at full occupancy of what fits.  OUT_FP writes the
 // packed-order x_hat + exact salient tail; INPLACE (the output quantizer, P == K) writes
 // the row back over itself, G_ZERO positions (salient columns) passing through.
-template <int MODE, bool INPLACE>
+// H2: the two f16 planes + row exponent of quant_fp_wave_kernel<..., H2>
+template <int MODE, bool INPLACE, bool H2 = false>
 __global__ __launch_bounds__(256) void quant_f32w_kernel(
     float* __restrict__ x, int M, int K, int q_max, int nga, const u32x4* __restrict__ ent,
     int P, const int32_t* __restrict__ nonsal, int Kn, const int32_t* __restrict__ sal,
-    int S, int S_pad, const uint32_t* __restrict__ cmax, float* __restrict__ out) {
+    int S, int S_pad, const uint32_t* __restrict__ cmax, float* __restrict__ out,
+    int* __restrict__ aexp = nullptr, size_t hplane = 0) {
+  static_assert(!(H2 && INPLACE), "the two-plane output is the GEMM operand");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_f32w[];
   const int NCH = P / 8;
   const int W = INPLACE ? K : P + S_pad, WCH = W / 8;
@@ -1103,20 +1135,34 @@ __global__ __launch_bounds__(256) void quant_f32w_kernel(
       }
     }
     float s_row = s_all, r_row = r_all;
+    float ym = 0.f;  // H2: max |x_hat| of the row (see quant_fp_wave_kernel)
     if (MODE == MODE_TOKEN) {
-      s_row = group_scale<F32>(wave_max(lmax), q_max);
+      const float rm = wave_max(lmax);
+      s_row = group_scale<F32>(rm, q_max);
       r_row = 1.0f / s_row;
+      if (H2) ym = fast_code<F32>(rm, s_row, r_row) * s_row;
     } else if (MODE == MODE_GROUP) {
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
       for (int g = lane; g < nga; g += 64) {
-        const float sg = group_scale<F32>(__uint_as_float(gmax[g]), q_max);
+        const float gm = __uint_as_float(gmax[g]);
+        const float sg = group_scale<F32>(gm, q_max);
         scr[g] = make_float2(sg, 1.0f / sg);
+        if (H2) ym = fmaxf(ym, fast_code<F32>(gm, sg, 1.0f / sg) * sg);
       }
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    } else if (H2) {
+      ym = fast_code<F32>(wave_max(lmax), s_row, r_row) * s_row;
+    }
+    int eh = 0;
+    if constexpr (H2) {
+      for (int j = lane; j < S; j += 64) ym = fmaxf(ym, fabsf(row[sal[j]]));
+      eh = row_exp_of(wave_max(ym));
+      if (lane == 0) aexp[m] = eh;
     }
     float* o = (INPLACE ? x : out) + (size_t)m * W;
+    uint16_t* oh = (uint16_t*)out + (size_t)m * W;
     for (int c0 = lane; c0 < NCH; c0 += 64 * EB) {
       load_ent(c0);
 #pragma unroll
@@ -1137,8 +1183,12 @@ __global__ __launch_bounds__(256) void quant_f32w_kernel(
             r[j] = __builtin_copysignf(fast_code<F32>(t, sr.x, sr.y) * sr.x, t);
           }
         }
-        ((u32x4*)o)[2 * c] = ((const u32x4*)r)[0];
-        ((u32x4*)o)[2 * c + 1] = ((const u32x4*)r)[1];
+        if constexpr (H2) {
+          store_h2x8(oh + 8 * c, hplane, r, eh);
+        } else {
+          ((u32x4*)o)[2 * c] = ((const u32x4*)r)[0];
+          ((u32x4*)o)[2 * c + 1] = ((const u32x4*)r)[1];
+        }
       }
     }
     if (!INPLACE) {
@@ -1149,8 +1199,12 @@ __global__ __launch_bounds__(256) void quant_f32w_kernel(
           const int i = (c - NCH) * 8 + j;
           r[j] = i < S ? row[sal[i]] : 0.f;
         }
-        ((u32x4*)o)[2 * c] = ((const u32x4*)r)[0];
-        ((u32x4*)o)[2 * c + 1] = ((const u32x4*)r)[1];
+        if constexpr (H2) {
+          store_h2x8(oh + 8 * c, hplane, r, eh);
+        } else {
+          ((u32x4*)o)[2 * c] = ((const u32x4*)r)[0];
+          ((u32x4*)o)[2 * c + 1] = ((const u32x4*)r)[1];
+        }
       }
     }
     __builtin_amdgcn_wave_barrier();
@@ -1158,23 +1212,24 @@ __global__ __launch_bounds__(256) void quant_f32w_kernel(
   }
 }
 
-template <int MODE, bool INPLACE>
+template <int MODE, bool INPLACE, bool H2 = false>
 static int quant_f32w_launch(void* x, int M, int K, int q_max, int nga, const uint32_t* ent,
                              int P, const int32_t* nonsal, int Kn, const int32_t* sal, int S,
-                             int S_pad, const uint32_t* cmax, void* out, hipStream_t s) {
+                             int S_pad, const uint32_t* cmax, void* out, hipStream_t s,
+                             int* aexp = nullptr, size_t hplane = 0) {
   const size_t wb = (size_t)round_up(4L * K, 16) + (size_t)round_up(12L * nga, 16);
   int nw = (int)((160 * 1024) / wb);
   if (nw < 1) return SQMP_EUNSUPPORTED;
   nw = nw > 4 ? 4 : nw;
   const size_t lds = nw * wb;
-  SQMP_HIP_CHECK(hipFuncSetAttribute((const void*)quant_f32w_kernel<MODE, INPLACE>,
+  SQMP_HIP_CHECK(hipFuncSetAttribute((const void*)quant_f32w_kernel<MODE, INPLACE, H2>,
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   const int per_cu = (int)((160 * 1024) / lds);
   int grid = 256 * (per_cu < 1 ? 1 : per_cu);
   if (grid > cdiv(M, nw)) grid = cdiv(M, nw);
-  quant_f32w_kernel<MODE, INPLACE><<<dim3(grid), dim3(64 * nw), lds, s>>>(
+  quant_f32w_kernel<MODE, INPLACE, H2><<<dim3(grid), dim3(64 * nw), lds, s>>>(
       (float*)x, M, K, q_max, nga, (const u32x4*)ent, P, nonsal, Kn, sal, S, S_pad, cmax,
-      (float*)out);
+      (float*)out, aexp, hplane);
   SQMP_LAUNCH_CHECK();
   return SQMP_OK;
 }
@@ -1216,20 +1271,21 @@ static int quant_launch(void* x, int M, int K, int q_max, int G, int nga, const 
   return SQMP_OK;
 }
 
-template <class DT, int MODE, int RCH, int VCH>
+template <class DT, int MODE, int RCH, int VCH, bool H2 = false>
 static int quant_fpw_launch(void* x, int M, int K, int q_max, int nga, const uint32_t* ent, int P,
                             const int32_t* nonsal, int Kn, const int32_t* sal, int S, int S_pad,
-                            const uint32_t* cmax, void* out, size_t lds, hipStream_t s) {
+                            const uint32_t* cmax, void* out, size_t lds, hipStream_t s,
+                            int* aexp = nullptr, size_t hplane = 0) {
   typedef typename DT::T T;
-  SQMP_HIP_CHECK(hipFuncSetAttribute((const void*)quant_fp_wave_kernel<DT, MODE, RCH, VCH>,
+  SQMP_HIP_CHECK(hipFuncSetAttribute((const void*)quant_fp_wave_kernel<DT, MODE, RCH, VCH, H2>,
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   int per_cu = (int)((160 * 1024) / lds);
   per_cu = per_cu < 1 ? 1 : (per_cu > 8 ? 8 : per_cu);
   int grid = 256 * per_cu;
   if (grid > cdiv(M, 4)) grid = cdiv(M, 4);
-  quant_fp_wave_kernel<DT, MODE, RCH, VCH><<<dim3(grid), dim3(256), lds, s>>>(
+  quant_fp_wave_kernel<DT, MODE, RCH, VCH, H2><<<dim3(grid), dim3(256), lds, s>>>(
       (const T*)x, M, K, q_max, nga, (const u32x4*)ent, P, nonsal, Kn, sal, S, S_pad, cmax,
-      (T*)out);
+      (T*)out, aexp, hplane);
   SQMP_LAUNCH_CHECK();
   return SQMP_OK;
 }
@@ -1265,6 +1321,35 @@ static int quant_dispatch(void* x, int M, int K, int amode, int q_max, int G, in
                    : amode == SQMP_ACT_PER_TENSOR ? MODE_TENSOR
                                                   : MODE_GROUP;
   if constexpr (DT::id == SQMP_F32) {
+    // the two-plane operand of sqmp_gemm_h2d (planes [2][roundup(M, 128)][P + S_pad], row
+    // exponents in out_scale): the wave kernel up to 4096 columns, else quant_f32w_kernel
+    if (out_kind == SQMP_OUT_H2) {
+      if (!ent || K % 8 != 0 || P % 8 != 0 || ((uintptr_t)x) % 16 != 0 || ((uintptr_t)out) % 16 != 0)
+        return SQMP_EUNSUPPORTED;
+      const size_t hplane = (size_t)round_up(M, 128) * (P + S_pad);
+      int* aexp = (int*)out_scale;
+      if (K <= 4096 && P <= 4096) {
+        const size_t lds = quant_fp_wave_lds_bytes(K, P, nga, S_pad, sizeof(float));
+        if (lds <= 160 * 1024) {
+          const bool sm = K <= 2048 && P <= 2048;
+#define SQMP_QH(MODE)                                                                          \
+  (sm ? quant_fpw_launch<DT, MODE, 8, 4, true>(x, M, K, q_max, nga, ent, P, nonsal, Kn, sal, S,  \
+                                               S_pad, cmax, out, lds, s, aexp, hplane)        \
+      : quant_fpw_launch<DT, MODE, 16, 8, true>(x, M, K, q_max, nga, ent, P, nonsal, Kn, sal, S, \
+                                                S_pad, cmax, out, lds, s, aexp, hplane))
+          if (mode == MODE_TOKEN) return SQMP_QH(MODE_TOKEN);
+          if (mode == MODE_TENSOR) return SQMP_QH(MODE_TENSOR);
+          return SQMP_QH(MODE_GROUP);
+#undef SQMP_QH
+        }
+      }
+#define SQMP_QH(MODE)                                                                           \
+  quant_f32w_launch<MODE, false, true>(x, M, K, q_max, nga, ent, P, nonsal, Kn, sal, S, S_pad, cmax, \
+                                       out, s, aexp, hplane)
+      return mode == MODE_TOKEN ? SQMP_QH(MODE_TOKEN)
+           : mode == MODE_TENSOR ? SQMP_QH(MODE_TENSOR) : SQMP_QH(MODE_GROUP);
+#undef SQMP_QH
+    }
     // fp32 rows longer than the register-staged wave kernel holds, and the in-place output
     // quantizer: one wave per row from LDS (quant_f32w_kernel)
     if (ent && K % 8 == 0 && P % 8 == 0 && (((uintptr_t)x) % 16 == 0) &&
@@ -1417,8 +1502,10 @@ static int quant_act_impl(void* x, int dtype, int M, int K, int amode, int n_bit
                        amode != SQMP_ACT_PER_GROUP_MEAN3STD) ||
         group_size % 64 != 0)
       return SQMP_EUNSUPPORTED;
-  } else if (out_kind == SQMP_OUT_FP || out_kind == SQMP_OUT_I8 || out_kind == SQMP_OUT_F8) {
+  } else if (out_kind == SQMP_OUT_FP || out_kind == SQMP_OUT_I8 || out_kind == SQMP_OUT_F8 ||
+             out_kind == SQMP_OUT_H2) {
     if (Kp < K || Kp % 128 != 0 || S_pad < S || S_pad % 64 != 0 || !out) return SQMP_EINVAL;
+    if (out_kind == SQMP_OUT_H2 && (dtype != SQMP_F32 || !out_scale)) return SQMP_EINVAL;
     if (out_kind == SQMP_OUT_F8) {
       if (!out_scale || (S_pad > 0 && !out_xs)) return SQMP_EINVAL;
       // e4m3 holds every integer code up to 16 exactly, e2m3 up to 7; one scale per row
@@ -1570,11 +1657,12 @@ static int quant_act_impl(void* x, int dtype, int M, int K, int amode, int n_bit
   // ---- fp32 rows (OUT_FP, and the in-place output quantizer): the lane-contiguous
   // pipeline's statistics and rank table (clean workspace, no memsets), the entry table
   // scattered from it in one launch, the fp32 wave quantizers
+  const bool h2 = out_kind == SQMP_OUT_H2;
   if (dtype == SQMP_F32 && !lc_off && Kn > 0 && amode != SQMP_ACT_PER_TENSOR && K % 8 == 0 &&
       (((uintptr_t)x) % 16 == 0) &&
-      ((out_kind == SQMP_OUT_FP && posmap && Kp % 8 == 0 && ((uintptr_t)out) % 16 == 0) ||
+      (((out_kind == SQMP_OUT_FP || h2) && posmap && Kp % 8 == 0 && ((uintptr_t)out) % 16 == 0) ||
        out_kind == SQMP_OUT_INPLACE) &&
-      (out_kind == SQMP_OUT_FP || clean)) {
+      (out_kind == SQMP_OUT_FP || h2 || clean)) {
     const bool inplace = out_kind == SQMP_OUT_INPLACE;
     const int P = inplace ? K : Kp;
     const size_t wb = (size_t)round_up(4L * K, 16) + (size_t)round_up(12L * (group ? cdiv(Kn, group_size) : 1), 16);
@@ -1595,6 +1683,8 @@ static int quant_act_impl(void* x, int dtype, int M, int K, int amode, int n_bit
                                  out_scale, out_xs, s);
     }
   }
+
+  if (h2) return SQMP_EUNSUPPORTED;  // the two-plane output: the fp32 wave kernels only
 
   // ---- general path (fp32, 8-bit int output, large rows, other group sizes)
   // SQMP_QA_REUSE_STATS: the rank partials of the previous call on this workspace (a

@@ -68,23 +68,6 @@ __device__ inline void split3(float v, uint32_t& h, uint32_t& m, uint32_t& l) {
 // / 2^bexp[n] into [2^13, 2^14) at their maximum, v' = h + l with h = f16(v'),
 // l = f16(v' - h), three products (al.bh + ah.bl + ah.bh) on v_mfma_f32_16x16x32_f16, the
 // scales undone in the epilogue.
-// v (|v| < 2^14) -> (h, l) f16 bit patterns, h = f16(v), l = f16(v - h): v - h is exact in
-// fp32 and l keeps its 11 leading bits, so |v - h - l| <= 2^-22 |v| (+ the f16 subnormal
-// floor 2^-25)
-__device__ inline void split2h(float v, uint32_t& h, uint32_t& l) {
-  const _Float16 hh = (_Float16)v;
-  const _Float16 ll = (_Float16)(v - (float)hh);
-  h = (uint32_t)(*(const uint16_t*)&hh);
-  l = (uint32_t)(*(const uint16_t*)&ll);
-}
-
-// the exponent e with max |row| * 2^e in [2^13, 2^14) (0 for an all-zero row)
-__device__ inline int row_exp_of(float mx) {
-  // floor(log2 mx) from the exponent field (a subnormal mx counts as 2^-127: the scaled
-  // maximum then stays below 2^14 all the same)
-  return mx > 0.f ? 13 - ((int)((__float_as_uint(mx) >> 23) & 0xFFu) - 127) : 0;
-}
-
 template <bool COLMAX, int WN, bool H = false, int BN = 128, int BK = 32>
 __global__ __launch_bounds__(128 * WN, 4 / WN) void gemm_x3_kernel(
     const float* __restrict__ A, const uint16_t* __restrict__ B3, const float* __restrict__ bias,

@@ -18,6 +18,36 @@ inline bool nt_output(size_t bytes) {
   return bytes >= ((size_t)64 << 20);
 }
 
+// The two-piece fp16 form of fp32 values (sqmp_gemm_h2 / _h2d, the fp32 quantizer's
+// SQMP_OUT_H2 mode): rows scaled by 2^e so that their maximum lies in [2^13, 2^14), then
+// v (|v| < 2^14) -> (h, l) f16 bit patterns, h = f16(v), l = f16(v - h): v - h is exact in
+// fp32 and l keeps its 11 leading bits, so |v - h - l| <= 2^-22 |v| (+ the f16 subnormal
+// floor 2^-25)
+__device__ inline void split2h(float v, uint32_t& h, uint32_t& l) {
+  const _Float16 hh = (_Float16)v;
+  const _Float16 ll = (_Float16)(v - (float)hh);
+  h = (uint32_t)(*(const uint16_t*)&hh);
+  l = (uint32_t)(*(const uint16_t*)&ll);
+}
+
+// the exponent e with max |row| * 2^e in [2^13, 2^14) (0 for an all-zero row)
+__device__ inline int row_exp_of(float mx) {
+  // floor(log2 mx) from the exponent field (a subnormal mx counts as 2^-127: the scaled
+  // maximum then stays below 2^14 all the same)
+  return mx > 0.f ? 13 - ((int)((__float_as_uint(mx) >> 23) & 0xFFu) - 127) : 0;
+}
+
+// 8 consecutive fp32 values of a row with exponent e -> 16 B of each plane at p (the l plane
+// `hplane` halves further)
+__device__ inline void store_h2x8(uint16_t* p, size_t hplane, const float* r, int e) {
+  uint32_t h[8], l[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) split2h(__builtin_ldexpf(r[j], e), h[j], l[j]);
+  *(u32x4*)p = u32x4{h[0] | (h[1] << 16), h[2] | (h[3] << 16), h[4] | (h[5] << 16), h[6] | (h[7] << 16)};
+  *(u32x4*)(p + hplane) =
+      u32x4{l[0] | (l[1] << 16), l[2] | (l[3] << 16), l[4] | (l[5] << 16), l[6] | (l[7] << 16)};
+}
+
 // cmax[c] = bits(max_r |x[r][c]|) over a contiguous D matrix [R][C] (fp32 bits of the
 // D value; non-negative floats order like their bit patterns).  Zeroes cmax first.
 int launch_colmax(const void* x, int dtype, int R, int C, uint32_t* cmax, hipStream_t s,

@@ -518,12 +518,17 @@ class W4A4Linear(nn.Module):
                    and ops.fqt_eligible(pw, amode, bits, ag, x2.shape[0],
                                         force=self.kernel == "fqt")
                    and ops.f8_input_ok(xc))
+        # fp32 layers: the quantizer writes sqmp_gemm_h2d's two f16 planes itself
+        use_h2 = (not use_f8 and not use_i8 and not use_fqt and self.kernel == "auto"
+                  and ops.h2_planes_ok(pw, amode))
         if use_f8:
             a8, sa, xs = ops.quant_act_f8(xc, pw, amode, bits)
         elif use_i8:
             a8, sa, xs = ops.quant_act_i8(xc, pw, amode, bits)
         elif use_fqt:
             c4 = ops.quant_act_c4(xc, pw, amode, bits, ag, stats_of=x)
+        elif use_h2:
+            a2 = ops.quant_act_fp(xc, pw, amode, bits, ag, stats_of=x, h2=True)
         else:
             a = ops.quant_act_fp(xc, pw, amode, bits, ag, stats_of=x)
         if mutate_input:
@@ -547,6 +552,8 @@ class W4A4Linear(nn.Module):
             y = ops.gemm_i8(a8, sa, xs, pw, bias)
         elif use_fqt:
             y = ops.gemm_fqt(*c4, pw, bias, ag, colmax=colmax)
+        elif use_h2:
+            y = ops.gemm_h2_planes(a2, pw, bias, colmax=colmax)
         else:
             y = ops.gemm_fq(a, pw, bias, colmax=colmax)
         if ospec is not None:                                                # :308-316

@@ -275,7 +275,7 @@ def _sibling_ok(src: PackedWeight, dst: PackedWeight) -> bool:
 
 
 def quant_act_fp(x2: torch.Tensor, pw: PackedWeight, act_quant: str, n_bits: int,
-                 group_size: int, stats_of: Optional[torch.Tensor] = None) -> torch.Tensor:
+                 group_size: int, stats_of: Optional[torch.Tensor] = None, h2: bool = False):
     """x [M, K] -> A [M, Kp + S_pad] in D: x_hat in packed order + exact salient tail.
 
     The returned tensor is an M-row view of an allocation padded to a multiple of 256 rows
@@ -283,10 +283,21 @@ def quant_act_fp(x2: torch.Tensor, pw: PackedWeight, act_quant: str, n_bits: int
 
     stats_of: the tensor whose identity names this batch (the module's input x).  Layers
     that quantize the same x with the same salient set and sort (q/k/v, gate/up) reuse the
-    first call's column statistics and rank instead of recomputing them."""
+    first call's column statistics and rank instead of recomputing them.
+
+    h2 (fp32, h2_planes_ok): the same values as sqmp_gemm_h2d's operand instead, written by
+    the quantizer itself (SQMP_OUT_H2): (f16 planes [2, roundup(M, 128), L], int32 row
+    exponents, M) -- bit-identical to sqmp_split2_f16 of the fp32 A."""
     _require_gpu(x2, "quant_act")
     M, K = x2.shape
-    a = torch.empty((_pad_rows(M), pw.Kp + pw.S_pad), dtype=x2.dtype, device=x2.device)[:M]
+    L = pw.Kp + pw.S_pad
+    if h2:
+        ldr = (M + 127) // 128 * 128
+        planes = torch.empty((2, ldr, L), dtype=torch.float16, device=x2.device)
+        aexp = torch.empty(max(ldr, 1), dtype=torch.int32, device=x2.device)
+        a = planes
+    else:
+        a = torch.empty((_pad_rows(M), L), dtype=x2.dtype, device=x2.device)[:M]
     lib = load()
     nb = _ws_bytes(M, K, pw.Kp)
     stream = torch.cuda.current_stream(x2.device).cuda_stream
@@ -298,7 +309,8 @@ def quant_act_fp(x2: torch.Tensor, pw: PackedWeight, act_quant: str, n_bits: int
         skey = (src.data_ptr(), tuple(src.shape), src.dtype, src._version, pw.sal_key,
                 act_quant, M, K)
         la = e.get("last_a")
-        if (SIB_REUSE and la is not None and la[0]() is src and la[1] == skey + (n_bits, group_size)
+        if (not h2 and SIB_REUSE and la is not None and la[0]() is src
+                and la[1] == skey + (n_bits, group_size)
                 and la[2]() is not None and _sibling_ok(la[2](), pw)):
             # a sibling of the layer that produced la[3] on this same input
             check(lib.sqmp_permute_act(_p(la[3]), _p(a), _p(_sibling_map(la[2](), pw)),
@@ -316,7 +328,8 @@ def quant_act_fp(x2: torch.Tensor, pw: PackedWeight, act_quant: str, n_bits: int
     status = lib.sqmp_quant_act_v2(_p(x2), _dtype_code(x2.dtype), M, K, ACT_MODES[act_quant],
                                    n_bits, group_size, _p(pw.amap), pw.Kp, _p(pw.nonsal),
                                    _p(pw.salient), pw.S, pw.S_pad, _p(pw.posmap), flags,
-                                   _lib.OUT_FP, _p(a), None, None, _p(e["buf"]),
+                                   _lib.OUT_H2 if h2 else _lib.OUT_FP, _p(a),
+                                   _p(aexp) if h2 else None, None, _p(e["buf"]),
                                    e["buf"].numel(), ctypes.c_void_p(stream))
     if status != _lib.SQMP_OK:
         _WS.pop((x2.device.index, stream, K, pw.Kp, "in"), None)  # it may be left dirty
@@ -325,11 +338,11 @@ def quant_act_fp(x2: torch.Tensor, pw: PackedWeight, act_quant: str, n_bits: int
         e["stats"] = (weakref.ref(stats_of if stats_of is not None else x2), skey,
                       pw.codes.data_ptr())
         e["last_a"] = None
-        if SIB_REUSE and a.numel() * a.element_size() <= SIB_MAX_BYTES:
+        if not h2 and SIB_REUSE and a.numel() * a.element_size() <= SIB_MAX_BYTES:
             # held while the input lives: freeing the input drops the operand with it
             e["last_a"] = (weakref.ref(stats_of if stats_of is not None else x2, _drop_last_a(e)),
                            skey + (n_bits, group_size), weakref.ref(pw), a)
-    return a
+    return (planes, aexp, M) if h2 else a
 
 
 def _drop_last_a(e):
@@ -710,6 +723,31 @@ def h2d_operand(pw: PackedWeight) -> torch.Tensor:
                                    _stream(planes)), "pack_h2d")
         pw.h2d = wt
     return pw.h2d
+
+
+def h2_planes_ok(pw: PackedWeight, act_quant: str) -> bool:
+    """Whether an fp32 layer's forward runs quantizer -> planes -> sqmp_gemm_h2d
+    (quant_act_fp(h2=True) + gemm_h2_planes) instead of the fp32 operand + split."""
+    L = pw.Kp + pw.S_pad
+    return (pw.dtype == torch.float32 and H2D and F32_GEMM == "h2" and L % 64 == 0
+            and pw.N % 4 == 0 and pw.K % 8 == 0 and pw.K - pw.S > 0
+            and act_quant != "per_tensor")
+
+
+def gemm_h2_planes(a2, pw: PackedWeight, bias: Optional[torch.Tensor],
+                   colmax: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """y = A . W_hat^T + bias on sqmp_gemm_h2d from quant_act_fp(h2=True)'s planes."""
+    planes, aexp, M = a2
+    _, bexp = h2_operand(pw)
+    wt = h2d_operand(pw)
+    ldr, L = planes.shape[1], planes.shape[2]
+    if L != pw.Kp + pw.S_pad:
+        raise ValueError("gemm_h2_planes: operand width does not match the packed weight")
+    y = torch.empty((M, pw.N), dtype=torch.float32, device=planes.device)
+    check(load().sqmp_gemm_h2d(_p(planes), ldr, _p(aexp), _p(wt), _p(bexp), _p(bias), _p(y), M,
+                               pw.N, L, _p(colmax) if colmax is not None else None,
+                               _stream(planes)), "gemm_h2d")
+    return y
 
 
 def gemm_h2(a: torch.Tensor, pw: PackedWeight, bias: Optional[torch.Tensor],

@@ -224,3 +224,62 @@ def test_h2d_bit_identical_to_h2(M, K, N, p, has_bias):
     assert torch.equal(y1.view(torch.int32), y0.view(torch.int32))
     assert torch.equal(y2.view(torch.int32), y0.view(torch.int32))
     assert torch.equal(c1, c0)
+
+
+@pytest.mark.parametrize("act,K,M,p", [
+    ("per_group", 1024, 300, 0.10),     # the register-staged wave quantizer
+    ("per_token", 2048, 129, 0.05),
+    ("per_group", 8192, 260, 0.05),     # rows longer than 4096: quant_f32w_kernel
+    ("per_token", 8192, 64, 0.0),       # no salient channel
+])
+def test_quantizer_h2_planes_bit_identical(act, K, M, p):
+    """SQMP_OUT_H2: the fp32 quantizer writes sqmp_gemm_h2d's planes and row exponents itself,
+    bit-identical to sqmp_split2_f16 of its SQMP_OUT_FP operand; the layer forward on that
+    path (quantizer -> planes -> sqmp_gemm_h2d, output quantization fused) equals the forward
+    on the fp32 operand + sqmp_gemm_h2, bit for bit."""
+    from smoothquant import ops
+    from smoothquant._lib import load
+    dev = _dev()
+    rng = np.random.default_rng(31)
+    N = 1024
+    W = (rng.standard_normal((N, K)) * 0.02).astype(np.float32)
+    x = rng.standard_normal((M, K)).astype(np.float32)
+    x[:, rng.choice(K, max(1, K // 100), replace=False)] *= 30.0
+    q = make_layer(W, (rng.standard_normal(N) * 0.1).astype(np.float32), "fp32", dev,
+                   weight_quant="per_group", act_quant=act,
+                   importance=torch.from_numpy(np.abs(x).mean(0)) if p else None,
+                   salient_prop=p, group_size=128)
+    pw = q.packed()
+    assert ops.h2_planes_ok(pw, act)
+    xt = torch.from_numpy(x).to(dev)
+    planes, aexp, m = ops.quant_act_fp(xt.clone(), pw, act, 4, 128, h2=True)
+    a = ops.quant_act_fp(xt.clone(), pw, act, 4, 128)
+    L = pw.Kp + pw.S_pad
+    ldr = planes.shape[1]
+    ref = torch.empty_like(planes)
+    rexp = torch.empty(ldr, dtype=torch.int32, device=dev)
+    ops.check(load().sqmp_split2_f16(ops._p(a), M, L, ldr, ops._p(ref), ops._p(rexp),
+                                     ops._stream(a)), "split2")
+    torch.cuda.synchronize()
+    assert m == M
+    assert torch.equal(aexp[:M], rexp[:M])
+    assert torch.equal(planes[:, :M].view(torch.int16), ref[:, :M].view(torch.int16))
+    # the layer forward, and (square weights: the reference's output quantizer needs N == K
+    # with salient channels) with output quantization, its column maxima fused
+    layers = [q]
+    if K <= 2048:
+        W2 = (rng.standard_normal((K, K)) * 0.02).astype(np.float32)
+        layers.append(make_layer(W2, None, "fp32", dev, weight_quant="per_group", act_quant=act,
+                                 quantize_output=True,
+                                 importance=torch.from_numpy(np.abs(x).mean(0)) if p else None,
+                                 salient_prop=p, group_size=128))
+    old = ops.H2D
+    try:
+        for layer in layers:
+            ops.H2D = True
+            y1 = layer(xt.clone())
+            ops.H2D = False
+            y0 = layer(xt.clone())
+            assert torch.equal(y1.view(torch.int32), y0.view(torch.int32))
+    finally:
+        ops.H2D = old
