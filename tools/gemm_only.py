@@ -19,10 +19,16 @@ dev = torch.device("cuda")
 act = next((a for a in extra if a.startswith("per_")), "per_group" if kind in ("fq", "fqt", "c4") else "per_token")
 q, x, lin = bench.make_layer(dev, act, seed=1,
                              dtype=torch.float32 if kind == "h2" else torch.float16)
-if kind == "h2":
-    kind = "fq"  # the fp32 layer's gemm_fq runs sqmp_gemm_h2
 pw = q.packed()
-if kind == "fq":
+if kind == "h2" and not ops.h2_planes_ok(pw, act):
+    kind = "fq"  # the fp32 layer's gemm_fq runs sqmp_gemm_h2
+if kind == "h2":  # the fp32 forward's path: quantizer -> f16 planes -> sqmp_gemm_h2d
+    a2 = ops.quant_act_fp(x, pw, act, 4, bench.G, h2=True)
+    for _ in range(iters):
+        if prepass:
+            ops.quant_act_fp(x, pw, act, 4, bench.G, h2=True)
+        ops.gemm_h2_planes(a2, pw, lin.bias)
+elif kind == "fq":
     a = ops.quant_act_fp(x, pw, act, 4, bench.G)
     for _ in range(iters):
         if prepass:
