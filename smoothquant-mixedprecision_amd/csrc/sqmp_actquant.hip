@@ -518,6 +518,18 @@ __global__ __launch_bounds__(256) void lc_table_kernel(
   for (int r = Kn + t; r < lc_len; r += nt) lctab[r] = lc_none;
 }
 
+// The F8 quantizer's table in packed-POSITION order: lctab[p] = amap[p] | p << 16 for the
+// positions of a non-salient column, the (zero word, sink word) entry for salient / padding
+// positions and for p in [P, lc_len): a thread's entries are then consecutive output positions.
+__global__ __launch_bounds__(256) void pos_table_kernel(const int32_t* __restrict__ amap, int P,
+                                                        uint32_t* __restrict__ lctab, int lc_len,
+                                                        uint32_t lc_none) {
+  const int p = blockIdx.x * 256 + threadIdx.x;
+  if (p >= lc_len) return;
+  const int c = p < P ? amap[p] : -1;
+  lctab[p] = c >= 0 ? (uint32_t)c | ((uint32_t)p << 16) : lc_none;
+}
+
 // ---------------------------------------------------------------- rank + table, one launch
 // For lists up to RT_MAX entries: every workgroup stages all L keys key[nonsal[j]] in LDS
 // and ranks R * 256 / TPO owners, TPO lanes per group of R owners splitting the competitors
@@ -1601,9 +1613,7 @@ static int quant_act_impl(void* x, int dtype, int M, int K, int amode, int n_bit
       st = launch_colmax(x, dtype, M, K, cmax, s, false);
       if (st) return st;
     }
-    const int nthr = K > Kn ? K : (Kn > 0 ? Kn : 1);
-    lc_table_kernel<<<dim3(cdiv(nthr, 256)), dim3(256), 0, s>>>(
-        TAB_LIST, nonsal, Kn, K, posmap, counts, colsorted, nullptr, lctab, lc_len, lc_none);
+    pos_table_kernel<<<dim3(cdiv(lc_len, 256)), dim3(256), 0, s>>>(amap, Kp, lctab, lc_len, lc_none);
     SQMP_LAUNCH_CHECK();
     st = launch_quant_lc(dtype, amode == SQMP_ACT_PER_TENSOR ? 1 : 0, x, M, K, q_max, 1, lctab,
                          Kn, amap, Kp, salient, S, S_pad, cmax, nonsal, out, nullptr, 0, s,

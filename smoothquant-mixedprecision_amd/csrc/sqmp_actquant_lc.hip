@@ -490,9 +490,34 @@ __device__ __forceinline__ void quant_lc_body(
           }
         }
       } else if (F8) {
+        // F8 = 1: the table is in packed-POSITION order (pos_table_kernel), so this thread's
+        // RPL codes are positions rb .. rb + RPL - 1 of both rows: packed in registers and
+        // stored straight to global memory (no LDS scatter, no second pass)
+        if (rb < P) {
+          uint32_t w0[RPL / 4], w1[RPL / 4];
 #pragma unroll
-        for (int i = 0; i < RPL; ++i)
-          lc_buf[tab[i] >> 16] = f8_pair<DT>(v[i], c);
+          for (int d = 0; d < RPL / 4; ++d) {
+            const uint32_t b0 = f8_pair<DT>(v[4 * d], c), b1 = f8_pair<DT>(v[4 * d + 1], c);
+            const uint32_t b2 = f8_pair<DT>(v[4 * d + 2], c), b3 = f8_pair<DT>(v[4 * d + 3], c);
+            // v_perm_b32 selector bytes: 0-3 = lo operand, 4-7 = hi operand
+            const uint32_t lo0 = __builtin_amdgcn_perm(b1, b0, 0x0c0c0400u);
+            const uint32_t hi0 = __builtin_amdgcn_perm(b3, b2, 0x04000c0cu);
+            const uint32_t lo1 = __builtin_amdgcn_perm(b1, b0, 0x0c0c0602u);
+            const uint32_t hi1 = __builtin_amdgcn_perm(b3, b2, 0x06020c0cu);
+            w0[d] = lo0 | hi0;
+            w1[d] = lo1 | hi1;
+          }
+          unsigned char* b0p = (unsigned char*)out + (size_t)m0 * P + rb;
+#pragma unroll
+          for (int d = 0; d < RPL / 16; ++d)
+            ((u32x4*)b0p)[d] = u32x4{w0[4 * d], w0[4 * d + 1], w0[4 * d + 2], w0[4 * d + 3]};
+          if (has1) {
+            unsigned char* b1p = (unsigned char*)out + (size_t)(m0 + 1) * P + rb;
+#pragma unroll
+            for (int d = 0; d < RPL / 16; ++d)
+              ((u32x4*)b1p)[d] = u32x4{w1[4 * d], w1[4 * d + 1], w1[4 * d + 2], w1[4 * d + 3]};
+          }
+        }
         if (tid == 0) {
           out_scale[m0] = c.s[0];
           if (has1) out_scale[m0 + 1] = c.s[1];
@@ -507,32 +532,12 @@ __device__ __forceinline__ void quant_lc_body(
         }
       }
     }
-    // salient columns' own packed positions hold 0 (their weight codes are 0 too)
-    if (F8 != 3)
+    // salient columns' own packed positions hold 0 (their weight codes are 0 too; the F8
+    // position-order table gathers the zero word for them)
+    if (F8 == 0)
       for (uint64_t zm = zmask; zm; zm &= zm - 1) lc_buf[zp0 + __builtin_ctzll(zm)] = 0u;
     __syncthreads();
 
-    if (F8 == 1) {
-      // codes: 16 positions per chunk, byte 0 / byte 2 of each word -> rows m0 / m0 + 1
-      unsigned char* b0 = (unsigned char*)out + (size_t)m0 * P;
-      unsigned char* b1 = (unsigned char*)out + (size_t)(m0 + 1) * P;
-      for (int c = tid; c < P / 16; c += nthr) {
-        u32x4 y0, y1;
-#pragma unroll
-        for (int h = 0; h < 4; ++h) {
-          const u32x4 w = ((const u32x4*)lc_buf)[4 * c + h];
-          // v_perm_b32 selector bytes: 0-3 = lo operand, 4-7 = hi operand, 0x0c = 0x00
-          const uint32_t a0 = __builtin_amdgcn_perm(w[1], w[0], 0x0c0c0400u);
-          const uint32_t a1 = __builtin_amdgcn_perm(w[3], w[2], 0x04000c0cu);
-          const uint32_t c0 = __builtin_amdgcn_perm(w[1], w[0], 0x0c0c0602u);
-          const uint32_t c1 = __builtin_amdgcn_perm(w[3], w[2], 0x06020c0cu);
-          y0[h] = a0 | a1;
-          y1[h] = c0 | c1;
-        }
-        ((u32x4*)b0)[c] = y0;
-        if (has1) ((u32x4*)b1)[c] = y1;
-      }
-    }
     if (F8) {
       // exact salient columns -> out_xs [M][S_pad]
       T* x0 = out_xs + (size_t)m0 * S_pad;
@@ -753,7 +758,10 @@ static int quant_lc_launch(const void* x, int M, int K, int q_max, int G, const 
                            const LcSib& sib = LcSib{}) {
   typedef typename DT::T T;
   const void* kf = (const void*)quant_lc_kernel<DT, MODE, LC_RPL, GS, F8, NOUT>;
-  const int nw = lc_waves(K, Kn);
+  int nw = lc_waves(K, Kn);
+  // F8: every packed position is some thread's (position-order table)
+  if (F8 == 1 && cdiv(P, 64 * LC_RPL) > nw) nw = cdiv(P, 64 * LC_RPL);
+  if (nw > LC_MAXW) return SQMP_EUNSUPPORTED;
   const size_t lds = sizeof(uint32_t) * (size_t)(P + S_pad + 8) * NOUT;
   SQMP_HIP_CHECK(hipFuncSetAttribute(kf, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   int per_cu = occ_per_cu(kf, 64 * nw, lds);

@@ -32,6 +32,7 @@ OPERAND_CASES = [
     ("fp16", "per_tensor", 0.10, 64, 130, 2048, 384),
     ("bf16", "per_token", 0.10, 128, 64, 1024, 256),
     ("bf16", "per_tensor", 0.0, 256, 33, 512, 256),
+    ("fp16", "per_token", 0.05, 128, 31, 1032, 256),     # K % 128 != 0: padding positions
 ]
 
 
