@@ -501,7 +501,7 @@ def main(argv=None):
         kname = ("sqmp::fq7::gemm_fq7_kernel<F16,1,256,2,0,true,3> (activation order, sqmp_gemm_fqt7)"
                  if c4[1].dim() == 3 else
                  "sqmp::gemm_fq6_kernel<F16,1,256,true> (activation order, sqmp_gemm_fqt)")
-    elif fp32 and ops.h2_planes_ok(pw, args.act):
+    elif fp32 and ops.h2_planes_ok(pw, args.act, M):
         # the forward's fp32 path: the quantizer writes the two f16 planes, sqmp_gemm_h2d
         a2 = ops.quant_act_fp(x, pw, args.act, 4, G, h2=True)
         gemm = lambda: ops.gemm_h2_planes(a2, pw, lin.bias)  # noqa: E731

@@ -520,7 +520,7 @@ class W4A4Linear(nn.Module):
                    and ops.f8_input_ok(xc))
         # fp32 layers: the quantizer writes sqmp_gemm_h2d's two f16 planes itself
         use_h2 = (not use_f8 and not use_i8 and not use_fqt and self.kernel == "auto"
-                  and ops.h2_planes_ok(pw, amode))
+                  and ops.h2_planes_ok(pw, amode, x2.shape[0]))
         if use_f8:
             a8, sa, xs = ops.quant_act_f8(xc, pw, amode, bits)
         elif use_i8:

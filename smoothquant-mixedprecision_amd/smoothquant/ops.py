@@ -725,13 +725,18 @@ def h2d_operand(pw: PackedWeight) -> torch.Tensor:
     return pw.h2d
 
 
-def h2_planes_ok(pw: PackedWeight, act_quant: str) -> bool:
+def _h2d_rows_ok(M: int, L: int) -> bool:
+    """sqmp_gemm_h2d addresses both activation planes with 32-bit buffer offsets."""
+    return 4 * ((M + 127) // 128 * 128) * L < (1 << 32)
+
+
+def h2_planes_ok(pw: PackedWeight, act_quant: str, M: int = 0) -> bool:
     """Whether an fp32 layer's forward runs quantizer -> planes -> sqmp_gemm_h2d
     (quant_act_fp(h2=True) + gemm_h2_planes) instead of the fp32 operand + split."""
     L = pw.Kp + pw.S_pad
     return (pw.dtype == torch.float32 and H2D and F32_GEMM == "h2" and L % 64 == 0
             and pw.N % 4 == 0 and pw.K % 8 == 0 and pw.K - pw.S > 0
-            and act_quant != "per_tensor")
+            and act_quant != "per_tensor" and _h2d_rows_ok(M, L))
 
 
 def gemm_h2_planes(a2, pw: PackedWeight, bias: Optional[torch.Tensor],
@@ -760,7 +765,7 @@ def gemm_h2(a: torch.Tensor, pw: PackedWeight, bias: Optional[torch.Tensor],
         raise ValueError("gemm_h2: A must be fp32 [M, Kp + S_pad] with row stride Kp + S_pad")
     planes, bexp = h2_operand(pw)
     lib = load()
-    if H2D and L % 64 == 0 and pw.N % 4 == 0 and M > 0:
+    if H2D and L % 64 == 0 and pw.N % 4 == 0 and M > 0 and _h2d_rows_ok(M, L):
         wt = h2d_operand(pw)
         ldr = (M + 127) // 128 * 128
         a2 = torch.empty((2, ldr, L), dtype=torch.float16, device=a.device)

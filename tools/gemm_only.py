@@ -20,7 +20,7 @@ act = next((a for a in extra if a.startswith("per_")), "per_group" if kind in ("
 q, x, lin = bench.make_layer(dev, act, seed=1,
                              dtype=torch.float32 if kind == "h2" else torch.float16)
 pw = q.packed()
-if kind == "h2" and not ops.h2_planes_ok(pw, act):
+if kind == "h2" and not ops.h2_planes_ok(pw, act, x.shape[0]):
     kind = "fq"  # the fp32 layer's gemm_fq runs sqmp_gemm_h2
 if kind == "h2":  # the fp32 forward's path: quantizer -> f16 planes -> sqmp_gemm_h2d
     a2 = ops.quant_act_fp(x, pw, act, 4, bench.G, h2=True)
