@@ -15,7 +15,8 @@
 // Why a second kernel: gemm_x3_kernel<H> stages both operands through registers into a
 // single-buffered LDS tile with two barriers per 64-position stage, and splits A while
 // staging (1.8 ms at config 2 in fp32, MFMA busy 44 %, 5.1x its algorithmic HBM bytes).  Here
-//   * the activation planes [2][Mp][L] come pre-split (sqmp_split2_f16) and move by LDS-DMA:
+//   * the activation planes [2][Mp][L] come pre-split -- written by the fp32 quantizer itself
+//     (sqmp_quant_act_v2 SQMP_OUT_H2) or by sqmp_split2_f16 -- and move by LDS-DMA:
 //     TM = 128 rows x 64 positions x 2 planes = 32 KiB per stage, 4 slots, 3 stages in flight,
 //     all pieces issued by waves 0-3 (the loader split of gemm_fq6/fq7);
 //   * the weight planes live in a tile-major copy (sqmp_pack_h2d, once per layer) from which a
