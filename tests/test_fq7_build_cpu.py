@@ -77,3 +77,28 @@ def test_one_wave_gemm_accumulators_stay_in_agprs(tmp_path, name, ns, mfma):
                 n_mfma += 1
         assert own == 0, "compiler-emitted accumulator moves"
         assert n_mfma == mfma
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC) and shutil.which("hipcc") is None,
+                    reason="hipcc not available")
+def test_h2d_kernels_do_not_spill(tmp_path):
+    """sqmp_gemm_h2d holds the next stage's weight planes in VGPRs across hand-counted
+    s_waitcnt (as fq7): every variant (COLMAX x TM 128 / 64) compiles without spills or
+    scratch, at two waves per SIMD."""
+    src = os.path.join(ROOT, "smoothquant-mixedprecision_amd", "csrc", "sqmp_gemm_h2d.hip")
+    r = subprocess.run([HIPCC, "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-I",
+                        os.path.join(ROOT, "include"), "-c", src, "-o", str(tmp_path / "h2d.o"),
+                        "-Rpass-analysis=kernel-resource-usage"],
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    blocks = re.split(r"remark: Function Name: ", r.stderr)
+    seen = 0
+    for b in blocks[1:]:
+        if "gemm_h2d_kernel" not in b.split()[0]:
+            continue
+        seen += 1
+        spill = int(re.search(r"VGPRs Spill: (\d+)", b).group(1))
+        scratch = int(re.search(r"ScratchSize \[bytes/lane\]: (\d+)", b).group(1))
+        vgprs = int(re.search(r"VGPRs: (\d+)", b).group(1))
+        assert spill == 0 and scratch == 0 and vgprs <= 256, (b.split()[0], spill, scratch, vgprs)
+    assert seen == 4
