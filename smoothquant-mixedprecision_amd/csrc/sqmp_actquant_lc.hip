@@ -636,9 +636,88 @@ struct PermArgs {
   int N, Np, Kp, Gw, ngw, Kn, Kq, S_pad, RB;
 };
 
+// Even RB: rows in PAIRS interleaved in LDS (word k of pair r2 = (W_hat[n0 + 2 r2][k],
+// W_hat[n0 + 2 r2 + 1][k])), so one random-position ds_read_b32 of the rank-order gather
+// serves two rows -- half the gather instructions and their bank conflicts of the 16-bit
+// reads (4.35 conflict cycles per LDS instruction, profiles/r04_pmc_c4_conflict_split.txt).
+template <class DT>
+__device__ __forceinline__ void perm_weight_pairs(const PermArgs& a, const uint32_t* __restrict__ lctab,
+                                                  const int bid) {
+  typedef typename DT::T T;
+  extern __shared__ __attribute__((aligned(16))) uint32_t pw_lds[];  // [RB / 2][Kp] row pairs
+  const T* wscale = (const T*)a.wscale;
+  const T* wsal = (const T*)a.wsal;
+  T* wp = (T*)a.wp;
+  const int RB = a.RB, Kp = a.Kp, n0 = bid * RB, tid = threadIdx.x;
+  const int dw = Kp / 8;  // bpack dwords per codes row
+#pragma unroll 2
+  for (int i = tid; i < (RB / 2) * dw; i += blockDim.x) {
+    const int r2 = i / dw, d = i - r2 * dw, na = n0 + 2 * r2;
+    const int p0 = bpack_pos(d, 0);  // its 8 positions p0 .. p0 + 7 (one group: Gw % 8 == 0)
+    const int g = min(p0 / a.Gw, a.ngw - 1);
+    uint32_t w[8];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int n = na + h;
+      uint32_t c = 0u;
+      float sc = 0.f;
+      if (n < a.N) {
+        c = a.codes[(size_t)n * dw + d];
+        sc = DT::to_f(wscale[(size_t)g * a.Np + n]);
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const T v = n < a.N ? DT::from_f((float)((int)((c >> bpack_shift(e)) & 0xFu) - 8) * sc)
+                            : DT::from_f(0.f);
+        const uint32_t b = (uint32_t)__builtin_bit_cast(uint16_t, v);
+        w[e] = h ? (w[e] | (b << 16)) : b;
+      }
+    }
+    u32x4* dst = (u32x4*)(pw_lds + (size_t)r2 * Kp + p0);
+    dst[0] = u32x4{w[0], w[1], w[2], w[3]};
+    dst[1] = u32x4{w[4], w[5], w[6], w[7]};
+  }
+  __syncthreads();
+  const int W = a.Kq + a.S_pad, nch = W / 8;
+  for (int c = tid; c < nch; c += blockDim.x) {
+    const int j0 = 8 * c;
+    if (j0 < a.Kq) {
+      int pos[8];
+      const u32x4 t0 = ((const u32x4*)(lctab + j0))[0], t1 = ((const u32x4*)(lctab + j0))[1];
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        pos[e] = j0 + e < a.Kn ? (int)((e < 4 ? t0[e] : t1[e - 4]) >> 16) : -1;
+      for (int r2 = 0; r2 < RB / 2; ++r2) {
+        uint32_t v[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = pos[e] >= 0 ? pw_lds[(size_t)r2 * Kp + pos[e]] : 0u;
+        u32x4 lo, hi;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          lo[k] = __builtin_amdgcn_perm(v[2 * k + 1], v[2 * k], 0x05040100u);
+          hi[k] = __builtin_amdgcn_perm(v[2 * k + 1], v[2 * k], 0x07060302u);
+        }
+        *(u32x4*)(wp + (size_t)(n0 + 2 * r2) * W + j0) = lo;
+        *(u32x4*)(wp + (size_t)(n0 + 2 * r2 + 1) * W + j0) = hi;
+      }
+    } else {
+      for (int r = 0; r < RB; ++r) {
+        const int n = n0 + r;
+        u32x4 v = u32x4{0u, 0u, 0u, 0u};
+        if (n < a.N) v = *(const u32x4*)(wsal + (size_t)n * a.S_pad + (j0 - a.Kq));
+        *(u32x4*)(wp + (size_t)n * W + j0) = v;
+      }
+    }
+  }
+}
+
 template <class DT>
 __device__ __forceinline__ void perm_weight_body(const PermArgs& a, const uint32_t* __restrict__ lctab,
                                                  const int bid) {
+  if (a.RB % 2 == 0) {
+    perm_weight_pairs<DT>(a, lctab, bid);
+    return;
+  }
   typedef typename DT::T T;
   extern __shared__ __attribute__((aligned(16))) uint32_t pw_lds[];  // [RB][Kp] D values
   T* wl = (T*)pw_lds;
