@@ -77,10 +77,12 @@ def parse(argv=None):
 
 
 @torch.no_grad()
-def run_windows(model, ids, seq, n):
-    """Evaluator loop (run_experiments.py:86-123): returns (ppl, seconds for n windows)."""
+def run_windows(model, ids, seq, n, warm=1):
+    """Evaluator loop (run_experiments.py:86-123): returns (ppl, seconds for n windows) after
+    `warm` untimed windows (kernel selection, allocator, the clock the chip settles at)."""
     nlls = []
-    model(ids[:, :seq])  # warm-up window (kernel selection, allocator)
+    for _ in range(warm):
+        model(ids[:, :seq])
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(n):
