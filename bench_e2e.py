@@ -77,12 +77,17 @@ def parse(argv=None):
 
 
 @torch.no_grad()
-def run_windows(model, ids, seq, n, warm=1):
+def run_windows(model, ids, seq, n, warm=1, warm_s=0.0):
     """Evaluator loop (run_experiments.py:86-123): returns (ppl, seconds for n windows) after
-    `warm` untimed windows (kernel selection, allocator, the clock the chip settles at)."""
+    `warm` untimed windows, and more until `warm_s` seconds have passed (kernel selection,
+    allocator, the clock the chip settles at)."""
     nlls = []
-    for _ in range(warm):
+    t_w = time.perf_counter()
+    k = 0
+    while k < warm or time.perf_counter() - t_w < warm_s:
         model(ids[:, :seq])
+        torch.cuda.synchronize()
+        k += 1
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(n):
