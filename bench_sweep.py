@@ -84,6 +84,11 @@ def main():
                 rows.append(row)
                 del model
                 torch.cuda.empty_cache()
+    # the fp16 model timed again after the quantized runs, the faster of the two reported: its
+    # first timing in a process runs ~1.8x slow even after seconds of warm-up windows (the same
+    # is seen in bench_e2e's first unquantized round, whose best-of-rounds hides it)
+    _, dt16b = bench_e2e.run_windows(base, ids, args.seq, args.windows)
+    dt16 = min(dt16, dt16b)
     print(json.dumps({"metric": "Llama-2-7B W4A4/W4A8 sweep (config 5), 1 GPU",
                       "fp16_tokens_per_s": round(tokens / dt16, 1), "ppl_fp16": round(ppl16, 4),
                       "combinations": len(rows), "layers": cfg.num_hidden_layers,
