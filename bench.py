@@ -26,6 +26,13 @@ Also printed in the same JSON line:
   llama_layer   BASELINE config 4's workload: one Llama-2-7B decoder layer's 7 linears at
                 2048 tokens (G=64, 5 % salient), W4A4 vs unquantized fp16 F.linear, per
                 linear and in total (measured after the timed region)
+  per_token     the same layer with per_token 4-bit activations (the FP8 GEMM)
+  fp32          the same layer in fp32 (config 3's dtype): step, h2d GEMM, fraction of the
+                three-product f16 floor, counter traffic of the same library
+  e2e           the metric's Llama-2-7B W4A4 tokens/s (bench_e2e.run: 32 layers, random-init
+                fp16 weights, 8 x 2048-token windows, batch 1) next to unquantized fp16, the
+                reference fake-quant forward on the GPU, PPL deltas, and the torch-CPU fp32
+                baseline (extrapolated from 1 and 2 layers, cores stated)
 Secondary measurements (GEMM alone, prepass, vendor dense GEMM, reference fake-quant on
 the GPU) run BEFORE the W warm-up steps, followed by --settle-ms (default 300) of untimed
 steps, so the timed region starts on a chip that holds the clock it settles at under this
@@ -72,7 +79,9 @@ def parse(argv=None):
                          "runs on the f16 MFMA as sqmp_gemm_h2)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--no-layer", action="store_true",
-                    help="skip the secondary lines (per_token, llama_layer)")
+                    help="skip the secondary lines (per_token, llama_layer, fp32, e2e)")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end Llama-2-7B leg")
+    ap.add_argument("--e2e-windows", type=int, default=8)
     ap.add_argument("--rehearsal", action="store_true",
                     help="CPU/gloo rehearsal of the launcher and timing path (no GPU): the "
                          "step is the CPU fake-quant layer on a 64-row batch")
@@ -191,6 +200,12 @@ def cpu_model() -> str:
     return "unknown"
 
 
+CORES_NOTE = ("cores = the torch intra-op threads used = this job's CPU share on the GPU box "
+              "(the lease sets OMP_NUM_THREADS=16 and its rules size worker pools to that share: "
+              "os.cpu_count() / the process affinity show the whole shared machine, whose other "
+              "CPUs serve other jobs), so the baseline runs on every core the job may use")
+
+
 def cpu_baseline(act, rows=M, runs=3):
     """The reference's fake-quant layer on PyTorch-CPU (oracle/torch_cpu.py, pinned
     bit-exact to the reference goldens), fp32 as in the reference's CPU scripts, every
@@ -218,9 +233,7 @@ def cpu_baseline(act, rows=M, runs=3):
         "host_cpu_count": os.cpu_count(),
         "process_affinity_cpus": affinity,
         "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS"),
-        "cores_note": ("cores = the torch intra-op threads used (OMP_NUM_THREADS, set by the GPU "
-                       "box to this job's CPU share); host_cpu_count / process_affinity_cpus are "
-                       "the machine's and the process's CPU counts"),
+        "cores_note": CORES_NOTE,
         "kind": "torch-cpu-fp32",
         "cpu_model": cpu_model(),
         "sample": (f"oracle/torch_cpu.py CPUFakeQuantLinear (the reference's fake_quant ops, "
@@ -404,6 +417,88 @@ def per_token_leg(dev, iters=200):
         "prepass_avg_ms": round(quant_ms, 4),
         "note": "HIP events, 200 back-to-back calls each after 20 warm-up; frac = GEMM "
                 "achieved / dense peak of the kernel's MFMA dtype (FP8 5033 TFLOP/s)",
+    }
+
+
+def fp32_leg(dev, iters=100):
+    """BASELINE config 3's dtype (the reference runs OPT in fp32, run_experiments.py:152-154) on
+    the config-2 layer: W4A4Linear.forward in fp32 (the quantizer writes the two f16 planes,
+    sqmp_gemm_h2d runs 3 f16 MFMAs per product); step and GEMM timed with HIP events on the
+    launch stream.  floor_frac = the three-product f16 floor (3 x 2MN(Kp + S_pad) / P_f16) /
+    GEMM time; traffic from the committed counter profile of the same library."""
+    from smoothquant import ops
+    q, x, lin = make_layer(dev, "per_group", seed=777, dtype=torch.float32)
+    pw = q.packed()
+    stream = torch.cuda.current_stream(dev)
+    flops = 2.0 * M * N * K
+    if not ops.h2_planes_ok(pw, "per_group", M, G):
+        return {"note": "the fp32 planes path does not take this layer"}
+    a2 = ops.quant_act_fp(x, pw, "per_group", 4, G, h2=True)
+    gemm = lambda: ops.gemm_h2_planes(a2, pw, lin.bias)  # noqa: E731
+    step = lambda: q(x)  # noqa: E731
+    for fn in (gemm, step):
+        for _ in range(10):
+            fn()
+    gemm_ms = time_events(gemm, iters, stream)
+    step_ms = time_events(step, iters, stream)
+    floor_s = 3 * 2.0 * M * N * (pw.Kp + pw.S_pad) / (PEAK_TFLOPS["f16"] * 1e12)
+    traffic, tprof = pick_traffic("pmc_gemm_h2d_fp32.json", gemm_ms * 1e3)
+    alg = M * (pw.Kp + pw.S_pad) * 4 + N * (pw.Kp + pw.S_pad) * 4 + M * N * 4
+    return {
+        "workload": "the config-2 layer in fp32 (weight per_group(sorted) int4 + act per_group "
+                    "4-bit, 10% salient), the reference's OPT dtype",
+        "kernel": "sqmp::h2d::gemm_h2d_kernel (row-scaled two-piece fp16 planes, 3 f16 MFMAs "
+                  "per product, fp32 accumulation)",
+        "ms_per_step": round(step_ms, 4),
+        "TFLOP_per_s": round(flops / (step_ms * 1e-3) / 1e12, 1),
+        "gemm_avg_ms": round(gemm_ms, 4),
+        "gemm_TFLOP_per_s": round(flops / (gemm_ms * 1e-3) / 1e12, 1),
+        "floor_frac": round(floor_s / (gemm_ms * 1e-3), 4),
+        "three_product_floor_ms": round(floor_s * 1e3, 4),
+        "algorithmic_bytes": alg,
+        "traffic": traffic,
+        "traffic_over_algorithmic": None if not traffic else round(traffic / alg, 2),
+        "traffic_profile": tprof,
+        "note": "HIP events, 100 back-to-back calls each after 10 warm-up",
+    }
+
+
+def e2e_leg(windows=8, cpu=True):
+    """BASELINE config 4 end to end (the metric's Llama-2-7B W4A4 tokens/s): bench_e2e.run on
+    the Llama-2-7B architecture with random-init fp16 weights on the device, G=64, 5 % salient,
+    per_group(sorted) weights and activations (quantize_llama_like), batch 1, `windows` windows
+    of 2048 tokens (the reference's Evaluator, run_experiments.py:86-123): W4A4, unquantized
+    fp16, the reference's fake-quant forward restated in PyTorch ops on the GPU (fp16 GEMM and
+    fp32 GEMM: the PPL noise of its own accumulation order), and the torch-CPU fp32 baseline
+    extrapolated from 1 and 2 decoder layers."""
+    import bench_e2e
+    args = bench_e2e.parse(["--model", "llama2-7b", "--windows", str(windows), "--rounds", "2"]
+                           + ([] if cpu else ["--no-cpu"]))
+    r = bench_e2e.run(args)
+    torch.cuda.empty_cache()
+    cpu = r.get("cpu_baseline")
+    if cpu is not None:
+        cpu = dict(cpu, cores_note=CORES_NOTE)
+    return {
+        "workload": (f"Llama-2-7B prefill (32 layers, random-init fp16 weights on the device), "
+                     f"W4A4 G={r['config']['group_size']}, {int(r['config']['salient_prop'] * 100)}% "
+                     f"salient, per_group(sorted) W and A (quantize_llama_like), batch 1, "
+                     f"{windows} x {r['config']['seq_len']}-token windows"),
+        "w4a4_tokens_per_s": r["value"],
+        "fp16_tokens_per_s": r["unquantized_tokens_per_s"],
+        "w4a4_over_fp16": r["w4a4_over_unquantized"],
+        "reference_fakequant_gpu_tokens_per_s": r.get("reference_fakequant_tokens_per_s"),
+        "speedup_vs_reference_fakequant": r.get("speedup_vs_reference_fakequant"),
+        "ppl_w4a4": r["ppl_w4a4"], "ppl_fp16": r["ppl_unquantized"],
+        "ppl_delta_vs_fp16": round(r["ppl_w4a4"] - r["ppl_unquantized"], 4),
+        "ppl_reference_fakequant": r.get("ppl_reference_fakequant"),
+        "ppl_delta_vs_reference": r.get("ppl_delta_vs_reference"),
+        "reference_gemm_order_noise": r.get("reference_gemm_order_noise"),
+        "cpu_baseline": cpu,
+        "setup_s": r.get("setup_s"),
+        "note": "PPL of a random-init model (~ vocab size): only differences mean anything; the "
+                "W4A4 delta vs the reference fake-quant reads against the reference's own "
+                "fp16-vs-fp32-GEMM difference (reference_gemm_order_noise)",
     }
 
 
@@ -647,6 +742,9 @@ def main(argv=None):
         out["per_token"] = per_token_leg(dev)
     if not fp32 and not args.no_layer:
         out["llama_layer"] = llama_layer(dev)
+        out["fp32"] = fp32_leg(dev)
+    if not fp32 and not args.no_layer and not args.no_e2e and world == 1:
+        out["e2e"] = e2e_leg(args.e2e_windows, cpu=rank == 0 and not args.no_cpu)
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(args.act)
     if rank == 0:

@@ -209,7 +209,13 @@ def swap_reference(model, accum32):
 
 
 def main(argv=None):
-    args = parse(argv)
+    out = run(parse(argv))
+    print(json.dumps(out), flush=True)
+    return out
+
+
+def run(args):
+    """The measurements of the module docstring for parsed `args`; returns the JSON dict."""
     from functools import partial
 
     from smoothquant import fake_quant as FQ
@@ -297,7 +303,6 @@ def main(argv=None):
         cpu = cpu_baseline(args, G)
         cpu["w4a4_gpu_over_cpu"] = round(out["value"] / cpu["tokens_per_s"], 1)
         out["cpu_baseline"] = cpu
-    print(json.dumps(out), flush=True)
     return out
 
 

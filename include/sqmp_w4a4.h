@@ -186,6 +186,10 @@ int sqmp_quant_act(void* x, int dtype, int M, int K, int amode, int n_bits,
                                  stage (codes [R][Kq/2] as [R/64][Kq/64][64][4][2] dwords,
                                  scales [R/64][ngq][32][2], xs [R][S_pad] as
                                  [R/64][S_pad/64][64][4][2][8]), R = roundup(M, 256) */
+#define SQMP_QA_WPT 64        /* sqmp_quant_act_c4: the permuted weight written in sqmp_gemm_fqa's
+                                 tile-major register layout (sqmp_fqa_wpt_elems elements: rows
+                                 roundup(N, 512), zeros past N) with the activation operands
+                                 row-major (exclusive with the TILED flags) */
 
 /* sqmp_quant_act with the per-weight map posmap (int32 [K]: packed position of column k,
  * the inverse of perm; NULL = derive it per call) and flags.  With posmap, OUT_FP on
@@ -335,6 +339,25 @@ int sqmp_gemm_fqt7j(const void* codes_t, const void* scale_t, const void* sal_t,
 int sqmp_gemm_fqt8(const void* codes_t, const void* scale_t, const void* sal_t, const void* wp,
                    const void* bias, void* y, int dtype, int M, int N, int Kq, int S_pad, int G,
                    int ngq, uint32_t* colmax, void* stream);
+
+/* The activation-order GEMM with the int4 act codes decoded once per workgroup into an LDS
+ * tile and the permuted weight in registers (128 tokens x 512 weight rows per workgroup):
+ * y[M][N] = D(x_hat . W_hat^T + bias) on sqmp_quant_act_c4's ROW-MAJOR activation operands
+ * (acodes [R][Kq/2] bytes, ascale D [ngq][ldsc], xs D [R][S_pad], R >= roundup(M, 128) rows,
+ * ldsc >= roundup(M, 128)) and the SQMP_QA_WPT weight (wpt).  The same products as
+ * sqmp_gemm_fqt7 up to the fp32 accumulation order.  Kq % 64 == 0, S_pad % 64 == 0, G a power
+ * of two >= 64, N % 8 == 0, fp16 / bf16; colmax NULL: no fused column statistics.
+ * Kq = 0: the dense GEMM y = xs . wpt^T (acodes / ascale unused; the dense-core measurement). */
+int sqmp_gemm_fqa(const void* acodes, const void* ascale, const void* xs, const void* wpt,
+                  const void* bias, void* y, int dtype, int M, int N, int Kq, int S_pad, int G,
+                  int ldsc, uint32_t* colmax, void* stream);
+
+/* Elements of sqmp_gemm_fqa's weight operand: roundup(N, 512) * (Kq + S_pad). */
+size_t sqmp_fqa_wpt_elems(int N, int Kq, int S_pad);
+
+/* A dense D [N][L] matrix (L % 64 == 0) in sqmp_gemm_fqa's weight layout (wpt of
+ * sqmp_fqa_wpt_elems(N, L, 0) elements). */
+int sqmp_pack_wpt(const void* w, int dtype, int N, int L, void* wpt, void* stream);
 
 /* The activation-order GEMM on SQMP_QA_TILED32 operands at ONE wave per SIMD on the 32x32x16
  * MFMA (256 weight rows x 256 tokens per tile, each wave 256 rows x 64 tokens with 256 fp32

@@ -1496,7 +1496,11 @@ static int quant_act_impl(void* x, int dtype, int M, int K, int amode, int n_bit
   if (n_bits < 2 || n_bits > 8) return SQMP_EUNSUPPORTED;
   if (S < 0 || S > K || !x || !amap || (K - S > 0 && !nonsal)) return SQMP_EINVAL;
   if (flags & ~(SQMP_QA_CLEAN_WS | SQMP_QA_REUSE_STATS | SQMP_QA_STATS_GIVEN | SQMP_QA_TILED |
-                SQMP_QA_TILED4 | SQMP_QA_TILED32))
+                SQMP_QA_TILED4 | SQMP_QA_TILED32 | SQMP_QA_WPT))
+    return SQMP_EINVAL;
+  // the fqa weight layout goes with the row-major activation operands, and needs the weight
+  if ((flags & SQMP_QA_WPT) &&
+      (!cw || (flags & (SQMP_QA_TILED | SQMP_QA_TILED4 | SQMP_QA_TILED32))))
     return SQMP_EINVAL;
   if ((flags & (SQMP_QA_TILED | SQMP_QA_TILED4 | SQMP_QA_TILED32)) && out_kind != SQMP_OUT_C4)
     return SQMP_EINVAL;
@@ -1795,7 +1799,7 @@ extern "C" int sqmp_quant_act_c4(void* x, int dtype, int M, int K, int amode, in
   if (!codes || !wscale || !wp || (S > 0 && !wsal) || N <= 0 || Gw <= 0 || ngw <= 0)
     return SQMP_EINVAL;
   if (Gw % 8 || Kp > 32768) return SQMP_EUNSUPPORTED;
-  const C4Weight cw{codes, wscale, wsal, wp, N, Kp, Gw, ngw};
+  const C4Weight cw{codes, wscale, wsal, wp, N, Kp, Gw, ngw, (flags & SQMP_QA_WPT) ? 1 : 0};
   return quant_act_impl(x, dtype, M, K, amode, n_bits, group_size, amap, Kp, nonsal, salient, S,
                         S_pad, posmap, flags, SQMP_OUT_C4, acodes, ascale, xs, workspace,
                         ws_bytes, stream, &cw);

@@ -632,9 +632,21 @@ struct PermArgs {
   const uint32_t* codes;  // bpack [Np][Kp/2]
   const void* wscale;     // D [ngw][Np]
   const void* wsal;       // D [N][S_pad]
-  void* wp;               // D [Np][Kq + S_pad]
+  void* wp;               // D [Np][Kq + S_pad], or (wpt) sqmp_gemm_fqa's tile-major layout
   int N, Np, Kp, Gw, ngw, Kn, Kq, S_pad, RB;
+  int wpt;                // 1: wp[n][j0 .. j0 + 7] at fqa_wpt_off(n, j0) (rows roundup(N, 512))
 };
+
+// the 16-B chunk of wp row n at position j0 (j0 % 8 == 0): row-major, or sqmp_gemm_fqa's
+// [n / 64][j0 / 64][(n / 16) % 4][(j0 / 32) % 2][lane = 16 ((j0 / 8) % 4) + n % 16][8]
+template <class T>
+__device__ __forceinline__ T* wp_chunk(const PermArgs& a, T* wp, int n, int j0) {
+  const int W = a.Kq + a.S_pad;
+  if (!a.wpt) return wp + (size_t)n * W + j0;
+  const size_t f = (((size_t)(n >> 6) * (W >> 6) + (j0 >> 6)) * 8 + ((n >> 4) & 3) * 2 + ((j0 >> 5) & 1)) * 64 +
+                   ((j0 >> 3) & 3) * 16 + (n & 15);
+  return wp + f * 8;
+}
 
 // Even RB: rows in PAIRS interleaved in LDS (word k of pair r2 = (W_hat[n0 + 2 r2][k],
 // W_hat[n0 + 2 r2 + 1][k])), so one random-position ds_read_b32 of the rank-order gather
@@ -697,15 +709,15 @@ __device__ __forceinline__ void perm_weight_pairs(const PermArgs& a, const uint3
           lo[k] = __builtin_amdgcn_perm(v[2 * k + 1], v[2 * k], 0x05040100u);
           hi[k] = __builtin_amdgcn_perm(v[2 * k + 1], v[2 * k], 0x07060302u);
         }
-        *(u32x4*)(wp + (size_t)(n0 + 2 * r2) * W + j0) = lo;
-        *(u32x4*)(wp + (size_t)(n0 + 2 * r2 + 1) * W + j0) = hi;
+        *(u32x4*)wp_chunk(a, wp, n0 + 2 * r2, j0) = lo;
+        *(u32x4*)wp_chunk(a, wp, n0 + 2 * r2 + 1, j0) = hi;
       }
     } else {
       for (int r = 0; r < RB; ++r) {
         const int n = n0 + r;
         u32x4 v = u32x4{0u, 0u, 0u, 0u};
         if (n < a.N) v = *(const u32x4*)(wsal + (size_t)n * a.S_pad + (j0 - a.Kq));
-        *(u32x4*)(wp + (size_t)n * W + j0) = v;
+        *(u32x4*)wp_chunk(a, wp, n, j0) = v;
       }
     }
   }
@@ -759,14 +771,14 @@ __device__ __forceinline__ void perm_weight_body(const PermArgs& a, const uint32
         T v[8];
 #pragma unroll
         for (int e = 0; e < 8; ++e) v[e] = pos[e] >= 0 ? wl[(size_t)r * Kp + pos[e]] : DT::from_f(0.f);
-        *(u32x4*)(wp + (size_t)(n0 + r) * W + j0) = *(const u32x4*)v;
+        *(u32x4*)wp_chunk(a, wp, n0 + r, j0) = *(const u32x4*)v;
       }
     } else {
       for (int r = 0; r < RB; ++r) {
         const int n = n0 + r;
         u32x4 v = u32x4{0u, 0u, 0u, 0u};
         if (n < a.N) v = *(const u32x4*)(wsal + (size_t)n * a.S_pad + (j0 - a.Kq));
-        *(u32x4*)(wp + (size_t)n * W + j0) = v;
+        *(u32x4*)wp_chunk(a, wp, n, j0) = v;
       }
     }
   }
@@ -926,7 +938,7 @@ int launch_perm_weight_c4(int dtype, const uint32_t* lctab, const void* codes,
                           int Kn, int S_pad, void* wp, hipStream_t s) {
   const int Np = pad_n(N), RB = pw_rows(Kp);
   const int Kq = (int)round_up(Kn, 64);
-  PermArgs pa{(const uint32_t*)codes, wscale, wsal, wp, N, Np, Kp, Gw, ngw, Kn, Kq, S_pad, RB};
+  PermArgs pa{(const uint32_t*)codes, wscale, wsal, wp, N, Np, Kp, Gw, ngw, Kn, Kq, S_pad, RB, 0};
   const size_t lds = (size_t)RB * Kp * 2;
   const dim3 grid((unsigned)(Np / RB));
   if (dtype == SQMP_F16) {
@@ -968,7 +980,10 @@ int launch_quant_lc_c4(int dtype, const void* x, int M, int K, int q_max, int G,
   const int nw = lc_waves(K, Kn);
   const int Np = pad_n(cw->N), RB = pw_rows(cw->Kp);
   PermArgs pa{(const uint32_t*)cw->codes, cw->wscale, cw->wsal, cw->wp, cw->N, Np, cw->Kp,
-              cw->Gw, cw->ngw, Kn, Kq, S_pad, RB};
+              cw->Gw, cw->ngw, Kn, Kq, S_pad, RB, cw->wpt};
+  // the permutation's rows: pad_n(N), or roundup(N, 512) for sqmp_gemm_fqa's layout (rows
+  // past N hold zeros)
+  const int Nrows = cw->wpt ? (int)round_up(cw->N, 512) : Np;
   const size_t lq = sizeof(uint32_t) * (size_t)(P + S_pad + 8), lp = (size_t)RB * cw->Kp * 2;
   const size_t lds = lq > lp ? lq : lp;
   const void* kf = dtype == SQMP_BF16 ? (const void*)quant_c4_fused_kernel<BF16>
@@ -980,7 +995,7 @@ int launch_quant_lc_c4(int dtype, const void* x, int M, int K, int q_max, int G,
   const int q_env = qe ? atoi(qe) : 0;
   const int qpc = q_env > 0 ? q_env : (per_cu > 2 ? per_cu - 2 : 1);
   const int nq = lc_grid((M + 1) / 2, qpc < per_cu ? qpc : per_cu);
-  const dim3 grid(nq + Np / RB), block(64 * nw);
+  const dim3 grid(nq + Nrows / RB), block(64 * nw);
   if (dtype == SQMP_F16) {
     SQMP_HIP_CHECK(hipFuncSetAttribute((const void*)quant_c4_fused_kernel<F16>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));

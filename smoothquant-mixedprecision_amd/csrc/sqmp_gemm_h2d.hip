@@ -352,6 +352,8 @@ extern "C" int sqmp_gemm_h2d(const void* a2, int ldr, const int* aexp, const voi
   const size_t a_plane = (size_t)ldr * L;
   // (32-bit buffer offsets: both planes of the tile rows within 4 GiB)
   if ((size_t)2 * a_plane * 2 >= (1ull << 32)) return SQMP_EINVAL;
+  // ... and the weight planes (sqmp_pack_h2d: 2 planes of roundup(N, 256) rows x L halves)
+  if ((size_t)4 * (size_t)round_up(N, 256) * (size_t)L >= (1ull << 32)) return SQMP_EUNSUPPORTED;
 #define SQMP_H2D(CM)                                                                            \
   if (tm == 128) SQMP_H2D_TM(CM, 128); else SQMP_H2D_TM(CM, 64)
 #define SQMP_H2D_TM(CM, TMV)                                                                    \

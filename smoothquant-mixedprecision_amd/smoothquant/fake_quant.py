@@ -520,7 +520,7 @@ class W4A4Linear(nn.Module):
                    and ops.f8_input_ok(xc))
         # fp32 layers: the quantizer writes sqmp_gemm_h2d's two f16 planes itself
         use_h2 = (not use_f8 and not use_i8 and not use_fqt and self.kernel == "auto"
-                  and ops.h2_planes_ok(pw, amode, x2.shape[0]))
+                  and ops.h2_planes_ok(pw, amode, x2.shape[0], ag))
         if use_f8:
             a8, sa, xs = ops.quant_act_f8(xc, pw, amode, bits)
         elif use_i8:
@@ -543,7 +543,8 @@ class W4A4Linear(nn.Module):
         fuse = (ospec is not None and ospec[0] in ("per_group", "per_tensor") and _OQ_FUSE
                 and not use_i8
                 and (not use_f8 or ops.f8_colmax_ok(pw))       # the 16x16x128 FP8 kernel
-                and (not use_fqt or c4[1].dim() == 3)          # the tile-major fqt7 GEMM
+                and (not use_fqt or c4[1].dim() == 3           # the tile-major fqt7 GEMM
+                     or c4[3].dim() == 3)                        # or the fqa GEMM
                 and (self.salient_indices is None or pw.K - pw.S > 0))
         colmax = ops.out_quant_workspace(x2.shape[0], pw.N, x2.device)["buf"] if fuse else None
         if use_f8:
@@ -631,6 +632,16 @@ class SiblingGroup:
     def _key(x):
         return (x.data_ptr(), tuple(x.shape), tuple(x.stride()), x.dtype, x._version)
 
+    @staticmethod
+    def _sig(m):
+        """What a member's output depends on besides its input: the resolved act / output
+        quantizers (a caller may rebind them, e.g. the reference's W4A8 idiom), the kernel
+        choice and the bias; the packed weight is compared by identity (packed() returns a new
+        PackedWeight whenever a buffer was replaced or written in place)."""
+        b = m.bias
+        return (m.kernel, resolve_quantizer(m.act_quant), resolve_quantizer(m.output_quant),
+                None if b is None else (b.data_ptr(), b._version, b.dtype))
+
     def _plan(self, x2):
         """(packed weights, biases, (mode, bits, group_size)) when the grouped kernels cover
         every member for this input, else None."""
@@ -661,7 +672,10 @@ class SiblingGroup:
         i = self.members.index(member)
         key = self._key(x)
         e = self._stash.pop(i, None)
-        if e is not None and e[0]() is x and e[1] == key:
+        # a stashed output only while the input AND everything the member's forward reads are
+        # unchanged since the group ran (a rebound quantizer, a new weight: computed again)
+        if (e is not None and e[0]() is x and e[1] == key and e[3] == self._sig(member)
+                and member.packed() is e[4]):
             return e[2]
         plan = self._plan(x2)
         if plan is None:
@@ -672,7 +686,8 @@ class SiblingGroup:
         if x.dim() == 3:
             ys = [y.view(x.shape[0], x.shape[1], -1) for y in ys]
         ref = weakref.ref(x)
-        self._stash = {j: (ref, key, y) for j, y in enumerate(ys) if j != i}
+        self._stash = {j: (ref, key, y, self._sig(self.members[j]), pws[j])
+                       for j, y in enumerate(ys) if j != i}
         return ys[i]
 
 

@@ -420,7 +420,11 @@ def group_eligible(pws, act_quant: str, act_bits: int, group_size: int, M: int) 
     group, 4 (Kp + S_pad + 8) bytes of quantizer LDS per member within 150 KiB, one K
     (<= 16384, % 8 == 0) / Kp / S_pad / group geometry / salient set / dtype
     (fp16 / bf16) for all, 2 or 3 layers."""
-    if not 2 <= len(pws) <= 3 or act_quant not in _SORTED or act_bits > 8:
+    # (mirrors what sqmp_quant_act_group / sqmp_gemm_fq7_group accept, so that a refusal
+    # never reaches the library: a non-empty batch, 2..8-bit codes, J = 2 tiles)
+    if not 2 <= len(pws) <= 3 or act_quant not in _SORTED or not 2 <= act_bits <= 8:
+        return False
+    if M <= 0 or FQ7_J != 2:
         return False
     if not 16 <= group_size <= 1024 or group_size & (group_size - 1):
         return False
@@ -460,6 +464,9 @@ FQT8 = os.environ.get("SQMP_FQT8", "0") == "1"
 # the one-wave-per-SIMD activation-order GEMM on the 32x32x16 MFMA (sqmp_gemm_fqt9) on the
 # SQMP_QA_TILED32 operands
 FQT9 = os.environ.get("SQMP_FQT9", "0") == "1"
+# the activation-order GEMM with the act codes decoded once per workgroup into LDS and the
+# permuted weight in registers (sqmp_gemm_fqa on the row-major act operands + SQMP_QA_WPT)
+FQA = os.environ.get("SQMP_FQA", "0") == "1"
 
 
 def _fqt_j() -> int:
@@ -499,7 +506,8 @@ def quant_act_c4(x2: torch.Tensor, pw: PackedWeight, act_quant: str, n_bits: int
     Kq = (Kn + 63) // 64 * 64
     ngq = (Kn + group_size - 1) // group_size
     dev = x2.device
-    tiled = FQT7 and Kq % 128 == 0
+    fqa = FQA
+    tiled = FQT7 and Kq % 128 == 0 and not fqa
     tj = _fqt_j()
     t32 = tiled and FQT9
     if t32:
@@ -531,7 +539,14 @@ def quant_act_c4(x2: torch.Tensor, pw: PackedWeight, act_quant: str, n_bits: int
         flags |= _lib.QA_REUSE_STATS
     if pw.posmap is None:
         pw.posmap = build_posmap(pw.perm, K)
-    wp = torch.empty((pad_n(pw.N), Kq + pw.S_pad), dtype=pw.dtype, device=dev)
+    if fqa:
+        # sqmp_gemm_fqa's tile-major weight: [roundup(N, 512) / 64][(Kq + S_pad) / 64][4096]
+        # (3-d marks the layout)
+        nt_rows = (pw.N + 511) // 512 * 512
+        wp = torch.empty((nt_rows // 64, (Kq + pw.S_pad) // 64, 4096), dtype=pw.dtype, device=dev)
+        flags |= _lib.QA_WPT
+    else:
+        wp = torch.empty((pad_n(pw.N), Kq + pw.S_pad), dtype=pw.dtype, device=dev)
     # one call: quantizer + weight permutation in the same launch
     status = lib.sqmp_quant_act_c4(_p(x2), _dtype_code(x2.dtype), M, K, ACT_MODES[act_quant],
                                    n_bits, group_size, _p(pw.amap), pw.Kp, _p(pw.nonsal),
@@ -556,6 +571,12 @@ def gemm_fqt(codes: torch.Tensor, scales: torch.Tensor, xs: torch.Tensor, wp: to
     M = xs.shape[0]
     y = torch.empty((M, pw.N), dtype=pw.dtype, device=codes.device)
     Kq = codes.shape[1] * 2
+    if wp.dim() == 3:       # SQMP_QA_WPT: sqmp_gemm_fqa on the row-major act operands
+        check(load().sqmp_gemm_fqa(_p(codes), _p(scales), _p(xs) if pw.S_pad else None, _p(wp),
+                                   _p(bias), _p(y), _dtype_code(pw.dtype), M, pw.N, Kq,
+                                   pw.S_pad, group_size, scales.shape[1], _p(colmax),
+                                   _stream(codes)), "gemm_fqa")
+        return y
     if scales.dim() == 4:   # SQMP_QA_TILED32
         if colmax is not None:
             raise ValueError("gemm_fqt: the TILED32 GEMM has no fused column statistics")
@@ -725,18 +746,30 @@ def h2d_operand(pw: PackedWeight) -> torch.Tensor:
     return pw.h2d
 
 
-def _h2d_rows_ok(M: int, L: int) -> bool:
-    """sqmp_gemm_h2d addresses both activation planes with 32-bit buffer offsets."""
-    return 4 * ((M + 127) // 128 * 128) * L < (1 << 32)
+def _h2d_rows_ok(M: int, L: int, N: int = 0) -> bool:
+    """sqmp_gemm_h2d addresses both activation planes, and both weight planes (roundup(N, 256)
+    rows), with 32-bit buffer offsets."""
+    return (4 * ((M + 127) // 128 * 128) * L < (1 << 32)
+            and 4 * ((N + 255) // 256 * 256) * L < (1 << 32))
 
 
-def h2_planes_ok(pw: PackedWeight, act_quant: str, M: int = 0) -> bool:
+_LC_OFF = os.environ.get("SQMP_DISABLE_LC") is not None  # (the library reads it once too)
+
+
+def h2_planes_ok(pw: PackedWeight, act_quant: str, M: int = 0, group_size: int = 0) -> bool:
     """Whether an fp32 layer's forward runs quantizer -> planes -> sqmp_gemm_h2d
-    (quant_act_fp(h2=True) + gemm_h2_planes) instead of the fp32 operand + split."""
+    (quant_act_fp(h2=True) + gemm_h2_planes) instead of the fp32 operand + split: every
+    condition under which the SQMP_OUT_H2 quantizer (sqmp_actquant.hip, the fp32 wave kernels)
+    and sqmp_gemm_h2d accept the call -- a non-empty batch, the lane-contiguous pipeline on,
+    the per-wave row buffer (4 K bytes + 12 bytes per act group) within 160 KiB, 32-bit
+    plane offsets."""
     L = pw.Kp + pw.S_pad
+    Kn = pw.K - pw.S
+    ngroups = (Kn + group_size - 1) // group_size if act_quant.startswith("per_group") and group_size > 0 else 1
+    wb = (4 * pw.K + 15) // 16 * 16 + (12 * ngroups + 15) // 16 * 16
     return (pw.dtype == torch.float32 and H2D and F32_GEMM == "h2" and L % 64 == 0
-            and pw.N % 4 == 0 and pw.K % 8 == 0 and pw.K - pw.S > 0
-            and act_quant != "per_tensor" and _h2d_rows_ok(M, L))
+            and pw.N % 4 == 0 and pw.K % 8 == 0 and Kn > 0 and M > 0 and not _LC_OFF
+            and wb <= 160 * 1024 and act_quant != "per_tensor" and _h2d_rows_ok(M, L, pw.N))
 
 
 def gemm_h2_planes(a2, pw: PackedWeight, bias: Optional[torch.Tensor],
@@ -765,7 +798,7 @@ def gemm_h2(a: torch.Tensor, pw: PackedWeight, bias: Optional[torch.Tensor],
         raise ValueError("gemm_h2: A must be fp32 [M, Kp + S_pad] with row stride Kp + S_pad")
     planes, bexp = h2_operand(pw)
     lib = load()
-    if H2D and L % 64 == 0 and pw.N % 4 == 0 and M > 0 and _h2d_rows_ok(M, L):
+    if H2D and L % 64 == 0 and pw.N % 4 == 0 and M > 0 and _h2d_rows_ok(M, L, pw.N):
         wt = h2d_operand(pw)
         ldr = (M + 127) // 128 * 128
         a2 = torch.empty((2, ldr, L), dtype=torch.float16, device=a.device)

@@ -128,3 +128,62 @@ def test_group_falls_back_when_not_covered():
     assert layers[0].__dict__["_sqmp_group"]._plan(x) is None
     for q, r in zip(layers, alone):
         assert torch.equal(_bits(q(x)), _bits(r))
+
+
+def test_stash_not_returned_after_member_changes():
+    """after q_proj ran the group on x, rebinding k_proj's act quantizer
+    (the reference's W4A8 idiom, fake_quant.py:246-263 partials), its output quantizer or its
+    weight makes k_proj compute its own output -- never the stashed one."""
+    dev = _dev()
+    from functools import partial
+
+    from smoothquant import fake_quant as fq
+    layers, x = _siblings(dev, 256, 1024, (512, 512, 512), 64, 0.05, torch.float16, seed=11)
+    fq.link_siblings(*layers)
+    # (1) k's act quantizer rebound to 8 bits after q's call
+    layers[0](x)
+    layers[1].act_quant = partial(fq.quantize_activation_per_group_absmax_sort, n_bits=8,
+                                  group_size=64)
+    y1 = layers[1](x)
+    for m in layers:
+        m.__dict__.pop("_sqmp_group")
+    assert torch.equal(_bits(y1), _bits(layers[1](x)))
+    # (2) v's weight replaced after q's call
+    layers2, x2 = _siblings(dev, 256, 1024, (512, 512, 512), 64, 0.05, torch.float16, seed=12)
+    fq.link_siblings(*layers2)
+    layers2[0](x2)
+    layers2[2].weight = torch.randn(512, 1024, device=dev, dtype=torch.float16) * 0.02
+    y2 = layers2[2](x2)
+    for m in layers2:
+        m.__dict__.pop("_sqmp_group")
+    assert torch.equal(_bits(y2), _bits(layers2[2](x2)))
+    # (3) output quantization switched on for k after q's call
+    layers3, x3 = _siblings(dev, 256, 1024, (512, 512, 512), 64, 0.05, torch.float16, seed=13)
+    fq.link_siblings(*layers3)
+    layers3[0](x3)
+    layers3[1].output_quant = layers3[1].act_quant
+    y3 = layers3[1](x3)
+    for m in layers3:
+        m.__dict__.pop("_sqmp_group")
+    assert torch.equal(_bits(y3), _bits(layers3[1](x3)))
+
+
+def test_empty_batch_linked_and_fp32():
+    """an empty batch through linked siblings (group_eligible refuses M == 0, each
+    member computes alone) and through an fp32 layer (h2_planes_ok refuses M == 0) returns an
+    empty output instead of raising."""
+    dev = _dev()
+    from smoothquant import fake_quant as fq
+    from smoothquant import ops
+    layers, x = _siblings(dev, 64, 512, (256, 256), 64, 0.05, torch.float16, seed=14)
+    fq.link_siblings(*layers)
+    x0 = x[:0]
+    assert not ops.group_eligible([q.packed() for q in layers], "per_group", 4, 64, 0)
+    for q in layers:
+        y = q(x0)
+        assert y.shape == (0, 256)
+    lin = torch.nn.Linear(512, 256).to(dev, torch.float32)
+    q32 = fq.W4A4Linear.from_float(lin, weight_quant="per_group", act_quant="per_group",
+                                   importance=torch.rand(512), salient_prop=0.05, group_size=64)
+    y = q32(torch.zeros(0, 512, device=dev))
+    assert y.shape == (0, 256) and y.dtype == torch.float32

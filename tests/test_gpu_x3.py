@@ -250,7 +250,7 @@ def test_quantizer_h2_planes_bit_identical(act, K, M, p):
                    importance=torch.from_numpy(np.abs(x).mean(0)) if p else None,
                    salient_prop=p, group_size=128)
     pw = q.packed()
-    assert ops.h2_planes_ok(pw, act)
+    assert ops.h2_planes_ok(pw, act, M, 128)
     xt = torch.from_numpy(x).to(dev)
     planes, aexp, m = ops.quant_act_fp(xt.clone(), pw, act, 4, 128, h2=True)
     a = ops.quant_act_fp(xt.clone(), pw, act, 4, 128)

@@ -84,7 +84,7 @@ step() {
       timeout -k 10 900 python bench_sweep.py > "$O/sweep.jsonl" 2> "$O/sweep.err" || fail sweep "$O/sweep.err"
       tail -2 "$O/sweep.jsonl" ;;
     layer)
-      timeout -k 10 400 python bench_llama.py > "$O/layer.json" 2> "$O/layer.err" || fail layer "$O/layer.err"
+      timeout -k 10 400 python bench_e2e.py --model llama2-7b > "$O/layer.json" 2> "$O/layer.err" || fail layer "$O/layer.err"
       cat "$O/layer.json" ;;
     profpy:*)
       local rest=${s#profpy:}; local script=${rest%%:*}; local args=""

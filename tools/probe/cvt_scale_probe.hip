@@ -1,0 +1,86 @@
+// Probe: do gfx950's scaled conversions from fp8 (e4m3) / fp6 (e2m3) to f16 compute
+// D(code * scale) with ONE round-to-nearest-even of the exact product for an ARBITRARY f32
+// scale (not only its exponent)?  If so, decoding an int4 activation code to the reference's
+// x_hat = D(code * s) is one instruction per two (fp8) or per 32 (fp6) values.
+// Output: mismatch counts against the host's exact D(c * s) for every c in [-7, 7] over many
+// random f16 scales (normal range, plus tiny and large ones).
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <math.h>
+
+typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+typedef _Float16 h32 __attribute__((ext_vector_type(32)));
+typedef unsigned u6 __attribute__((ext_vector_type(6)));
+
+__global__ void k8(const float* sc, unsigned short* out, int ns) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= ns) return;
+  const float s = sc[i];
+  for (int c = -7; c <= 7; c += 2) {
+    // two codes (c, c + 1) as e4m3 bytes in the low word
+    int w = __builtin_amdgcn_cvt_pk_fp8_f32((float)c, (float)(c + 1), 0, false);
+    h2 r = __builtin_amdgcn_cvt_scalef32_pk_f16_fp8((unsigned)w, s, false);
+    out[i * 16 + (c + 7)] = __builtin_bit_cast(unsigned short, (_Float16)r[0]);
+    if (c + 1 <= 7) out[i * 16 + (c + 8)] = __builtin_bit_cast(unsigned short, (_Float16)r[1]);
+  }
+}
+__global__ void k6(const float* sc, unsigned short* out, int ns) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= ns) return;
+  const float s = sc[i];
+  h32 v;
+  for (int e = 0; e < 32; ++e) v[e] = (_Float16)(float)((e % 15) - 7);
+  u6 p = __builtin_amdgcn_cvt_scalef32_pk32_fp6_f16(v, 1.0f);
+  h32 r = __builtin_amdgcn_cvt_scalef32_pk32_f16_fp6(p, s);
+  for (int c = -7; c <= 7; ++c) out[i * 16 + (c + 7)] = __builtin_bit_cast(unsigned short, (_Float16)r[c + 7]);
+}
+
+static unsigned short f16_rne(double v) {
+  _Float16 h = (_Float16)v;  // host: exact double -> f16 RNE
+  return *(unsigned short*)&h;
+}
+
+int main() {
+  const int ns = 1 << 16;
+  float* hs = (float*)malloc(ns * 4);
+  srand(1);
+  for (int i = 0; i < ns; ++i) {
+    // random f16 scale: exponent -20 .. 10, random mantissa
+    unsigned short b = (unsigned short)(((rand() % 31) + 5) << 10 | (rand() & 0x3FF));
+    if (i < 64) b = (unsigned short)(1 + i);  // f16 subnormal scales
+    _Float16 h = *(_Float16*)&b;
+    hs[i] = (float)h;
+  }
+  float* ds;
+  unsigned short* dout;
+  hipMalloc(&ds, ns * 4);
+  hipMalloc(&dout, ns * 16 * 2);
+  hipMemcpy(ds, hs, ns * 4, hipMemcpyHostToDevice);
+  unsigned short* ho = (unsigned short*)malloc(ns * 16 * 2);
+  for (int which = 0; which < 2; ++which) {
+    hipMemset(dout, 0, ns * 32);
+    if (which == 0) k8<<<ns / 256, 256>>>(ds, dout, ns);
+    else k6<<<ns / 256, 256>>>(ds, dout, ns);
+    hipDeviceSynchronize();
+    hipMemcpy(ho, dout, ns * 32, hipMemcpyDeviceToHost);
+    long bad = 0, bad_sub = 0;
+    int shown = 0;
+    for (int i = 0; i < ns; ++i)
+      for (int c = -7; c <= 7; ++c) {
+        const unsigned short ref = f16_rne((double)c * (double)hs[i]);
+        const unsigned short got = ho[i * 16 + c + 7];
+        if (ref != got && !(c == 0 && (ref & 0x7FFF) == 0 && (got & 0x7FFF) == 0)) {
+          if (i < 64) ++bad_sub; else ++bad;
+          if (shown < 6) {
+            printf("  %s mismatch s=%.9g c=%d ref=0x%04x got=0x%04x\n", which ? "fp6" : "fp8",
+                   hs[i], c, ref, got);
+            ++shown;
+          }
+        }
+      }
+    printf("%s: %ld mismatches over %d normal scales x 15 codes, %ld over 64 subnormal scales\n",
+           which ? "pk32_f16_fp6" : "pk_f16_fp8", bad, ns - 64, bad_sub);
+  }
+  return 0;
+}
