@@ -180,12 +180,6 @@ int sqmp_quant_act(void* x, int dtype, int M, int K, int amode, int n_bits,
                                  J = 2 and N = M gives their sizes) instead of row-major */
 #define SQMP_QA_TILED4 16     /* as SQMP_QA_TILED with 64-row blocks (J = 4), the operands of
                                  sqmp_gemm_fqt7j with J = 4 */
-#define SQMP_QA_TILED32 32    /* SQMP_OUT_C4: the operands of sqmp_gemm_fqt9 -- 64-row blocks of
-                                 two 32-row token tiles, lane 32 h + r of a block holding row
-                                 32 j + r at positions 16 s + 8 h .. + 7 of each 64-position
-                                 stage (codes [R][Kq/2] as [R/64][Kq/64][64][4][2] dwords,
-                                 scales [R/64][ngq][32][2], xs [R][S_pad] as
-                                 [R/64][S_pad/64][64][4][2][8]), R = roundup(M, 256) */
 #define SQMP_QA_WPT 64        /* sqmp_quant_act_c4: the permuted weight written in sqmp_gemm_fqa's
                                  tile-major register layout (sqmp_fqa_wpt_elems elements: rows
                                  roundup(N, 512), zeros past N) with the activation operands
@@ -331,14 +325,9 @@ int sqmp_gemm_fqt7j(const void* codes_t, const void* scale_t, const void* sal_t,
                     const void* bias, void* y, int dtype, int M, int N, int Kq, int S_pad, int G,
                     int ngq, int J, uint32_t* colmax, void* stream);
 
-/* sqmp_gemm_fqt7j(J = 4)'s operands (SQMP_QA_TILED4) and results at ONE wave per SIMD: 256
- * weight rows x 256 tokens per tile, each wave 256 rows x 64 tokens with its 256 fp32
- * accumulators in the accumulator registers -- half the LDS reads and act-code decode per MFMA
- * of the two-wave kernels.  Kq % 128 == 0, S_pad % 64 == 0, G % 64 == 0, N % 8 == 0, fp16 /
- * bf16; colmax NULL: no statistics. */
-int sqmp_gemm_fqt8(const void* codes_t, const void* scale_t, const void* sal_t, const void* wp,
-                   const void* bias, void* y, int dtype, int M, int N, int Kq, int S_pad, int G,
-                   int ngq, uint32_t* colmax, void* stream);
+/* Re-read the launch-variant knobs (the SQMP_* A/B and tuning variables of DESIGN.md §7), which
+ * the library otherwise reads once, at load: for tools that switch a variant in-process. */
+int sqmp_reload_knobs(void);
 
 /* The activation-order GEMM with the int4 act codes decoded once per workgroup into an LDS
  * tile and the permuted weight in registers (128 tokens x 512 weight rows per workgroup):
@@ -358,15 +347,6 @@ size_t sqmp_fqa_wpt_elems(int N, int Kq, int S_pad);
 /* A dense D [N][L] matrix (L % 64 == 0) in sqmp_gemm_fqa's weight layout (wpt of
  * sqmp_fqa_wpt_elems(N, L, 0) elements). */
 int sqmp_pack_wpt(const void* w, int dtype, int N, int L, void* wpt, void* stream);
-
-/* The activation-order GEMM on SQMP_QA_TILED32 operands at ONE wave per SIMD on the 32x32x16
- * MFMA (256 weight rows x 256 tokens per tile, each wave 256 rows x 64 tokens with 256 fp32
- * accumulators in the accumulator registers): the results of sqmp_gemm_fqt7 up to the
- * accumulation order.  Kq % 128 == 0, S_pad % 64 == 0, G % 64 == 0, N % 8 == 0, fp16 / bf16;
- * no fused column statistics. */
-int sqmp_gemm_fqt9(const void* codes_t, const void* scale_t, const void* sal_t, const void* wp,
-                   const void* bias, void* y, int dtype, int M, int N, int Kq, int S_pad, int G,
-                   int ngq, void* stream);
 
 /* Sibling operand reuse: dst = the SQMP_OUT_FP operand of a layer whose weight shares the
  * quantized input, the salient set and the act mode with the layer that produced src (q/k/v,

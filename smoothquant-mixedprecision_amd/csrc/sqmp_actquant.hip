@@ -792,7 +792,7 @@ __global__ __launch_bounds__(256) void rank_bucket_kernel(
 
 // SQMP_RANK_TABLE_OFF=1 keeps rank_count + lc_table (A/B diagnostics).
 static bool rank_table_fits(int L) {
-  static const bool off = getenv("SQMP_RANK_TABLE_OFF") != nullptr;
+  const bool off = knob("SQMP_RANK_TABLE_OFF") != nullptr;
   return !off && L > 0 && L <= RT_MAX;
 }
 
@@ -834,9 +834,9 @@ static int launch_rank_table(const uint32_t* key, const int32_t* nonsal, int L,
                              const SibTables& sib = SibTables{}) {
   // TPO lanes per group of R owners (SQMP_RT_TPO = 8 / 16 / 32 and SQMP_RT_R = 1 / 2 / 4
   // override, tuning only, read per launch)
-  const char* te = getenv("SQMP_RT_TPO");
-  const char* re = getenv("SQMP_RT_R");
-  const char* be = getenv("SQMP_RT_SB");
+  const char* te = knob("SQMP_RT_TPO");
+  const char* re = knob("SQMP_RT_R");
+  const char* be = knob("SQMP_RT_SB");
   // two owners per lane group above 8192 entries (half the workgroups staging the whole key
   // list: Llama down_proj's 10458-column prepass 61 -> 55.6 us; profiles/r03_prepass_sweep.txt)
   int tpo = L <= 2048 ? 16 : 32, r = L > 8192 ? 2 : 1, sb = 24;
@@ -844,9 +844,9 @@ static int launch_rank_table(const uint32_t* key, const int32_t* nonsal, int L,
   if (re && (atoi(re) == 1 || atoi(re) == 2 || atoi(re) == 4)) r = atoi(re);
   if (be && (atoi(be) == 8 || atoi(be) == 16 || atoi(be) == 24)) sb = atoi(be);
   // SQMP_RT_BUCKET=1: the bucketed kernel (A/B), TPO lanes per owner (SQMP_RT_BTPO, 4)
-  const char* bk = getenv("SQMP_RT_BUCKET");
+  const char* bk = knob("SQMP_RT_BUCKET");
   if (bk && atoi(bk) == 1 && L <= 65535) {
-    const char* bt = getenv("SQMP_RT_BTPO");
+    const char* bt = knob("SQMP_RT_BTPO");
     int btpo = bt ? atoi(bt) : 4;
     if (btpo != 1 && btpo != 2 && btpo != 4 && btpo != 8 && btpo != 16) btpo = 4;
     const int bgrid = cdiv((long)L * btpo, 256L);
@@ -1496,13 +1496,13 @@ static int quant_act_impl(void* x, int dtype, int M, int K, int amode, int n_bit
   if (n_bits < 2 || n_bits > 8) return SQMP_EUNSUPPORTED;
   if (S < 0 || S > K || !x || !amap || (K - S > 0 && !nonsal)) return SQMP_EINVAL;
   if (flags & ~(SQMP_QA_CLEAN_WS | SQMP_QA_REUSE_STATS | SQMP_QA_STATS_GIVEN | SQMP_QA_TILED |
-                SQMP_QA_TILED4 | SQMP_QA_TILED32 | SQMP_QA_WPT))
+                SQMP_QA_TILED4 | SQMP_QA_WPT))
     return SQMP_EINVAL;
   // the fqa weight layout goes with the row-major activation operands, and needs the weight
   if ((flags & SQMP_QA_WPT) &&
-      (!cw || (flags & (SQMP_QA_TILED | SQMP_QA_TILED4 | SQMP_QA_TILED32))))
+      (!cw || (flags & (SQMP_QA_TILED | SQMP_QA_TILED4))))
     return SQMP_EINVAL;
-  if ((flags & (SQMP_QA_TILED | SQMP_QA_TILED4 | SQMP_QA_TILED32)) && out_kind != SQMP_OUT_C4)
+  if ((flags & (SQMP_QA_TILED | SQMP_QA_TILED4)) && out_kind != SQMP_OUT_C4)
     return SQMP_EINVAL;
   // column maxima already in the workspace (written by sqmp_gemm_fq_colmax's epilogue)
   const bool stats_given = (flags & SQMP_QA_STATS_GIVEN) != 0;
@@ -1558,7 +1558,7 @@ static int quant_act_impl(void* x, int dtype, int M, int K, int amode, int n_bit
   const bool sorted = amode == SQMP_ACT_PER_GROUP || amode == SQMP_ACT_PER_GROUP_MEAN3STD;
   const int q_max = (1 << (n_bits - 1)) - 1;
   // SQMP_DISABLE_LC=1 selects the previous row kernels (A/B timing diagnostics only)
-  static const bool lc_off = getenv("SQMP_DISABLE_LC") != nullptr;
+  const bool lc_off = knob("SQMP_DISABLE_LC") != nullptr;
   const bool use_lc = out_kind == SQMP_OUT_FP && !lc_off &&
                       quant_lc_supported(dtype, M, K, group, group_size, Kn, Kp, S_pad, x, out);
   const int lmode = group ? 2 : amode == SQMP_ACT_PER_TENSOR ? 1 : 0;
@@ -1640,8 +1640,7 @@ static int quant_act_impl(void* x, int dtype, int M, int K, int amode, int n_bit
     if (st) return st;
     return launch_quant_lc_c4(dtype, x, M, K, q_max, group_size, lctab, Kn, Kp, salient, S,
                               S_pad, cmax, nonsal, out, out_scale,
-                              (flags & SQMP_QA_TILED32) ? -(int)(cdiv(Kn, group_size) * 8 + 1)
-                              : (flags & SQMP_QA_TILED4) ? -(int)(cdiv(Kn, group_size) * 8 + 4)
+                              (flags & SQMP_QA_TILED4) ? -(int)(cdiv(Kn, group_size) * 8 + 4)
                               : (flags & SQMP_QA_TILED) ? -(int)(cdiv(Kn, group_size) * 8 + 2)
                                                         : (int)round_up(M, 256),
                               out_xs, kc, (int)k64, s, cw);

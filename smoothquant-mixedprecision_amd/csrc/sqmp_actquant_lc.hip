@@ -428,27 +428,7 @@ __device__ __forceinline__ void quant_lc_body(
               d1[h] |= __builtin_amdgcn_perm(hi, lo, 0x0c060c02u) << (4 * p);
             }
           const int u = (rb >> 4) & 3;
-          if (ldsc < 0 && ((-ldsc) & 7) == 1) {
-            // SQMP_QA_TILED32 (sqmp_gemm_fqt9): B32[nb][kt][lane = 32 h + r][s][j] for 64-row
-            // blocks nb of two 32-row token tiles j: dword (s, j) of lane (h, r) = the codes of
-            // row 32 j + r at positions 16 s + 8 h .. + 7 of stage kt (element e at nibble
-            // bpack_shift(e), as d0 / d1 hold them)
-            const int ngq = (-ldsc) >> 3;
-            const int nb = m0 >> 6, j = (m0 >> 5) & 1, r = m0 & 31;
-            uint32_t* t = (uint32_t*)out + ((size_t)nb * (Kq / 64) + (rb >> 6)) * 512 + 2 * u + j;
-            t[r * 8] = d0[0];
-            t[(32 + r) * 8] = d0[1];
-            if (has1) {
-              t[(r + 1) * 8] = d1[0];
-              t[(33 + r) * 8] = d1[1];
-            }
-            if (rb % G == 0) {
-              // S32[nb][g][r][j]
-              uint16_t* sc = (uint16_t*)out_scale + ((size_t)(nb * ngq + rb / G) * 32 + r) * 2 + j;
-              sc[0] = (uint16_t)(c.sd & 0xFFFFu);
-              if (has1) sc[2] = (uint16_t)(c.sd >> 16);
-            }
-          } else if (ldsc < 0) {
+          if (ldsc < 0) {
             // Bt[nb][kb][lane][j][s] (TJ = 2 or 4 row tiles of 16 per 16 TJ-row block nb):
             // dword d of the row's block kb at lane 16 (d / 2) + r16, slot 2 j + d % 2 (m0
             // even: both rows share nb and j).  Lanes u and u ^ 1 hold the two slots of a
@@ -554,14 +534,7 @@ __device__ __forceinline__ void quant_lc_body(
         z1[1] = __builtin_amdgcn_perm(a[3], a[2], 0x07060302u);
         z1[2] = __builtin_amdgcn_perm(b[1], b[0], 0x07060302u);
         z1[3] = __builtin_amdgcn_perm(b[3], b[2], 0x07060302u);
-        if (F8 == 3 && ldsc < 0 && ((-ldsc) & 7) == 1) {
-          // SQMP_QA_TILED32: X32[nb][kd][lane = 32 h + r][s][j][8]: chunk cc of block kd holds
-          // positions 8 cc .. + 7 = k-step s = cc / 2, half h = cc % 2
-          const int nb = m0 >> 6, j = (m0 >> 5) & 1, r = m0 & 31, kd = c >> 3, cc = c & 7;
-          u32x4* t = (u32x4*)out_xs + ((size_t)nb * (S_pad / 64) + kd) * 512 + 2 * (cc >> 1) + j;
-          t[((cc & 1) * 32 + r) * 8] = z0;
-          if (has1) t[((cc & 1) * 32 + r + 1) * 8] = z1;
-        } else if (F8 == 3 && ldsc < 0) {
+        if (F8 == 3 && ldsc < 0) {
           // Salt[nb][kd][lane][j][s][8]: chunk cc of block kd = c(q, s) = 4 (q & 1) + 2 s + q / 2
           const int TJ = (-ldsc) & 7;
           const int nb = m0 / (16 * TJ), j = (m0 >> 4) & (TJ - 1), r = m0 & 15, kd = c >> 3, cc = c & 7;
@@ -856,7 +829,7 @@ static int quant_lc_launch(const void* x, int M, int K, int q_max, int G, const 
   const size_t lds = sizeof(uint32_t) * (size_t)(P + S_pad + 8) * NOUT;
   SQMP_HIP_CHECK(hipFuncSetAttribute(kf, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   int per_cu = occ_per_cu(kf, 64 * nw, lds);
-  if (const char* e = getenv("SQMP_LC_PERCU"))  // tuning only (0 / unparsable: the default)
+  if (const char* e = knob("SQMP_LC_PERCU"))  // tuning only (0 / unparsable: the default)
     if (atoi(e) > 0) per_cu = atoi(e);
   const int grid = lc_grid((M + 1) / 2, per_cu);
   quant_lc_kernel<DT, MODE, LC_RPL, GS, F8, NOUT><<<dim3(grid), dim3(64 * nw), lds, s>>>(
@@ -927,7 +900,7 @@ int launch_quant_lc_group(int dtype, const void* x, int M, int K, int q_max, int
 
 static int pw_rows(int Kp) {
   // rows per permutation batch: 16 KiB of dequantized rows; Np % 256 == 0, so RB | Np
-  const char* e = getenv("SQMP_PW_RB");  // tuning only, read per launch
+  const char* e = knob("SQMP_PW_RB");  // tuning only (sqmp_knobs.hip)
   const int env = e ? atoi(e) : 0;
   int rb = env > 0 ? env : 16384 / (Kp * 2);
   return rb >= 8 ? 8 : rb >= 4 ? 4 : rb >= 2 ? 2 : 1;
@@ -991,7 +964,7 @@ int launch_quant_lc_c4(int dtype, const void* x, int M, int K, int q_max, int G,
   const int per_cu = occ_per_cu(kf, 64 * nw, lds);
   // quantizer workgroups per CU: the rest of every CU's slots go to the permutation
   // workgroups (issued after them), so the two run side by side
-  const char* qe = getenv("SQMP_C4_QPERCU");  // tuning only, read per launch
+  const char* qe = knob("SQMP_C4_QPERCU");  // tuning only (sqmp_knobs.hip)
   const int q_env = qe ? atoi(qe) : 0;
   const int qpc = q_env > 0 ? q_env : (per_cu > 2 ? per_cu - 2 : 1);
   const int nq = lc_grid((M + 1) / 2, qpc < per_cu ? qpc : per_cu);

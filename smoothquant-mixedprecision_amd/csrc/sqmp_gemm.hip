@@ -214,7 +214,7 @@ static int generic_launch(const void* a, const void* codes, const void* wscale,
   typedef typename DT::T T;
   const int tiles_m = cdiv(M, BM), tiles_n = cdiv(N, BN);
   static const bool f32_4w = [] {  // A/B knob: the 4-wave build for fp32 too
-    const char* e = getenv("SQMP_F32_WN2");
+    const char* e = knob("SQMP_F32_WN2");
     return e && atoi(e) == 1;
   }();
   if constexpr (std::is_same<DT, F32>::value) if (!f32_4w) {

@@ -653,18 +653,18 @@ static int gemm_f8_impl(const void* a8, const float* ascale, const void* xs, con
   const dim3 grid(tiles_m * tiles_n), block(512);
   // Gw % 128 == 0 runs the 16x16x128 kernel (SQMP_F8_V1=1 keeps the 32x32x64 one, A/B)
   static const bool v1_only = [] {
-    const char* e = getenv("SQMP_F8_V1");
+    const char* e = knob("SQMP_F8_V1");
     return e && atoi(e) != 0;
   }();
   const bool v2 = Gw % 128 == 0 && !v1_only;
   if (colmax && !v2) return SQMP_EUNSUPPORTED;  // fused statistics: the 16x16x128 kernel only
   // M-tiles per raster group (SQMP_GROUP_M: A/B knob, read per launch)
-  const char* ge = getenv("SQMP_GROUP_M");
+  const char* ge = knob("SQMP_GROUP_M");
   const int group_m = ge && atoi(ge) > 0 ? atoi(ge) : 4;
   const bool nt = nt_output((size_t)M * N * (dtype == SQMP_F32 ? 4 : 2));
   // default 2 (loader split): same-box config-2 per_token step 334.5 -> 324.0 us; setprio for
   // waves 4-7 +-0 (profiles/r03_ab_f8_opt.txt).  SQMP_F8_OPT: A/B knob, read per launch
-  const char* oe = getenv("SQMP_F8_OPT");
+  const char* oe = knob("SQMP_F8_OPT");
   const int opt = oe ? atoi(oe) & 3 : 2;
 #define SQMP_F8V2(DTT, O)                                                                    \
   gemm_f8v2_kernel<DTT, O><<<grid, block, 0, s>>>(                                           \
@@ -672,7 +672,7 @@ static int gemm_f8_impl(const void* a8, const float* ascale, const void* xs, con
       (const DTT::T*)wsal, (const DTT::T*)bias, (DTT::T*)y, M, N, Kp, S_pad, Gw, ngw, tiles_m, \
       tiles_n, group_m, colmax, nt ? 1 : 0)
 #ifdef SQMP_DIAG_BUILD
-  const char* de = getenv("SQMP_F8_DIAG");  // read per launch
+  const char* de = knob("SQMP_F8_DIAG");  // (sqmp_knobs.hip)
   const int diag = de ? atoi(de) : 0;
 #define SQMP_F8D(DTT, D)                                                                     \
   gemm_f8v2_kernel<DTT, 2, D><<<grid, block, 0, s>>>(                                        \

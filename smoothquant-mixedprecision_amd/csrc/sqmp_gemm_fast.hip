@@ -723,7 +723,7 @@ __global__ __launch_bounds__(256, 1) void gemm_i8v2_kernel(
 // 8 measured equal at config 2, 1 and 2 0.5-1 % slower)
 static int fq6_group_m() {
   static int v = [] {
-    const char* e = getenv("SQMP_GROUP_M");
+    const char* e = knob("SQMP_GROUP_M");
     return e && atoi(e) > 0 ? atoi(e) : 4;
   }();
   return v;

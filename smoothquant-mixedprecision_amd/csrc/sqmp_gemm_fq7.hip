@@ -592,15 +592,15 @@ __global__ void pack_sal_kernel(const T* __restrict__ wsal, T* __restrict__ Salt
 // 2048 x 4096 -> 4096 69.9 / 68.7 / 68.2 / 69.1 us, -> 11008 170.8 / 171.6 / 169.8 / 172.1,
 // 2048 x 11008 -> 4096 173.3 / 172.8 / 171.6 / 176.7, config 2 in packed order 467.3 / 463.1
 // / 459.6 / 473.6; profiles/r03_ab_group_m.txt); SQMP_FQ7_GROUP_M overrides
-static int group_m_env() {  // read per launch (in-process A/B)
-  const char* e = getenv("SQMP_FQ7_GROUP_M");
+static int group_m_env() {  // (A/B knob; sqmp_knobs.hip)
+  const char* e = knob("SQMP_FQ7_GROUP_M");
   return e && atoi(e) > 0 ? atoi(e) : 4;
 }
 
 // the activation-order (TR) launch: 4 weight-row tiles per raster group (same box, config 2:
 // GEMM 422.5 vs 429.8 us at 8, alternating runs); SQMP_FQT7_GROUP_M overrides
-static int group_m_tr_env() {  // read per launch (in-process A/B)
-  const char* e = getenv("SQMP_FQT7_GROUP_M");
+static int group_m_tr_env() {  // (A/B knob; sqmp_knobs.hip)
+  const char* e = knob("SQMP_FQT7_GROUP_M");
   return e && atoi(e) > 0 ? atoi(e) : 4;
 }
 
@@ -610,8 +610,8 @@ static int group_m_tr_env() {  // read per launch (in-process A/B)
 // 128-row tiles with more than one tile per CU: 8 (two workgroups per CU, 128 VGPRs), same
 // box (profiles/r03_ab_fq7_two_wg_per_cu.txt): 2048 x 4096 -> 11008 179.5 -> 159.6 us; at one
 // tile per CU (2048 x 4096 -> 4096, 2048 x 11008 -> 4096) within +-1 % of 3
-static int opt_pk_env(int tm, long tiles) {  // read per launch (in-process A/B)
-  const char* e = getenv("SQMP_FQ7_OPT");
+static int opt_pk_env(int tm, long tiles) {  // (A/B knob; sqmp_knobs.hip)
+  const char* e = knob("SQMP_FQ7_OPT");
   return e ? atoi(e) : (tm == 128 && tiles > 256 ? 8 : 3);
 }
 
@@ -619,16 +619,16 @@ static int opt_pk_env(int tm, long tiles) {  // read per launch (in-process A/B)
 // default 3 (setprio + loader split): same box, interleaved rounds at config 2, 421.6 us
 // against 431.4 us for 0 (either bit alone +-0.3 %, PF = 3 +-0.1 %; tools/ab_fqt7.py,
 // profiles/r03_ab_fqt7.txt)
-static int opt_tr_env() {  // read per launch (in-process A/B)
-  const char* e = getenv("SQMP_FQT7_OPT");
+static int opt_tr_env() {  // (A/B knob; sqmp_knobs.hip)
+  const char* e = knob("SQMP_FQT7_OPT");
   return e ? atoi(e) : 3;
 }
 
 #ifdef SQMP_DIAG_BUILD
 // timing-diagnostic variants (wrong results by design) only in a diagnostics build:
 // SQMP_DIAG=1 python smoothquant-mixedprecision_amd/build_ext.py --force
-static int diag_env() {  // read per launch (in-process A/B)
-  const char* e = getenv("SQMP_FQ7_DIAG");
+static int diag_env() {  // (A/B knob; sqmp_knobs.hip)
+  const char* e = knob("SQMP_FQ7_DIAG");
   return e ? atoi(e) : 0;
 }
 #endif
@@ -715,7 +715,7 @@ static int dispatch_group(Fq7Grp& g, int M, int Kp, int S_pad, int Gw, int ngw, 
   long t256 = 0;
   for (int p = 0; p < g.n; ++p) t256 += (long)cdiv(M, 256) * cdiv(g.N[p], 256);
   int tm = t256 >= 512 ? 256 : 128;
-  if (const char* e = getenv("SQMP_FQ7G_TM")) tm = atoi(e) == 256 ? 256 : 128;
+  if (const char* e = knob("SQMP_FQ7G_TM")) tm = atoi(e) == 256 ? 256 : 128;
   if (std::is_same<DT, BF16>::value) tm = 128;  // (bf16 at 256 x 256 puts an array in scratch)
   const int tiles_m = cdiv(M, tm);
   int end = 0;

@@ -27,6 +27,8 @@
 // at chunk c ^ ((t >> 1) & 7) -- conflict-free for the ds_read_b128 fragment reads.
 #include <stdlib.h>
 
+#include <type_traits>
+
 #include "sqmp_mfma.h"
 
 namespace sqmp {
@@ -88,20 +90,25 @@ __device__ inline int lane_now() {
   return (int)l;
 }
 
-constexpr int TT = 128;               // tokens per tile
-constexpr int TW = 512;               // weight rows per tile: 8 waves x 64
-constexpr int NS = 3;                 // act tile ring slots
-constexpr int SLOT = TT * 128;        // 128 tokens x 64 positions x 2 B
-constexpr int WSTG = TT * 128;        // per-wave epilogue staging: 128 tokens x 64 rows x 2 B
-constexpr int LDS_BYTES = 8 * WSTG > NS * SLOT ? 8 * WSTG : NS * SLOT;
-constexpr int PF = 2;                 // act fragment read-ahead (blocks)
+constexpr int NS = 3;   // act tile ring slots
+constexpr int PF = 2;   // act fragment read-ahead (blocks)
+constexpr int WSTG = 16384;  // per-wave epilogue staging: 128 accumulators x 64 lanes x 2 B
 
 // chunk (8 positions) of bpack dword d of a 64-position block (sqmp_common.h bpack_pos)
 __device__ inline int chunk_of(int d) { return 2 * (d & 3) + (d >> 2); }
 
+// RB = 16-row weight blocks per wave (4: 128 tokens x 512 weight rows per workgroup, 8 waves of
+// 128 tokens x 64 rows; 2: 256 tokens x 256 weight rows, 8 waves of 256 x 32).  TB = 32 / RB
+// token blocks of 16 per wave keep 128 fp32 accumulators per lane either way: RB = 2 fetches
+// the register operand half as often per FLOP (wp once per 256 tokens) but reads twice the LDS
+// act tile per MFMA and decodes twice the codes per lane.
 // OPT bit 0: waves 4-7 at s_setprio 1 through the K loop (MI355X_MICROARCH.md "Two waves per
-// SIMD" item 4)
-template <class DT, int OPT>
+// SIMD" item 4).
+// DIAG (timing diagnostics, wrong results by design, SQMP_DIAG_BUILD only; 0 = the product
+// kernel): 1 no wp register loads after the prologue, 2 no act decode / LDS writes after the
+// prologue, 3 the decode without its LDS writes, 4 half the act fragment LDS reads (each used
+// for two blocks), 5 no per-stage barrier
+template <class DT, int RB, int OPT, int DIAG = 0>
 __global__ __launch_bounds__(512, 1) void gemm_fqa_kernel(
     const unsigned char* __restrict__ codes, const typename DT::T* __restrict__ ascale,
     const typename DT::T* __restrict__ xs, const typename DT::T* __restrict__ wpt,
@@ -109,6 +116,12 @@ __global__ __launch_bounds__(512, 1) void gemm_fqa_kernel(
     int S_pad, int gsh, int ldsc, int tiles_t, int tiles_w, int group_m,
     uint32_t* __restrict__ colmax, int nt) {
   typedef typename DT::T T;
+  constexpr int TB = 32 / RB, TT = 16 * TB, WR = 16 * RB, TW = 8 * WR;
+  constexpr int SLOT = TT * 128;        // TT tokens x 64 positions x 2 B
+  constexpr int LDS_BYTES = 8 * WSTG > NS * SLOT ? 8 * WSTG : NS * SLOT;
+  constexpr int CPL = TT / 64;          // bpack dwords (8 codes) a decode lane takes per stage
+  constexpr int LPT = 8 / CPL;          // decode lanes per token
+  constexpr int XP = SLOT / 8192;       // salient-tail DMA pieces per wave and stage
   __shared__ __attribute__((aligned(16))) unsigned char lds[LDS_BYTES];
 
   int tt, tw;
@@ -118,78 +131,96 @@ __global__ __launch_bounds__(512, 1) void gemm_fqa_kernel(
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r16 = lane & 15, q = lane >> 4;
   const int nkm = Kq / 64, nks = S_pad / 64, nkt = nkm + nks;
-  const int nb = tw * 8 + wave;  // this wave's 64-row block of wpt
+  const int nw0 = n0 + WR * wave;        // this wave's first weight row
+  const int nb = nw0 >> 6, rb0 = (nw0 >> 4) & 3;  // its 64-row block of wpt, first row block
 
-  // ---- wp: the register operand, 8 x 1 KiB per wave and stage
-  const rsrc_t rW = make_rsrc(wpt + (size_t)nb * nkt * 4096);
+  // ---- wp: the register operand, 2 RB x 1 KiB per wave and stage (fragments (rb, h) of the
+  // wave's rows: consecutive 1-KiB pieces from rb0)
+  const rsrc_t rW = make_rsrc(wpt + (size_t)nb * nkt * 4096 + rb0 * 1024);
   const uint32_t vW = (uint32_t)lane * 16u;
-  auto issue_w = [&](int kt, u32x4(&w)[8]) {
+  auto issue_w = [&](int kt, u32x4(&w)[2 * RB]) {
+    if (DIAG == 1 && kt > 0) return;
     const uint32_t so = (uint32_t)kt * 8192u, so1 = so + 4096u;  // (12-bit instruction offsets)
     ld16<0>(w[0], rW, vW, so);
     ld16<1024>(w[1], rW, vW, so);
     ld16<2048>(w[2], rW, vW, so);
     ld16<3072>(w[3], rW, vW, so);
-    ld16<0>(w[4], rW, vW, so1);
-    ld16<1024>(w[5], rW, vW, so1);
-    ld16<2048>(w[6], rW, vW, so1);
-    ld16<3072>(w[7], rW, vW, so1);
+    if constexpr (RB == 4) {
+      ld16<0>(w[4], rW, vW, so1);
+      ld16<1024>(w[5], rW, vW, so1);
+      ld16<2048>(w[6], rW, vW, so1);
+      ld16<3072>(w[7], rW, vW, so1);
+    }
   };
 
   // ---- act codes (row-major bpack rows of Kq / 2 bytes) + group scales [ngq][ldsc]: decode
-  // lane (dt = token, dh) takes bpack dwords 2 dh, 2 dh + 1 of its token's 64-block
-  const int dt = tid >> 2, dh = tid & 3, todd = dt & 1;
+  // lane (dt = token, dh) takes bpack dwords CPL dh .. CPL dh + CPL - 1 of its token's 64-block
+  const int dt = tid / LPT, dh = tid % LPT, todd = dt & 1;
   const rsrc_t rC = make_rsrc(codes + (size_t)m0 * (Kq / 2));
   const rsrc_t rS = make_rsrc(ascale + m0);
-  const uint32_t vC = (uint32_t)dt * (uint32_t)(Kq / 2) + (uint32_t)dh * 8u;
+  const uint32_t vC = (uint32_t)dt * (uint32_t)(Kq / 2) + (uint32_t)dh * (4u * CPL);
   const uint32_t vS = (uint32_t)dt * 2u;
+  typedef typename std::conditional<CPL == 2, u32x2, u32x4>::type CRegs;
   struct Cd {
-    u32x2 c;
+    CRegs c;
     uint32_t s;
   };
   auto issue_c = [&](int kt, Cd& d) {
-    ld8(d.c, rC, vC, (uint32_t)kt * 32u);
+    if (DIAG == 2 && kt > 1) return;
+    if constexpr (CPL == 2)
+      ld8(d.c, rC, vC, (uint32_t)kt * 32u);
+    else
+      ld16<0>(d.c, rC, vC, (uint32_t)kt * 32u);
     ldu16(d.s, rS, vS, (uint32_t)(((kt * 64) >> gsh) * ldsc) * (uint32_t)sizeof(T));
   };
-  // this lane's two chunk write offsets in a slot, in write order (odd tokens write their
-  // second dword first: the 8 lanes of a ds_write_b128 bank group then cover 8 chunks)
+  // write offset of this lane's e-th decoded dword (CPL = 2: odd tokens write their second
+  // dword first, so the 8 lanes of a ds_write_b128 bank group cover 8 chunks)
   const int swz = (dt >> 1) & 7;
-  // (chunk_of(2 dh + 1) = chunk_of(2 dh) ^ 2: the second offset is the first ^ 32)
-  const uint32_t wo0 = (uint32_t)(dt * 128 + ((chunk_of(2 * dh + todd) ^ swz) << 4));
+  const uint32_t wrow = (uint32_t)(dt * 128);
+  auto wr_off = [&](int e) -> uint32_t {
+    const int d = CPL * dh + (CPL == 2 ? (e ^ todd) : e);
+    return wrow + (uint32_t)((chunk_of(d) ^ swz) << 4);
+  };
   const DecK dk = make_deck();
   auto decode_one = [&](const Cd& d, int e) -> u32x4 {
-    const uint32_t w = (e ^ todd) ? d.c.y : d.c.x;
+    uint32_t w;
+    if constexpr (CPL == 2)
+      w = (e ^ todd) ? d.c.y : d.c.x;  // (a select: no run-time vector index)
+    else
+      w = d.c[e];
     return Dec<DT>::run(w, Dec<DT>::prep(d.s & 0xFFFFu), dk);
   };
 
-  // ---- the salient tail's exact x by LDS-DMA: piece p = 2 wave + i covers tokens 8 p .. 8 p + 7,
-  // lane l moving logical chunk (l & 7) ^ swz(token) of token 8 p + (l >> 3) into physical
+  // ---- the salient tail's exact x by LDS-DMA: piece p = XP wave + i covers tokens 8 p .. 8 p +
+  // 7, lane l moving logical chunk (l & 7) ^ swz(token) of token 8 p + (l >> 3) into physical
   // chunk l & 7
   const rsrc_t rX = make_rsrc(xs + (size_t)m0 * (S_pad > 0 ? S_pad : 1));
   auto issue_x = [&](int kd, unsigned char* slot) {
     const int l = lane_now();  // (recomputed: not live through the codes stages)
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int row = 8 * (2 * wave + i) + (l >> 3);
+    for (int i = 0; i < XP; ++i) {
+      const int row = 8 * (XP * wave + i) + (l >> 3);
       const uint32_t xo = (uint32_t)((row * S_pad + 8 * ((l & 7) ^ ((row >> 1) & 7))) * (int)sizeof(T));
-      dma16(rX, xo, (uint32_t)kd * 64u * (uint32_t)sizeof(T), slot + (2 * wave + i) * 1024);
+      dma16(rX, xo, (uint32_t)kd * 64u * (uint32_t)sizeof(T), slot + (XP * wave + i) * 1024);
     }
   };
 
-  f32x4 acc[8][4];
+  f32x4 acc[TB][RB];
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+  for (int i = 0; i < TB; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < RB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // act fragment t = 8 h + i: token block i, sub-step h
+  // act fragment t = TB h + i: token block i, sub-step h
   const int rsw = (r16 >> 1) & 7;
   const uint32_t ro0 = (uint32_t)(r16 * 128 + ((q ^ rsw) << 4));
   const uint32_t ro1 = (uint32_t)(r16 * 128 + (((4 + q) ^ rsw) << 4));
   auto bld = [&](const unsigned char* __restrict__ slot, int t) {
-    return *(const u32x4*)(slot + (t & 7) * 2048 + ((t >> 3) ? ro1 : ro0));
+    if (DIAG == 4) t &= ~1;
+    return *(const u32x4*)(slot + (t % TB) * 2048 + ((t / TB) ? ro1 : ro0));
   };
 
-  u32x4 W[2][8];
+  u32x4 W[2][2 * RB];
   Cd cd[2];
 
   // prologue: codes(0) -> decode -> slot 0 (Kq = 0, a dense GEMM: x(0) by DMA); wp(0); codes(1)
@@ -199,14 +230,15 @@ __global__ __launch_bounds__(512, 1) void gemm_fqa_kernel(
     issue_x(0, lds);
   issue_w(0, W[0]);
   issue_c(nkm > 1 ? 1 : 0, cd[1]);
-  vmwait<10>();
+  vmwait<2 * RB + 2>();
   if (nkm > 0) {
     fence(cd[0].c);
     fence(cd[0].s);
-    const u32x4 v0 = decode_one(cd[0], 0);
-    const u32x4 v1 = decode_one(cd[0], 1);
-    *(u32x4*)(lds + wo0) = v0;
-    *(u32x4*)(lds + (wo0 ^ 32u)) = v1;
+#pragma unroll
+    for (int e = 0; e < CPL; ++e) {
+      const u32x4 v = decode_one(cd[0], e);
+      *(u32x4*)(lds + wr_off(e)) = v;
+    }
   }
   if ((OPT & 1) && wave >= 4) __builtin_amdgcn_s_setprio(1);
 
@@ -216,20 +248,21 @@ __global__ __launch_bounds__(512, 1) void gemm_fqa_kernel(
   // stage after the loop (LAST, nkt odd) issues none -- a dead asm output's register could be
   // reused while its load is still in flight.
   int sc = 0;  // kt % NS
+  constexpr int NBLK = 2 * TB;  // MFMA blocks per stage (RB MFMAs each)
   auto stage = [&](int kt, auto pc, auto lastc) {
     constexpr int P = decltype(pc)::value;
     constexpr bool LAST = decltype(lastc)::value;
     vmwait<0>();
     lgkwait0();
 #pragma unroll
-    for (int f = 0; f < 8; ++f) fence(W[P][f]);
+    for (int f = 0; f < 2 * RB; ++f) fence(W[P][f]);
     fence(cd[P ^ 1].c);
     fence(cd[P ^ 1].s);
-    barrier();  // slot sc complete (decode writes / DMA of the previous stage)
+    if (DIAG != 5) barrier();  // slot sc complete (decode writes / DMA of the previous stage)
     const int sn = sc == NS - 1 ? 0 : sc + 1;
     const unsigned char* __restrict__ slot = lds + sc * SLOT;
     unsigned char* nslot = lds + sn * SLOT;
-    const bool dec = kt + 1 < nkm;
+    const bool dec = kt + 1 < nkm && (DIAG != 2 || kt < 1);
     const bool dma = kt + 1 >= nkm && kt + 1 < nkt;
     if constexpr (!LAST) {
       if (dma) issue_x(kt + 1 - nkm, nslot);
@@ -241,15 +274,19 @@ __global__ __launch_bounds__(512, 1) void gemm_fqa_kernel(
 #pragma unroll
     for (int t = 0; t < PF; ++t) b[t] = bld(slot, t);
 #pragma unroll
-    for (int t = 0; t < 16; ++t) {
-      if (t + PF < 16) b[(t + PF) % (PF + 1)] = bld(slot, t + PF);
+    for (int t = 0; t < NBLK; ++t) {
+      if (t + PF < NBLK) b[(t + PF) % (PF + 1)] = bld(slot, t + PF);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) Mfma<DT>::run(acc[t & 7][j], W[P][2 * j + (t >> 3)], b[t % (PF + 1)]);
+      for (int j = 0; j < RB; ++j)
+        Mfma<DT>::run(acc[t % TB][j], W[P][2 * j + t / TB], b[t % (PF + 1)]);
       if (dec) {
-        if (t == 1) dv = decode_one(cd[P ^ 1], 0);
-        if (t == 3) *(u32x4*)(nslot + wo0) = dv;
-        if (t == 5) dv = decode_one(cd[P ^ 1], 1);
-        if (t == 7) *(u32x4*)(nslot + (wo0 ^ 32u)) = dv;
+        // decode dword e at block 4 e + 1, its LDS write at block 4 e + 3
+#pragma unroll
+        for (int e = 0; e < CPL; ++e) {
+          if (t == 4 * e + 1) dv = decode_one(cd[P ^ 1], e);
+          if (t == 4 * e + 3 && DIAG != 3) *(u32x4*)(nslot + wr_off(e)) = dv;
+          if (t == 4 * e + 3 && DIAG == 3) fence(dv);
+        }
       }
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -266,18 +303,18 @@ __global__ __launch_bounds__(512, 1) void gemm_fqa_kernel(
   }
   if (kt < nkt) stage(kt, Z(), L1());
 
-  // ---- epilogue: each wave stages its 128 x 64 tile in its own 16-KiB region (token row of
-  // 128 B, 8-B unit u = 4 j + q at u ^ (token & 15): the 16 tokens of a ds_write_b64 hit 16
-  // units), then stores whole 128-B row pieces, one 16-B chunk per lane
+  // ---- epilogue: each wave stages its TT x WR tile in its own 16-KiB region (token row of 2 WR
+  // bytes, 8-B unit u = 4 j + q at u ^ (token % (4 RB))), then stores whole row pieces, one 16-B
+  // chunk per lane
   vmwait<0>();
   lgkwait0();
   barrier();  // every wave is past its last read of the ring
   if ((OPT & 1) && wave >= 4) __builtin_amdgcn_s_setprio(0);
+  constexpr int RS = 2 * WR, UM = 4 * RB - 1;  // staged row bytes, unit swizzle mask
   unsigned char* st = lds + wave * WSTG;
-  const int nw0 = n0 + 64 * wave;
-  float cm[4][4];
+  float cm[RB][4];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
+  for (int j = 0; j < RB; ++j) {
     float bv[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -286,7 +323,7 @@ __global__ __launch_bounds__(512, 1) void gemm_fqa_kernel(
       cm[j][r] = 0.f;
     }
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
+    for (int i = 0; i < TB; ++i) {
       const int tl = 16 * i + r16;
       T v[4];
 #pragma unroll
@@ -295,14 +332,14 @@ __global__ __launch_bounds__(512, 1) void gemm_fqa_kernel(
 #pragma unroll
         for (int r = 0; r < 4; ++r) cm[j][r] = fmaxf(cm[j][r], fabsf(DT::to_f(v[r])));
       }
-      *(u32x2*)(st + tl * 128 + (((4 * j + q) ^ (tl & 15)) << 3)) = *(const u32x2*)v;
+      *(u32x2*)(st + tl * RS + (((4 * j + q) ^ (tl & UM)) << 3)) = *(const u32x2*)v;
     }
   }
   if (colmax) {
     // fused output-quant statistics (as sqmp_gemm_fq_colmax): max over the lane's tokens, then
     // the 16 token lanes, one atomic per column and wave (bits of |y| order like unsigned ints)
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+    for (int j = 0; j < RB; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         float v = cm[j][r];
@@ -315,12 +352,13 @@ __global__ __launch_bounds__(512, 1) void gemm_fqa_kernel(
       }
   }
   lgkwait0();  // the wave's own staging writes (no other wave reads this region)
-  const int v8 = lane & 7;
+  constexpr int CPR = RS / 16, RPI = 64 / CPR;  // 16-B chunks per staged row, rows per pass
+  const int v8 = lane % CPR;
   const bool nok = nw0 + 8 * v8 < N;  // N % 8 == 0 (launcher)
 #pragma unroll 4
-  for (int it = 0; it < 16; ++it) {
-    const int row = 8 * it + (lane >> 3), s = row & 15;
-    const u32x4 a = *(const u32x4*)(st + row * 128 + ((v8 ^ (s >> 1)) << 4));
+  for (int it = 0; it < TT / RPI; ++it) {
+    const int row = RPI * it + lane / CPR, s = row & UM;
+    const u32x4 a = *(const u32x4*)(st + row * RS + ((v8 ^ (s >> 1)) << 4));
     const u32x4 val = (s & 1) ? u32x4{a[2], a[3], a[0], a[1]} : a;
     if (m0 + row < M && nok) {
       T* dst = Y + (size_t)(m0 + row) * N + nw0 + 8 * v8;
@@ -351,20 +389,57 @@ __global__ void pack_wpt_kernel(const T* __restrict__ w, T* __restrict__ wpt, in
   *(u32x4*)(wpt + idx * 8) = v;
 }
 
-// the launch: XCD x runs all token tiles of weight-row tile x (group_m = every token tile):
-// its 32 concurrent workgroups stream the same wp rows through their L2
-template <class DT>
+// SQMP_FQA_RB = 2 / 4 (A/B knob): 16-row weight blocks per wave, default 4
+static int rb_knob() {
+  const char* e = knob("SQMP_FQA_RB");
+  return e && atoi(e) == 2 ? 2 : 4;
+}
+#ifdef SQMP_DIAG_BUILD
+static int diag_knob() {
+  const char* e = knob("SQMP_FQA_DIAG");
+  return e ? atoi(e) : 0;
+}
+#endif
+
+// the launch: XCD x runs all token tiles of a weight-row tile (group_m = every token tile): the
+// 32 concurrent workgroups of an XCD stream the same wp rows through its L2
+template <class DT, int RB>
 static int launch(const void* codes, const void* ascale, const void* xs, const void* wpt,
                   const void* bias, void* y, int M, int N, int Kq, int S_pad, int gsh, int ldsc,
                   uint32_t* colmax, hipStream_t s) {
   typedef typename DT::T T;
+  constexpr int TT = 16 * (32 / RB), TW = 128 * RB;
   const int tiles_t = cdiv(M, TT), tiles_w = cdiv(N, TW);
   const int nt = nt_output((size_t)M * N * sizeof(T)) ? 1 : 0;
-  gemm_fqa_kernel<DT, 1><<<dim3(tiles_t * tiles_w), dim3(512), 0, s>>>(
-      (const unsigned char*)codes, (const T*)ascale, (const T*)xs, (const T*)wpt, (const T*)bias,
-      (T*)y, M, N, Kq, S_pad, gsh, ldsc, tiles_t, tiles_w, tiles_t, colmax, nt);
+#define SQMP_FQA_L(D)                                                                           \
+  gemm_fqa_kernel<DT, RB, 1, D><<<dim3(tiles_t * tiles_w), dim3(512), 0, s>>>(                  \
+      (const unsigned char*)codes, (const T*)ascale, (const T*)xs, (const T*)wpt, (const T*)bias, \
+      (T*)y, M, N, Kq, S_pad, gsh, ldsc, tiles_t, tiles_w, tiles_t, colmax, nt)
+#ifdef SQMP_DIAG_BUILD
+  if (std::is_same<DT, F16>::value) {
+    switch (diag_knob()) {
+      case 1: SQMP_FQA_L(1); SQMP_LAUNCH_CHECK(); return SQMP_OK;
+      case 2: SQMP_FQA_L(2); SQMP_LAUNCH_CHECK(); return SQMP_OK;
+      case 3: SQMP_FQA_L(3); SQMP_LAUNCH_CHECK(); return SQMP_OK;
+      case 4: SQMP_FQA_L(4); SQMP_LAUNCH_CHECK(); return SQMP_OK;
+      case 5: SQMP_FQA_L(5); SQMP_LAUNCH_CHECK(); return SQMP_OK;
+      default: break;
+    }
+  }
+#endif
+  SQMP_FQA_L(0);
+#undef SQMP_FQA_L
   SQMP_LAUNCH_CHECK();
   return SQMP_OK;
+}
+
+template <class DT>
+static int dispatch(const void* codes, const void* ascale, const void* xs, const void* wpt,
+                    const void* bias, void* y, int M, int N, int Kq, int S_pad, int gsh, int ldsc,
+                    uint32_t* colmax, hipStream_t s) {
+  if (rb_knob() == 2)
+    return launch<DT, 2>(codes, ascale, xs, wpt, bias, y, M, N, Kq, S_pad, gsh, ldsc, colmax, s);
+  return launch<DT, 4>(codes, ascale, xs, wpt, bias, y, M, N, Kq, S_pad, gsh, ldsc, colmax, s);
 }
 
 }  // namespace fqa
@@ -382,7 +457,7 @@ extern "C" int sqmp_gemm_fqa(const void* acodes, const void* ascale, const void*
   if (!acodes || !ascale || !wpt || !y || (S_pad > 0 && !xs)) return SQMP_EINVAL;
   if (M < 0 || N <= 0 || Kq < 0 || Kq % 64 || S_pad < 0 || S_pad % 64 || G <= 0) return SQMP_EINVAL;
   if (Kq + S_pad == 0) return SQMP_EINVAL;
-  if (ldsc < (M + fqa::TT - 1) / fqa::TT * fqa::TT) return SQMP_EINVAL;
+  if (ldsc < (M + 255) / 256 * 256) return SQMP_EINVAL;  // (256-token tiles at RB = 2)
   if (dtype != SQMP_F16 && dtype != SQMP_BF16) return SQMP_EUNSUPPORTED;
   if (G % 64 || (G & (G - 1)) || N % 8) return SQMP_EUNSUPPORTED;
   // 32-bit buffer offsets: the codes / xs rows of one tile and a wave's wp block
@@ -392,8 +467,8 @@ extern "C" int sqmp_gemm_fqa(const void* acodes, const void* ascale, const void*
   while ((1 << gsh) < G) ++gsh;
   hipStream_t s = (hipStream_t)stream;
   if (dtype == SQMP_F16)
-    return fqa::launch<F16>(acodes, ascale, xs, wpt, bias, y, M, N, Kq, S_pad, gsh, ldsc, colmax, s);
-  return fqa::launch<BF16>(acodes, ascale, xs, wpt, bias, y, M, N, Kq, S_pad, gsh, ldsc, colmax, s);
+    return fqa::dispatch<F16>(acodes, ascale, xs, wpt, bias, y, M, N, Kq, S_pad, gsh, ldsc, colmax, s);
+  return fqa::dispatch<BF16>(acodes, ascale, xs, wpt, bias, y, M, N, Kq, S_pad, gsh, ldsc, colmax, s);
 }
 
 // dense W [N][L] (L % 64 == 0) -> the wpt layout (rows roundup(N, 512), zeros past N)

@@ -347,7 +347,7 @@ extern "C" int sqmp_gemm_h2d(const void* a2, int ldr, const int* aexp, const voi
   const int tm = (long)cdiv(M, 128) * tiles_n >= 256 ? 128 : 64;
   const int tiles_m = cdiv(M, tm);
   const int nt = nt_output((size_t)M * N * sizeof(float)) ? 1 : 0;
-  const char* ge = getenv("SQMP_H2D_GROUP_M");  // A/B knob, read per launch
+  const char* ge = knob("SQMP_H2D_GROUP_M");  // A/B knob (sqmp_knobs.hip)
   const int gm = ge && atoi(ge) > 0 ? atoi(ge) : 4;
   const size_t a_plane = (size_t)ldr * L;
   // (32-bit buffer offsets: both planes of the tile rows within 4 GiB)

@@ -355,12 +355,12 @@ extern "C" int sqmp_gemm_h2(const float* a, const int* aexp, const void* b2, con
   // 128 x 128 tiles) wherever they still give every CU a workgroup
   const int tiles_n2 = cdiv(N, 256);
   static const bool wide_ok = [] {  // SQMP_H2_WIDE=0: 128 x 128 tiles only (A/B knob)
-    const char* e = getenv("SQMP_H2_WIDE");
+    const char* e = knob("SQMP_H2_WIDE");
     return !e || atoi(e) != 0;
   }();
   const bool wide = wide_ok && (long)tiles_m * tiles_n2 >= 256;
   static const bool bk64 = [] {  // SQMP_H2_BK64=0: K stages of 32 (A/B knob)
-    const char* e = getenv("SQMP_H2_BK64");
+    const char* e = knob("SQMP_H2_BK64");
     return !e || atoi(e) != 0;
   }();
   const bool k64 = bk64 && L % 64 == 0;
@@ -368,7 +368,7 @@ extern "C" int sqmp_gemm_h2(const float* a, const int* aexp, const void* b2, con
   // row tiles per raster group: 4 (same box, config-2 fp32 step: 1 / 2 / 4 / 8 / 16 / 32 ->
   // 2078.7 / 2074.1 / 2002.3 / 2037.9 / 2146.8 / 2178.6 us, profiles/r03_ab_h2_group_m.txt);
   // SQMP_H2_GROUP_M: A/B knob, read per launch
-  const char* ge = getenv("SQMP_H2_GROUP_M");
+  const char* ge = knob("SQMP_H2_GROUP_M");
   const int gm = ge && atoi(ge) > 0 ? atoi(ge) : 4;
 #define SQMP_H2(CM, WN, BNV, TN)                                                                 \
   (k64 ? gemm_x3_kernel<CM, WN, true, BNV, 64><<<tiles_m * TN, 128 * WN, 0, (hipStream_t)stream>>>( \

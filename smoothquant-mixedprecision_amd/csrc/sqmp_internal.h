@@ -6,15 +6,19 @@
 
 namespace sqmp {
 
+// The value of launch knob `name` (an SQMP_* environment variable, read once at library load
+// and again by sqmp_reload_knobs; sqmp_knobs.hip), or NULL when unset.
+const char* knob(const char* name);
+
 // Whether a GEMM stores its output with non-temporal (streaming) stores.  An output larger
 // than a quarter of the 256-MiB Infinity Cache left dirty there is written back to HBM during
 // the kernels that follow -- at config 2 the next forward's prepass, which then shares HBM
 // with 134 MB of write-back.  Same-box step A/B (GEMM time unchanged;
 // profiles/r03_step_ab_nt.txt): per_group 523.1 -> 502.3 us, per_token 359.9 -> 351.2 us,
 // fp32 2068 -> 2044 us.  Smaller outputs stay cached for their consumer.
-// SQMP_NT_STORES = 0 / 1 forces it off / on (read per launch).
+// SQMP_NT_STORES = 0 / 1 forces it off / on.
 inline bool nt_output(size_t bytes) {
-  if (const char* e = getenv("SQMP_NT_STORES")) return atoi(e) != 0;
+  if (const char* e = knob("SQMP_NT_STORES")) return atoi(e) != 0;
   return bytes >= ((size_t)64 << 20);
 }
 

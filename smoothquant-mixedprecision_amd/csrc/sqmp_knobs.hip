@@ -1,0 +1,47 @@
+// Launch-variant knobs (the SQMP_* A/B and tuning variables of DESIGN.md §7): read ONCE, when
+// the library is loaded, into a table; the launchers look values up there instead of calling
+// getenv per launch.  sqmp_reload_knobs() re-reads the environment: the in-process A/B tools
+// (tools/ab_*.py, tools/step_ab.py) and the tests that switch a variant call it after changing
+// os.environ.
+#include <stdlib.h>
+#include <string.h>
+
+#include "sqmp_internal.h"
+
+namespace sqmp {
+
+static const char* const kKnobs[] = {
+    "SQMP_NT_STORES",   "SQMP_RANK_TABLE_OFF", "SQMP_RT_TPO",      "SQMP_RT_R",
+    "SQMP_RT_SB",       "SQMP_RT_BUCKET",      "SQMP_RT_BTPO",     "SQMP_DISABLE_LC",
+    "SQMP_LC_PERCU",    "SQMP_PW_RB",          "SQMP_C4_QPERCU",   "SQMP_F32_WN2",
+    "SQMP_F8_V1",       "SQMP_GROUP_M",        "SQMP_F8_OPT",      "SQMP_F8_DIAG",
+    "SQMP_FQ7_GROUP_M", "SQMP_FQT7_GROUP_M",   "SQMP_FQ7_OPT",     "SQMP_FQT7_OPT",
+    "SQMP_FQ7_DIAG",    "SQMP_FQ7G_TM",        "SQMP_H2D_GROUP_M", "SQMP_H2_WIDE",
+    "SQMP_H2_BK64",     "SQMP_H2_GROUP_M",     "SQMP_COLMAX_RPB",  "SQMP_FQA_RB",
+    "SQMP_FQA_DIAG",
+};
+constexpr int NKNOBS = (int)(sizeof(kKnobs) / sizeof(kKnobs[0]));
+static char* g_knob[NKNOBS];
+
+static void load_knobs() {
+  for (int i = 0; i < NKNOBS; ++i) {
+    free(g_knob[i]);
+    const char* e = getenv(kKnobs[i]);
+    g_knob[i] = e ? strdup(e) : nullptr;
+  }
+}
+
+__attribute__((constructor)) static void knobs_at_load() { load_knobs(); }
+
+const char* knob(const char* name) {
+  for (int i = 0; i < NKNOBS; ++i)
+    if (strcmp(name, kKnobs[i]) == 0) return g_knob[i];
+  return nullptr;  // (a name missing from the table reads as unset)
+}
+
+}  // namespace sqmp
+
+extern "C" int sqmp_reload_knobs(void) {
+  sqmp::load_knobs();
+  return SQMP_OK;
+}

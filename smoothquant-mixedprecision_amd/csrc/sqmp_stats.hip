@@ -73,7 +73,7 @@ static void colmax_launch(const void* x, int R, int C, uint32_t* cmax, hipStream
   // fewer atomics per column; profiles/r03_prepass_sweep.txt)
   while (rows_per_block > 32 && (long)cblocks_v * cdiv(R, rows_per_block) < 1024)
     rows_per_block >>= 1;
-  if (const char* e = getenv("SQMP_COLMAX_RPB")) rows_per_block = atoi(e);
+  if (const char* e = knob("SQMP_COLMAX_RPB")) rows_per_block = atoi(e);
   dim3 block(256);
   if (vec_ok) {
     dim3 grid(cblocks_v, cdiv(R, rows_per_block));

@@ -26,7 +26,7 @@ ACT_PER_GROUP_MEAN3STD = 4
 W_PER_CHANNEL, W_PER_TENSOR, W_PER_GROUP, W_PER_GROUP_UNSORTED, W_NONE = 0, 1, 2, 3, 4
 W_PER_GROUP_MEAN3STD = 5
 OUT_FP, OUT_I8, OUT_INPLACE, OUT_F8, OUT_C4, OUT_H2 = 0, 1, 2, 3, 5, 6
-QA_CLEAN_WS, QA_REUSE_STATS, QA_STATS_GIVEN, QA_TILED, QA_TILED4, QA_TILED32 = 1, 2, 4, 8, 16, 32
+QA_CLEAN_WS, QA_REUSE_STATS, QA_STATS_GIVEN, QA_TILED, QA_TILED4 = 1, 2, 4, 8, 16
 QA_WPT = 64
 
 _vp, _i, _sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t
@@ -77,8 +77,6 @@ SIGNATURES = {
     "sqmp_permute_act": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _vp]),
     "sqmp_gemm_fqt7j": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _vp,
                              _vp]),
-    "sqmp_gemm_fqt8": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _vp, _vp]),
-    "sqmp_gemm_fqt9": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _vp]),
     "sqmp_gemm_fqt7_colmax": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i,
                                    _vp, _vp]),
     "sqmp_fq7_sizes": (_i, [_i, _i, _i, _i, _i, ctypes.POINTER(_sz), ctypes.POINTER(_sz),
@@ -93,6 +91,7 @@ SIGNATURES = {
     "sqmp_gemm_fqa": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _vp,
                            _vp]),
     "sqmp_fqa_wpt_elems": (_sz, [_i, _i, _i]),
+    "sqmp_reload_knobs": (_i, []),
     "sqmp_pack_wpt": (_i, [_vp, _i, _i, _i, _vp, _vp]),
     "sqmp_split2_f16": (_i, [_vp, _i, _i, _i, _vp, _vp, _vp]),
     "sqmp_row_exp": (_i, [_vp, _i, _i, _vp, _vp]),
@@ -144,3 +143,10 @@ def check(status: int, what: str):
 
 def version() -> str:
     return load().sqmp_version().decode()
+
+
+def reload_knobs():
+    """Re-read the library's SQMP_* launch knobs (read once at load) after os.environ changed:
+    the in-process A/B tools and the tests that switch a launch variant call this."""
+    if _lib is not None:
+        _lib.sqmp_reload_knobs()

@@ -487,6 +487,13 @@ class W4A4Linear(nn.Module):
         if x.device.type != "cuda":
             raise RuntimeError("W4A4Linear.forward runs on a ROCm GPU only (HIP kernels); "
                                f"got a tensor on {x.device}")
+        if x2.shape[0] == 0:
+            # an empty batch: nothing to quantize or multiply (the kernels take no 0-row
+            # operands: a 0-element tensor has no device pointer)
+            pw = self.packed()
+            if x2.dtype != pw.dtype:
+                raise RuntimeError(f"expected input dtype {pw.dtype}, got {x2.dtype}")
+            return x.new_empty(tuple(x_shape[:-1]) + (self.out_features,))
         grp = self.__dict__.get("_sqmp_group")
         if grp is not None:
             y = grp.forward(self, x, x2)

@@ -459,20 +459,13 @@ FQT7 = os.environ.get("SQMP_FQT7", "1") == "1"
 # its register operand's row tiles per wave: 2 (256 weight rows x 256 tokens per tile) or 4
 # (128 x 512: half the permuted-weight LDS traffic per MFMA, twice the act-code decode)
 FQT7_J = int(os.environ.get("SQMP_FQT7_J", "2"))
-# the one-wave-per-SIMD activation-order GEMM (sqmp_gemm_fqt8) on the J = 4 operands
-FQT8 = os.environ.get("SQMP_FQT8", "0") == "1"
-# the one-wave-per-SIMD activation-order GEMM on the 32x32x16 MFMA (sqmp_gemm_fqt9) on the
-# SQMP_QA_TILED32 operands
-FQT9 = os.environ.get("SQMP_FQT9", "0") == "1"
 # the activation-order GEMM with the act codes decoded once per workgroup into LDS and the
 # permuted weight in registers (sqmp_gemm_fqa on the row-major act operands + SQMP_QA_WPT)
 FQA = os.environ.get("SQMP_FQA", "0") == "1"
 
 
 def _fqt_j() -> int:
-    """Tile-major operand layout of the activation-order path: 4 under FQT8, else FQT7_J."""
-    if FQT8:
-        return 4
+    """Tile-major operand layout of the activation-order path (FQT7_J: 2 or 4)."""
     return FQT7_J if FQT7_J in (2, 4) else 2
 
 
@@ -509,13 +502,7 @@ def quant_act_c4(x2: torch.Tensor, pw: PackedWeight, act_quant: str, n_bits: int
     fqa = FQA
     tiled = FQT7 and Kq % 128 == 0 and not fqa
     tj = _fqt_j()
-    t32 = tiled and FQT9
-    if t32:
-        R = max(256, (M + 255) // 256 * 256)
-        codes = torch.empty((R, Kq // 2), dtype=torch.uint8, device=dev)
-        scales = torch.empty((R // 64, ngq, 32, 2), dtype=x2.dtype, device=dev)  # 4-d: TILED32
-        xs = torch.empty((R, max(pw.S_pad, 64)), dtype=x2.dtype, device=dev)[:M]
-    elif tiled:
+    if tiled:
         R = max(128 * tj, (M + 128 * tj - 1) // (128 * tj) * (128 * tj))
         codes = torch.empty((R, Kq // 2), dtype=torch.uint8, device=dev)
         scales = torch.empty((R // (16 * tj), ngq, 16 * tj), dtype=x2.dtype, device=dev)
@@ -528,8 +515,7 @@ def quant_act_c4(x2: torch.Tensor, pw: PackedWeight, act_quant: str, n_bits: int
     nb = _ws_bytes(M, K, pw.Kp)
     stream = torch.cuda.current_stream(dev).cuda_stream
     e = _act_ws(dev, stream, K, pw.Kp, nb)
-    flags = _lib.QA_CLEAN_WS | (_lib.QA_TILED32 if t32 else
-                                ((_lib.QA_TILED4 if tj == 4 else _lib.QA_TILED) if tiled else 0))
+    flags = _lib.QA_CLEAN_WS | ((_lib.QA_TILED4 if tj == 4 else _lib.QA_TILED) if tiled else 0)
     src = x2 if stats_of is None else stats_of
     skey = (src.data_ptr(), tuple(src.shape), src.dtype, src._version, pw.sal_key, act_quant,
             M, K)
@@ -576,18 +562,6 @@ def gemm_fqt(codes: torch.Tensor, scales: torch.Tensor, xs: torch.Tensor, wp: to
                                    _p(bias), _p(y), _dtype_code(pw.dtype), M, pw.N, Kq,
                                    pw.S_pad, group_size, scales.shape[1], _p(colmax),
                                    _stream(codes)), "gemm_fqa")
-        return y
-    if scales.dim() == 4:   # SQMP_QA_TILED32
-        if colmax is not None:
-            raise ValueError("gemm_fqt: the TILED32 GEMM has no fused column statistics")
-        check(load().sqmp_gemm_fqt9(_p(codes), _p(scales), _p(xs), _p(wp), _p(bias), _p(y),
-                                    _dtype_code(pw.dtype), M, pw.N, Kq, pw.S_pad, group_size,
-                                    scales.shape[1], _stream(codes)), "gemm_fqt9")
-        return y
-    if scales.dim() == 3 and scales.shape[2] == 64 and FQT8:
-        check(load().sqmp_gemm_fqt8(_p(codes), _p(scales), _p(xs), _p(wp), _p(bias), _p(y),
-                                    _dtype_code(pw.dtype), M, pw.N, Kq, pw.S_pad, group_size,
-                                    scales.shape[1], _p(colmax), _stream(codes)), "gemm_fqt8")
         return y
     if scales.dim() == 3:   # tile-major (SQMP_QA_TILED: 32-row blocks, TILED4: 64-row)
         check(load().sqmp_gemm_fqt7j(_p(codes), _p(scales), _p(xs), _p(wp), _p(bias), _p(y),

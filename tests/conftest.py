@@ -10,3 +10,17 @@ for p in (ROOT, PKG):
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a ROCm MI355X device (run on the GPU box)")
+
+
+import pytest  # noqa: E402
+
+
+@pytest.fixture(autouse=True)
+def _library_knobs_follow_env():
+    """The library reads its SQMP_* launch knobs once (sqmp_knobs.hip): a test that switches a
+    variant through os.environ / monkeypatch gets them re-read on entry to its calls via
+    smoothquant._lib.reload_knobs, and every test starts and ends with the environment's."""
+    from smoothquant import _lib
+    _lib.reload_knobs()
+    yield
+    _lib.reload_knobs()

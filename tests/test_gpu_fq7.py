@@ -158,13 +158,16 @@ def test_fq7_variants_bit_identical(env, vals, M, K, N):
     try:
         for v in vals:
             os.environ[env] = v
+            __import__("smoothquant._lib", fromlist=["_lib"]).reload_knobs()  # (knobs are read once at load)
             cm = torch.zeros(pw.N + 8, dtype=torch.int32, device=dev)
             outs.append((ops.gemm_fq7(a, pw, lin.bias, cm), cm))
     finally:
         if old is None:
             os.environ.pop(env, None)
+            __import__("smoothquant._lib", fromlist=["_lib"]).reload_knobs()  # (knobs are read once at load)
         else:
             os.environ[env] = old
+            __import__("smoothquant._lib", fromlist=["_lib"]).reload_knobs()  # (knobs are read once at load)
     y0, c0 = outs[0]
     assert rel(y0, _ref(a, pw, lin.bias)) < TOL[torch.float16]
     for y, c in outs[1:]:

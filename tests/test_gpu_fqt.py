@@ -349,87 +349,3 @@ def test_standalone_perm_matches_fused():
                                     ctypes.c_void_p(stream))
     assert st == 0
     assert torch.equal(wp.view(torch.int16), wp2.view(torch.int16))
-
-
-@pytest.mark.parametrize("M,K,N,Gs,p,dt,aq", CASES + [(4096, 4096, 4096, 128, 0.10, torch.float16, "per_group")])
-def test_fqt8_matches_fqt7j(M, K, N, Gs, p, dt, aq):
-    """sqmp_gemm_fqt8 (one wave per SIMD) on the SQMP_QA_TILED4 operands == sqmp_gemm_fqt7j
-    (J = 4) on the same operands, bit for bit (the same MFMA sequence per output), the fused
-    column statistics too; test_fqt_operands_exact_and_y pins fqt7j against the oracle."""
-    dev = _dev()
-    from smoothquant import ops
-    q, lin, x = _layer(dev, M, K, N, Gs, p, dt, aq=aq)
-    pw = q.packed()
-    Kq = (pw.K - pw.S + 63) // 64 * 64
-    if Kq % 128:
-        pytest.skip("tile-major operands need Kq % 128 == 0")
-    saved = ops.FQT7, ops.FQT7_J, ops.FQT8
-    ops.FQT7, ops.FQT7_J, ops.FQT8 = True, 4, False
-    try:
-        codes, scales, xs, wp = ops.quant_act_c4(x, pw, aq, 4, Gs)
-        assert scales.shape[2] == 64
-        c7 = torch.zeros(pw.N, dtype=torch.int32, device=dev)
-        y7 = ops.gemm_fqt(codes, scales, xs, wp, pw, lin.bias, Gs, colmax=c7)
-        ops.FQT8 = True
-        c8 = torch.zeros(pw.N, dtype=torch.int32, device=dev)
-        y8 = ops.gemm_fqt(codes, scales, xs, wp, pw, lin.bias, Gs, colmax=c8)
-        y8n = ops.gemm_fqt(codes, scales, xs, wp, pw, None, Gs)
-    finally:
-        ops.FQT7, ops.FQT7_J, ops.FQT8 = saved
-    assert torch.equal(y7.view(torch.int16), y8.view(torch.int16))
-    assert torch.equal(c7, c8)
-    b = lin.bias.detach().float() if lin.bias is not None else 0.0
-    assert rel(y8n.float() + b, y8.float()) < 2e-2
-
-
-def untile_c4_32(codes_t, scales_t, xs_t, M, Kq, S_pad):
-    """SQMP_QA_TILED32 operands (64-row blocks; lane 32 h + r holds row 32 j + r at positions
-    16 s + 8 h .. + 7 of a 64-position stage) -> row-major codes [M, Kq/2] (dword h * 4 + s of a
-    stage), scales [ngq, R], xs [M, S_pad]."""
-    R = codes_t.shape[0]
-    KB = Kq // 64
-    w = codes_t.contiguous().view(torch.int32).reshape(R // 64, KB, 2, 32, 4, 2)  # nb kb h r s j
-    codes = w.permute(0, 5, 3, 1, 2, 4).reshape(R, KB * 8).contiguous().view(torch.uint8)[:M]
-    ngq = scales_t.shape[1]
-    scales = scales_t.permute(1, 0, 3, 2).reshape(ngq, R)
-    xs = None
-    if S_pad:
-        W = xs_t.stride(0)
-        flat = torch.as_strided(xs_t, (R * W,), (1,))[: R * S_pad]
-        t = flat.reshape(R // 64, S_pad // 64, 2, 32, 4, 2, 8)          # nb kd h r s j e
-        xs = t.permute(0, 5, 3, 1, 4, 2, 6).reshape(R, S_pad)[:M]
-    return codes, scales, xs
-
-
-@pytest.mark.parametrize("M,K,N,Gs,p,dt,aq", CASES + [(16384, 4096, 4096, 128, 0.10, torch.float16, "per_group")])
-def test_fqt9_operands_and_y(M, K, N, Gs, p, dt, aq):
-    """sqmp_gemm_fqt9 (one wave per SIMD, 32x32x16 MFMA) on the SQMP_QA_TILED32 operands: the
-    operands equal the SQMP_QA_TILED ones element for element (untiled both ways; fqt7's
-    operands are pinned to the oracle in test_fqt_operands_exact_and_y), and y equals fqt7's
-    within the accumulation-order tolerance."""
-    dev = _dev()
-    from smoothquant import ops
-    q, lin, x = _layer(dev, M, K, N, Gs, p, dt, aq=aq)
-    pw = q.packed()
-    Kq = (pw.K - pw.S + 63) // 64 * 64
-    if Kq % 128:
-        pytest.skip("tile-major operands need Kq % 128 == 0")
-    saved = ops.FQT7, ops.FQT7_J, ops.FQT8, ops.FQT9
-    try:
-        ops.FQT7, ops.FQT7_J, ops.FQT8, ops.FQT9 = True, 2, False, False
-        c7 = ops.quant_act_c4(x, pw, aq, 4, Gs)
-        y7 = ops.gemm_fqt(*c7, pw, lin.bias, Gs)
-        ops.FQT9 = True
-        c9 = ops.quant_act_c4(x, pw, aq, 4, Gs)
-        assert c9[1].dim() == 4
-        y9 = ops.gemm_fqt(*c9, pw, lin.bias, Gs)
-    finally:
-        ops.FQT7, ops.FQT7_J, ops.FQT8, ops.FQT9 = saved
-    a7 = untile_c4(c7[0], c7[1], c7[2], M, Kq, pw.S_pad)
-    a9 = untile_c4_32(c9[0], c9[1], c9[2], M, Kq, pw.S_pad)
-    assert torch.equal(a7[0], a9[0])
-    assert torch.equal(a7[1][:, :M].view(torch.int16), a9[1][:, :M].view(torch.int16))
-    if pw.S_pad:
-        assert torch.equal(a7[2].view(torch.int16), a9[2].view(torch.int16))
-    assert torch.equal(c7[3].view(torch.int16), c9[3].view(torch.int16))
-    assert rel(y9, y7) < (1e-3 if dt == torch.float16 else 8e-3)

@@ -64,6 +64,7 @@ def test_group_gemm_equals_own(tm, M, K, Ns, G, p, dt, monkeypatch):
     dev = _dev()
     from smoothquant import ops
     monkeypatch.setenv("SQMP_FQ7G_TM", tm)
+    __import__("smoothquant._lib", fromlist=["_lib"]).reload_knobs()  # (knobs are read once at load)
     layers, x = _siblings(dev, M, K, Ns, G, p, dt, seed=5)
     pws = [q.packed() for q in layers]
     a = ops.quant_act_fp_group(x, pws, "per_group", 4, G)
@@ -158,7 +159,9 @@ def test_stash_not_returned_after_member_changes():
         m.__dict__.pop("_sqmp_group")
     assert torch.equal(_bits(y2), _bits(layers2[2](x2)))
     # (3) output quantization switched on for k after q's call
-    layers3, x3 = _siblings(dev, 256, 1024, (512, 512, 512), 64, 0.05, torch.float16, seed=13)
+    # (N == K: with salient channels the reference's output quantizer indexes y's columns by
+    # the input's salient mask, fake_quant.py:311-314)
+    layers3, x3 = _siblings(dev, 256, 1024, (1024, 1024, 1024), 64, 0.05, torch.float16, seed=13)
     fq.link_siblings(*layers3)
     layers3[0](x3)
     layers3[1].output_quant = layers3[1].act_quant

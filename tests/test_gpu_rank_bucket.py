@@ -41,9 +41,11 @@ def test_bucketed_rank_bit_identical(M, K, Ns, G, p, dt, kind, btpo, monkeypatch
     x = _inputs(kind, x).contiguous()
     pws = [q.packed() for q in layers]
     monkeypatch.setenv("SQMP_RT_BTPO", btpo)
+    __import__("smoothquant._lib", fromlist=["_lib"]).reload_knobs()  # (knobs are read once at load)
     outs = {}
     for on in ("0", "1"):
         monkeypatch.setenv("SQMP_RT_BUCKET", on)
+        __import__("smoothquant._lib", fromlist=["_lib"]).reload_knobs()  # (knobs are read once at load)
         if len(pws) > 1:
             outs[on] = [a.clone() for a in ops.quant_act_fp_group(x, pws, "per_group", 4, G)]
         else:

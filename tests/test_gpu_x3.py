@@ -174,12 +174,15 @@ def test_h2_raster_groups_bit_identical(M, N):
     try:
         for g in ("4", "1", "8", "32"):
             os.environ["SQMP_H2_GROUP_M"] = g
+            __import__("smoothquant._lib", fromlist=["_lib"]).reload_knobs()  # (knobs are read once at load)
             ys.append(ops.gemm_h2(a, pw, None))
     finally:
         if old is None:
             os.environ.pop("SQMP_H2_GROUP_M", None)
+            __import__("smoothquant._lib", fromlist=["_lib"]).reload_knobs()  # (knobs are read once at load)
         else:
             os.environ["SQMP_H2_GROUP_M"] = old
+            __import__("smoothquant._lib", fromlist=["_lib"]).reload_knobs()  # (knobs are read once at load)
     for y in ys[1:]:
         assert torch.equal(y.view(torch.int32), ys[0].view(torch.int32))
 

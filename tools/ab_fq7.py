@@ -31,6 +31,7 @@ for (M, K, N, G, p) in SHAPES:
     ref = None
     for v in vals:
         os.environ[var] = v
+        __import__("smoothquant._lib", fromlist=["_lib"]).reload_knobs()  # (knobs are read once at load)
         y = run()
         torch.cuda.synchronize()
         if ref is None:
@@ -40,6 +41,7 @@ for (M, K, N, G, p) in SHAPES:
     for _ in range(rounds):
         for v in vals:
             os.environ[var] = v
+            __import__("smoothquant._lib", fromlist=["_lib"]).reload_knobs()  # (knobs are read once at load)
             for _ in range(10):
                 run()
             a0, b0 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

@@ -4,9 +4,9 @@ variants.  python tools/ab_fqt7.py [variants, "+"- or comma-separated] [rounds] 
 ENV (default SQMP_FQT7_OPT) names the per-launch variable; SQMP_FQ7_DIAG selects the timing
 diagnostics of a SQMP_DIAG=1 build (wrong results by design: no equality check then).  A
 variant "J4:3" runs the 64-row-block operands (ops.FQT7_J = 4) with value 3; "P..." times the
-prepass (quant_act_c4) of that variant instead of the GEMM; "F8:v" runs sqmp_gemm_fqt8 (one
-wave per SIMD) on the J = 4 operands, "F9:v" sqmp_gemm_fqt9 (one wave per SIMD, 32x32x16 MFMA) on
-the TILED32 operands."""
+prepass (quant_act_c4) of that variant instead of the GEMM; "A" runs sqmp_gemm_fqa (act codes
+decoded once per workgroup into LDS) on its own operands.  (The one-wave-per-SIMD fqt8 / fqt9
+variants were removed in round 5: profiles/r04_ab_fqt8.txt, r04_ab_fqt9.txt.)"""
 import os
 import sys
 
@@ -30,18 +30,15 @@ stream = torch.cuda.current_stream(dev)
 def parse(v):
     pre = v.startswith("P")
     v = v[1:] if pre else v
-    if v.startswith("F8"):
-        return pre, 8, v[3:] or "0"
-    if v.startswith("F9"):
-        return pre, 9, v[3:] or "0"
+    if v.startswith("A"):
+        return pre, 0, v[2:] or "0"
     j, val = (int(v[1:v.index(":")]), v[v.index(":") + 1:]) if v.startswith("J") else (2, v)
     return pre, j, val
 
 
 def use(j):
-    ops.FQT8 = j == 8
-    ops.FQT9 = j == 9
-    ops.FQT7_J = 4 if j == 8 else (2 if j == 9 else j)
+    ops.FQA = j == 0
+    ops.FQT7_J = j if j in (2, 4) else 2
 
 
 ops_c4 = {}
@@ -68,6 +65,7 @@ def runner(v):
 ref = None
 for v in variants:
     os.environ[ENV] = parse(v)[2]
+    __import__("smoothquant._lib", fromlist=["_lib"]).reload_knobs()  # (knobs are read once at load)
     run = runner(v)
     y = run()
     if parse(v)[0]:
@@ -75,7 +73,7 @@ for v in variants:
     torch.cuda.synchronize()
     if ref is None:
         ref = y.clone()
-    if parse(v)[1] == 9:  # another accumulation order (32x32x16 MFMA): tolerance, not bits
+    if parse(v)[1] == 0:  # fqa: another accumulation order -- tolerance, not bits
         assert float((y.float() - ref.float()).norm() / ref.float().norm()) < 1e-3, f"variant {v} changed y"
     else:
         assert ENV.endswith("_DIAG") or torch.equal(y.view(torch.int16), ref.view(torch.int16)), f"variant {v} changed y"
@@ -89,6 +87,7 @@ flops = 2.0 * bench.M * bench.N * bench.K
 for r in range(rounds):
     for v in variants:
         os.environ[ENV] = parse(v)[2]
+        __import__("smoothquant._lib", fromlist=["_lib"]).reload_knobs()  # (knobs are read once at load)
         run = runner(v)
         for _ in range(10):
             run()

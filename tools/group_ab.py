@@ -37,6 +37,7 @@ for rnd in range(3):
         for combo in combos:
             for (k, _), v in zip(axes, combo):
                 os.environ[k] = v
+                __import__("smoothquant._lib", fromlist=["_lib"]).reload_knobs()  # (knobs are read once at load)
             tag = " ".join(f"{k}={v}" for (k, _), v in zip(axes, combo)) or "default"
             fn = lambda: ops.gemm_fq7_group(a, pws, [None] * len(pws))  # noqa: E731
             for _ in range(3):
@@ -44,6 +45,7 @@ for rnd in range(3):
             res.setdefault((name, tag), []).append(bench.time_events(fn, iters, stream) * 1e3)
         for k, _ in axes:
             os.environ.pop(k, None)
+            __import__("smoothquant._lib", fromlist=["_lib"]).reload_knobs()  # (knobs are read once at load)
         own = lambda: [ops.gemm_fq7(ai, pw, None) for ai, pw in zip(a, pws)]  # noqa: E731
         for _ in range(3):
             own()

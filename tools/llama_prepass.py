@@ -39,6 +39,7 @@ stream = torch.cuda.current_stream(dev)
 for combo in itertools.product(*[v for _, v in axes]) if axes else [()]:
     for (k, _), v in zip(axes, combo):
         os.environ[k] = v
+        __import__("smoothquant._lib", fromlist=["_lib"]).reload_knobs()  # (knobs are read once at load)
     tag = " ".join(f"{k}={v}" for (k, _), v in zip(axes, combo)) or "default"
     res = []
     for K, x, pw in cases:

@@ -34,6 +34,7 @@ for name, K, Ns in (("qkv", 4096, (4096, 4096, 4096)), ("o", 4096, (4096,)),
 for combo in itertools.product(*[v for _, v in axes]) if axes else [()]:
     for (k, _), v in zip(axes, combo):
         os.environ[k] = v
+        __import__("smoothquant._lib", fromlist=["_lib"]).reload_knobs()  # (knobs are read once at load)
     tag = " ".join(f"{k}={v}" for (k, _), v in zip(axes, combo)) or "default"
     for M in Ms:
         for name, pws, x in cases:

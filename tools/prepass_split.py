@@ -87,6 +87,7 @@ if len(sys.argv) > 2:
     for combo in itertools.product(*[v for _, v in axes]):
         for (k, _), v in zip(axes, combo):
             os.environ[k] = v
+            __import__("smoothquant._lib", fromlist=["_lib"]).reload_knobs()  # (knobs are read once at load)
         wp.zero_()
         perm_only()
         torch.cuda.synchronize()

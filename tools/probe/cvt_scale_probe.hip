@@ -82,5 +82,78 @@ int main() {
     printf("%s: %ld mismatches over %d normal scales x 15 codes, %ld over 64 subnormal scales\n",
            which ? "pk32_f16_fp6" : "pk_f16_fp8", bad, ns - 64, bad_sub);
   }
+  int thr_main();
+  return thr_main();
+}
+
+// ---- throughput: cycles per 32 decoded values for one wave per SIMD (s_memtime), three forms
+// (result folded into a checksum so nothing is dead)
+typedef unsigned u4 __attribute__((ext_vector_type(4)));
+template <int FORM>
+__global__ void thr(const unsigned* in, unsigned* out, long* cyc, int iters, float s) {
+  unsigned w0 = in[threadIdx.x], w1 = in[threadIdx.x + 64], w2 = in[threadIdx.x + 128];
+  unsigned acc = 0;
+  const _Float16 sh = (_Float16)s;
+  h2 s2 = {sh, sh};
+  const long t0 = clock64();
+  for (int it = 0; it < iters; ++it) {
+    if (FORM == 0) {  // 13 VALU per 8 int4 codes (the current Dec<F16>::run), x4
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        const unsigned w = w0 + d, t = w >> 8;
+        unsigned b[4] = {(w & 0x000F000Fu) | 0x64006400u, (w & 0x00F000F0u) | 0x54005400u,
+                         (t & 0x000F000Fu) | 0x64006400u, (t & 0x00F000F0u) | 0x54005400u};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          h2 hv = __builtin_bit_cast(h2, b[i]);
+          const h2 o = (i & 1) ? h2{(_Float16)72.f, (_Float16)72.f} : h2{(_Float16)1032.f, (_Float16)1032.f};
+          hv = (hv - o) * s2;
+          acc ^= __builtin_bit_cast(unsigned, hv);
+        }
+      }
+    } else if (FORM == 1) {  // cvt_scalef32_pk_f16_fp8: 16 per 32 codes
+#pragma unroll
+      for (int d = 0; d < 8; ++d) {
+        const unsigned w = w0 + d;
+        h2 a = __builtin_amdgcn_cvt_scalef32_pk_f16_fp8(w, s, false);
+        h2 b = __builtin_amdgcn_cvt_scalef32_pk_f16_fp8(w, s, true);
+        acc ^= __builtin_bit_cast(unsigned, a) ^ __builtin_bit_cast(unsigned, b);
+      }
+    } else {  // cvt_scalef32_pk32_f16_fp6: 1 per 32 codes
+      u6 p = {w0 + it, w1, w2, w0 ^ w1, w1 ^ w2, w2 ^ w0};
+      h32 r = __builtin_amdgcn_cvt_scalef32_pk32_f16_fp6(p, s);
+#pragma unroll
+      for (int e = 0; e < 32; e += 2) acc ^= __builtin_bit_cast(unsigned, h2{r[e], r[e + 1]});
+    }
+    w0 += acc & 1;
+  }
+  const long t1 = clock64();
+  out[blockIdx.x * blockDim.x + threadIdx.x] = acc;
+  if (threadIdx.x == 0) cyc[blockIdx.x] = t1 - t0;
+}
+
+int thr_main() {
+  unsigned *din, *dout;
+  long* dc;
+  hipMalloc(&din, 4096);
+  hipMalloc(&dout, 1 << 20);
+  hipMalloc(&dc, 1 << 12);
+  hipMemset(din, 0x37, 4096);
+  long hc[256];
+  const int iters = 4096;
+  const char* names[3] = {"int4 magic decode (13 VALU / 8)", "pk_f16_fp8 (1 / 2)", "pk32_f16_fp6 (1 / 32)"};
+  for (int f = 0; f < 3; ++f) {
+    for (int rep = 0; rep < 2; ++rep) {
+      // 256 blocks of one wave: about one wave per SIMD
+      if (f == 0) thr<0><<<256, 64>>>(din, dout, dc, iters, 0.37f);
+      if (f == 1) thr<1><<<256, 64>>>(din, dout, dc, iters, 0.37f);
+      if (f == 2) thr<2><<<256, 64>>>(din, dout, dc, iters, 0.37f);
+      hipDeviceSynchronize();
+    }
+    hipMemcpy(hc, dc, 256 * 8, hipMemcpyDeviceToHost);
+    long mn = hc[0];
+    for (int i = 1; i < 256; ++i) mn = hc[i] < mn ? hc[i] : mn;
+    printf("%-34s %.1f clock64 ticks per 32 values per wave\n", names[f], (double)mn / iters);
+  }
   return 0;
 }

@@ -26,6 +26,7 @@ for K, N in ((4096, 4096), (11008, 4096)):
     for combo in itertools.product(*[v for _, v in axes]) if axes else [()]:
         for (k, _), v in zip(axes, combo):
             os.environ[k] = v
+            __import__("smoothquant._lib", fromlist=["_lib"]).reload_knobs()  # (knobs are read once at load)
         tag = " ".join(f"{k}={v}" for (k, _), v in zip(axes, combo))
         line = []
         for M in (1024, 2048, 4096, 8192, 16384):

@@ -50,6 +50,7 @@ for name, M, K, Ns in (("qkv", 2048, 4096, (4096, 4096, 4096)), ("gate_up", 2048
     for _ in range(rounds):
         for tag, opt, fn in variants:
             os.environ["SQMP_FQ7_OPT"] = opt
+            __import__("smoothquant._lib", fromlist=["_lib"]).reload_knobs()  # (knobs are read once at load)
             for _ in range(5):
                 fn()
             a0, b0 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

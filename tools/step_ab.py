@@ -25,6 +25,7 @@ stream = torch.cuda.current_stream(dev)
 ref = None
 for v in vals:
     os.environ[var] = v
+    __import__("smoothquant._lib", fromlist=["_lib"]).reload_knobs()  # (knobs are read once at load)
     y = q(x)
     torch.cuda.synchronize()
     if ref is None:
@@ -35,6 +36,7 @@ flops = 2.0 * bench.M * bench.N * bench.K
 for _ in range(rounds):
     for v in vals:
         os.environ[var] = v
+        __import__("smoothquant._lib", fromlist=["_lib"]).reload_knobs()  # (knobs are read once at load)
         for _ in range(20):
             q(x)
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
