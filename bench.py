@@ -367,6 +367,12 @@ def llama_layer(dev, iters=40):
         "per_linear": {name: {"w4a4_ms": round(a, 4), "fp16_ms": round(b, 4),
                               "fp16_over_w4a4": round(b / a, 3)}
                        for (name, _, _, _), a, b in zip(LLAMA_LINEARS, pw4, pf16)},
+        # the sibling groups as units (their first member's time covers the whole group)
+        "per_group": {g: {"w4a4_ms": round(sum(pw4[i] for i in ix), 4),
+                          "fp16_ms": round(sum(pf16[i] for i in ix), 4),
+                          "fp16_over_w4a4": round(sum(pf16[i] for i in ix) / sum(pw4[i] for i in ix), 3)}
+                      for g, ix in (("qkv", (0, 1, 2)), ("o", (3,)), ("gate_up", (4, 5)),
+                                    ("down", (6,)))},
         "note": "median of 40 layer passes, best of 2 interleaved rounds; q/k/v and gate/up are "
                 "linked sibling groups (as quantize_llama_like links them): the first member's "
                 "time covers the group's one quantizer pass and one GEMM launch, the others "

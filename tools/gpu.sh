@@ -16,7 +16,7 @@
 #                    summarise with tools/pmc_summary.py
 #   e2e              bench_e2e.py per model (MODELS, E2E_ARGS env; configs 3, 4)
 #   sweep            bench_sweep.py (config 5)
-#   layer            bench_llama.py (config 4 end to end)
+#   layer            bench_e2e.py --model llama2-7b (config 4 end to end)
 #   py:SCRIPT[:ARGS] python SCRIPT ARGS (comma-separated args)
 #   profpy:SCRIPT[:ARGS]  the same under rocprofv3 --kernel-trace --stats
 #   trace:SCRIPT[:ARGS]   the same under rocprofv3 --kernel-trace (per-dispatch CSV)
