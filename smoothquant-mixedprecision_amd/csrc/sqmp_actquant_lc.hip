@@ -200,6 +200,24 @@ __device__ inline uint32_t f8_pair(uint32_t v, const PairScale& c) {
 
 }  // namespace
 
+// Timing stamps (SQMP_DIAG_BUILD only): thread 0 of quantizer workgroup b records the 100-MHz
+// real-time counter at kernel entry (0), after the prologue (1) and, for its first row pair,
+// after the interleave (2), the gather + statistics (3) and the quantize / scatter (4)
+// barriers and at the pair's end (5), and when it leaves (6); (7) once the salient mask's
+// loads (issued after the first pair's) have landed: tools/lc_stamps.py
+#ifdef SQMP_DIAG_BUILD
+__device__ unsigned long long sqmp_lc_stamps[8192][8];
+#define LC_STAMP(k)                                                   \
+  do {                                                                \
+    if (threadIdx.x == 0 && bid < 8192)                               \
+      sqmp_lc_stamps[bid][k] = __builtin_amdgcn_s_memrealtime();      \
+  } while (0)
+#else
+#define LC_STAMP(k) \
+  do {              \
+  } while (0)
+#endif
+
 // RPL = ranks per thread; GS = the group size when it is below RPL (RPL / GS groups per
 // thread), else 0.  blockDim = 64 * NW.  F8 = 1 (token / tensor modes): out is e4m3 codes
 // [M][P] (bytes), out_scale the fp32 row scales, out_xs the exact salient columns [M][S_pad].
@@ -262,6 +280,7 @@ __device__ __forceinline__ void quant_lc_body(
   const int xcd = bid & 7, per = nblk >> 3, rem = nblk & 7;
   const int wg = (xcd < rem ? xcd * (per + 1) : rem * (per + 1) + (xcd - rem) * per) + (bid >> 3);
   // (runs of floor or ceil(npair / nblk) pairs: every XCD gets an eighth of the rows)
+  LC_STAMP(0);
   const int rp_end = (int)((long)(wg + 1) * npair / nblk);
   int rp = (int)((long)wg * npair / nblk);
   if (rp < rp_end) load_pair(rp);
@@ -289,8 +308,16 @@ __device__ __forceinline__ void quant_lc_body(
     return zm;
   };
   const uint64_t zmask = zmask_of(amap);
+#ifdef SQMP_DIAG_BUILD
+  if (zmask == 0x5A5A5A5A5A5A5A5Aull) lc_buf[0] = 1u;  // (keeps the stamp behind zmask's loads)
+#endif
+  LC_STAMP(7);
   const int RW = W + 8;  // LDS region stride (words; a multiple of 8)
   for (int c = tid; c < (NOUT > 1 ? NOUT * RW : W + 2); c += nthr) lc_buf[c] = 0u;
+  // the salient columns' input positions, once per workgroup (every row pair gathers them:
+  // an LDS read instead of a dependent global load per pair)
+  uint32_t* const sal_l = lc_buf + NOUT * RW;
+  for (int j = tid; j < S; j += nthr) sal_l[j] = (uint32_t)sal[j];
   // the column statistics of this call, read by the (completed) table kernel: restore the
   // clean-workspace zeros
   if (key_clear)
@@ -309,6 +336,8 @@ __device__ __forceinline__ void quant_lc_body(
     tens = pair_scale<DT>(mb | (mb << 16), qmf, rqf);
   }
   __syncthreads();
+  LC_STAMP(1);
+  const int rp0 = rp;
 
   for (; rp < rp_end; ++rp) {
     const int m0 = 2 * rp;
@@ -358,13 +387,14 @@ __device__ __forceinline__ void quant_lc_body(
     // overlaps this pair's gather, quantization and stores (same VGPR count)
     if (rp + 1 < rp_end) load_pair(rp + 1);
     __syncthreads();
+    if (rp == rp0) LC_STAMP(2);
 
     // ---- gather; exact salient columns into the tail (>= K)
     uint32_t v[RPL];
 #pragma unroll
     for (int i = 0; i < RPL; ++i) v[i] = lc_buf[tab[i] & 0xFFFFu];
     for (int j = tid; j < S; j += nthr) {
-      const uint32_t xs = lc_buf[sal[j]];
+      const uint32_t xs = lc_buf[sal_l[j]];
       lc_buf[P + j] = xs;
 #pragma unroll
       for (int o = 1; o < NOUT; ++o) lc_buf[o * RW + P + j] = xs;  // the shared salient tail
@@ -373,6 +403,7 @@ __device__ __forceinline__ void quant_lc_body(
     // ---- scales, then quantize + scatter
     if (MODE == LC_MODE_GROUP && GS > 0) {
       __syncthreads();  // every gather done before the scatter below
+      if (rp == rp0) LC_STAMP(3);
 #pragma unroll
       for (int g = 0; g < RPL / (GS > 0 ? GS : RPL); ++g) {
         uint32_t mx = 0u;
@@ -398,6 +429,7 @@ __device__ __forceinline__ void quant_lc_body(
           }
         }
         __syncthreads();  // every gather done before the scatter below (+ token maxima)
+        if (rp == rp0) LC_STAMP(3);
         if (MODE == LC_MODE_TOKEN) {
           float m0f = 0.f, m1f = 0.f;
           for (int w = 0; w < NW; ++w) {
@@ -410,6 +442,7 @@ __device__ __forceinline__ void quant_lc_body(
         c = pair_scale<DT>(mx, qmf, rqf);
       } else {
         __syncthreads();
+        if (rp == rp0) LC_STAMP(3);
       }
       if (F8 == 3) {
         // ranks rb .. rb + 15 = positions 16 u .. 16 u + 15 of bpack block rb / 64: dwords u
@@ -517,6 +550,7 @@ __device__ __forceinline__ void quant_lc_body(
     if (F8 == 0)
       for (uint64_t zm = zmask; zm; zm &= zm - 1) lc_buf[zp0 + __builtin_ctzll(zm)] = 0u;
     __syncthreads();
+    if (rp == rp0) LC_STAMP(4);
 
     if (F8) {
       // exact salient columns -> out_xs [M][S_pad]
@@ -548,6 +582,7 @@ __device__ __forceinline__ void quant_lc_body(
         }
       }
       __syncthreads();  // the buffer is rewritten by the next pair
+      if (rp == rp0) LC_STAMP(5);
       continue;
     }
     // ---- de-interleave 16-B chunks and store both rows of every output
@@ -576,7 +611,9 @@ __device__ __forceinline__ void quant_lc_body(
       }
     }
     __syncthreads();  // the buffer is rewritten by the next pair
+    if (rp == rp0) LC_STAMP(5);
   }
+  LC_STAMP(6);
 }
 
 
@@ -641,6 +678,31 @@ __device__ __forceinline__ void perm_weight_pairs(const PermArgs& a, const uint3
     const int p0 = bpack_pos(d, 0);  // its 8 positions p0 .. p0 + 7 (one group: Gw % 8 == 0)
     const int g = min(p0 / a.Gw, a.ngw - 1);
     uint32_t w[8];
+    if constexpr (std::is_same<DT, F16>::value) {
+      // fp16: the GEMM's decode -- nibbles of elements 2k, 2k + 1 at bits 0 and 16 (bpack_shift),
+      // | 0x6400 = 1024 + nibble, - 1032 = code, * scale = D(code * scale) in one rounding (the
+      // product is exact before it), two rows per pk op; rows >= N stay +0
+      uint32_t pr[2][4];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int n = na + h;
+        const bool in = n < a.N;
+        const uint32_t c = in ? a.codes[(size_t)n * dw + d] : 0u;
+        const _Float16 s1 = in ? wscale[(size_t)g * a.Np + n] : (_Float16)0.f;
+        const h16x2 sc = {s1, s1};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const h16x2 f = __builtin_bit_cast(h16x2, ((c >> (4 * k)) & 0x000F000Fu) | 0x64006400u);
+          const h16x2 y = (f + (h16x2){(_Float16)-1032.f, (_Float16)-1032.f}) * sc;
+          pr[h][k] = in ? __builtin_bit_cast(uint32_t, y) : 0u;
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        w[2 * k] = __builtin_amdgcn_perm(pr[1][k], pr[0][k], 0x05040100u);
+        w[2 * k + 1] = __builtin_amdgcn_perm(pr[1][k], pr[0][k], 0x07060302u);
+      }
+    } else {
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int n = na + h;
@@ -657,6 +719,7 @@ __device__ __forceinline__ void perm_weight_pairs(const PermArgs& a, const uint3
         const uint32_t b = (uint32_t)__builtin_bit_cast(uint16_t, v);
         w[e] = h ? (w[e] | (b << 16)) : b;
       }
+    }
     }
     u32x4* dst = (u32x4*)(pw_lds + (size_t)r2 * Kp + p0);
     dst[0] = u32x4{w[0], w[1], w[2], w[3]};
@@ -782,6 +845,11 @@ __global__ __launch_bounds__(1024) void quant_c4_fused_kernel(
 
 constexpr int LC_RPL = 16;
 
+// dynamic LDS words of quant_lc_body: NOUT regions of P + S_pad + 8 words + the salient list
+static size_t lc_lds_words(int P, int S_pad, int nout) {
+  return (size_t)(P + S_pad + 8) * nout + S_pad;
+}
+
 // Workgroups of `block` threads and `lds` dynamic LDS bytes a CU holds at once for kernel f
 // (registers included: the C4 quantizer's 70 VGPRs allow 7 four-wave workgroups, not the 8
 // its LDS would), cached per (kernel, block, lds)
@@ -826,7 +894,7 @@ static int quant_lc_launch(const void* x, int M, int K, int q_max, int G, const 
   // F8: every packed position is some thread's (position-order table)
   if (F8 == 1 && cdiv(P, 64 * LC_RPL) > nw) nw = cdiv(P, 64 * LC_RPL);
   if (nw > LC_MAXW) return SQMP_EUNSUPPORTED;
-  const size_t lds = sizeof(uint32_t) * (size_t)(P + S_pad + 8) * NOUT;
+  const size_t lds = sizeof(uint32_t) * lc_lds_words(P, S_pad, NOUT);
   SQMP_HIP_CHECK(hipFuncSetAttribute(kf, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   int per_cu = occ_per_cu(kf, 64 * nw, lds);
   if (const char* e = knob("SQMP_LC_PERCU"))  // tuning only (0 / unparsable: the default)
@@ -844,7 +912,7 @@ bool quant_lc_supported(int dtype, int M, int K, int amode_group, int G, int Kn,
   if (dtype != SQMP_F16 && dtype != SQMP_BF16) return false;
   if (M <= 0 || K % 8 != 0 || K > 16384 || Kn > 16384 || P + S_pad >= 65536) return false;
   if (((uintptr_t)x) % 16 != 0 || ((uintptr_t)out) % 16 != 0) return false;
-  if ((size_t)4 * (P + S_pad + 8) > 150 * 1024) return false;
+  if ((size_t)4 * lc_lds_words(P, S_pad, 1) > 150 * 1024) return false;
   if (lc_waves(K, Kn) > LC_MAXW) return false;
   if (amode_group) {
     // power-of-two groups that never straddle a wave's 64 * RPL ranks; below RPL only 8
@@ -884,8 +952,8 @@ int launch_quant_lc_group(int dtype, const void* x, int M, int K, int q_max, int
                           const int32_t* nonsal, void* out, uint32_t* key_clear, int clear_words,
                           const LcSib& sib, hipStream_t s) {
   if (G < LC_RPL || sib.n < 0 || sib.n > 2) return SQMP_EUNSUPPORTED;
-  // one LDS region of P + S_pad + 8 words per output
-  if ((size_t)4 * (P + S_pad + 8) * (sib.n + 1) > 150 * 1024) return SQMP_EUNSUPPORTED;
+  // one LDS region of P + S_pad + 8 words per output (+ the salient list)
+  if ((size_t)4 * lc_lds_words(P, S_pad, sib.n + 1) > 150 * 1024) return SQMP_EUNSUPPORTED;
 #define SQMP_LCG(DTT, NO)                                                                     \
   quant_lc_launch<DTT, LC_MODE_GROUP, 0, 0, NO>(x, M, K, q_max, G, lctab, Kn, amap, P, sal, S, \
                                                S_pad, cmax, nonsal, out, key_clear,            \
@@ -957,7 +1025,7 @@ int launch_quant_lc_c4(int dtype, const void* x, int M, int K, int q_max, int G,
   // the permutation's rows: pad_n(N), or roundup(N, 512) for sqmp_gemm_fqa's layout (rows
   // past N hold zeros)
   const int Nrows = cw->wpt ? (int)round_up(cw->N, 512) : Np;
-  const size_t lq = sizeof(uint32_t) * (size_t)(P + S_pad + 8), lp = (size_t)RB * cw->Kp * 2;
+  const size_t lq = sizeof(uint32_t) * lc_lds_words(P, S_pad, 1), lp = (size_t)RB * cw->Kp * 2;
   const size_t lds = lq > lp ? lq : lp;
   const void* kf = dtype == SQMP_BF16 ? (const void*)quant_c4_fused_kernel<BF16>
                                        : (const void*)quant_c4_fused_kernel<F16>;
@@ -989,3 +1057,18 @@ int launch_quant_lc_c4(int dtype, const void* x, int M, int K, int q_max, int G,
 }
 
 }  // namespace sqmp
+
+#ifdef SQMP_DIAG_BUILD
+// the quantizer's timing stamps of the last launch (diagnostics build only)
+// (host == NULL: clear them)
+extern "C" int sqmp_diag_lc_stamps(unsigned long long* host, int nblk) {
+  if (nblk > 8192) nblk = 8192;
+  if (!host) {
+    void* d = nullptr;
+    if (hipGetSymbolAddress(&d, HIP_SYMBOL(sqmp::sqmp_lc_stamps)) != hipSuccess) return -3;
+    return hipMemset(d, 0, sizeof(unsigned long long) * 8 * 8192) == hipSuccess ? 0 : -3;
+  }
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(sqmp::sqmp_lc_stamps), sizeof(unsigned long long) * 8 * nblk, 0,
+                             hipMemcpyDeviceToHost) == hipSuccess ? 0 : -3;
+}
+#endif

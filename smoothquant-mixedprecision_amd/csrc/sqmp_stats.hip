@@ -10,16 +10,23 @@ namespace sqmp {
 // ------------------------------------------------------------------ column absmax
 // Block = 4 waves; a lane owns VEC consecutive columns (one 16-B load per row), the four
 // waves split the block's row chunk, partial maxima meet in LDS, then one global
-// atomicMax per column per block.
+// atomicMax per column per block.  1-D grid of cblocks x row-block tiles, row-block major,
+// dealt to the XCDs in contiguous eighths (blocks go round-robin over the 8 XCDs): XCD x
+// reads the rows the lane-contiguous quantizer's workgroups on XCD x read next (its row pairs
+// also come in contiguous eighths), so an input of up to 8 x 4 MiB is still in that XCD's L2
+// when the quantizer loads it.
 template <class DT, int VEC>
 __global__ __launch_bounds__(256) void colmax_kernel(const typename DT::T* __restrict__ x,
                                                      int R, int C, int rows_per_block,
-                                                     uint32_t* __restrict__ cmax) {
+                                                     int cblocks, uint32_t* __restrict__ cmax) {
   typedef typename DT::T T;
   __shared__ float red[4][64 * VEC];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int c0 = (blockIdx.x * 64 + lane) * VEC;
-  const int r0 = blockIdx.y * rows_per_block;
+  const int nb = gridDim.x, xcd = blockIdx.x & 7, per = nb >> 3, rem = nb & 7;
+  const int t = (xcd < rem ? xcd * (per + 1) : rem * (per + 1) + (xcd - rem) * per) + (blockIdx.x >> 3);
+  const int bx = t % cblocks, by = t / cblocks;
+  const int c0 = (bx * 64 + lane) * VEC;
+  const int r0 = by * rows_per_block;
   const int r1 = min(R, r0 + rows_per_block);
   float m[VEC];
 #pragma unroll
@@ -54,9 +61,9 @@ __global__ __launch_bounds__(256) void colmax_kernel(const typename DT::T* __res
 #pragma unroll
   for (int i = 0; i < VEC; ++i) red[wid][lane * VEC + i] = m[i];
   __syncthreads();
-  for (int t = threadIdx.x; t < 64 * VEC; t += 256) {
-    const float v = fmaxf(fmaxf(red[0][t], red[1][t]), fmaxf(red[2][t], red[3][t]));
-    const int c = blockIdx.x * 64 * VEC + t;
+  for (int u = threadIdx.x; u < 64 * VEC; u += 256) {
+    const float v = fmaxf(fmaxf(red[0][u], red[1][u]), fmaxf(red[2][u], red[3][u]));
+    const int c = bx * 64 * VEC + u;
     if (c < C && v > 0.f) atomicMax(&cmax[c], __float_as_uint(v));
   }
 }
@@ -75,12 +82,14 @@ static void colmax_launch(const void* x, int R, int C, uint32_t* cmax, hipStream
     rows_per_block >>= 1;
   if (const char* e = knob("SQMP_COLMAX_RPB")) rows_per_block = atoi(e);
   dim3 block(256);
+  const int rblocks = cdiv(R, rows_per_block);
   if (vec_ok) {
-    dim3 grid(cblocks_v, cdiv(R, rows_per_block));
-    colmax_kernel<DT, VEC><<<grid, block, 0, s>>>((const T*)x, R, C, rows_per_block, cmax);
+    colmax_kernel<DT, VEC><<<dim3(cblocks_v * rblocks), block, 0, s>>>(
+        (const T*)x, R, C, rows_per_block, cblocks_v, cmax);
   } else {
-    dim3 grid(cdiv(C, 64), cdiv(R, rows_per_block));
-    colmax_kernel<DT, 1><<<grid, block, 0, s>>>((const T*)x, R, C, rows_per_block, cmax);
+    const int cb = cdiv(C, 64);
+    colmax_kernel<DT, 1><<<dim3(cb * rblocks), block, 0, s>>>((const T*)x, R, C, rows_per_block,
+                                                             cb, cmax);
   }
 }
 

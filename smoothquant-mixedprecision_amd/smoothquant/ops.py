@@ -417,7 +417,7 @@ def group_eligible(pws, act_quant: str, act_bits: int, group_size: int, M: int) 
     """Whether quant_act_fp_group + gemm_fq7_group compute these sibling layers: sorted
     per_group activations of <= 8 bits in power-of-two groups of 16 .. 1024 on the
     packed-order path (below FQT_MIN_ROWS rows), 4-bit fq7 weights in whole 64-blocks per
-    group, 4 (Kp + S_pad + 8) bytes of quantizer LDS per member within 150 KiB, one K
+    group, 4 (Kp + S_pad + 8) bytes of quantizer LDS per member (+ 4 S_pad) within 150 KiB, one K
     (<= 16384, % 8 == 0) / Kp / S_pad / group geometry / salient set / dtype
     (fp16 / bf16) for all, 2 or 3 layers."""
     # (mirrors what sqmp_quant_act_group / sqmp_gemm_fq7_group accept, so that a refusal
@@ -435,8 +435,8 @@ def group_eligible(pws, act_quant: str, act_bits: int, group_size: int, M: int) 
     p0 = pws[0]
     if not FQ7_AUTO or p0.dtype not in (torch.float16, torch.bfloat16) or p0.K - p0.S <= 0:
         return False
-    # the quantizer holds one LDS region of Kp + S_pad + 8 words per member
-    if 4 * (p0.Kp + p0.S_pad + 8) * len(pws) > 150 * 1024:
+    # the quantizer holds one LDS region of Kp + S_pad + 8 words per member + the salient list
+    if 4 * ((p0.Kp + p0.S_pad + 8) * len(pws) + p0.S_pad) > 150 * 1024:
         return False
     return all(fq7_eligible(pw) and pw.Gw % 64 == 0 and pw.K == p0.K and pw.Kp == p0.Kp
                and pw.S_pad == p0.S_pad and pw.S == p0.S and pw.Gw == p0.Gw
