@@ -259,20 +259,25 @@ __device__ __forceinline__ void quant_lc_body(
   // the first row pair's loads go out before the prologue (their latency covers it)
   const int npair = (M + 1) / 2;
   u32x4 nx0[LC_CH], nx1[LC_CH];
+  // Every call issues exactly 2 LC_CH loads (pair index and chunk clamped, never
+  // conditional): the compiler's vmcnt waits count them, so waiting for an older load (the
+  // table entries of the current pair) does not wait for the prefetched pair as well
   auto load_pair = [&](int rp) {
+    rp = rp < npair - 1 ? rp : npair - 1;
     const int m0 = 2 * rp;
     const bool has1 = m0 + 1 < M;
     const u32x4* s0 = (const u32x4*)(x + (size_t)m0 * K);
     const u32x4* s1 = (const u32x4*)(x + (size_t)(has1 ? m0 + 1 : m0) * K);
 #pragma unroll
     for (int i = 0; i < LC_CH; ++i) {
-      const int c = tid + nthr * i;
-      if (c < nchk) {
-        nx0[i] = s0[c];
-        nx1[i] = has1 ? s1[c] : u32x4{0u, 0u, 0u, 0u};
-      }
+      // (chunks past the row reload its last one, rows past M row m0: those lanes are never
+      // written to LDS or stored)
+      const int c = min(tid + nthr * i, nchk - 1);
+      nx0[i] = s0[c];
+      nx1[i] = s1[c];
     }
   };
+
   // Row pairs in contiguous runs per workgroup, consecutive runs on one XCD (blocks are dealt
   // round-robin over the 8 XCDs): the workgroups that write one 32-row block of the
   // tile-major outputs (and neighbouring rows of the row-major ones) share an L2, so its
@@ -283,31 +288,41 @@ __device__ __forceinline__ void quant_lc_body(
   LC_STAMP(0);
   const int rp_end = (int)((long)(wg + 1) * npair / nblk);
   int rp = (int)((long)wg * npair / nblk);
-  if (rp < rp_end) load_pair(rp);
 
   // ---- once per workgroup: salient-position mask, zeroed buffer (+ two spare words: W =
-  // a zero read by padding table entries, W + 1 = a write-only sink for their scatter)
+  // a zero read by padding table entries, W + 1 = a write-only sink for their scatter).
+  // Issue order: the mask's and the salient list's loads first, the first row pair's x
+  // after them, so that the mask's wait (vmcnt counts in issue order) does not wait for x and
+  // the prologue runs under x's latency.
   const int zp0 = 64 * tid;
-  auto zmask_of = [&](const int32_t* am) {
-    uint64_t zm = 0;
-    if (am) {  // NULL: in-place output quantization, salient columns pass through
-      if (zp0 + 64 <= K && ((uintptr_t)am & 15) == 0) {
+  const bool zvec = F8 == 0 && amap && zp0 + 64 <= K && ((uintptr_t)amap & 15) == 0;
+  u32x4 zraw[F8 == 0 ? 16 : 1];
+  if (zvec) {
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const u32x4 e = ((const u32x4*)(am + zp0))[i];
+    for (int i = 0; i < 16; ++i) zraw[i] = ((const u32x4*)(amap + zp0))[i];
+  }
+  // the salient list in two registers per thread (unconditional loads from a clamped index --
+  // lctab stands in for an empty list -- so no select waits for them)
+  const bool sal_reg = S <= 2 * nthr;
+  const int32_t* const salp = S > 0 ? sal : (const int32_t*)lctab;
+  uint32_t salr[2];
 #pragma unroll
-          for (int j = 0; j < 4; ++j) zm |= (uint64_t)(e[j] >> 31) << (4 * i + j);
-        }
-      } else {
-        for (int i = 0; i < 64; ++i) {
-          const int p = zp0 + i;
-          if (p < K && am[p] < 0) zm |= 1ull << i;
-        }
-      }
+  for (int k = 0; k < 2; ++k) salr[k] = (uint32_t)salp[min(tid + k * nthr, S > 0 ? S - 1 : 0)];
+  __builtin_amdgcn_sched_barrier(0);
+  load_pair(rp);
+  __builtin_amdgcn_sched_barrier(0);
+  uint64_t zmask = 0;  // (used by OUT_FP only)
+  if (zvec) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) zmask |= (uint64_t)(zraw[i][j] >> 31) << (4 * i + j);
+  } else if (F8 == 0 && amap) {  // NULL: in-place output quantization, salient columns pass through
+    for (int i = 0; i < 64; ++i) {
+      const int p = zp0 + i;
+      if (p < K && amap[p] < 0) zmask |= 1ull << i;
     }
-    return zm;
-  };
-  const uint64_t zmask = zmask_of(amap);
+  }
 #ifdef SQMP_DIAG_BUILD
   if (zmask == 0x5A5A5A5A5A5A5A5Aull) lc_buf[0] = 1u;  // (keeps the stamp behind zmask's loads)
 #endif
@@ -317,7 +332,13 @@ __device__ __forceinline__ void quant_lc_body(
   // the salient columns' input positions, once per workgroup (every row pair gathers them:
   // an LDS read instead of a dependent global load per pair)
   uint32_t* const sal_l = lc_buf + NOUT * RW;
-  for (int j = tid; j < S; j += nthr) sal_l[j] = (uint32_t)sal[j];
+  if (sal_reg) {
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+      if (tid + k * nthr < S) sal_l[tid + k * nthr] = salr[k];
+  } else {
+    for (int j = tid; j < S; j += nthr) sal_l[j] = (uint32_t)sal[j];
+  }
   // the column statistics of this call, read by the (completed) table kernel: restore the
   // clean-workspace zeros
   if (key_clear)
@@ -385,7 +406,7 @@ __device__ __forceinline__ void quant_lc_body(
     }
     // prefetch the next pair: its registers are free once interleaved, and its latency now
     // overlaps this pair's gather, quantization and stores (same VGPR count)
-    if (rp + 1 < rp_end) load_pair(rp + 1);
+    load_pair(rp + 1 < rp_end ? rp + 1 : rp);  // (the last pair reloads itself, unused)
     __syncthreads();
     if (rp == rp0) LC_STAMP(2);
 
