@@ -151,11 +151,19 @@ struct Fq7Grp {
 // i > 0 addressed through the scalar offset, the two fragment offsets kept instead of the lane
 // index, which the salient tail and the epilogue compute again; spill-free at TM = 128 only,
 // checked by tests/test_fq7_build_cpu.py)
+// bit 4 -- K split inside the workgroup (packed order, TM = 128, J = 2, with bit 3's register
+// budget): 1024 threads as two 8-wave halves on the same tile, half 0 the stages [0, h), half 1
+// [h, nkt) with the salient tail, each on its own 4-slot ring (2 x 64 KiB); half 1 hands its
+// fp32 accumulators to half 0 through LDS, half 0 adds them and runs the epilogue.  Sixteen
+// waves per CU on one tile instead of eight: a one-tile-per-CU grid (2048-token Llama
+// o_proj / down_proj) gets two waves per SIMD more, without a second tile's A and W traffic.
+// The partial sums are added in a different order than in one pass (y within fp32 rounding
+// of the unsplit kernel's, not bit-identical).
 // GRP: a grouped launch over the problems of `grp` (A, Bt, St, Salt, bias, Y, colmax, N and
 // tiles_n are taken from the block's problem; the other arguments are shared)
 template <class DT, int GB, int TM, int J, int DIAG = 0, bool TR = false, int OPT = 0,
           bool GRP = false>
-__global__ __launch_bounds__(512, (OPT & 8) ? 4 : 1) void gemm_fq7_kernel(
+__global__ __launch_bounds__((OPT & 16) ? 1024 : 512, ((OPT & 8) && !(OPT & 16)) ? 4 : 1) void gemm_fq7_kernel(
     const typename DT::T* __restrict__ A, const uint32_t* __restrict__ Bt,
     const typename DT::T* __restrict__ St, const typename DT::T* __restrict__ Salt,
     const typename DT::T* __restrict__ bias, typename DT::T* __restrict__ Y, int M, int N,
@@ -171,7 +179,12 @@ __global__ __launch_bounds__(512, (OPT & 8) ? 4 : 1) void gemm_fq7_kernel(
   // OPT bit 2: 3 on the activation-order kernel)
   constexpr int PF = (TM == 256 && !(OPT & 4)) ? 2 : 3;
   constexpr int EPI = TR ? TN * (2 * TM + 16) : TM * TN * 2;  // epilogue staging bytes
-  constexpr int LDS_BYTES = NS * SLOT > EPI ? NS * SLOT : EPI;
+  constexpr bool KS2 = (OPT & 16) != 0;  // K split over two 8-wave halves (bit 4)
+  static_assert(!KS2 || (!TR && TM == 128 && J == 2 && (OPT & 8)), "bit 4: packed order, TM 128, J 2, bit 3");
+  constexpr int NH = KS2 ? 2 : 1;                 // rings (halves)
+  constexpr int PART = KS2 ? TM * TN * 4 : 0;     // half 1's fp32 accumulators
+  constexpr int LDS0 = NH * NS * SLOT > EPI ? NH * NS * SLOT : EPI;
+  constexpr int LDS_BYTES = LDS0 > PART ? LDS0 : PART;
   static_assert(J <= I, "sub-step 1 decode must finish before block I");
   __shared__ __attribute__((aligned(16))) unsigned char lds[LDS_BYTES];
 
@@ -204,11 +217,21 @@ __global__ __launch_bounds__(512, (OPT & 8) ? 4 : 1) void gemm_fq7_kernel(
     tile_coords(tiles_m, tiles_n, group_m, tm, tn);
   }
   const int m0 = tm * TM, n0 = tn * TN;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lane = threadIdx.x & 63;
+  const int wave_wg = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+  const int half = KS2 ? wave_wg >> 3 : 0;        // (bit 4) this wave's K half
+  const int wave = KS2 ? wave_wg & 7 : wave_wg;   // wave within its half
+  const int tid = KS2 ? wave * 64 + lane : (int)threadIdx.x;  // thread within its half
   const int r16 = lane & 15, q = lane >> 4;
   const int lda = Kp + S_pad;
   const int nkm = Kp / 64, nks = S_pad / 64, nkt = nkm + nks;
+  // this half's stages [k_lo, k_hi): bit 4 splits at an even h <= nkm - 2 near nkt / 2 (both
+  // halves' codes stage counts stay even); the salient tail is half 1's
+  const int hsplit = KS2 ? min(nkm - 2, (nkt / 2 + 1) & ~1) : nkt;
+  const int k_lo = half == 1 ? hsplit : 0, k_hi = (KS2 && half == 0) ? hsplit : nkt;
+  const int kc_hi = KS2 ? min(k_hi, nkm) : nkm;   // end of this half's codes stages
+  const bool has_tail = KS2 ? k_hi > nkm : nks > 0;
+  unsigned char* const ring = lds + half * (NS * SLOT);
   const int nb = tn * 8 + wave;  // this wave's WR-row weight block
 
   // ---- A (x_hat) by LDS-DMA: piece i of wave w = rows 64 i + 8 w + (lane >> 3), the lane
@@ -230,8 +253,8 @@ __global__ __launch_bounds__(512, (OPT & 8) ? 4 : 1) void gemm_fq7_kernel(
   // A pieces this wave issues per stage (the vmcnt of one stage's DMA)
   const int na_w = SPLIT ? (wave < 4 ? 2 * NA : 0) : NA;
   auto issue_a = [&](int kt) {
-    if (kt < nkt && (DIAG != 2 || kt < PA) && (!SPLIT || wave < 4)) {
-      unsigned char* slot = lds + (kt % NS) * SLOT;
+    if (kt < k_hi && (DIAG != 2 || kt < PA) && (!SPLIT || wave < 4)) {
+      unsigned char* slot = ring + (kt % NS) * SLOT;
       const uint32_t so = (uint32_t)(DIAG == 7 ? (kt & 1) : kt) * 64 * sizeof(T);
 #pragma unroll
       for (int o = 0; o < NO; ++o)
@@ -371,7 +394,7 @@ __global__ __launch_bounds__(512, (OPT & 8) ? 4 : 1) void gemm_fq7_kernel(
   // ops issued after B(kt) when stage kt starts: A(kt - 1 + PA) (or, at kt = 0, the
   // prologue's A(1 .. PA-1)); A(kt) is older than B(kt) and so covered by the same wait
   auto wait_stage = [&](int kt) {
-    const int n = kt == 0 ? na_w * min(PA - 1, nkt - 1) : (kt - 1 + PA < nkt ? na_w : 0);
+    const int n = kt == k_lo ? na_w * min(PA - 1, k_hi - k_lo - 1) : (kt - 1 + PA < k_hi ? na_w : 0);
     vmwait_dyn(n);
   };
 
@@ -380,11 +403,11 @@ __global__ __launch_bounds__(512, (OPT & 8) ? 4 : 1) void gemm_fq7_kernel(
   Codes cs[2];
   Dense dd;  // one set: sub-step 0 of stage kd + 1 lands while sub-step 1 of kd computes
 
-  // prologue: A(0), B(0), A(1 .. PA-1)
-  issue_a(0);
-  issue_codes(0, cs[0]);
+  // prologue: A(k_lo), B(k_lo), A(k_lo + 1 .. k_lo + PA - 1)
+  issue_a(k_lo);
+  issue_codes(k_lo, cs[0]);
 #pragma unroll
-  for (int p = 1; p < PA; ++p) issue_a(p);
+  for (int p = 1; p < PA; ++p) issue_a(k_lo + p);
 
   // codes stage kt on set P; the next codes stage's loads go to the other set, and after
   // the last codes stage the first salient stage's two sub-steps
@@ -395,15 +418,15 @@ __global__ __launch_bounds__(512, (OPT & 8) ? 4 : 1) void gemm_fq7_kernel(
     if (DIAG != 4) barrier();
     if (!last) issue_codes(kt + 1, cs[P ^ 1]);
     issue_a(kt + PA);
-    compute_codes(lds + (kt % NS) * SLOT, cs[P]);
-    if (last && nks > 0) {
+    compute_codes(ring + (kt % NS) * SLOT, cs[P]);
+    if (last && has_tail) {
       issue_dense(0, dd, Z());
       issue_dense(0, dd, O());
     }
   };
   if ((OPT & 1) && wave >= 4) __builtin_amdgcn_s_setprio(1);
-  int kt = 0;
-  for (; kt + 2 < nkm; kt += 2) {
+  int kt = k_lo;  // (even)
+  for (; kt + 2 < kc_hi; kt += 2) {
     codes_step(kt, Z(), false);
     codes_step(kt + 1, O(), false);
   }
@@ -414,7 +437,7 @@ __global__ __launch_bounds__(512, (OPT & 8) ? 4 : 1) void gemm_fq7_kernel(
   // after block I - 1, sub-step 1 of kd + 1 at the end; so at the top of stage kd the ops
   // younger than its sub-step 0 are its sub-step 1 (4), and at block I those younger
   // than its sub-step 1 are A(k + PA).
-  for (int kd = 0; kd < nks; ++kd) {
+  for (int kd = 0; kd < (KS2 ? (has_tail ? nks : 0) : nks); ++kd) {
     const int k = nkm + kd;
     vmwait<J>();
 #pragma unroll
@@ -422,7 +445,7 @@ __global__ __launch_bounds__(512, (OPT & 8) ? 4 : 1) void gemm_fq7_kernel(
     barrier();
     issue_a(k + PA);
     const bool more = kd + 1 < nks;
-    compute_dense(lds + (k % NS) * SLOT, dd, [&](int t) {
+    compute_dense(ring + (k % NS) * SLOT, dd, [&](int t) {
       if (t == I - 1) {
         if (k + PA < nkt)
           vmwait_dyn(na_w);
@@ -436,10 +459,36 @@ __global__ __launch_bounds__(512, (OPT & 8) ? 4 : 1) void gemm_fq7_kernel(
     if (more) issue_dense(kd + 1, dd, O());
   }
 
+  if constexpr (KS2) {
+    // the two halves ran k_hi - k_lo per-stage barriers each: the shorter half adds the
+    // difference, so that every s_barrier below pairs the same arrivals
+    const int extra = (nkt - hsplit) - hsplit;
+    for (int e = 0; e < (half == 0 ? extra : -extra); ++e) barrier();
+  }
   // ---- epilogue: the TM x TN tile staged in LDS (row m: 2 TN bytes, 16-B chunk c at
   // c ^ (m & 15)), stored as whole rows, one 16-B chunk per lane
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   barrier();  // every wave is past its last read of the ring
+  if constexpr (KS2) {
+    // half 1's accumulators to half 0 through LDS (lane-contiguous f32x4: conflict-free)
+    f32x4* part = (f32x4*)lds;
+    if (half == 1) {
+#pragma unroll
+      for (int i = 0; i < I; ++i)
+#pragma unroll
+        for (int j = 0; j < J; ++j) part[((wave * I + i) * J + j) * 64 + lane] = acc[i][j];
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    barrier();
+    if (half == 0) {
+#pragma unroll
+      for (int i = 0; i < I; ++i)
+#pragma unroll
+        for (int j = 0; j < J; ++j) acc[i][j] += part[((wave * I + i) * J + j) * 64 + lane];
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    barrier();  // the partials are read before the staging below overwrites them
+  }
   if constexpr (TR) {
     // y^T staged [nl TN][ml TM] at a row stride of 2 TM + 16 bytes (the four q groups of a
     // write land 16 banks apart), stored as TM-wide row pieces of Y[n][m]
@@ -506,10 +555,11 @@ __global__ __launch_bounds__(512, (OPT & 8) ? 4 : 1) void gemm_fq7_kernel(
         for (int r = 0; r < 4; ++r) cmx[j][r] = fmaxf(cmx[j][r], fabsf(DT::to_f(v[r])));
       }
       const int c = nl >> 3;
-      *(u32x2*)(lds + ml * (TN * 2) + ((c ^ (ml & 15)) << 4) + (nl & 4) * 2) = *(const u32x2*)v;
+      if (!KS2 || half == 0)
+        *(u32x2*)(lds + ml * (TN * 2) + ((c ^ (ml & 15)) << 4) + (nl & 4) * 2) = *(const u32x2*)v;
     }
   }
-  if (colmax) {
+  if (colmax && (!KS2 || half == 0)) {
 #pragma unroll
     for (int j = 0; j < J; ++j)
 #pragma unroll
@@ -533,7 +583,7 @@ __global__ __launch_bounds__(512, (OPT & 8) ? 4 : 1) void gemm_fq7_kernel(
     const int ml = RPP * k + etid / CPR;
     const int gm = m0 + ml;
     const u32x4 val = *(const u32x4*)(lds + ml * (TN * 2) + ((c ^ (ml & 15)) << 4));
-    if (gm < M && cok) {
+    if (gm < M && cok && (!KS2 || half == 0)) {
       u32x4* dst = (u32x4*)(Y + (size_t)gm * N + n0 + c * 8);
       if (nt)  // streaming stores of a large output (nt_output)
         store16_nt(dst, val);
@@ -604,15 +654,30 @@ static int group_m_tr_env() {  // (A/B knob; sqmp_knobs.hip)
   return e && atoi(e) > 0 ? atoi(e) : 4;
 }
 
+// K split inside the workgroup (OPT bit 4) for the fp16 packed-order 128-row tiles, only where
+// Kp >= 256 (each half at least two codes stages).  Default (1): grids of at most one 128-row
+// tile per CU, i.e. where the unsplit kernel runs eight waves per CU -- same box, Llama-2-7B at
+// 2048 tokens: o_proj 93.4 -> 89.8 us, down_proj 222.7 -> 211.6 us (profiles/r05_ab_fq7_ksplit.txt).
+// 0 off; 2 every 128-row grid (q/k/v 214 -> 225 us: two unsplit workgroups per CU hide more);
+// 3 as 2 and 128-row tiles for the grouped launches that take 256 (gate/up 338 -> 380 us).
+// (A/B knob SQMP_FQ7_KS)
+static int ks_env() {  // (A/B knob; sqmp_knobs.hip)
+  const char* e = knob("SQMP_FQ7_KS");
+  return e ? atoi(e) : 1;
+}
+
 // the packed-order launch's OPT variant (A/B knob, see gemm_fq7_kernel): default 3, same box
 // (profiles/r03_ab_fq7_opt.txt): 2048 x 4096 -> 4096 67.2 -> 65.6 us, -> 11008 182.4 -> 181.9,
 // 11008 -> 4096 164.5 -> 163.9, config 2 in packed order 461.2 -> 448.3
 // 128-row tiles with more than one tile per CU: 8 (two workgroups per CU, 128 VGPRs), same
 // box (profiles/r03_ab_fq7_two_wg_per_cu.txt): 2048 x 4096 -> 11008 179.5 -> 159.6 us; at one
 // tile per CU (2048 x 4096 -> 4096, 2048 x 11008 -> 4096) within +-1 % of 3
-static int opt_pk_env(int tm, long tiles) {  // (A/B knob; sqmp_knobs.hip)
+static int opt_pk_env(int tm, long tiles, int kp) {  // (A/B knob; sqmp_knobs.hip)
   const char* e = knob("SQMP_FQ7_OPT");
-  return e ? atoi(e) : (tm == 128 && tiles > 256 ? 8 : 3);
+  if (e) return atoi(e);
+  const int ks = ks_env();
+  if (tm == 128 && kp >= 256 && (ks >= 2 || (ks == 1 && tiles <= 256))) return 24;
+  return tm == 128 && tiles > 256 ? 8 : 3;
 }
 
 // the activation-order launch's OPT variant (A/B knob, see gemm_fq7_kernel)
@@ -641,18 +706,21 @@ static int launch_k(const void* a, const void* bt, const void* st, const void* s
   const int tiles_m = cdiv(M, TM), tiles_n = cdiv(N, 128 * J);
   const int nt = nt_output((size_t)M * N * sizeof(T)) ? 1 : 0;
 #define SQMP_PK(O)                                                                              \
-  gemm_fq7_kernel<DT, GB, TM, J, DIAG, false, O><<<dim3(tiles_m * tiles_n), dim3(512), 0, s>>>( \
+  gemm_fq7_kernel<DT, GB, TM, J, DIAG, false, O><<<dim3(tiles_m * tiles_n), dim3((O) & 16 ? 1024 : 512), 0, s>>>( \
       (const T*)a, (const uint32_t*)bt, (const T*)st, (const T*)salt, (const T*)bias, (T*)y, M,  \
       N, Kp, S_pad, Gw, ngw, tiles_m, tiles_n, group_m_env(), colmax, nt, Fq7Grp{})
   // OPT variants (setprio for waves 4-7, loader split) for the fp16 J = 2 kernels, the
   // 2048-token Llama GEMMs (A/B knob SQMP_FQ7_OPT, read per launch)
   if constexpr (std::is_same<DT, F16>::value && J == 2 && GB == 1 && DIAG == 0) {
-    switch (opt_pk_env(TM, (long)tiles_m * tiles_n)) {
+    switch (opt_pk_env(TM, (long)tiles_m * tiles_n, Kp)) {
       case 1: SQMP_PK(1); break;
       case 2: SQMP_PK(2); break;
       case 3: SQMP_PK(3); break;
       case 8: if constexpr (TM == 128) { SQMP_PK(8); } else { SQMP_PK(0); } break;
       case 9: if constexpr (TM == 128) { SQMP_PK(9); } else { SQMP_PK(3); } break;
+      case 24:  // (the K split needs two codes stages per half: Kp >= 256)
+        if constexpr (TM == 128) { if (Kp >= 256) { SQMP_PK(24); } else { SQMP_PK(8); } } else { SQMP_PK(3); }
+        break;
       default: SQMP_PK(0); break;
     }
   } else {
@@ -714,7 +782,7 @@ static int dispatch_group(Fq7Grp& g, int M, int Kp, int S_pad, int Gw, int ngw, 
   typedef typename DT::T T;
   long t256 = 0;
   for (int p = 0; p < g.n; ++p) t256 += (long)cdiv(M, 256) * cdiv(g.N[p], 256);
-  int tm = t256 >= 512 ? 256 : 128;
+  int tm = t256 >= 512 && ks_env() < 3 ? 256 : 128;
   if (const char* e = knob("SQMP_FQ7G_TM")) tm = atoi(e) == 256 ? 256 : 128;
   if (std::is_same<DT, BF16>::value) tm = 128;  // (bf16 at 256 x 256 puts an array in scratch)
   const int tiles_m = cdiv(M, tm);
@@ -725,12 +793,14 @@ static int dispatch_group(Fq7Grp& g, int M, int Kp, int S_pad, int Gw, int ngw, 
     g.tile_end[p] = end;
   }
 #define SQMP_G(TMV, O)                                                                          \
-  gemm_fq7_kernel<DT, 1, TMV, 2, 0, false, O, true><<<dim3(end), dim3(512), 0, s>>>(            \
+  gemm_fq7_kernel<DT, 1, TMV, 2, 0, false, O, true><<<dim3(end), dim3((O) & 16 ? 1024 : 512), 0, s>>>( \
       (const T*)nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, M, 0, Kp, S_pad, Gw, ngw, \
       tiles_m, 0, group_m_env(), nullptr, nt, g)
   if (tm == 256) {
     if constexpr (std::is_same<DT, F16>::value) SQMP_G(256, 3);
-  } else if (opt_pk_env(128, end) == 8) {
+  } else if (opt_pk_env(128, end, Kp) == 24 && std::is_same<DT, F16>::value) {
+    if constexpr (std::is_same<DT, F16>::value) SQMP_G(128, 24);
+  } else if (opt_pk_env(128, end, Kp) == 8) {
     SQMP_G(128, 8);
   } else {
     SQMP_G(128, 3);

@@ -159,7 +159,14 @@ def test_config_workload_matches_reference(case):
         assert r < tol, (n, r)
         ospec = resolve_quantizer(m.output_quant)
         if ospec is None:
-            assert torch.equal(y.reshape(y_pre.shape), y_pre), n  # forward = this GEMM
+            # forward = this GEMM: bit for bit, except where the forward ran a sibling group's
+            # launch and this layer alone takes the K-split kernel (one 128-row tile per CU,
+            # SQMP_FQ7_KS; fp32 partial sums in another order) -- then within the pair
+            # tolerance of it, and the forward itself within tol of the fp64 product
+            yf = y.reshape(y_pre.shape)
+            if not torch.equal(yf, y_pre):
+                assert _rel(yf.float().cpu().numpy(), y_pre.float().cpu().numpy()) < 1e-3, n
+                assert _rel(yf.float().cpu().numpy(), yr.cpu().numpy()) < tol, n
         else:
             # output quantization (fake_quant.py:308-316) is discontinuous in the GEMM
             # output, so it is checked on OUR pre-quant output: the forward's y must be

@@ -173,3 +173,57 @@ def test_fq7_variants_bit_identical(env, vals, M, K, N):
     for y, c in outs[1:]:
         assert torch.equal(y.view(torch.int16), y0.view(torch.int16))
         assert torch.equal(c, c0)
+
+
+@pytest.mark.parametrize("ks", ["1", "2"])  # (1: one-tile-per-CU grids, the default; 2: all)
+@pytest.mark.parametrize("M,K,N,Gs,p", [
+    (2048, 4096, 4096, 64, 0.05),     # Llama o_proj: 256 tiles, one per CU
+    (2048, 11008, 4096, 64, 0.05),    # down_proj: odd stage count (extra barrier in half 0)
+    (700, 2048, 1032, 128, 0.05),     # ragged rows and columns
+    (257, 256, 264, 64, 0.0),         # Kp = 256: the smallest split (two codes stages per half)
+    (64, 192, 256, 64, 0.0),          # Kp < 256: no split, the unsplit kernel runs
+])
+def test_fq7_ksplit(ks, M, K, N, Gs, p, monkeypatch):
+    """K split inside the workgroup (SQMP_FQ7_KS, OPT bit 4): the two halves' fp32 partial
+    sums are added in another order than one pass, so y matches the unsplit kernel within the
+    pair tolerance (not bit for bit), the fp32 operand product within TOL, and the fused
+    column maxima are those of the stored y."""
+    dev = _dev()
+    from smoothquant import ops
+    q, lin, x = _layer(dev, M, K, N, Gs, p, torch.float16)
+    pw = q.packed()
+    a = ops.quant_act_fp(x, pw, "per_group", 4, Gs)
+    reload = __import__("smoothquant._lib", fromlist=["_lib"]).reload_knobs
+    monkeypatch.setenv("SQMP_FQ7_KS", "0")  # the unsplit kernel
+    reload()
+    y0 = ops.gemm_fq7(a, pw, lin.bias)
+    monkeypatch.setenv("SQMP_FQ7_KS", ks)
+    reload()
+    cm = torch.zeros(pw.N + 8, dtype=torch.int32, device=dev)
+    y1 = ops.gemm_fq7(a, pw, lin.bias, cm)
+    assert rel(y1, y0) < TOL_PAIR[torch.float16]
+    assert rel(y1, _ref(a, pw, lin.bias)) < TOL[torch.float16]
+    assert torch.equal(cm[: pw.N], y1.float().abs().amax(0).view(torch.int32))
+
+
+@pytest.mark.parametrize("ks", ["2", "3"])
+@pytest.mark.parametrize("Ns", [(4096, 4096, 4096), (11008, 11008)])
+def test_fq7_ksplit_grouped(ks, Ns, monkeypatch):
+    """The grouped sibling launch with the K split (A/B settings: 2 on every 128-row grid --
+    q/k/v; 3 also 128-row tiles for gate/up): every member within the pair tolerance of the
+    unsplit grouped launch."""
+    dev = _dev()
+    from smoothquant import ops
+    from smoothquant.fake_quant import link_siblings
+    layers = [_layer(dev, 2048, 4096, n, 64, 0.05, torch.float16, seed=3)[0] for n in Ns]
+    _, _, x = _layer(dev, 2048, 4096, Ns[0], 64, 0.05, torch.float16, seed=3)
+    link_siblings(*layers)
+    reload = __import__("smoothquant._lib", fromlist=["_lib"]).reload_knobs
+    outs = {}
+    for v in ("0", ks):
+        monkeypatch.setenv("SQMP_FQ7_KS", v)
+        reload()
+        xi = x.clone()  # (a new input object: the group runs again)
+        outs[v] = [m(xi).clone() for m in layers]
+    for y1, y0 in zip(outs[ks], outs["0"]):
+        assert rel(y1, y0) < TOL_PAIR[torch.float16]

@@ -61,8 +61,13 @@ def test_group_quantizer_equals_own(M, K, Ns, G, p, dt, mode):
     (300, 768, (768, 768, 768), 64, 0.10, torch.bfloat16),
 ])
 def test_group_gemm_equals_own(tm, M, K, Ns, G, p, dt, monkeypatch):
+    """The grouped launch computes each member's tiles exactly as the member's own launch of
+    the same kernel variant (the K split, SQMP_FQ7_KS, off here: a one-tile-per-CU member
+    alone takes the split kernel by default, whose fp32 partial sums add in another order --
+    test_gpu_fq7.py::test_fq7_ksplit bounds that difference)."""
     dev = _dev()
     from smoothquant import ops
+    monkeypatch.setenv("SQMP_FQ7_KS", "0")
     monkeypatch.setenv("SQMP_FQ7G_TM", tm)
     __import__("smoothquant._lib", fromlist=["_lib"]).reload_knobs()  # (knobs are read once at load)
     layers, x = _siblings(dev, M, K, Ns, G, p, dt, seed=5)
