@@ -2,6 +2,7 @@
 2) under a per-launch variable: interleaved rounds, HIP events, y bit-identical across variants.
 
     python tools/ab_fq7.py ENV=v1/v2/... [rounds] [iters]        (e.g. SQMP_FQ7_OPT=0/1/2/3)
+    AB_STRICT=0: y within 1e-3 (relative Frobenius) instead of bit-identical (the K split)
 """
 import os
 import sys
@@ -36,7 +37,11 @@ for (M, K, N, G, p) in SHAPES:
         torch.cuda.synchronize()
         if ref is None:
             ref = y.clone()
-        assert torch.equal(y.view(torch.int16), ref.view(torch.int16)), f"{var}={v} changed y"
+        if os.environ.get("AB_STRICT", "1") == "1":
+            assert torch.equal(y.view(torch.int16), ref.view(torch.int16)), f"{var}={v} changed y"
+        else:  # (variants that add partial sums in another order: the K split, OPT bit 4)
+            d = float((y.float() - ref.float()).norm() / ref.float().norm())
+            assert d < 1e-3, f"{var}={v}: rel {d}"
     res = {v: [] for v in vals}
     for _ in range(rounds):
         for v in vals:
