@@ -295,11 +295,18 @@ __device__ __forceinline__ void quant_lc_body(
   // after them, so that the mask's wait (vmcnt counts in issue order) does not wait for x and
   // the prologue runs under x's latency.
   const int zp0 = 64 * tid;
-  const bool zvec = F8 == 0 && amap && zp0 + 64 <= K && ((uintptr_t)amap & 15) == 0;
-  u32x4 zraw[F8 == 0 ? 16 : 1];
-  if (zvec) {
+  // the salient mask of 64-position chunk c (bit i: amap[64 c + i] < 0, positions < K) is one
+  // wave ballot over a coalesced dword per lane; wave w takes chunks w, w + NW, ... (at most
+  // 16: K <= 16384, NW >= K / 1024) and parks the masks in LDS for their owner, thread c
+  const int nzc = F8 == 0 && amap ? (K + 63) >> 6 : 0;
+  uint32_t zraw[F8 == 0 ? 16 : 1];
+  if (F8 == 0) {
+    const int32_t* const am = amap ? amap : (const int32_t*)lctab;  // (NULL: loads unused)
 #pragma unroll
-    for (int i = 0; i < 16; ++i) zraw[i] = ((const u32x4*)(amap + zp0))[i];
+    for (int i = 0; i < 16; ++i) {
+      const int p = 64 * (wave + NW * i) + lane;  // (clamped: an unconditional load)
+      zraw[i] = (uint32_t)am[min(p, K - 1)];
+    }
   }
   // the salient list in two registers per thread (unconditional loads from a clamped index --
   // lctab stands in for an empty list -- so no select waits for them)
@@ -311,20 +318,22 @@ __device__ __forceinline__ void quant_lc_body(
   __builtin_amdgcn_sched_barrier(0);
   load_pair(rp);
   __builtin_amdgcn_sched_barrier(0);
-  uint64_t zmask = 0;  // (used by OUT_FP only)
-  if (zvec) {
+  // (amap NULL: in-place output quantization, salient columns pass through: no mask)
+  uint32_t* const zm_l = lc_buf + NOUT * (W + 8) + S_pad;  // [nzc] u64 masks
+  if (F8 == 0) {
 #pragma unroll
-    for (int i = 0; i < 16; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) zmask |= (uint64_t)(zraw[i][j] >> 31) << (4 * i + j);
-  } else if (F8 == 0 && amap) {  // NULL: in-place output quantization, salient columns pass through
-    for (int i = 0; i < 64; ++i) {
-      const int p = zp0 + i;
-      if (p < K && amap[p] < 0) zmask |= 1ull << i;
+    for (int i = 0; i < 16; ++i) {
+      const int c = wave + NW * i;
+      const int p = 64 * c + lane;
+      const uint64_t b = __ballot(p < K && (int)zraw[i] < 0);
+      if (c < nzc && lane == 0) {
+        zm_l[2 * c] = (uint32_t)b;
+        zm_l[2 * c + 1] = (uint32_t)(b >> 32);
+      }
     }
   }
 #ifdef SQMP_DIAG_BUILD
-  if (zmask == 0x5A5A5A5A5A5A5A5Aull) lc_buf[0] = 1u;  // (keeps the stamp behind zmask's loads)
+  if (zraw[0] == 0x5A5A5A5Au) lc_buf[0] = 1u;  // (keeps the stamp behind the mask's loads)
 #endif
   LC_STAMP(7);
   const int RW = W + 8;  // LDS region stride (words; a multiple of 8)
@@ -359,6 +368,9 @@ __device__ __forceinline__ void quant_lc_body(
   __syncthreads();
   LC_STAMP(1);
   const int rp0 = rp;
+  const uint64_t zmask = F8 == 0 && tid < nzc
+                             ? (uint64_t)zm_l[2 * tid] | ((uint64_t)zm_l[2 * tid + 1] << 32)
+                             : 0ull;
 
   for (; rp < rp_end; ++rp) {
     const int m0 = 2 * rp;
@@ -638,8 +650,15 @@ __device__ __forceinline__ void quant_lc_body(
 }
 
 
+// The packed-order group quantizer (one output) is held to 80 VGPRs (six waves per SIMD, no
+// spills): Llama down_proj's 11-wave workgroups then run two per CU instead of one, its 1024
+// row pairs in two rounds instead of four sequential pairs per workgroup.
+template <int MODE, int F8, int NOUT>
+constexpr int lc_waves_per_eu() { return MODE == LC_MODE_GROUP && F8 == 0 && NOUT == 1 ? 6 : 1; }
+
 template <class DT, int MODE, int RPL, int GS, int F8 = 0, int NOUT = 1>
-__global__ __launch_bounds__(1024) void quant_lc_kernel(
+__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(lc_waves_per_eu<MODE, F8, NOUT>())))
+void quant_lc_kernel(
     const typename DT::T* x, int M, int K, int q_max, int G,
     const uint32_t* __restrict__ lctab, int Kn, const int32_t* __restrict__ amap, int P,
     const int32_t* __restrict__ sal, int S, int S_pad, const uint32_t* __restrict__ cmax,
@@ -866,9 +885,10 @@ __global__ __launch_bounds__(1024) void quant_c4_fused_kernel(
 
 constexpr int LC_RPL = 16;
 
-// dynamic LDS words of quant_lc_body: NOUT regions of P + S_pad + 8 words + the salient list
+// dynamic LDS words of quant_lc_body: NOUT regions of P + S_pad + 8 words, the salient list
+// and the salient masks of the 64-position chunks (2 words each, K <= P)
 static size_t lc_lds_words(int P, int S_pad, int nout) {
-  return (size_t)(P + S_pad + 8) * nout + S_pad;
+  return (size_t)(P + S_pad + 8) * nout + S_pad + 2 * (size_t)((P + 63) / 64);
 }
 
 // Workgroups of `block` threads and `lds` dynamic LDS bytes a CU holds at once for kernel f

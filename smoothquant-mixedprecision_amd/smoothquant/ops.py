@@ -435,8 +435,8 @@ def group_eligible(pws, act_quant: str, act_bits: int, group_size: int, M: int) 
     p0 = pws[0]
     if not FQ7_AUTO or p0.dtype not in (torch.float16, torch.bfloat16) or p0.K - p0.S <= 0:
         return False
-    # the quantizer holds one LDS region of Kp + S_pad + 8 words per member + the salient list
-    if 4 * ((p0.Kp + p0.S_pad + 8) * len(pws) + p0.S_pad) > 150 * 1024:
+    # the quantizer holds one LDS region of Kp + S_pad + 8 words per member + the salient list / masks
+    if 4 * ((p0.Kp + p0.S_pad + 8) * len(pws) + p0.S_pad + 2 * ((p0.Kp + 63) // 64)) > 150 * 1024:
         return False
     return all(fq7_eligible(pw) and pw.Gw % 64 == 0 and pw.K == p0.K and pw.Kp == p0.Kp
                and pw.S_pad == p0.S_pad and pw.S == p0.S and pw.Gw == p0.Gw
