@@ -333,7 +333,7 @@ __device__ __forceinline__ void quant_lc_body(
     }
   }
 #ifdef SQMP_DIAG_BUILD
-  if (zraw[0] == 0x5A5A5A5Au) lc_buf[0] = 1u;  // (keeps the stamp behind the mask's loads)
+  if (F8 == 0 && zraw[0] == 0x5A5A5A5Au) lc_buf[0] = 1u;  // (keeps the stamp behind the mask's loads)
 #endif
   LC_STAMP(7);
   const int RW = W + 8;  // LDS region stride (words; a multiple of 8)
