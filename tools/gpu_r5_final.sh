@@ -13,4 +13,7 @@ python tools/pmc_summary.py "$O/pmc" fqt 0 214000000 16 "$O/r05_pmc_gemm_fqt7_pe
 python tools/pmc_summary.py "$O/pmc" f8 0 237000000 32 "$O/r05_pmc_gemm_f8v2_per_token.json" gemm_f8 || exit 1
 python tools/pmc_summary.py "$O/pmc" h2 0 640000000 16 "$O/r05_pmc_gemm_h2d_fp32.json" gemm_h2d || exit 1
 tail -3 "$O/llama_layer_trace.txt"
+# only the summaries travel back (gpurun merges <= 64 MiB): drop the raw counter / trace dirs
+rm -rf "$O/pmc" "$O/prof" "$O/kernel_trace_layer_trace.csv"
+du -sh "$O"
 echo "final ok"
