@@ -940,7 +940,14 @@ static int quant_lc_launch(const void* x, int M, int K, int q_max, int G, const 
   int per_cu = occ_per_cu(kf, 64 * nw, lds);
   if (const char* e = knob("SQMP_LC_PERCU"))  // tuning only (0 / unparsable: the default)
     if (atoi(e) > 0) per_cu = atoi(e);
-  const int grid = lc_grid((M + 1) / 2, per_cu);
+  const int npair = (M + 1) / 2;
+  int grid = lc_grid(npair, per_cu);
+  // the e4m3 output (row-major, no 32-row blocks to keep together): runs of 3 pairs where the
+  // pairs exceed one round of slots -- config 2 per_token 46.4 -> 43.3 us against runs of 8
+  // (1 / 2 / 4 / 5 / 6 pairs: 46.5 / 47.5 / 43.9 / 44.3 / 45.7 us; profiles/r05_ab_lc_ppw.txt)
+  if (F8 == 1 && npair > 256 * per_cu) grid = cdiv(npair, 3);
+  if (const char* e = knob("SQMP_LC_PPW"))  // (A/B: exact row pairs per workgroup)
+    if (atoi(e) > 0) grid = cdiv(npair, atoi(e));
   quant_lc_kernel<DT, MODE, LC_RPL, GS, F8, NOUT><<<dim3(grid), dim3(64 * nw), lds, s>>>(
       (const T*)x, M, K, q_max, G, lctab, Kn, amap, P, sal, S, S_pad, cmax, nonsal, (T*)out,
       key_clear, clear_words, out_scale, (T*)out_xs, Kq, ldsc, sib);

@@ -18,7 +18,7 @@ static const char* const kKnobs[] = {
     "SQMP_FQ7_GROUP_M", "SQMP_FQT7_GROUP_M",   "SQMP_FQ7_OPT",     "SQMP_FQT7_OPT",
     "SQMP_FQ7_DIAG",    "SQMP_FQ7G_TM", "SQMP_FQ7_KS",        "SQMP_H2D_GROUP_M", "SQMP_H2_WIDE",
     "SQMP_H2_BK64",     "SQMP_H2_GROUP_M",     "SQMP_COLMAX_RPB",  "SQMP_FQA_RB",
-    "SQMP_FQA_DIAG",
+    "SQMP_FQA_DIAG",      "SQMP_LC_PPW",
 };
 constexpr int NKNOBS = (int)(sizeof(kKnobs) / sizeof(kKnobs[0]));
 static char* g_knob[NKNOBS];
