@@ -1083,7 +1083,9 @@ int launch_quant_lc_c4(int dtype, const void* x, int M, int K, int q_max, int G,
   const char* qe = knob("SQMP_C4_QPERCU");  // tuning only (sqmp_knobs.hip)
   const int q_env = qe ? atoi(qe) : 0;
   const int qpc = q_env > 0 ? q_env : (per_cu > 2 ? per_cu - 2 : 1);
-  const int nq = lc_grid((M + 1) / 2, qpc < per_cu ? qpc : per_cu);
+  int nq = lc_grid((M + 1) / 2, qpc < per_cu ? qpc : per_cu);
+  if (const char* e = knob("SQMP_LC_PPW"))  // (A/B: exact row pairs per quantizer workgroup)
+    if (atoi(e) > 0) nq = cdiv((M + 1) / 2, atoi(e));
   const dim3 grid(nq + Nrows / RB), block(64 * nw);
   if (dtype == SQMP_F16) {
     SQMP_HIP_CHECK(hipFuncSetAttribute((const void*)quant_c4_fused_kernel<F16>,
