@@ -136,7 +136,9 @@ struct Fq7Grp {
 // register loads after the prologue, 2 no A DMA after the prologue, 3 no int4 decode, 4 no
 // per-stage barrier, 5 half the A fragment LDS reads (each fragment used for two blocks), 6 the
 // A pieces written by ds_write_b128 from registers instead of LDS-DMA, 7 the A DMA from two
-// L2-hot stages only, 8 the A loads into a scratch register (VMEM issue without the LDS write)
+// L2-hot stages only, 8 the A loads into a scratch register (VMEM issue without the LDS write);
+// activation-order (TR) epilogue: 9 none (the accumulators kept live, nothing staged or
+// stored), 10 staged in LDS but not stored, 11 stored without the LDS staging writes
 // J = 16-row weight tiles per wave: tile TM x TN with TN = 8 * 16 J (J = 4: 128 x 512;
 // J = 2: 256 x 256, fq6's decode-optimal shape -- a decoded fragment feeds TM / 16 MFMAs)
 // TR (sqmp_gemm_fqt on the tile-major activation operands): A = the permuted weight wp,
@@ -467,6 +469,13 @@ __global__ __launch_bounds__((OPT & 16) ? 1024 : 512, ((OPT & 8) && !(OPT & 16))
   }
   // ---- epilogue: the TM x TN tile staged in LDS (row m: 2 TN bytes, 16-B chunk c at
   // c ^ (m & 15)), stored as whole rows, one 16-B chunk per lane
+  if constexpr (TR && DIAG == 9) {
+#pragma unroll
+    for (int i = 0; i < I; ++i)
+#pragma unroll
+      for (int j = 0; j < J; ++j) asm volatile("" ::"v"(acc[i][j]));
+    return;
+  }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   barrier();  // every wave is past its last read of the ring
   if constexpr (KS2) {
@@ -503,7 +512,10 @@ __global__ __launch_bounds__((OPT & 16) ? 1024 : 512, ((OPT & 8) && !(OPT & 16))
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const T v = DT::from_f(acc[i][j][r] + bv);
-          *(T*)(lds + (WR * wave + 16 * j + 4 * q + r) * RS + ml * 2) = v;
+          if (DIAG == 11)
+            asm volatile("" ::"v"(v));
+          else
+            *(T*)(lds + (WR * wave + 16 * j + 4 * q + r) * RS + ml * 2) = v;
           if (colmax && n0 + WR * wave + 16 * j + 4 * q + r < N) cm = fmaxf(cm, fabsf(DT::to_f(v)));
         }
       if (colmax) {
@@ -522,7 +534,7 @@ __global__ __launch_bounds__((OPT & 16) ? 1024 : 512, ((OPT & 8) && !(OPT & 16))
     for (int k = tid; k < TN * CPR; k += 512) {
       const int nl = k / CPR, c = k % CPR;
       const int gn = n0 + nl, gm = m0 + c * 8;
-      if (gn < N && gm < M)  // M % 8 == 0 (launcher)
+      if (gn < N && gm < M && DIAG != 10)  // M % 8 == 0 (launcher)
       {
         const u32x4 v = *(const u32x4*)(lds + nl * RS + c * 16);
         if (nt)  // streaming stores of a large output (nt_output)
@@ -840,6 +852,9 @@ static int dispatch_tr(const void* wp, const void* codes_t, const void* scale_t,
       case 5: SQMP_TRD(5); break;
       case 6: SQMP_TRD(6); break;
       case 7: SQMP_TRD(7); break;
+      case 9: SQMP_TRD(9); break;
+      case 10: SQMP_TRD(10); break;
+      case 11: SQMP_TRD(11); break;
       default: SQMP_TRD(8); break;
     }
     SQMP_LAUNCH_CHECK();
