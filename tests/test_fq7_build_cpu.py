@@ -9,6 +9,7 @@ import os
 import re
 import shutil
 import subprocess
+import sys
 
 import pytest
 
@@ -21,11 +22,22 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 @pytest.mark.skipif(not os.path.exists(HIPCC) and shutil.which("hipcc") is None,
                     reason="hipcc not available")
 def test_fq7_kernels_do_not_spill(tmp_path):
+    # (the device assembly for the SGPR hazard scan, compiled alongside)
+    asm = subprocess.Popen([HIPCC, "-O3", "-std=c++17", "--offload-arch=gfx950", "--cuda-device-only",
+                            "-S", "-I", os.path.join(ROOT, "include"), SRC, "-o", str(tmp_path / "fq7.s")],
+                           stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
     r = subprocess.run([HIPCC, "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-I",
                         os.path.join(ROOT, "include"), "-c", SRC, "-o", str(tmp_path / "fq7.o"),
                         "-Rpass-analysis=kernel-resource-usage"],
                        capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-2000:]
+    assert asm.wait(timeout=600) == 0
+    # no hand-written VMEM instruction reads an SGPR a VALU instruction (a spill restore by
+    # v_readlane) wrote fewer than 5 wait states before: the compiler pads only the VMEM
+    # instructions it can see (tools/check_asm_sgpr_hazard.py)
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import check_asm_sgpr_hazard as H
+    assert H.main(str(tmp_path / "fq7.s")) == 0
     blocks = re.split(r"remark: Function Name: ", r.stderr)
     seen = 0
     for b in blocks[1:]:
