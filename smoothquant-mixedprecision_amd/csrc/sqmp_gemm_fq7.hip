@@ -70,15 +70,6 @@ __device__ inline void vmwait_dyn(int n) {
     default: vmwait<0>(); break;
   }
 }
-#ifndef SQMP_PERSIST_DBG
-#define SQMP_PERSIST_DBG 0
-#endif
-#ifndef SQMP_PERSIST_OPT
-#define SQMP_PERSIST_OPT 67
-#endif
-#if (SQMP_PERSIST_DBG & 256)
-__device__ uint32_t sqmp_p67_dbg[256 * 8 * 64 * 12];
-#endif
 // (bit 6) the same with the counts of a tile's first stage after an epilogue's 16 stores
 __device__ inline void vmwait_dyn2(int n) {
   switch (n) {
@@ -204,7 +195,10 @@ struct Fq7Grp {
 // operand are issued BEFORE this tile's epilogue stores (so waiting for them does not wait for
 // the stores: vmcnt counts in issue order), the epilogue stages y in two 128-token halves
 // above ring slots 0-1, and the third A stage follows the epilogue -- the store drain overlaps
-// the next tile's K loop instead of idling the CU between workgroups;
+// the next tile's K loop instead of idling the CU between workgroups.  Opt-in only
+// (SQMP_FQT7_OPT=67): bit-identical to 3 but 435.6 against 427.7 us on config 2 (the store
+// drain it hides is smaller than the bias fetch and the two extra barriers per tile it adds;
+// profiles/r05_ab_fqt7_persist.txt);
 // bit 4 -- K split inside the workgroup (packed order, TM = 128, J = 2, with bit 3's register
 // budget): 1024 threads as two 8-wave halves on the same tile, half 0 the stages [0, h), half 1
 // [h, nkt) with the salient tail, each on its own 4-slot ring (2 x 64 KiB); half 1 hands its
@@ -462,7 +456,7 @@ __global__ __launch_bounds__((OPT & 16) ? 1024 : 512, ((OPT & 8) && !(OPT & 16))
   auto wait_stage = [&](int kt) {
     const int n = kt == k_lo ? na_w * min(PA - 1, k_hi - k_lo - 1) : (kt - 1 + PA < k_hi ? na_w : 0);
     if constexpr (PERSIST) {
-      if ((SQMP_PERSIST_DBG & 8) || (kt == k_lo && extra0 < 0))
+      if (kt == k_lo && extra0 < 0)
         vmwait<0>();
       else
         vmwait_dyn2(kt == k_lo ? n + extra0 : n);
@@ -499,18 +493,6 @@ __global__ __launch_bounds__((OPT & 16) ? 1024 : 512, ((OPT & 8) && !(OPT & 16))
     wait_stage(kt);
     fence_codes(cs[P]);
     if (DIAG != 4) barrier();
-#if (SQMP_PERSIST_DBG & 256)
-    if (kt == 0 && blockIdx.x < 256) {
-      const u32x4 av = ald(ring, 0);
-      uint32_t* d = sqmp_p67_dbg + ((blockIdx.x * 8 + wave) * 64 + lane_now()) * 12;
-      const uint32_t sv = *(const uint32_t*)&cs[P].s;
-      const u32x4 v0 = {cs[P].w[0][0], cs[P].w[0][1], cs[P].w[0][2], cs[P].w[0][3]};
-      const u32x4 v1 = {sv, (uint32_t)nb, (uint32_t)tile, (uint32_t)m0};
-      store16_asm(d, v0);
-      store16_asm(d + 4, v1);
-      store16_asm(d + 8, av);
-    }
-#endif
     if (!last) issue_codes(kt + 1, cs[P ^ 1]);
     issue_a(kt + PA);
     compute_codes(ring + (kt % NS) * SLOT, cs[P]);
@@ -553,9 +535,7 @@ __global__ __launch_bounds__((OPT & 16) ? 1024 : 512, ((OPT & 8) && !(OPT & 16))
     });
     if (more) issue_dense(kd + 1, dd, O());
   }
-    if constexpr ((SQMP_PERSIST_DBG & 16) != 0) break;
     // ---- (bit 6) epilogue of this tile, the next tile's first stages issued first
-    if constexpr ((SQMP_PERSIST_DBG & 32) != 0) { vmwait<0>(); __builtin_amdgcn_s_setprio(0); }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     barrier();  // every wave is past its last read of the ring
     const int em0 = m0, en0 = n0;
@@ -566,7 +546,7 @@ __global__ __launch_bounds__((OPT & 16) ? 1024 : 512, ((OPT & 8) && !(OPT & 16))
     static_assert(BOFF + 2 * TM <= LDS_BYTES, "bit 6: staging + bias above two ring slots");
     // this tile's bias into LDS by one asm load per lane of wave 0 (a compiler load would be
     // waited for with vmcnt(0), i.e. behind the next tile's stages issued below)
-    if ((SQMP_PERSIST_DBG & 64) == 0 && wave == 0 && bias) {
+    if (wave == 0 && bias) {
       const rsrc_t rBias = make_rsrc(bias);
       u32x4 bw;
       // (M % 8 == 0, launcher: an 8-row chunk is wholly inside or wholly past M; a chunk past
@@ -580,7 +560,7 @@ __global__ __launch_bounds__((OPT & 16) ? 1024 : 512, ((OPT & 8) && !(OPT & 16))
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     barrier();
     const int nxt = tile + (int)gridDim.x;
-    const bool has_next = (SQMP_PERSIST_DBG & 128) ? false : nxt < ntiles;
+    const bool has_next = nxt < ntiles;
     if (has_next) {
       tile = nxt;
       tile_coords(tiles_m, tiles_n, group_m, tm, tn, tile);
@@ -591,11 +571,9 @@ __global__ __launch_bounds__((OPT & 16) ? 1024 : 512, ((OPT & 8) && !(OPT & 16))
       rB = make_rsrc(Bt + (size_t)nb * nkm * (128 * J));
       rS = make_rsrc(St + (size_t)nb * ngw * (16 * J));
       rD = make_rsrc(Salt + (size_t)nb * (nks > 0 ? nks : 1) * (1024 * J));
-      if (!(SQMP_PERSIST_DBG & 2)) {
       issue_a_p(k_lo, std::true_type{});
       issue_codes_p(k_lo, cs[0], std::true_type{});
       issue_a_p(k_lo + 1, std::true_type{});
-      }
     }
     // y^T in two 128-token halves staged above ring slots 0-1 (waves 4 h .. 4 h + 3 own half h)
 #pragma unroll
@@ -604,8 +582,7 @@ __global__ __launch_bounds__((OPT & 16) ? 1024 : 512, ((OPT & 8) && !(OPT & 16))
 #pragma unroll
         for (int i = 0; i < I; ++i) {
           const int ml = 16 * i + er16;
-          const float bv = (SQMP_PERSIST_DBG & 64) ? (bias && em0 + ml < M ? DT::to_f(bias[em0 + ml]) : 0.f)
-                                                   : bias ? DT::to_f(*(const T*)(lds + BOFF + 2 * ml)) : 0.f;
+          const float bv = bias ? DT::to_f(*(const T*)(lds + BOFF + 2 * ml)) : 0.f;
 #pragma unroll
           for (int j = 0; j < J; ++j)
 #pragma unroll
@@ -634,13 +611,11 @@ __global__ __launch_bounds__((OPT & 16) ? 1024 : 512, ((OPT & 8) && !(OPT & 16))
     if (!has_next) return;
     // the stores this wave just issued (all of them on a whole tile)
     extra0 = em0 + TM <= M && en0 + TN <= N ? HT * CPR / 512 * 2 : -1;
-    if (SQMP_PERSIST_DBG & 1) extra0 = -1;
-    if (SQMP_PERSIST_DBG & 2) extra0 = 0;
 #pragma unroll
     for (int i = 0; i < I; ++i)
 #pragma unroll
       for (int j = 0; j < J; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    first = (SQMP_PERSIST_DBG & 2) != 0;
+    first = false;
     continue;
   }  // (tile loop)
   } else {
@@ -1127,11 +1102,11 @@ static int dispatch_tr(const void* wp, const void* codes_t, const void* scale_t,
       case 4: SQMP_TR(4); break;
       case 5: SQMP_TR(5); break;
 #define SQMP_TRP(O)                                                                             \
-  gemm_fq7_kernel<DT, 1, TM, J, 0, true, O><<<dim3((SQMP_PERSIST_DBG & 4) ? tiles_m * tiles_n : min(tiles_m * tiles_n, persist_grid())), dim3(512), 0, s>>>( \
+  gemm_fq7_kernel<DT, 1, TM, J, 0, true, O><<<dim3(min(tiles_m * tiles_n, persist_grid())), dim3(512), 0, s>>>( \
       (const T*)wp, (const uint32_t*)codes_t, (const T*)scale_t, (const T*)sal_t, (const T*)bias, \
       (T*)y, N, M, Kq, S_pad, G, ngq, tiles_m, tiles_n, group_m_tr_env(), colmax, nt, Fq7Grp{})
       // (bit 6: persistent grid; TM = 256 only)
-      case 67: if constexpr (TM == 256) { if (!colmax) { SQMP_TRP(SQMP_PERSIST_OPT); } else { SQMP_TR(3); } } else { SQMP_TR(3); } break;
+      case 67: if constexpr (TM == 256) { if (!colmax) { SQMP_TRP(67); } else { SQMP_TR(3); } } else { SQMP_TR(3); } break;
 #undef SQMP_TRP
 #define SQMP_TR128(O)                                                                           \
   gemm_fq7_kernel<DT, 1, 128, 2, 0, true, O><<<dim3(cdiv(N, 128) * tiles_n), dim3(512), 0, s>>>( \
@@ -1299,10 +1274,3 @@ extern "C" int sqmp_gemm_fqt7j(const void* codes_t, const void* scale_t, const v
 }
 
 }  // namespace sqmp
-
-#if (SQMP_PERSIST_DBG & 256)
-extern "C" int sqmp_diag_p67(uint32_t* host) {
-  return hipMemcpyFromSymbol(host, HIP_SYMBOL(sqmp::fq7::sqmp_p67_dbg), sizeof(uint32_t) * 256 * 8 * 64 * 12, 0,
-                             hipMemcpyDeviceToHost) == hipSuccess ? 0 : -3;
-}
-#endif

@@ -353,9 +353,9 @@ def test_standalone_perm_matches_fused():
 
 @pytest.mark.parametrize("M,K,N", [
     (16384, 4096, 4096),   # config 2: 1024 tiles, four per workgroup of the persistent grid
-    (8192, 2048, 1000),    # partial weight-row tiles: stage 0 after a partial epilogue waits for all
-    (4096, 1024, 2048),    # fewer tiles than workgroups: one tile each, no next tile
-    (16640, 1024, 520),    # ragged tokens and weight rows
+    (8192, 4096, 1000),    # partial weight-row tiles: stage 0 after a partial epilogue waits for all
+    (4096, 4096, 2048),    # fewer tiles than workgroups: one tile each, no next tile
+    (16640, 4096, 520),    # ragged tokens and weight rows
 ])
 def test_fqt7_persistent_bit_identical(M, K, N, monkeypatch):
     """The persistent activation-order grid (SQMP_FQT7_OPT=67: the next tile's first stages
