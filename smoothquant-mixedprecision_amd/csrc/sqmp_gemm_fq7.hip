@@ -70,15 +70,6 @@ __device__ inline void vmwait_dyn(int n) {
     default: vmwait<0>(); break;
   }
 }
-// (bit 6) the same with the counts of a tile's first stage after an epilogue's 16 stores
-__device__ inline void vmwait_dyn2(int n) {
-  switch (n) {
-    case 16: vmwait<16>(); break;
-    case 24: vmwait<24>(); break;
-    case 32: vmwait<32>(); break;
-    default: vmwait_dyn(n); break;
-  }
-}
 __device__ inline void barrier() {
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");  // no LDS read moves above the barrier
@@ -87,56 +78,28 @@ __device__ inline void barrier() {
 
 // LDS-DMA of 16 B per lane to the wave-uniform LDS base + 16 * lane.  s_nop 0: the M0
 // write -> LDS-DMA wait state (hipcc pads nothing inside an asm string).
-template <bool PAD = false>
 __device__ inline void dma16(const rsrc_t& r, uint32_t voff, uint32_t soff, unsigned char* lds_dst) {
   const uint32_t m0v = __builtin_amdgcn_readfirstlane(
       (uint32_t)(size_t)(__attribute__((address_space(3))) unsigned char*)lds_dst);
-  if constexpr (PAD)
-    asm volatile("s_mov_b32 m0, %0\n\ts_nop 4\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds" ::"s"(m0v),
-                 "v"(voff), "s"(r), "s"(soff)
-                 : "memory", "m0");
-  else
-    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds" ::"s"(m0v),
-                 "v"(voff), "s"(r), "s"(soff)
-                 : "memory", "m0");
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds" ::"s"(m0v),
+               "v"(voff), "s"(r), "s"(soff)
+               : "memory", "m0");
 }
-// register loads, counted in vmcnt together with the DMA.  PAD: five wait states inside the
-// same asm statement before the load -- an SGPR operand the compiler restored from a spill
-// lane (v_readlane, a VALU write of an SGPR) right before the statement needs them before a
-// VMEM instruction reads it, and the compiler cannot see the VMEM instruction inside the asm
-// to pad it (tools/check_asm_sgpr_hazard.py; tests/test_fq7_build_cpu.py)
-template <int OFF, bool PAD = false>
+// register loads, counted in vmcnt together with the DMA
+template <int OFF>
 __device__ inline void ld16(u32x4& d, const rsrc_t& r, uint32_t voff, uint32_t soff) {
-  if constexpr (PAD)
-    asm volatile("s_nop 4\n\tbuffer_load_dwordx4 %0, %1, %2, %3 offen offset:%4"
-                 : "=v"(d)
-                 : "v"(voff), "s"(r), "s"(soff), "n"(OFF));
-  else
-    asm volatile("buffer_load_dwordx4 %0, %1, %2, %3 offen offset:%4"
-                 : "=v"(d)
-                 : "v"(voff), "s"(r), "s"(soff), "n"(OFF));
+  asm volatile("buffer_load_dwordx4 %0, %1, %2, %3 offen offset:%4"
+               : "=v"(d)
+               : "v"(voff), "s"(r), "s"(soff), "n"(OFF));
 }
-template <bool PAD = false>
 __device__ inline void ld8(u32x2& d, const rsrc_t& r, uint32_t voff, uint32_t soff) {
-  if constexpr (PAD)
-    asm volatile("s_nop 4\n\tbuffer_load_dwordx2 %0, %1, %2, %3 offen" : "=v"(d) : "v"(voff), "s"(r), "s"(soff));
-  else
-    asm volatile("buffer_load_dwordx2 %0, %1, %2, %3 offen" : "=v"(d) : "v"(voff), "s"(r), "s"(soff));
+  asm volatile("buffer_load_dwordx2 %0, %1, %2, %3 offen" : "=v"(d) : "v"(voff), "s"(r), "s"(soff));
 }
-template <bool PAD = false>
 __device__ inline void ld4(uint32_t& d, const rsrc_t& r, uint32_t voff, uint32_t soff) {
-  if constexpr (PAD)
-    asm volatile("s_nop 4\n\tbuffer_load_dword %0, %1, %2, %3 offen" : "=v"(d) : "v"(voff), "s"(r), "s"(soff));
-  else
-    asm volatile("buffer_load_dword %0, %1, %2, %3 offen" : "=v"(d) : "v"(voff), "s"(r), "s"(soff));
+  asm volatile("buffer_load_dword %0, %1, %2, %3 offen" : "=v"(d) : "v"(voff), "s"(r), "s"(soff));
 }
-__device__ inline void ldu16(uint32_t& d, const rsrc_t& r, uint32_t voff, uint32_t soff) {
-  asm volatile("buffer_load_ushort %0, %1, %2, %3 offen" : "=v"(d) : "v"(voff), "s"(r), "s"(soff));
-}
-template <bool PAD = false>
-__device__ inline void ld_s(u32x2& d, const rsrc_t& r, uint32_t voff, uint32_t soff) { ld8<PAD>(d, r, voff, soff); }
-template <bool PAD = false>
-__device__ inline void ld_s(uint32_t& d, const rsrc_t& r, uint32_t voff, uint32_t soff) { ld4<PAD>(d, r, voff, soff); }
+__device__ inline void ld_s(u32x2& d, const rsrc_t& r, uint32_t voff, uint32_t soff) { ld8(d, r, voff, soff); }
+__device__ inline void ld_s(uint32_t& d, const rsrc_t& r, uint32_t voff, uint32_t soff) { ld4(d, r, voff, soff); }
 template <class V>
 __device__ inline void fence(V& v) {
   asm volatile("" : "+v"(v));
@@ -190,15 +153,6 @@ struct Fq7Grp {
 // i > 0 addressed through the scalar offset, the two fragment offsets kept instead of the lane
 // index, which the salient tail and the epilogue compute again; spill-free at TM = 128 only,
 // checked by tests/test_fq7_build_cpu.py)
-// bit 6 -- (activation order, TM = 256, J = 2) persistent grid of one workgroup per CU: each
-// workgroup runs tiles blockIdx.x + k gridDim.x; the next tile's first two A stages and act
-// operand are issued BEFORE this tile's epilogue stores (so waiting for them does not wait for
-// the stores: vmcnt counts in issue order), the epilogue stages y in two 128-token halves
-// above ring slots 0-1, and the third A stage follows the epilogue -- the store drain overlaps
-// the next tile's K loop instead of idling the CU between workgroups.  Opt-in only
-// (SQMP_FQT7_OPT=67): bit-identical to 3 but 435.6 against 427.7 us on config 2 (the store
-// drain it hides is smaller than the bias fetch and the two extra barriers per tile it adds;
-// profiles/r05_ab_fqt7_persist.txt);
 // bit 4 -- K split inside the workgroup (packed order, TM = 128, J = 2, with bit 3's register
 // budget): 1024 threads as two 8-wave halves on the same tile, half 0 the stages [0, h), half 1
 // [h, nkt) with the salient tail, each on its own 4-slot ring (2 x 64 KiB); half 1 hands its
@@ -228,8 +182,6 @@ __global__ __launch_bounds__((OPT & 16) ? 1024 : 512, ((OPT & 8) && !(OPT & 16))
   constexpr int PF = (TM == 256 && !(OPT & 4)) ? 2 : 3;
   constexpr int EPI = TR ? TN * (2 * TM + 16) : TM * TN * 2;  // epilogue staging bytes
   constexpr bool KS2 = (OPT & 16) != 0;  // K split over two 8-wave halves (bit 4)
-  constexpr bool PERSIST = (OPT & 64) != 0;  // (bit 6) persistent activation-order grid
-  static_assert(!PERSIST || (TR && TM == 256 && J == 2 && !KS2), "bit 6: activation order, TM 256, J 2");
   static_assert(!KS2 || (!TR && TM == 128 && J == 2 && (OPT & 8)), "bit 4: packed order, TM 128, J 2, bit 3");
   constexpr int NH = KS2 ? 2 : 1;                 // rings (halves)
   constexpr int PART = KS2 ? TM * TN * 4 : 0;     // half 1's fp32 accumulators
@@ -266,9 +218,7 @@ __global__ __launch_bounds__((OPT & 16) ? 1024 : 512, ((OPT & 8) && !(OPT & 16))
   } else {
     tile_coords(tiles_m, tiles_n, group_m, tm, tn);
   }
-  int tile = blockIdx.x;  // (bit 6: this workgroup's current tile)
-  const int ntiles = tiles_m * tiles_n;
-  int m0 = tm * TM, n0 = tn * TN;
+  const int m0 = tm * TM, n0 = tn * TN;
   const int lane = threadIdx.x & 63;
   const int wave_wg = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
   const int half = KS2 ? wave_wg >> 3 : 0;        // (bit 4) this wave's K half
@@ -284,13 +234,13 @@ __global__ __launch_bounds__((OPT & 16) ? 1024 : 512, ((OPT & 8) && !(OPT & 16))
   const int kc_hi = KS2 ? min(k_hi, nkm) : nkm;   // end of this half's codes stages
   const bool has_tail = KS2 ? k_hi > nkm : nks > 0;
   unsigned char* const ring = lds + half * (NS * SLOT);
-  int nb = tn * 8 + wave;  // this wave's WR-row weight block
+  const int nb = tn * 8 + wave;  // this wave's WR-row weight block
 
   // ---- A (x_hat) by LDS-DMA: piece i of wave w = rows 64 i + 8 w + (lane >> 3), the lane
   // moving logical chunk brev3(p ^ ((row >> 1) & 7)) into physical chunk p = lane & 7
   constexpr bool SPLIT = (OPT & 2) != 0;
   constexpr int NO = SPLIT ? 2 : 1;       // waves whose pieces this wave issues
-  rsrc_t rA = make_rsrc(A + (size_t)m0 * lda);
+  const rsrc_t rA = make_rsrc(A + (size_t)m0 * lda);
   // (OPT bit 3: piece i > 0 is piece 0 moved by 64 i rows, through the scalar offset)
   constexpr int NAV = (OPT & 8) ? 1 : NA;
   uint32_t a_off[NO][NAV];
@@ -304,9 +254,7 @@ __global__ __launch_bounds__((OPT & 16) ? 1024 : 512, ((OPT & 8) && !(OPT & 16))
   }
   // A pieces this wave issues per stage (the vmcnt of one stage's DMA)
   const int na_w = SPLIT ? (wave < 4 ? 2 * NA : 0) : NA;
-  // (pad: the SGPR hazard padding of ld16 / dma16, at the bit-6 tile boundaries only)
-  auto issue_a_p = [&](int kt, auto pad) {
-    constexpr bool PD = decltype(pad)::value;
+  auto issue_a = [&](int kt) {
     if (kt < k_hi && (DIAG != 2 || kt < PA) && (!SPLIT || wave < 4)) {
       unsigned char* slot = ring + (kt % NS) * SLOT;
       const uint32_t so = (uint32_t)(DIAG == 7 ? (kt & 1) : kt) * 64 * sizeof(T);
@@ -326,20 +274,19 @@ __global__ __launch_bounds__((OPT & 16) ? 1024 : 512, ((OPT & 8) && !(OPT & 16))
             asm volatile("ds_write_b128 %0, %1" ::"v"(la), "v"(v) : "memory");
           } else {
             if constexpr ((OPT & 8) != 0)
-              dma16<PD>(rA, a_off[o][0], so + (uint32_t)(i * 64 * lda * (int)sizeof(T)), dst);
+              dma16(rA, a_off[o][0], so + (uint32_t)(i * 64 * lda * (int)sizeof(T)), dst);
             else
-              dma16<PD>(rA, a_off[o][i], so, dst);
+              dma16(rA, a_off[o][i], so, dst);
           }
         }
     }
   };
-  auto issue_a = [&](int kt) { issue_a_p(kt, std::false_type{}); };
 
   // ---- weight operand straight to registers (tile-major copies, sqmp_pack_fq7)
   // per wave block and stage: codes 512 J B, scales (per group) 32 J B, salient 2048 J B
-  rsrc_t rB = make_rsrc(Bt + (size_t)nb * nkm * (128 * J));
-  rsrc_t rS = make_rsrc(St + (size_t)nb * ngw * (16 * J));
-  rsrc_t rD = make_rsrc(Salt + (size_t)nb * (nks > 0 ? nks : 1) * (1024 * J));
+  const rsrc_t rB = make_rsrc(Bt + (size_t)nb * nkm * (128 * J));
+  const rsrc_t rS = make_rsrc(St + (size_t)nb * ngw * (16 * J));
+  const rsrc_t rD = make_rsrc(Salt + (size_t)nb * (nks > 0 ? nks : 1) * (1024 * J));
   const uint32_t vB = (uint32_t)lane * (8u * J), vD = (uint32_t)lane * (32u * J);
   const uint32_t vS = (uint32_t)r16 * (2u * J);
   // one stage ahead: stage kt computes on register set kt & 1 (codes) / kd & 1 (salient
@@ -356,18 +303,16 @@ __global__ __launch_bounds__((OPT & 16) ? 1024 : 512, ((OPT & 8) && !(OPT & 16))
     u32x4 w[2 * J];  // chunk c(q, s) of rows 16 j + r16, [j][s]
   };
 
-  auto issue_codes_p = [&](int kt, Codes& d, auto pad) {
-    constexpr bool PD = decltype(pad)::value;
+  auto issue_codes = [&](int kt, Codes& d) {
     if (DIAG == 1 && kt > 1) return;
-    ld16<0, PD>(d.w[0], rB, vB, (uint32_t)kt * (512u * J));
-    if (J == 4) ld16<16, PD>(d.w[J / 2 - 1], rB, vB, (uint32_t)kt * (512u * J));
+    ld16<0>(d.w[0], rB, vB, (uint32_t)kt * (512u * J));
+    if (J == 4) ld16<16>(d.w[J / 2 - 1], rB, vB, (uint32_t)kt * (512u * J));
     // Gw = 32: the lane's dwords lie in group 2 kt + (q & 1) (clamped: padding)
     const int g = GB == 1 ? min((kt * 64) / Gw, ngw - 1) : min(2 * kt + (q & 1), ngw - 1);
     const uint32_t vo = GB == 1 ? vS : (uint32_t)g * (32u * J) + vS;
     const uint32_t so = GB == 1 ? (uint32_t)g * (32u * J) : 0u;
-    ld_s<PD>(d.s, rS, vo, so);
+    ld_s(d.s, rS, vo, so);
   };
-  auto issue_codes = [&](int kt, Codes& d) { issue_codes_p(kt, d, std::false_type{}); };
   // salient stage kd, sub-step s: the fragments [j][s] (4 x 16 B per lane)
   auto issue_dense = [&](int kd, Dense& d, auto sc) {
     constexpr int S = decltype(sc)::value;
@@ -450,19 +395,9 @@ __global__ __launch_bounds__((OPT & 16) ? 1024 : 512, ((OPT & 8) && !(OPT & 16))
 
   // ops issued after B(kt) when stage kt starts: A(kt - 1 + PA) (or, at kt = 0, the
   // prologue's A(1 .. PA-1)); A(kt) is older than B(kt) and so covered by the same wait
-  // (bit 6) ops the previous tile's epilogue issued between B(0) and A(PA - 1) of this one: its
-  // stores (-1: unknown -- a partial tile -- so stage 0 waits for everything)
-  int extra0 = 0;
   auto wait_stage = [&](int kt) {
     const int n = kt == k_lo ? na_w * min(PA - 1, k_hi - k_lo - 1) : (kt - 1 + PA < k_hi ? na_w : 0);
-    if constexpr (PERSIST) {
-      if (kt == k_lo && extra0 < 0)
-        vmwait<0>();
-      else
-        vmwait_dyn2(kt == k_lo ? n + extra0 : n);
-    } else {
-      vmwait_dyn(n);
-    }
+    vmwait_dyn(n);
   };
 
   using Z = std::integral_constant<int, 0>;
@@ -470,155 +405,6 @@ __global__ __launch_bounds__((OPT & 16) ? 1024 : 512, ((OPT & 8) && !(OPT & 16))
   Codes cs[2];
   Dense dd;  // one set: sub-step 0 of stage kd + 1 lands while sub-step 1 of kd computes
 
-  if constexpr (PERSIST) {
-  // ---- (bit 6) one pass per tile of this workgroup
-  bool first = true;
-  for (;;) {
-  using PadT = std::true_type;
-  if (first) {
-    issue_a_p(k_lo, PadT{});
-    issue_codes_p(k_lo, cs[0], PadT{});
-#pragma unroll
-    for (int p = 1; p < PA; ++p) issue_a_p(k_lo + p, PadT{});
-  } else {
-    // the previous epilogue issued A(0), B(0), A(1): the last prologue stage now that its
-    // staging area (ring slots 2-3) is free
-    issue_a_p(k_lo + PA - 1, PadT{});
-  }
-
-  // codes stage kt on set P; the next codes stage's loads go to the other set, and after
-  // the last codes stage the first salient stage's two sub-steps
-  auto codes_step = [&](int kt, auto pc, bool last) {
-    constexpr int P = decltype(pc)::value;
-    wait_stage(kt);
-    fence_codes(cs[P]);
-    if (DIAG != 4) barrier();
-    if (!last) issue_codes(kt + 1, cs[P ^ 1]);
-    issue_a(kt + PA);
-    compute_codes(ring + (kt % NS) * SLOT, cs[P]);
-    if (last && has_tail) {
-      issue_dense(0, dd, Z());
-      issue_dense(0, dd, O());
-    }
-  };
-  if ((OPT & 1) && wave >= 4) __builtin_amdgcn_s_setprio(1);
-  int kt = k_lo;  // (even)
-  for (; kt + 2 < kc_hi; kt += 2) {
-    codes_step(kt, Z(), false);
-    codes_step(kt + 1, O(), false);
-  }
-  codes_step(kt, Z(), false);
-  codes_step(kt + 1, O(), true);
-  kt += 2;
-  // salient tail.  Issue order per stage kd: A(k + PA) at the top, sub-step 0 of kd + 1
-  // after block I - 1, sub-step 1 of kd + 1 at the end; so at the top of stage kd the ops
-  // younger than its sub-step 0 are its sub-step 1 (4), and at block I those younger
-  // than its sub-step 1 are A(k + PA).
-  for (int kd = 0; kd < (KS2 ? (has_tail ? nks : 0) : nks); ++kd) {
-    const int k = nkm + kd;
-    vmwait<J>();
-#pragma unroll
-    for (int j = 0; j < J; ++j) fence(dd.w[2 * j]);
-    barrier();
-    issue_a(k + PA);
-    const bool more = kd + 1 < nks;
-    compute_dense(ring + (k % NS) * SLOT, dd, [&](int t) {
-      if (t == I - 1) {
-        if (k + PA < nkt)
-          vmwait_dyn(na_w);
-        else
-          vmwait<0>();
-#pragma unroll
-        for (int j = 0; j < J; ++j) fence(dd.w[2 * j + 1]);
-        if (more) issue_dense(kd + 1, dd, Z());
-      }
-    });
-    if (more) issue_dense(kd + 1, dd, O());
-  }
-    // ---- (bit 6) epilogue of this tile, the next tile's first stages issued first
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    barrier();  // every wave is past its last read of the ring
-    const int em0 = m0, en0 = n0;
-    // (lane-derived offsets computed again here, volatile: not kept live through the K loop)
-    const int el = lane_now(), er16 = el & 15, eq = el >> 4, etid = wave * 64 + el;
-    constexpr int RS = 2 * TM + 16, EOFF = 2 * SLOT, HT = TN / 2, CPR = TM / 8;
-    constexpr int BOFF = EOFF + HT * RS;  // this tile's TM bias values (D)
-    static_assert(BOFF + 2 * TM <= LDS_BYTES, "bit 6: staging + bias above two ring slots");
-    // this tile's bias into LDS by one asm load per lane of wave 0 (a compiler load would be
-    // waited for with vmcnt(0), i.e. behind the next tile's stages issued below)
-    if (wave == 0 && bias) {
-      const rsrc_t rBias = make_rsrc(bias);
-      u32x4 bw;
-      // (M % 8 == 0, launcher: an 8-row chunk is wholly inside or wholly past M; a chunk past
-      // M loads row 0 and is never read for a stored row)
-      const int b = em0 + 8 * (el & (TM / 8 - 1));
-      ld16<0>(bw, rBias, (uint32_t)(b < M ? b : 0) * 2u, 0u);
-      vmwait<0>();
-      fence(bw);
-      if (el < TM / 8) *(u32x4*)(lds + BOFF + 16 * el) = bw;
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    barrier();
-    const int nxt = tile + (int)gridDim.x;
-    const bool has_next = nxt < ntiles;
-    if (has_next) {
-      tile = nxt;
-      tile_coords(tiles_m, tiles_n, group_m, tm, tn, tile);
-      m0 = tm * TM;
-      n0 = tn * TN;
-      nb = tn * 8 + wave;
-      rA = make_rsrc(A + (size_t)m0 * lda);
-      rB = make_rsrc(Bt + (size_t)nb * nkm * (128 * J));
-      rS = make_rsrc(St + (size_t)nb * ngw * (16 * J));
-      rD = make_rsrc(Salt + (size_t)nb * (nks > 0 ? nks : 1) * (1024 * J));
-      issue_a_p(k_lo, std::true_type{});
-      issue_codes_p(k_lo, cs[0], std::true_type{});
-      issue_a_p(k_lo + 1, std::true_type{});
-    }
-    // y^T in two 128-token halves staged above ring slots 0-1 (waves 4 h .. 4 h + 3 own half h)
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      if ((wave >> 2) == h) {
-#pragma unroll
-        for (int i = 0; i < I; ++i) {
-          const int ml = 16 * i + er16;
-          const float bv = bias ? DT::to_f(*(const T*)(lds + BOFF + 2 * ml)) : 0.f;
-#pragma unroll
-          for (int j = 0; j < J; ++j)
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-              *(T*)(lds + EOFF + (WR * (wave - 4 * h) + 16 * j + 4 * eq + r) * RS + ml * 2) =
-                  DT::from_f(acc[i][j][r] + bv);
-        }
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      barrier();
-#pragma unroll
-      for (int k = etid; k < HT * CPR; k += 512) {
-        const int nl = k / CPR, c = k % CPR;
-        const int gn = en0 + HT * h + nl, gm = em0 + c * 8;
-        if (gn < N && gm < M) {
-          const u32x4 v = *(const u32x4*)(lds + EOFF + nl * RS + c * 16);
-          if (nt)
-            store16_nt(Y + (size_t)gn * M + gm, v);
-          else
-            store16_asm(Y + (size_t)gn * M + gm, v);
-        }
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      barrier();  // the staging area is read before it is rewritten (next half / A(PA - 1))
-    }
-    if (!has_next) return;
-    // the stores this wave just issued (all of them on a whole tile)
-    extra0 = em0 + TM <= M && en0 + TN <= N ? HT * CPR / 512 * 2 : -1;
-#pragma unroll
-    for (int i = 0; i < I; ++i)
-#pragma unroll
-      for (int j = 0; j < J; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    first = false;
-    continue;
-  }  // (tile loop)
-  } else {
   // prologue: A(k_lo), B(k_lo), A(k_lo + 1 .. k_lo + PA - 1)
   issue_a(k_lo);
   issue_codes(k_lo, cs[0]);
@@ -673,7 +459,6 @@ __global__ __launch_bounds__((OPT & 16) ? 1024 : 512, ((OPT & 8) && !(OPT & 16))
       }
     });
     if (more) issue_dense(kd + 1, dd, O());
-  }
   }
 
   if constexpr (KS2) {
@@ -1037,19 +822,6 @@ static int dispatch_group(Fq7Grp& g, int M, int Kp, int S_pad, int Gw, int ngw, 
   return SQMP_OK;
 }
 
-// workgroups of the persistent activation-order grid (OPT bit 6): one per CU, a multiple of 8
-// (the XCD-aware tile map keeps each virtual block on its workgroup's XCD)
-static int persist_grid() {
-  static int g = 0;
-  if (!g) {
-    int dev = 0, cu = 0;
-    (void)hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cu <= 0) cu = 256;
-    g = cu / 8 * 8 > 0 ? cu / 8 * 8 : 8;
-  }
-  return g;
-}
-
 // the activation-order GEMM (TR): kernel M = weight rows N (wp rows), kernel N = tokens M
 // J = 2: 256 weight rows x 256 tokens (8 waves of 32 tokens); J = 4: 128 weight rows x 512
 // tokens (8 waves of 64 tokens: half the wp LDS-DMA and LDS fragment reads per MFMA, twice the
@@ -1101,13 +873,6 @@ static int dispatch_tr(const void* wp, const void* codes_t, const void* scale_t,
       case 3: SQMP_TR(3); break;
       case 4: SQMP_TR(4); break;
       case 5: SQMP_TR(5); break;
-#define SQMP_TRP(O)                                                                             \
-  gemm_fq7_kernel<DT, 1, TM, J, 0, true, O><<<dim3(min(tiles_m * tiles_n, persist_grid())), dim3(512), 0, s>>>( \
-      (const T*)wp, (const uint32_t*)codes_t, (const T*)scale_t, (const T*)sal_t, (const T*)bias, \
-      (T*)y, N, M, Kq, S_pad, G, ngq, tiles_m, tiles_n, group_m_tr_env(), colmax, nt, Fq7Grp{})
-      // (bit 6: persistent grid; TM = 256 only)
-      case 67: if constexpr (TM == 256) { if (!colmax) { SQMP_TRP(67); } else { SQMP_TR(3); } } else { SQMP_TR(3); } break;
-#undef SQMP_TRP
 #define SQMP_TR128(O)                                                                           \
   gemm_fq7_kernel<DT, 1, 128, 2, 0, true, O><<<dim3(cdiv(N, 128) * tiles_n), dim3(512), 0, s>>>( \
       (const T*)wp, (const uint32_t*)codes_t, (const T*)scale_t, (const T*)sal_t, (const T*)bias, \

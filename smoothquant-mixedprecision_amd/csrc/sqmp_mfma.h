@@ -8,10 +8,9 @@ typedef __attribute__((address_space(3))) void* lds_void_ptr;
 
 // XCD-aware bijective block remap + grouped ordering along M (tiles that share a weight
 // column block run together on one XCD).
-__device__ inline void tile_coords(int tiles_m, int tiles_n, int group_m, int& tm, int& tn,
-                                   int bid = -1) {
+__device__ inline void tile_coords(int tiles_m, int tiles_n, int group_m, int& tm, int& tn) {
   const int nwg = tiles_m * tiles_n;
-  if (bid < 0) bid = blockIdx.x;  // (a persistent grid passes its virtual block id)
+  const int bid = blockIdx.x;
   const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
   const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
   const int per_group = group_m * tiles_n;
@@ -127,11 +126,6 @@ __device__ inline void unpack_i8(uint32_t w, uint32_t& lo, uint32_t& hi) {
 // `if (nt) __builtin_nontemporal_store(v, p); else *p = v;` into one plain store.
 __device__ inline void store16_nt(void* p, const u32x4& v) {
   asm volatile("global_store_dwordx4 %0, %1, off nt" ::"v"(p), "v"(v) : "memory");
-}
-// the same store without nt, from asm (invisible to the compiler's vmcnt bookkeeping, as the
-// hand-counted kernels need)
-__device__ inline void store16_asm(void* p, const u32x4& v) {
-  asm volatile("global_store_dwordx4 %0, %1, off" ::"v"(p), "v"(v) : "memory");
 }
 
 __device__ inline void glds16(const void* src, unsigned char* lds_dst) {

@@ -350,29 +350,3 @@ def test_standalone_perm_matches_fused():
     assert st == 0
     assert torch.equal(wp.view(torch.int16), wp2.view(torch.int16))
 
-
-@pytest.mark.parametrize("M,K,N", [
-    (16384, 4096, 4096),   # config 2: 1024 tiles, four per workgroup of the persistent grid
-    (8192, 4096, 1000),    # partial weight-row tiles: stage 0 after a partial epilogue waits for all
-    (4096, 4096, 2048),    # fewer tiles than workgroups: one tile each, no next tile
-    (16640, 4096, 520),    # ragged tokens and weight rows
-])
-def test_fqt7_persistent_bit_identical(M, K, N, monkeypatch):
-    """The persistent activation-order grid (SQMP_FQT7_OPT=67: the next tile's first stages
-    issued before this tile's epilogue stores) computes every tile exactly as the default
-    launch: y bit for bit."""
-    dev = _dev()
-    from smoothquant import ops
-    q, lin, x = _layer(dev, M, K, N, 128, 0.10, torch.float16)
-    pw = q.packed()
-    c4 = ops.quant_act_c4(x, pw, "per_group", 4, 128)
-    if c4[1].dim() != 3:
-        pytest.skip("row-major act-order operands (Kq % 128 != 0): not the fqt7 kernel")
-    reload = __import__("smoothquant._lib", fromlist=["_lib"]).reload_knobs
-    outs = []
-    for v in ("3", "67"):
-        monkeypatch.setenv("SQMP_FQT7_OPT", v)
-        reload()
-        outs.append(ops.gemm_fqt(*c4, pw, lin.bias, 128).clone())
-        torch.cuda.synchronize()
-    assert torch.equal(outs[0].view(torch.int16), outs[1].view(torch.int16))
