@@ -570,6 +570,43 @@ __device__ inline void rank_stage_keys(const uint32_t* key, const int32_t* __res
   }
 }
 
+// DENSE staging (SQMP_RT_DENSE): every column's key key[0 .. K) by coalesced 16-B loads in ONE
+// batch (no nonsal -> key gather: one round trip instead of two dependent ones per batch),
+// padded to 4 K4 entries, then the salient columns' keys (loaded alongside) set to 0xFFFFFFFF,
+// above every real key: an owner then ranks against the non-salient columns in COLUMN order,
+// which is the list order (nonsal ascending), so its ties still break by list index.
+template <int CB>
+__device__ inline void rank_stage_dense(const uint32_t* __restrict__ key, int K, int K4,
+                                        const int32_t* __restrict__ sal, int S, uint32_t* rt_kv) {
+  const u32x4* k4 = (const u32x4*)key;
+  const u32x4 none = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
+  const int Kq = K >> 2;  // K % 4 == 0 (quant_lc_supported: K % 8 == 0)
+  const int tid = threadIdx.x;
+  // the first CB salient indices of this thread ride along with the first key batch
+  int sv[CB];
+  const int nb = (K4 + 256 * CB - 1) / (256 * CB);  // batches (uniform: barriers follow)
+  for (int b = 0; b < nb; ++b) {
+    const int c0 = tid + 256 * CB * b;
+    u32x4 v[CB];
+#pragma unroll
+    for (int u = 0; u < CB; ++u) {
+      const int c = c0 + 256 * u;
+      v[u] = c < Kq ? k4[c] : none;
+      if (b == 0) sv[u] = c < S ? sal[c] : -1;
+    }
+#pragma unroll
+    for (int u = 0; u < CB; ++u) {
+      const int c = c0 + 256 * u;
+      if (c < K4) ((u32x4*)rt_kv)[c] = v[u];
+    }
+  }
+  __syncthreads();  // every key is staged before a salient column's key is overwritten
+#pragma unroll
+  for (int u = 0; u < CB; ++u)
+    if (sv[u] >= 0) rt_kv[sv[u]] = 0xFFFFFFFFu;
+  for (int c = tid + 256 * CB; c < S; c += 256) rt_kv[sal[c]] = 0xFFFFFFFFu;
+}
+
 // Rank the R owners g0 .. g0 + R - 1 of this lane group (TPO lanes, `sub` = this lane's index
 // in it) against the L staged keys, then write their table entries (see rank_table_kernel).
 // An owner's table entries: its column and packed positions (this layer's and the
@@ -603,16 +640,24 @@ __device__ inline RankOwnerEnt<R> rank_owner_ents(int g0, int sub, int L,
   return e;
 }
 
-template <int TPO, int R>
+template <int TPO, int R, bool DENSE = false>
 __device__ inline void rank_owner_group(const uint32_t* rt_kv, int L, int L4, int g0, int sub,
                                         const RankOwnerEnt<R>& oe,
                                         int32_t* __restrict__ colsorted,
                                         uint32_t* __restrict__ lctab, const SibTables& sib) {
   uint32_t mine[R], cnt[R];
-  int ochunk[R];
+  int ochunk[R], oidx[R];
 #pragma unroll
   for (int o = 0; o < R; ++o) {
-    const int oi = g0 + o < L ? g0 + o : L - 1;
+    const int li = g0 + o < L ? g0 + o : L - 1;
+    // (DENSE: the staged array is column-indexed -- the owner sits at its column, which the
+    // group's sub 0 lane loaded; owners past the list rank column 0 and discard)
+    int oi = li;
+    if constexpr (DENSE) {
+      const int c = __shfl(oe.col[o], (int)(threadIdx.x & 63) & ~(TPO - 1), 64);
+      oi = c >= 0 ? c : 0;
+    }
+    oidx[o] = oi;
     mine[o] = rt_kv[oi];
     ochunk[o] = oi >> 2;
     cnt[o] = 0u;
@@ -630,7 +675,7 @@ __device__ inline void rank_owner_group(const uint32_t* rt_kv, int L, int L4, in
   }
 #pragma unroll
   for (int o = 0; o < R; ++o) {
-    const int oi = g0 + o < L ? g0 + o : L - 1;
+    const int oi = oidx[o];
     if (sub == (ochunk[o] % TPO))
       for (int e = 0; e < (oi & 3); ++e) cnt[o] += rt_kv[4 * ochunk[o] + e] == mine[o] ? 1u : 0u;
 #pragma unroll
@@ -644,24 +689,28 @@ __device__ inline void rank_owner_group(const uint32_t* rt_kv, int L, int L4, in
   }
 }
 
-template <int TPO, int R, int SB>
+template <int TPO, int R, int SB, bool DENSE = false>
 __global__ __launch_bounds__(256) void rank_table_kernel(
     const uint32_t* __restrict__ key, const int32_t* __restrict__ nonsal, int L,
     const int32_t* __restrict__ posmap, int32_t* __restrict__ colsorted,
-    uint32_t* __restrict__ lctab, int lc_len, uint32_t lc_none, SibTables sib) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t rt_kv[];  // roundup(L, 4 TPO)
+    uint32_t* __restrict__ lctab, int lc_len, uint32_t lc_none, SibTables sib,
+    int K = 0, const int32_t* __restrict__ sal = nullptr, int S = 0) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t rt_kv[];  // roundup(L or K, 4 TPO)
   const int tid = threadIdx.x;
-  const int L4 = (int)round_up_dev(L, 4 * TPO) >> 2;
+  const int L4 = (int)round_up_dev(DENSE ? K : L, 4 * TPO) >> 2;
   const int g0 = (blockIdx.x * (256 / TPO) + tid / TPO) * R;  // this lane group's first owner
   const RankOwnerEnt<R> oe = rank_owner_ents<R>(g0, tid % TPO, L, nonsal, posmap, sib);
-  rank_stage_keys<SB>(key, nonsal, L, L4, rt_kv);
+  if constexpr (DENSE)
+    rank_stage_dense<12>(key, K, L4, sal, S, rt_kv);
+  else
+    rank_stage_keys<SB>(key, nonsal, L, L4, rt_kv);
   const int nt = gridDim.x * 256;
   for (int r = L + blockIdx.x * 256 + tid; r < lc_len; r += nt) {
     lctab[r] = lc_none;
     for (int o = 0; o < sib.n; ++o) sib.lctab[o][r] = lc_none;
   }
   __syncthreads();
-  rank_owner_group<TPO, R>(rt_kv, L, L4, g0, tid % TPO, oe, colsorted, lctab, sib);
+  rank_owner_group<TPO, R, DENSE>(rt_kv, L, L4, g0, tid % TPO, oe, colsorted, lctab, sib);
 }
 
 // ---------------------------------------------------------------- bucketed rank + table
@@ -796,22 +845,22 @@ static bool rank_table_fits(int L) {
   return !off && L > 0 && L <= RT_MAX;
 }
 
-template <int SBV>
+template <int SBV, bool DN = false>
 static void rank_table_go(int tpo, int r, int grid, size_t lds, hipStream_t s,
                           const uint32_t* key, const int32_t* nonsal, int L,
                           const int32_t* posmap, int32_t* colsorted, uint32_t* lctab,
-                          int lc_len, uint32_t lc_none, const SibTables& sib) {
+                          int lc_len, uint32_t lc_none, const SibTables& sib, int K = 0,
+                          const int32_t* sal = nullptr, int S = 0) {
 #define SQMP_RT(T, RR)                                                                       \
   do {                                                                                      \
     static bool attr = false; /* up to 64 KiB of keys: raise the dynamic-LDS limit once */ \
     if (!attr) {                                                                            \
-      (void)hipFuncSetAttribute((const void*)rank_table_kernel<T, RR, SBV>,                 \
+      (void)hipFuncSetAttribute((const void*)rank_table_kernel<T, RR, SBV, DN>,             \
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 4 * RT_MAX);    \
       attr = true;                                                                          \
     }                                                                                       \
-    rank_table_kernel<T, RR, SBV><<<dim3(grid), dim3(256), lds, s>>>(key, nonsal, L, posmap, \
-                                                               colsorted, lctab, lc_len,    \
-                                                               lc_none, sib);               \
+    rank_table_kernel<T, RR, SBV, DN><<<dim3(grid), dim3(256), lds, s>>>(                   \
+        key, nonsal, L, posmap, colsorted, lctab, lc_len, lc_none, sib, K, sal, S);         \
   } while (0)
 #define SQMP_RT_T(T)            \
   switch (r) {                  \
@@ -828,10 +877,12 @@ static void rank_table_go(int tpo, int r, int grid, size_t lds, hipStream_t s,
 #undef SQMP_RT
 }
 
+// K / sal / S (K > 0): the column count and salient list, for the dense key staging
 static int launch_rank_table(const uint32_t* key, const int32_t* nonsal, int L,
                              const int32_t* posmap, int32_t* colsorted, uint32_t* lctab,
                              int lc_len, uint32_t lc_none, hipStream_t s,
-                             const SibTables& sib = SibTables{}) {
+                             const SibTables& sib = SibTables{}, int K = 0,
+                             const int32_t* sal = nullptr, int S = 0) {
   // TPO lanes per group of R owners (SQMP_RT_TPO = 8 / 16 / 32 and SQMP_RT_R = 1 / 2 / 4
   // override, tuning only, read per launch)
   const char* te = knob("SQMP_RT_TPO");
@@ -876,6 +927,17 @@ static int launch_rank_table(const uint32_t* key, const int32_t* nonsal, int L,
     return SQMP_OK;
   }
   const int grid = cdiv((long)L * tpo, 256L * r);
+  // every column's key staged by coalesced loads, the salient ones masked (rank_stage_dense;
+  // default: down_proj's packed-order prepass 49.9 -> 47.7 us, config-2 C4 prepass 73.0 ->
+  // 72.0 us, profiles/r05_ab_rank_dense.txt); SQMP_RT_DENSE=0: the list gather (A/B)
+  const char* de = knob("SQMP_RT_DENSE");
+  if (!(de && atoi(de) == 0) && K > 0 && K <= RT_MAX && K % 4 == 0 && (S == 0 || sal)) {
+    const size_t dlds = sizeof(uint32_t) * (size_t)round_up(K, 4 * tpo);
+    rank_table_go<24, true>(tpo, r, grid, dlds, s, key, nonsal, L, posmap, colsorted, lctab,
+                            lc_len, lc_none, sib, K, sal, S);
+    SQMP_LAUNCH_CHECK();
+    return SQMP_OK;
+  }
   const size_t lds = sizeof(uint32_t) * (size_t)round_up(L, 4 * tpo);
   if (sb == 8)
     rank_table_go<8>(tpo, r, grid, lds, s, key, nonsal, L, posmap, colsorted, lctab, lc_len,
@@ -1591,7 +1653,8 @@ static int quant_act_impl(void* x, int dtype, int M, int K, int amode, int n_bit
         if (st2) return st2;
         if (rank_table_fits(Kn)) {
           key_clear = cmax;  // cleared by the quantizer, after every rank_table read
-          return launch_rank_table(cmax, nonsal, Kn, pm, colsorted, lctab, lc_len, none, s);
+          return launch_rank_table(cmax, nonsal, Kn, pm, colsorted, lctab, lc_len, none, s,
+                                   SibTables{}, K, salient, S);
         }
         if (!clean) SQMP_HIP_CHECK(hipMemsetAsync(counts, 0, sizeof(int32_t) * k64, s));
         st2 = launch_rank_count(cmax, nonsal, Kn, counts, s);
@@ -1867,7 +1930,8 @@ extern "C" int sqmp_quant_act_group(void* x, int dtype, int M, int K, int amode,
   int r = amode == SQMP_ACT_PER_GROUP ? launch_colmax(x, dtype, M, K, cmax, s, false)
                                       : launch_colkey_mean3std(x, dtype, M, K, sums, cmax, s, true);
   if (r) return r;
-  r = launch_rank_table(cmax, nonsal, Kn, posmaps[0], colsorted, lctab, lc_len, lc_none, s, st);
+  r = launch_rank_table(cmax, nonsal, Kn, posmaps[0], colsorted, lctab, lc_len, lc_none, s, st, K,
+                        salient, S);
   if (r) return r;
   return launch_quant_lc_group(dtype, x, M, K, (1 << (n_bits - 1)) - 1, group_size, lctab, Kn,
                                amaps[0], Kp, salient, S, S_pad, cmax, nonsal, outs[0], cmax,

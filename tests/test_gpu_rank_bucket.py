@@ -53,3 +53,36 @@ def test_bucketed_rank_bit_identical(M, K, Ns, G, p, dt, kind, btpo, monkeypatch
         torch.cuda.synchronize()
     for a, b in zip(outs["0"], outs["1"]):
         assert torch.equal(a.view(torch.int16), b.view(torch.int16))
+
+
+@pytest.mark.parametrize("kind", ["random", "ties", "equal", "zeros"])
+@pytest.mark.parametrize("M,K,Ns,G,p,dt", [
+    (256, 1024, (512,), 64, 0.05, torch.float16),
+    (2048, 4096, (4096, 4096, 4096), 64, 0.05, torch.float16),
+    (300, 11008, (4096,), 64, 0.05, torch.float16),
+    (129, 768, (768, 768), 128, 0.10, torch.bfloat16),
+    (64, 192, (64,), 64, 0.05, torch.float16),
+    (96, 16384, (256,), 128, 0.30, torch.float16),
+])
+def test_dense_rank_staging_bit_identical(M, K, Ns, G, p, dt, kind, monkeypatch):
+    """The rank table with every column's key staged by coalesced loads and the salient
+    columns masked (the default: ties broken by column order = list order) against the list
+    gather (SQMP_RT_DENSE=0): bit-identical operands, ragged K, a salient list longer than
+    the first staging batch (30 % of 16384 columns)."""
+    dev = _dev()
+    from smoothquant import ops
+    lib = __import__("smoothquant._lib", fromlist=["_lib"])
+    layers, x = _siblings(dev, M, K, Ns, G, p, dt, seed=9)
+    x = _inputs(kind, x).contiguous()
+    pws = [q.packed() for q in layers]
+    outs = {}
+    for on in ("0", "1"):
+        monkeypatch.setenv("SQMP_RT_DENSE", on)
+        lib.reload_knobs()
+        if len(pws) > 1:
+            outs[on] = [a.clone() for a in ops.quant_act_fp_group(x, pws, "per_group", 4, G)]
+        else:
+            outs[on] = [ops.quant_act_fp(x, pws[0], "per_group", 4, G).clone()]
+        torch.cuda.synchronize()
+    for a, b in zip(outs["0"], outs["1"]):
+        assert torch.equal(a.view(torch.int16), b.view(torch.int16))
