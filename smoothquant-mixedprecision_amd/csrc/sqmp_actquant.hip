@@ -689,7 +689,104 @@ __device__ inline void rank_owner_group(const uint32_t* rt_kv, int L, int L4, in
   }
 }
 
-template <int TPO, int R, int SB, bool DENSE = false>
+// ---- 16-bit dense ranking (KW = 1 / 2: column maxima of f16 / bf16 data, whose keys are
+// the values' 15-bit f16 / bf16 patterns -- monotone for non-negative values): half the LDS
+// bytes, and two keys per packed u16 compare: [key < thr] = min(sat(thr - key), 1) with
+// v_pk_sub_u16 clamp / v_pk_min_u16 / v_pk_add_u16 (three packed ops per two compares, no
+// VCC round trip); the salient / padding sentinel 0xFFFF never counts (thr <= 0x8000).
+typedef unsigned short u16x2v __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x2r __attribute__((ext_vector_type(2)));
+template <int KW, int CB>
+__device__ inline void rank_stage_dense16(const uint32_t* __restrict__ key, int K, int K8,
+                                          const int32_t* __restrict__ sal, int S, uint16_t* kv) {
+  const u32x4* k4 = (const u32x4*)key;
+  const int Kq = K >> 2, Q = 2 * K8;  // u32x4 key chunks: real, staged (4 keys each)
+  const int tid = threadIdx.x;
+  int sv[CB];
+  const int nb = (Q + 256 * CB - 1) / (256 * CB);
+  for (int b = 0; b < nb; ++b) {
+    const int c0 = tid + 256 * CB * b;
+    u32x4 v[CB];
+#pragma unroll
+    for (int u = 0; u < CB; ++u) {
+      const int c = c0 + 256 * u;
+      v[u] = c < Kq ? k4[c] : u32x4{0u, 0u, 0u, 0u};
+      if (b == 0) sv[u] = c < S ? sal[c] : -1;
+    }
+#pragma unroll
+    for (int u = 0; u < CB; ++u) {
+      const int c = c0 + 256 * u;
+      if (c < Q) {
+        uint32_t h[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          h[e] = c < Kq ? (KW == 2 ? v[u][e] >> 16
+                                   : (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)__uint_as_float(v[u][e])))
+                        : 0xFFFFu;
+        ((u32x2r*)kv)[c] = u32x2r{h[0] | h[1] << 16, h[2] | h[3] << 16};
+      }
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < CB; ++u)
+    if (sv[u] >= 0) kv[sv[u]] = 0xFFFFu;
+  for (int c = tid + 256 * CB; c < S; c += 256) kv[sal[c]] = 0xFFFFu;
+}
+
+template <int TPO, int R>
+__device__ inline void rank_owner_group16(const uint16_t* kv, int L, int K8, int g0, int sub,
+                                          const RankOwnerEnt<R>& oe,
+                                          int32_t* __restrict__ colsorted,
+                                          uint32_t* __restrict__ lctab, const SibTables& sib) {
+  uint32_t mine[R], cnt[R];
+  int ochunk[R], oidx[R];
+#pragma unroll
+  for (int o = 0; o < R; ++o) {
+    const int c = __shfl(oe.col[o], (int)(threadIdx.x & 63) & ~(TPO - 1), 64);
+    oidx[o] = c >= 0 ? c : 0;
+    mine[o] = kv[oidx[o]];
+    ochunk[o] = oidx[o] >> 3;
+  }
+  const u32x4* kv8 = (const u32x4*)kv;
+  const uint32_t one = 0x00010001u;
+  uint32_t pk[R];
+#pragma unroll
+  for (int o = 0; o < R; ++o) pk[o] = 0u;
+#pragma unroll 2
+  for (int j8 = sub; j8 < K8; j8 += TPO) {
+    const u32x4 k = kv8[j8];
+#pragma unroll
+    for (int o = 0; o < R; ++o) {
+      const uint32_t t = j8 < ochunk[o] ? mine[o] + 1u : mine[o];
+      const uint32_t thr = t | t << 16;
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        // (asm: the compiler turns the builtin form back into compares + selects)
+        uint32_t x;
+        asm("v_pk_sub_u16 %0, %1, %2 clamp\n\tv_pk_min_u16 %0, %0, %3" : "=&v"(x) : "v"(thr), "v"(k[d]), "v"(one));
+        asm("v_pk_add_u16 %0, %0, %1" : "+v"(pk[o]) : "v"(x));
+      }
+    }
+  }
+#pragma unroll
+  for (int o = 0; o < R; ++o) {
+    cnt[o] = (pk[o] & 0xFFFFu) + (pk[o] >> 16);
+    const int oi = oidx[o];
+    if (sub == (ochunk[o] % TPO))
+      for (int e = 0; e < (oi & 7); ++e) cnt[o] += kv[8 * ochunk[o] + e] == mine[o] ? 1u : 0u;
+#pragma unroll
+    for (int w = 1; w < TPO; w <<= 1) cnt[o] += (uint32_t)__shfl_xor((int)cnt[o], w, 64);
+    if (sub == 0 && g0 + o < L) {
+      colsorted[cnt[o]] = oe.col[o];
+      lctab[cnt[o]] = oe.ent[o][0];
+      if (sib.n > 0) sib.lctab[0][cnt[o]] = oe.ent[o][1];
+      if (sib.n > 1) sib.lctab[1][cnt[o]] = oe.ent[o][2];
+    }
+  }
+}
+
+template <int TPO, int R, int SB, bool DENSE = false, int KW = 0>
 __global__ __launch_bounds__(256) void rank_table_kernel(
     const uint32_t* __restrict__ key, const int32_t* __restrict__ nonsal, int L,
     const int32_t* __restrict__ posmap, int32_t* __restrict__ colsorted,
@@ -697,10 +794,12 @@ __global__ __launch_bounds__(256) void rank_table_kernel(
     int K = 0, const int32_t* __restrict__ sal = nullptr, int S = 0) {
   extern __shared__ __attribute__((aligned(16))) uint32_t rt_kv[];  // roundup(L or K, 4 TPO)
   const int tid = threadIdx.x;
-  const int L4 = (int)round_up_dev(DENSE ? K : L, 4 * TPO) >> 2;
+  const int L4 = (int)round_up_dev(DENSE ? K : L, (KW ? 8 : 4) * TPO) >> 2;  // u32x4 words: L4 / (KW ? 2 : 1) chunks
   const int g0 = (blockIdx.x * (256 / TPO) + tid / TPO) * R;  // this lane group's first owner
   const RankOwnerEnt<R> oe = rank_owner_ents<R>(g0, tid % TPO, L, nonsal, posmap, sib);
-  if constexpr (DENSE)
+  if constexpr (KW != 0)
+    rank_stage_dense16<KW, 12>(key, K, L4 >> 1, sal, S, (uint16_t*)rt_kv);
+  else if constexpr (DENSE)
     rank_stage_dense<12>(key, K, L4, sal, S, rt_kv);
   else
     rank_stage_keys<SB>(key, nonsal, L, L4, rt_kv);
@@ -710,7 +809,10 @@ __global__ __launch_bounds__(256) void rank_table_kernel(
     for (int o = 0; o < sib.n; ++o) sib.lctab[o][r] = lc_none;
   }
   __syncthreads();
-  rank_owner_group<TPO, R, DENSE>(rt_kv, L, L4, g0, tid % TPO, oe, colsorted, lctab, sib);
+  if constexpr (KW != 0)
+    rank_owner_group16<TPO, R>((const uint16_t*)rt_kv, L, L4 >> 1, g0, tid % TPO, oe, colsorted, lctab, sib);
+  else
+    rank_owner_group<TPO, R, DENSE>(rt_kv, L, L4, g0, tid % TPO, oe, colsorted, lctab, sib);
 }
 
 // ---------------------------------------------------------------- bucketed rank + table
@@ -845,7 +947,7 @@ static bool rank_table_fits(int L) {
   return !off && L > 0 && L <= RT_MAX;
 }
 
-template <int SBV, bool DN = false>
+template <int SBV, bool DN = false, int KWV = 0>
 static void rank_table_go(int tpo, int r, int grid, size_t lds, hipStream_t s,
                           const uint32_t* key, const int32_t* nonsal, int L,
                           const int32_t* posmap, int32_t* colsorted, uint32_t* lctab,
@@ -855,11 +957,11 @@ static void rank_table_go(int tpo, int r, int grid, size_t lds, hipStream_t s,
   do {                                                                                      \
     static bool attr = false; /* up to 64 KiB of keys: raise the dynamic-LDS limit once */ \
     if (!attr) {                                                                            \
-      (void)hipFuncSetAttribute((const void*)rank_table_kernel<T, RR, SBV, DN>,             \
+      (void)hipFuncSetAttribute((const void*)rank_table_kernel<T, RR, SBV, DN, KWV>,        \
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 4 * RT_MAX);    \
       attr = true;                                                                          \
     }                                                                                       \
-    rank_table_kernel<T, RR, SBV, DN><<<dim3(grid), dim3(256), lds, s>>>(                   \
+    rank_table_kernel<T, RR, SBV, DN, KWV><<<dim3(grid), dim3(256), lds, s>>>(              \
         key, nonsal, L, posmap, colsorted, lctab, lc_len, lc_none, sib, K, sal, S);         \
   } while (0)
 #define SQMP_RT_T(T)            \
@@ -877,12 +979,20 @@ static void rank_table_go(int tpo, int r, int grid, size_t lds, hipStream_t s,
 #undef SQMP_RT
 }
 
-// K / sal / S (K > 0): the column count and salient list, for the dense key staging
+// the 16-bit dense rank's key kind: column maxima of f16 / bf16 data (the per_group sort
+// key), else 0 (fp32 data, mean3std keys: 32-bit keys)
+static int rank_key_kind(int amode, int dtype) {
+  if (amode != SQMP_ACT_PER_GROUP) return 0;
+  return dtype == SQMP_F16 ? 1 : dtype == SQMP_BF16 ? 2 : 0;
+}
+
+// K / sal / S (K > 0): the column count and salient list, for the dense key staging; kw: the
+// key kind (rank_key_kind)
 static int launch_rank_table(const uint32_t* key, const int32_t* nonsal, int L,
                              const int32_t* posmap, int32_t* colsorted, uint32_t* lctab,
                              int lc_len, uint32_t lc_none, hipStream_t s,
                              const SibTables& sib = SibTables{}, int K = 0,
-                             const int32_t* sal = nullptr, int S = 0) {
+                             const int32_t* sal = nullptr, int S = 0, int kw = 0) {
   // TPO lanes per group of R owners (SQMP_RT_TPO = 8 / 16 / 32 and SQMP_RT_R = 1 / 2 / 4
   // override, tuning only, read per launch)
   const char* te = knob("SQMP_RT_TPO");
@@ -932,6 +1042,20 @@ static int launch_rank_table(const uint32_t* key, const int32_t* nonsal, int L,
   // 72.0 us, profiles/r05_ab_rank_dense.txt); SQMP_RT_DENSE=0: the list gather (A/B)
   const char* de = knob("SQMP_RT_DENSE");
   if (!(de && atoi(de) == 0) && K > 0 && K <= RT_MAX && K % 4 == 0 && (S == 0 || sal)) {
+    // 16-bit keys (f16 / bf16 column maxima; down_proj prepass 47.5 -> 45.2 us,
+    // profiles/r05_ab_rank_k16.txt) unless SQMP_RT_K16=0 (A/B)
+    const char* k16 = knob("SQMP_RT_K16");
+    if (kw != 0 && !(k16 && atoi(k16) == 0)) {
+      const size_t hlds = sizeof(uint16_t) * (size_t)round_up(K, 8 * tpo);
+      if (kw == 2)
+        rank_table_go<24, true, 2>(tpo, r, grid, hlds, s, key, nonsal, L, posmap, colsorted,
+                                   lctab, lc_len, lc_none, sib, K, sal, S);
+      else
+        rank_table_go<24, true, 1>(tpo, r, grid, hlds, s, key, nonsal, L, posmap, colsorted,
+                                   lctab, lc_len, lc_none, sib, K, sal, S);
+      SQMP_LAUNCH_CHECK();
+      return SQMP_OK;
+    }
     const size_t dlds = sizeof(uint32_t) * (size_t)round_up(K, 4 * tpo);
     rank_table_go<24, true>(tpo, r, grid, dlds, s, key, nonsal, L, posmap, colsorted, lctab,
                             lc_len, lc_none, sib, K, sal, S);
@@ -1654,7 +1778,7 @@ static int quant_act_impl(void* x, int dtype, int M, int K, int amode, int n_bit
         if (rank_table_fits(Kn)) {
           key_clear = cmax;  // cleared by the quantizer, after every rank_table read
           return launch_rank_table(cmax, nonsal, Kn, pm, colsorted, lctab, lc_len, none, s,
-                                   SibTables{}, K, salient, S);
+                                   SibTables{}, K, salient, S, rank_key_kind(amode, dtype));
         }
         if (!clean) SQMP_HIP_CHECK(hipMemsetAsync(counts, 0, sizeof(int32_t) * k64, s));
         st2 = launch_rank_count(cmax, nonsal, Kn, counts, s);
@@ -1931,7 +2055,7 @@ extern "C" int sqmp_quant_act_group(void* x, int dtype, int M, int K, int amode,
                                       : launch_colkey_mean3std(x, dtype, M, K, sums, cmax, s, true);
   if (r) return r;
   r = launch_rank_table(cmax, nonsal, Kn, posmaps[0], colsorted, lctab, lc_len, lc_none, s, st, K,
-                        salient, S);
+                        salient, S, rank_key_kind(amode, dtype));
   if (r) return r;
   return launch_quant_lc_group(dtype, x, M, K, (1 << (n_bits - 1)) - 1, group_size, lctab, Kn,
                                amaps[0], Kp, salient, S, S_pad, cmax, nonsal, outs[0], cmax,
