@@ -77,3 +77,31 @@ def test_h2d_kernels_do_not_spill(tmp_path):
         vgprs = int(re.search(r"VGPRs: (\d+)", b).group(1))
         assert spill == 0 and scratch == 0 and vgprs <= 256, (b.split()[0], spill, scratch, vgprs)
     assert seen == 4
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC) and shutil.which("hipcc") is None,
+                    reason="hipcc not available")
+def test_asm_sgpr_hazard_other_kernels(tmp_path):
+    """The same inline-asm SGPR hazard scan (tools/check_asm_sgpr_hazard.py) on the other
+    sources whose kernels issue hand-written buffer loads / LDS-DMA / stores from asm."""
+    from concurrent.futures import ThreadPoolExecutor
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import check_asm_sgpr_hazard as H
+    csrc = os.path.dirname(SRC)
+    names = ["sqmp_gemm_f8", "sqmp_gemm_h2d", "sqmp_actquant_lc", "sqmp_gemm_fqa", "sqmp_gemm_fast",
+             "sqmp_gemm_x3"]
+
+    def asm(n):
+        out = str(tmp_path / (n + ".s"))
+        extra = ["-fno-slp-vectorize"] if n == "sqmp_gemm_f8" else []
+        r = subprocess.run([HIPCC, "-O3", "-std=c++17", "--offload-arch=gfx950", "--cuda-device-only",
+                            "-S", *extra, "-I", os.path.join(ROOT, "include"),
+                            os.path.join(csrc, n + ".hip"), "-o", out],
+                           capture_output=True, text=True, timeout=900)
+        return n, r.returncode, out
+
+    with ThreadPoolExecutor(max_workers=min(6, os.cpu_count() or 1)) as ex:
+        results = list(ex.map(asm, names))
+    for n, rc, out in results:
+        assert rc == 0, n
+        assert H.main(out) == 0, n
