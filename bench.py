@@ -16,9 +16,14 @@ GPU before that) and exits with its status.
 
 Also printed in the same JSON line:
   roofline      the dominant kernel (the GEMM), timed live with HIP events on the stream
-                it runs on; achieved = 2*M*N*K / average GEMM duration; `peak`/`frac` =
-                dense MFMA peak of the dtype the kernel computes in; `frac_contract_*` =
-                BASELINE.md §2's T_roof / time, T_roof = 2MNK'/P_i8 + 2MNS/P_f16 (120.9 us)
+                it runs on; achieved = 2*M*N*K / average GEMM duration; `peak` = the
+                north star's int8-MFMA roofline as a rate, 2*M*N*K / T_roof with BASELINE.md
+                §2's T_roof = 2MNK'/P_i8 + 2MNS/P_f16 (about 120 us: the int4 contraction on
+                the int8 MFMA, the salient columns on the f16 MFMA), so `frac` = T_roof / GEMM
+                time = the "fraction of the int8-MFMA roofline"; `frac_dtype_peak` = achieved
+                / the dense MFMA peak of the dtype the kernel computes in (f16 for the
+                faithful per_group kernel, whose exact operands rule out the int8 MFMA:
+                SURVEY.md §7 hard part 1); `frac_contract_step` = T_roof / step time
   cpu_baseline  the reference's fake-quant layer restated in PyTorch ops (oracle/
                 torch_cpu.py, pinned bit-exact to the reference goldens) in fp32 on this
                 host's cores: rank 0, N=1 only, median of 3 after 1 warm-up
@@ -705,19 +710,23 @@ def main(argv=None):
         "roofline": {
             "bound": "mfma",
             "achieved": round(achieved, 1),
-            "peak": PEAK_TFLOPS[kdt],
+            "peak": round(flops / t_roof / 1e12, 1),
+            "peak_kind": "int8-MFMA contract roofline: 2MNK / (2MNK'/P_i8 + 2MNS/P_f16)",
             "unit": "TFLOP/s",
-            "frac": round(achieved / PEAK_TFLOPS[kdt], 4),
+            "frac": round(t_roof / (gemm_ms * 1e-3), 4),
+            "frac_dtype_peak": round(achieved / PEAK_TFLOPS[kdt], 4),
+            "dtype_peak": PEAK_TFLOPS[kdt],
             "traffic": traffic,
             "traffic_profile": traffic_prof,
             "kernel": kname,
             "avg_ms": round(gemm_ms, 4),
             "algorithmic_flops_per_launch": flops,
             "t_roof_contract_us": round(t_roof * 1e6, 2),
-            "frac_contract_gemm": round(t_roof / (gemm_ms * 1e-3), 4),
             "frac_contract_step": round(t_roof / (ms_per_step * 1e-3), 4),
-            "note": ("frac = achieved / dense MFMA peak of the kernel's dtype; frac_contract_* "
-                     "= BASELINE.md §2 T_roof (2MNK'/P_i8 + 2MNS/P_f16) / GEMM time, / step time"
+            "note": ("frac = the fraction of the int8-MFMA roofline (BASELINE.md §2 T_roof = "
+                     "2MNK'/P_i8 + 2MNS/P_f16, over the GEMM time; peak = 2MNK / T_roof); "
+                     "frac_dtype_peak = achieved / the dense MFMA peak of the kernel's dtype "
+                     "(dtype_peak); frac_contract_step = T_roof / step time"
                      + ("; fp32: peak = the f32 MFMA (the dtype's own); the kernel executes "
                         "3 f16 MFMAs per product over Kp + S_pad positions: "
                         f"executed_f16_frac = {3 * achieved * (pw.Kp + pw.S_pad) / K / PEAK_TFLOPS['f16']:.4f}"

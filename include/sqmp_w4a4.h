@@ -180,10 +180,6 @@ int sqmp_quant_act(void* x, int dtype, int M, int K, int amode, int n_bits,
                                  J = 2 and N = M gives their sizes) instead of row-major */
 #define SQMP_QA_TILED4 16     /* as SQMP_QA_TILED with 64-row blocks (J = 4), the operands of
                                  sqmp_gemm_fqt7j with J = 4 */
-#define SQMP_QA_WPT 64        /* sqmp_quant_act_c4: the permuted weight written in sqmp_gemm_fqa's
-                                 tile-major register layout (sqmp_fqa_wpt_elems elements: rows
-                                 roundup(N, 512), zeros past N) with the activation operands
-                                 row-major (exclusive with the TILED flags) */
 
 /* sqmp_quant_act with the per-weight map posmap (int32 [K]: packed position of column k,
  * the inverse of perm; NULL = derive it per call) and flags.  With posmap, OUT_FP on
@@ -329,25 +325,6 @@ int sqmp_gemm_fqt7j(const void* codes_t, const void* scale_t, const void* sal_t,
  * the library otherwise reads once, at load: for tools that switch a variant in-process. */
 int sqmp_reload_knobs(void);
 
-/* The activation-order GEMM with the int4 act codes decoded once per workgroup into an LDS
- * tile and the permuted weight in registers (128 tokens x 512 weight rows per workgroup):
- * y[M][N] = D(x_hat . W_hat^T + bias) on sqmp_quant_act_c4's ROW-MAJOR activation operands
- * (acodes [R][Kq/2] bytes, ascale D [ngq][ldsc], xs D [R][S_pad], R >= roundup(M, 128) rows,
- * ldsc >= roundup(M, 128)) and the SQMP_QA_WPT weight (wpt).  The same products as
- * sqmp_gemm_fqt7 up to the fp32 accumulation order.  Kq % 64 == 0, S_pad % 64 == 0, G a power
- * of two >= 64, N % 8 == 0, fp16 / bf16; colmax NULL: no fused column statistics.
- * Kq = 0: the dense GEMM y = xs . wpt^T (acodes / ascale unused; the dense-core measurement). */
-int sqmp_gemm_fqa(const void* acodes, const void* ascale, const void* xs, const void* wpt,
-                  const void* bias, void* y, int dtype, int M, int N, int Kq, int S_pad, int G,
-                  int ldsc, uint32_t* colmax, void* stream);
-
-/* Elements of sqmp_gemm_fqa's weight operand: roundup(N, 512) * (Kq + S_pad). */
-size_t sqmp_fqa_wpt_elems(int N, int Kq, int S_pad);
-
-/* A dense D [N][L] matrix (L % 64 == 0) in sqmp_gemm_fqa's weight layout (wpt of
- * sqmp_fqa_wpt_elems(N, L, 0) elements). */
-int sqmp_pack_wpt(const void* w, int dtype, int N, int L, void* wpt, void* stream);
-
 /* Sibling operand reuse: dst = the SQMP_OUT_FP operand of a layer whose weight shares the
  * quantized input, the salient set and the act mode with the layer that produced src (q/k/v,
  * gate/up), rebuilt by moving positions instead of quantizing again: dst[m][p] =
@@ -393,6 +370,15 @@ typedef struct sqmp_fq7_problem {
 } sqmp_fq7_problem;
 int sqmp_gemm_fq7_group(const sqmp_fq7_problem* probs, int nprob, int dtype, int M, int Kp,
                         int S_pad, int Gw, int ngw, int J, void* stream);
+
+/* The kernel variant sqmp_gemm_fq7 (nprob = 0: the problem N[0] alone) or sqmp_gemm_fq7_group
+ * (nprob problems of N[0 .. nprob)) launches for these shapes: *tm = the row-tile height, *opt =
+ * the OPT bits of the packed-order kernel (bit 16 = the K split inside the workgroup: its fp32
+ * partial sums add in another order, so its y equals the unsplit kernel's only within fp32
+ * rounding; every other bit gives bit-identical y).  Tests and tools use it to know which
+ * launches must agree bit for bit. */
+int sqmp_fq7_plan(int dtype, int M, const int* N, int nprob, int Kp, int Gw, int J, int* tm,
+                  int* opt);
 
 /* The fp32 faithful GEMM on the f16 MFMA (the default for fp32 layers): every row of A and
  * of W is scaled by a power of two (exact) so that its maximum lies in [2^13, 2^14), each

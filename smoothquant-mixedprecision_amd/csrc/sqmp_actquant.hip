@@ -955,12 +955,10 @@ static void rank_table_go(int tpo, int r, int grid, size_t lds, hipStream_t s,
                           const int32_t* sal = nullptr, int S = 0) {
 #define SQMP_RT(T, RR)                                                                       \
   do {                                                                                      \
-    static bool attr = false; /* up to 64 KiB of keys: raise the dynamic-LDS limit once */ \
-    if (!attr) {                                                                            \
+    static uint64_t attr = 0; /* up to 64 KiB of keys: the dynamic-LDS limit, per device */ \
+    if (first_on_device(attr))                                                              \
       (void)hipFuncSetAttribute((const void*)rank_table_kernel<T, RR, SBV, DN, KWV>,        \
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 4 * RT_MAX);    \
-      attr = true;                                                                          \
-    }                                                                                       \
     rank_table_kernel<T, RR, SBV, DN, KWV><<<dim3(grid), dim3(256), lds, s>>>(              \
         key, nonsal, L, posmap, colsorted, lctab, lc_len, lc_none, sib, K, sal, S);         \
   } while (0)
@@ -1015,12 +1013,10 @@ static int launch_rank_table(const uint32_t* key, const int32_t* nonsal, int L,
                         sizeof(uint16_t) * (size_t)round_up(L, 2);
 #define SQMP_RB(T)                                                                            \
   do {                                                                                       \
-    static bool battr = false;                                                               \
-    if (!battr) {                                                                            \
+    static uint64_t battr = 0;                                                               \
+    if (first_on_device(battr))                                                              \
       (void)hipFuncSetAttribute((const void*)rank_bucket_kernel<T, 24>,                      \
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);     \
-      battr = true;                                                                          \
-    }                                                                                        \
     rank_bucket_kernel<T, 24><<<dim3(bgrid), dim3(256), blds, s>>>(key, nonsal, L, posmap,   \
                                                                   colsorted, lctab, lc_len,  \
                                                                   lc_none, sib);             \
@@ -1666,6 +1662,7 @@ extern "C" int sqmp_quant_act_v2(void* x, int dtype, int M, int K, int amode, in
                                  int S_pad, const int32_t* posmap, int flags, int out_kind,
                                  void* out, void* out_scale, void* out_xs, void* workspace,
                                  size_t ws_bytes, void* stream) {
+  SQMP_DEVICE_GUARD(stream);
   return quant_act_impl(x, dtype, M, K, amode, n_bits, group_size, amap, Kp, nonsal, salient, S,
                         S_pad, posmap, flags, out_kind, out, out_scale, out_xs, workspace,
                         ws_bytes, stream, nullptr);
@@ -1682,11 +1679,7 @@ static int quant_act_impl(void* x, int dtype, int M, int K, int amode, int n_bit
   if (n_bits < 2 || n_bits > 8) return SQMP_EUNSUPPORTED;
   if (S < 0 || S > K || !x || !amap || (K - S > 0 && !nonsal)) return SQMP_EINVAL;
   if (flags & ~(SQMP_QA_CLEAN_WS | SQMP_QA_REUSE_STATS | SQMP_QA_STATS_GIVEN | SQMP_QA_TILED |
-                SQMP_QA_TILED4 | SQMP_QA_WPT))
-    return SQMP_EINVAL;
-  // the fqa weight layout goes with the row-major activation operands, and needs the weight
-  if ((flags & SQMP_QA_WPT) &&
-      (!cw || (flags & (SQMP_QA_TILED | SQMP_QA_TILED4))))
+                SQMP_QA_TILED4))
     return SQMP_EINVAL;
   if ((flags & (SQMP_QA_TILED | SQMP_QA_TILED4)) && out_kind != SQMP_OUT_C4)
     return SQMP_EINVAL;
@@ -1950,6 +1943,7 @@ extern "C" int sqmp_quant_act(void* x, int dtype, int M, int K, int amode, int n
                               const int32_t* nonsal, const int32_t* salient, int S, int S_pad,
                               int out_kind, void* out, void* out_scale, void* out_xs,
                               void* workspace, size_t ws_bytes, void* stream) {
+  SQMP_DEVICE_GUARD(stream);
   return sqmp_quant_act_v2(x, dtype, M, K, amode, n_bits, group_size, amap, Kp, nonsal,
                            salient, S, S_pad, nullptr, 0, out_kind, out, out_scale, out_xs,
                            workspace, ws_bytes, stream);
@@ -1965,6 +1959,7 @@ static const uint32_t* ws_lctab(const void* workspace, int K, int Kp) {
 extern "C" int sqmp_perm_weight_c4(const void* workspace, int K, int Kp, int S, int S_pad,
                                    const void* codes, const void* wscale, const void* wsal,
                                    int dtype, int N, int Gw, int ngw, void* wp, void* stream) {
+  SQMP_DEVICE_GUARD(stream);
   if (!workspace || !codes || !wscale || !wp || (S > 0 && !wsal)) return SQMP_EINVAL;
   if (K <= 0 || S < 0 || S >= K || Kp < K || Kp % 128 || S_pad < S || S_pad % 64 || N <= 0 ||
       Gw <= 0 || ngw <= 0)
@@ -1982,10 +1977,11 @@ extern "C" int sqmp_quant_act_c4(void* x, int dtype, int M, int K, int amode, in
                                  void* ascale, void* xs, const void* codes, const void* wscale,
                                  const void* wsal, int N, int Gw, int ngw, void* wp,
                                  void* workspace, size_t ws_bytes, void* stream) {
+  SQMP_DEVICE_GUARD(stream);
   if (!codes || !wscale || !wp || (S > 0 && !wsal) || N <= 0 || Gw <= 0 || ngw <= 0)
     return SQMP_EINVAL;
   if (Gw % 8 || Kp > 32768) return SQMP_EUNSUPPORTED;
-  const C4Weight cw{codes, wscale, wsal, wp, N, Kp, Gw, ngw, (flags & SQMP_QA_WPT) ? 1 : 0};
+  const C4Weight cw{codes, wscale, wsal, wp, N, Kp, Gw, ngw};
   return quant_act_impl(x, dtype, M, K, amode, n_bits, group_size, amap, Kp, nonsal, salient, S,
                         S_pad, posmap, flags, SQMP_OUT_C4, acodes, ascale, xs, workspace,
                         ws_bytes, stream, &cw);
@@ -2003,6 +1999,7 @@ extern "C" int sqmp_quant_act_group(void* x, int dtype, int M, int K, int amode,
                                     const int32_t* salient, int S, int S_pad, int flags,
                                     void* const* outs, void* workspace, size_t ws_bytes,
                                     void* stream) {
+  SQMP_DEVICE_GUARD(stream);
   if (nout < 1 || nout > 3 || !amaps || !posmaps || !outs) return SQMP_EINVAL;
   for (int o = 0; o < nout; ++o)
     if (!amaps[o] || !posmaps[o] || !outs[o]) return SQMP_EINVAL;

@@ -682,20 +682,14 @@ struct PermArgs {
   const uint32_t* codes;  // bpack [Np][Kp/2]
   const void* wscale;     // D [ngw][Np]
   const void* wsal;       // D [N][S_pad]
-  void* wp;               // D [Np][Kq + S_pad], or (wpt) sqmp_gemm_fqa's tile-major layout
+  void* wp;               // D [Np][Kq + S_pad]
   int N, Np, Kp, Gw, ngw, Kn, Kq, S_pad, RB;
-  int wpt;                // 1: wp[n][j0 .. j0 + 7] at fqa_wpt_off(n, j0) (rows roundup(N, 512))
 };
 
-// the 16-B chunk of wp row n at position j0 (j0 % 8 == 0): row-major, or sqmp_gemm_fqa's
-// [n / 64][j0 / 64][(n / 16) % 4][(j0 / 32) % 2][lane = 16 ((j0 / 8) % 4) + n % 16][8]
+// the 16-B chunk of wp row n at position j0 (j0 % 8 == 0)
 template <class T>
 __device__ __forceinline__ T* wp_chunk(const PermArgs& a, T* wp, int n, int j0) {
-  const int W = a.Kq + a.S_pad;
-  if (!a.wpt) return wp + (size_t)n * W + j0;
-  const size_t f = (((size_t)(n >> 6) * (W >> 6) + (j0 >> 6)) * 8 + ((n >> 4) & 3) * 2 + ((j0 >> 5) & 1)) * 64 +
-                   ((j0 >> 3) & 3) * 16 + (n & 15);
-  return wp + f * 8;
+  return wp + (size_t)n * (a.Kq + a.S_pad) + j0;
 }
 
 // Even RB: rows in PAIRS interleaved in LDS (word k of pair r2 = (W_hat[n0 + 2 r2][k],
@@ -1027,7 +1021,7 @@ int launch_perm_weight_c4(int dtype, const uint32_t* lctab, const void* codes,
                           int Kn, int S_pad, void* wp, hipStream_t s) {
   const int Np = pad_n(N), RB = pw_rows(Kp);
   const int Kq = (int)round_up(Kn, 64);
-  PermArgs pa{(const uint32_t*)codes, wscale, wsal, wp, N, Np, Kp, Gw, ngw, Kn, Kq, S_pad, RB, 0};
+  PermArgs pa{(const uint32_t*)codes, wscale, wsal, wp, N, Np, Kp, Gw, ngw, Kn, Kq, S_pad, RB};
   const size_t lds = (size_t)RB * Kp * 2;
   const dim3 grid((unsigned)(Np / RB));
   if (dtype == SQMP_F16) {
@@ -1069,10 +1063,8 @@ int launch_quant_lc_c4(int dtype, const void* x, int M, int K, int q_max, int G,
   const int nw = lc_waves(K, Kn);
   const int Np = pad_n(cw->N), RB = pw_rows(cw->Kp);
   PermArgs pa{(const uint32_t*)cw->codes, cw->wscale, cw->wsal, cw->wp, cw->N, Np, cw->Kp,
-              cw->Gw, cw->ngw, Kn, Kq, S_pad, RB, cw->wpt};
-  // the permutation's rows: pad_n(N), or roundup(N, 512) for sqmp_gemm_fqa's layout (rows
-  // past N hold zeros)
-  const int Nrows = cw->wpt ? (int)round_up(cw->N, 512) : Np;
+              cw->Gw, cw->ngw, Kn, Kq, S_pad, RB};
+  const int Nrows = Np;  // the permutation's rows
   const size_t lq = sizeof(uint32_t) * lc_lds_words(P, S_pad, 1), lp = (size_t)RB * cw->Kp * 2;
   const size_t lds = lq > lp ? lq : lp;
   const void* kf = dtype == SQMP_BF16 ? (const void*)quant_c4_fused_kernel<BF16>

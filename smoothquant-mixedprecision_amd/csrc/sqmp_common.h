@@ -13,6 +13,40 @@
 
 namespace sqmp {
 
+// Every C entry that launches work runs it on its STREAM's device: the reference's callers
+// place layers on several GPUs (accelerate device_map="auto", run_experiments.py:146-148,
+// examples/ppl_eval.sh:17-18), so the caller's current device need not be the tensors'.  The
+// guard makes the stream's device current for the call and restores the caller's on return
+// (one hipGetDevice when they already agree; the null stream means the current device).
+class DeviceGuard {
+ public:
+  explicit DeviceGuard(void* stream) {
+    if (!stream) return;
+    int dev = -1, cur = -1;
+    if (hipStreamGetDevice((hipStream_t)stream, &dev) != hipSuccess) return;
+    if (hipGetDevice(&cur) == hipSuccess && cur != dev && hipSetDevice(dev) == hipSuccess)
+      prev_ = cur;
+  }
+  ~DeviceGuard() {
+    if (prev_ >= 0) (void)hipSetDevice(prev_);
+  }
+  DeviceGuard(const DeviceGuard&) = delete;
+  DeviceGuard& operator=(const DeviceGuard&) = delete;
+
+ private:
+  int prev_ = -1;
+};
+#define SQMP_DEVICE_GUARD(stream) ::sqmp::DeviceGuard sqmp_device_guard_((void*)(stream))
+
+// A launch attribute (hipFuncSetAttribute) belongs to the CURRENT device: a call site that
+// sets one once keeps a bit per device in `seen` (true the first time on this device).
+inline bool first_on_device(uint64_t& seen) {
+  int d = 0;
+  (void)hipGetDevice(&d);
+  const uint64_t bit = 1ull << (d & 63);
+  return (__atomic_fetch_or(&seen, bit, __ATOMIC_RELAXED) & bit) == 0;
+}
+
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));

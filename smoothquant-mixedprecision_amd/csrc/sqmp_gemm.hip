@@ -213,10 +213,8 @@ static int generic_launch(const void* a, const void* codes, const void* wscale,
                           int S_pad, int Gw, int ngw, uint32_t* colmax, hipStream_t s) {
   typedef typename DT::T T;
   const int tiles_m = cdiv(M, BM), tiles_n = cdiv(N, BN);
-  static const bool f32_4w = [] {  // A/B knob: the 4-wave build for fp32 too
-    const char* e = knob("SQMP_F32_WN2");
-    return e && atoi(e) == 1;
-  }();
+  const char* wn2 = knob("SQMP_F32_WN2");  // A/B knob: the 4-wave build for fp32 too
+  const bool f32_4w = wn2 && atoi(wn2) == 1;
   if constexpr (std::is_same<DT, F32>::value) if (!f32_4w) {
     gemm_generic_kernel<DT, WBITS, 4><<<dim3(tiles_m * tiles_n), dim3(512), 0, s>>>(
         (const T*)a, (const uint8_t*)codes, (const T*)wscale, (const T*)wsal, (const T*)bias,
@@ -252,6 +250,7 @@ extern "C" int sqmp_gemm_fq(const void* a, const void* codes, const void* wscale
                             const void* wsal, const void* bias, void* y, int dtype, int M,
                             int N, int Kp, int S_pad, int Gw, int ngw, int n_bits,
                             void* stream) {
+  SQMP_DEVICE_GUARD(stream);
   return sqmp_gemm_fq_colmax(a, codes, wscale, wsal, bias, y, dtype, M, N, Kp, S_pad, Gw, ngw,
                              n_bits, nullptr, stream);
 }
@@ -260,6 +259,7 @@ extern "C" int sqmp_gemm_fq_colmax(const void* a, const void* codes, const void*
                                    const void* wsal, const void* bias, void* y, int dtype,
                                    int M, int N, int Kp, int S_pad, int Gw, int ngw,
                                    int n_bits, uint32_t* colmax, void* stream) {
+  SQMP_DEVICE_GUARD(stream);
   int st = check_gemm_geometry(dtype, M, N, Kp, S_pad, Gw, ngw, n_bits);
   if (st) return st;
   if (!a || !codes || (n_bits && !wscale) || !y || (S_pad > 0 && !wsal)) return SQMP_EINVAL;
@@ -283,6 +283,7 @@ extern "C" int sqmp_gemm_i8(const int8_t* a8, const float* ascale, const void* x
                             const void* codes, const void* wscale, const void* wsal,
                             const void* bias, void* y, int dtype, int M, int N, int Kp,
                             int S_pad, int Gw, int ngw, int n_bits, void* stream) {
+  SQMP_DEVICE_GUARD(stream);
   int st = check_gemm_geometry(dtype, M, N, Kp, S_pad, Gw, ngw, n_bits);
   if (st) return st;
   if (dtype == SQMP_F32 || n_bits != 4 || Gw % 64 != 0) return SQMP_EUNSUPPORTED;
@@ -296,6 +297,7 @@ extern "C" int sqmp_gemm_i8(const int8_t* a8, const float* ascale, const void* x
 extern "C" int sqmp_gemm_fqt(const void* acodes, const void* ascale, const void* xs,
                              const void* wp, const void* bias, void* y, int dtype, int M, int N,
                              int Kq, int S_pad, int G, int ngq, void* stream) {
+  SQMP_DEVICE_GUARD(stream);
   using namespace sqmp;
   if (!acodes || !ascale || !wp || !y || (S_pad > 0 && !xs)) return SQMP_EINVAL;
   if (M < 0 || N <= 0 || Kq <= 0 || Kq % 64 || S_pad < 0 || S_pad % 64 || G <= 0 || ngq <= 0)

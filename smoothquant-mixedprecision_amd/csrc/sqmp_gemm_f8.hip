@@ -618,6 +618,7 @@ using namespace sqmp;
 
 extern "C" int sqmp_pack_f8(const void* codes, const void* wscale, int dtype, int N, int Kp,
                             int ngw, void* w8, float* ws32, void* stream) {
+  SQMP_DEVICE_GUARD(stream);
   if (!codes || !wscale || !ws32 || N <= 0 || Kp <= 0 || Kp % 128 != 0 || ngw <= 0)
     return SQMP_EINVAL;  // w8 = NULL: the scales only
   if (dtype != SQMP_F16 && dtype != SQMP_BF16) return SQMP_EUNSUPPORTED;
@@ -652,10 +653,8 @@ static int gemm_f8_impl(const void* a8, const float* ascale, const void* xs, con
   const int tiles_m = cdiv(M, 256), tiles_n = cdiv(N, 256);
   const dim3 grid(tiles_m * tiles_n), block(512);
   // Gw % 128 == 0 runs the 16x16x128 kernel (SQMP_F8_V1=1 keeps the 32x32x64 one, A/B)
-  static const bool v1_only = [] {
-    const char* e = knob("SQMP_F8_V1");
-    return e && atoi(e) != 0;
-  }();
+  const char* v1e = knob("SQMP_F8_V1");
+  const bool v1_only = v1e && atoi(v1e) != 0;
   const bool v2 = Gw % 128 == 0 && !v1_only;
   if (colmax && !v2) return SQMP_EUNSUPPORTED;  // fused statistics: the 16x16x128 kernel only
   // M-tiles per raster group (SQMP_GROUP_M: A/B knob, read per launch)
@@ -714,6 +713,7 @@ extern "C" int sqmp_gemm_f8(const void* a8, const float* ascale, const void* xs,
                             const float* ws32, const void* wsal, const void* bias, void* y,
                             int dtype, int M, int N, int Kp, int S_pad, int Gw, int ngw,
                             void* stream) {
+  SQMP_DEVICE_GUARD(stream);
   return gemm_f8_impl(a8, ascale, xs, w8, ws32, wsal, bias, y, dtype, M, N, Kp, S_pad, Gw, ngw,
                       nullptr, stream);
 }
@@ -723,6 +723,7 @@ extern "C" int sqmp_gemm_f8_colmax(const void* a8, const float* ascale, const vo
                                    const void* w8, const float* ws32, const void* wsal,
                                    const void* bias, void* y, int dtype, int M, int N, int Kp,
                                    int S_pad, int Gw, int ngw, uint32_t* colmax, void* stream) {
+  SQMP_DEVICE_GUARD(stream);
   if (!colmax) return SQMP_EINVAL;
   return gemm_f8_impl(a8, ascale, xs, w8, ws32, wsal, bias, y, dtype, M, N, Kp, S_pad, Gw, ngw,
                       colmax, stream);

@@ -722,11 +722,8 @@ __global__ __launch_bounds__(256, 1) void gemm_i8v2_kernel(
 // M-tiles per raster group (tile_coords): SQMP_GROUP_M overrides (A/B tuning knob; 4 and
 // 8 measured equal at config 2, 1 and 2 0.5-1 % slower)
 static int fq6_group_m() {
-  static int v = [] {
-    const char* e = knob("SQMP_GROUP_M");
-    return e && atoi(e) > 0 ? atoi(e) : 4;
-  }();
-  return v;
+  const char* e = knob("SQMP_GROUP_M");
+  return e && atoi(e) > 0 ? atoi(e) : 4;
 }
 
 template <class DT, int GB, int TM, bool TR = false>

@@ -692,6 +692,20 @@ static int opt_pk_env(int tm, long tiles, int kp) {  // (A/B knob; sqmp_knobs.hi
   return tm == 128 && tiles > 256 ? 8 : 3;
 }
 
+// The OPT variant a packed-order launch of TM-row tiles actually instantiates (launch_k's
+// switch: 8 / 9 need 128-row tiles, 24 also Kp >= 256; F16, J = 2, GB = 1 only -- else 0)
+static int eff_opt_pk(bool f16_j2_gb1, int tm, long tiles, int kp) {
+  if (!f16_j2_gb1) return 0;
+  const int o = opt_pk_env(tm, tiles, kp);
+  switch (o) {
+    case 1: case 2: case 3: return o;
+    case 8: return tm == 128 ? 8 : 0;
+    case 9: return tm == 128 ? 9 : 3;
+    case 24: return tm == 128 ? (kp >= 256 ? 24 : 8) : 3;
+    default: return 0;
+  }
+}
+
 // the activation-order launch's OPT variant (A/B knob, see gemm_fq7_kernel)
 // default 3 (setprio + loader split): same box, interleaved rounds at config 2, 421.6 us
 // against 431.4 us for 0 (either bit alone +-0.3 %, PF = 3 +-0.1 %; tools/ab_fqt7.py,
@@ -724,7 +738,7 @@ static int launch_k(const void* a, const void* bt, const void* st, const void* s
   // OPT variants (setprio for waves 4-7, loader split) for the fp16 J = 2 kernels, the
   // 2048-token Llama GEMMs (A/B knob SQMP_FQ7_OPT, read per launch)
   if constexpr (std::is_same<DT, F16>::value && J == 2 && GB == 1 && DIAG == 0) {
-    switch (opt_pk_env(TM, (long)tiles_m * tiles_n, Kp)) {
+    switch (eff_opt_pk(true, TM, (long)tiles_m * tiles_n, Kp)) {
       case 1: SQMP_PK(1); break;
       case 2: SQMP_PK(2); break;
       case 3: SQMP_PK(3); break;
@@ -763,13 +777,19 @@ static int launch(const void* a, const void* bt, const void* st, const void* sal
 #undef SQMP_L
 }
 
+// The row-tile height of a standalone packed-order launch (dispatch): J = 4: 128 x 512 tiles
+// (64-row tiles when those leave CUs idle); J = 2: 256 x 256 (128 x 256 when those leave CUs
+// idle; always 128 in bf16)
+static int tm_standalone(bool bf16, int M, int N, int J) {
+  if (J == 4) return (long)cdiv(M, 128) * cdiv(N, 512) >= 256 ? 128 : 64;
+  return (!bf16 && (long)cdiv(M, 256) * cdiv(N, 256) >= 512) ? 256 : 128;
+}
+
 template <class DT>
 static int dispatch(const void* a, const void* bt, const void* st, const void* salt,
                     const void* bias, void* y, int M, int N, int Kp, int S_pad, int Gw,
                     int ngw, int J, uint32_t* colmax, hipStream_t s) {
-  // J = 4: 128 x 512 tiles (64-row tiles when those leave CUs idle); J = 2: 256 x 256
-  // (128 x 256 when those leave CUs idle)
-  const int tm = J == 4 ? ((long)cdiv(M, 128) * cdiv(N, 512) >= 256 ? 128 : 64)
+  const int tm = J == 4 ? tm_standalone(false, M, N, J)
                         : ((long)cdiv(M, 256) * cdiv(N, 256) >= 512 ? 256 : 128);
   // (bf16 at 256 x 256 puts an array in scratch: 128-row tiles there)
   constexpr int TM2 = std::is_same<DT, BF16>::value ? 128 : 256;
@@ -788,15 +808,26 @@ static int dispatch(const void* a, const void* bt, const void* st, const void* s
 // group.  Row tiles of 256 where the problems' 256 x 256 tiles fill two rounds of the CUs, else
 // of 128 (two workgroups per CU where that gives more than one tile per CU), as dispatch();
 // SQMP_FQ7G_TM = 128 / 256 overrides (A/B, read per launch).
+static int tm_group(bool bf16, int M, const int* Ns, int n) {
+  long t256 = 0;
+  for (int p = 0; p < n; ++p) t256 += (long)cdiv(M, 256) * cdiv(Ns[p], 256);
+  int tm = t256 >= 512 && ks_env() < 3 ? 256 : 128;
+  if (const char* e = knob("SQMP_FQ7G_TM")) tm = atoi(e) == 256 ? 256 : 128;
+  return bf16 ? 128 : tm;  // (bf16 at 256 x 256 puts an array in scratch)
+}
+// the OPT variant dispatch_group launches
+static int group_opt(bool f16, int tm, long tiles, int kp) {
+  if (tm == 256) return f16 ? 3 : -1;
+  const int o = opt_pk_env(128, tiles, kp);
+  if (o == 24 && f16) return 24;
+  return o == 8 ? 8 : 3;
+}
+
 template <class DT>
 static int dispatch_group(Fq7Grp& g, int M, int Kp, int S_pad, int Gw, int ngw, int nt,
                           hipStream_t s) {
   typedef typename DT::T T;
-  long t256 = 0;
-  for (int p = 0; p < g.n; ++p) t256 += (long)cdiv(M, 256) * cdiv(g.N[p], 256);
-  int tm = t256 >= 512 && ks_env() < 3 ? 256 : 128;
-  if (const char* e = knob("SQMP_FQ7G_TM")) tm = atoi(e) == 256 ? 256 : 128;
-  if (std::is_same<DT, BF16>::value) tm = 128;  // (bf16 at 256 x 256 puts an array in scratch)
+  const int tm = tm_group(std::is_same<DT, BF16>::value, M, g.N, g.n);
   const int tiles_m = cdiv(M, tm);
   int end = 0;
   for (int p = 0; p < g.n; ++p) {
@@ -808,14 +839,19 @@ static int dispatch_group(Fq7Grp& g, int M, int Kp, int S_pad, int Gw, int ngw, 
   gemm_fq7_kernel<DT, 1, TMV, 2, 0, false, O, true><<<dim3(end), dim3((O) & 16 ? 1024 : 512), 0, s>>>( \
       (const T*)nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, M, 0, Kp, S_pad, Gw, ngw, \
       tiles_m, 0, group_m_env(), nullptr, nt, g)
-  if (tm == 256) {
-    if constexpr (std::is_same<DT, F16>::value) SQMP_G(256, 3);
-  } else if (opt_pk_env(128, end, Kp) == 24 && std::is_same<DT, F16>::value) {
-    if constexpr (std::is_same<DT, F16>::value) SQMP_G(128, 24);
-  } else if (opt_pk_env(128, end, Kp) == 8) {
-    SQMP_G(128, 8);
-  } else {
-    SQMP_G(128, 3);
+  switch (group_opt(std::is_same<DT, F16>::value, tm, end, Kp)) {
+    case 3:
+      if (tm == 256) {
+        if constexpr (std::is_same<DT, F16>::value) SQMP_G(256, 3);
+      } else {
+        SQMP_G(128, 3);
+      }
+      break;
+    case 24:
+      if constexpr (std::is_same<DT, F16>::value) SQMP_G(128, 24);
+      break;
+    case 8: SQMP_G(128, 8); break;
+    default: break;
   }
 #undef SQMP_G
   SQMP_LAUNCH_CHECK();
@@ -908,6 +944,7 @@ extern "C" int sqmp_fq7_sizes(int N, int Kp, int S_pad, int ngw, int J, size_t* 
 extern "C" int sqmp_pack_fq7(const void* codes, const void* wscale, const void* wsal, int dtype,
                              int N, int Kp, int S_pad, int ngw, int J, void* codes_t,
                              void* scale_t, void* sal_t, void* stream) {
+  SQMP_DEVICE_GUARD(stream);
   if (!codes || !wscale || !codes_t || !scale_t || !sal_t || (S_pad > 0 && !wsal))
     return SQMP_EINVAL;
   if (dtype != SQMP_F16 && dtype != SQMP_BF16) return SQMP_EUNSUPPORTED;
@@ -944,6 +981,7 @@ extern "C" int sqmp_gemm_fq7(const void* a, const void* codes_t, const void* sca
                              const void* sal_t, const void* bias, void* y, int dtype, int M,
                              int N, int Kp, int S_pad, int Gw, int ngw, int J, uint32_t* colmax,
                              void* stream) {
+  SQMP_DEVICE_GUARD(stream);
   if (!a || !codes_t || !scale_t || !sal_t || !y) return SQMP_EINVAL;
   if (M < 0 || N <= 0 || Kp <= 0 || Kp % 128 || S_pad < 0 || S_pad % 64 || Gw <= 0 || ngw <= 0)
     return SQMP_EINVAL;
@@ -959,6 +997,7 @@ extern "C" int sqmp_gemm_fq7(const void* a, const void* codes_t, const void* sca
 
 extern "C" int sqmp_gemm_fq7_group(const sqmp_fq7_problem* probs, int nprob, int dtype, int M,
                                    int Kp, int S_pad, int Gw, int ngw, int J, void* stream) {
+  SQMP_DEVICE_GUARD(stream);
   if (!probs || nprob < 1 || nprob > fq7::FQ7_GRP_MAX) return SQMP_EINVAL;
   if (M < 0 || Kp <= 0 || Kp % 128 || S_pad < 0 || S_pad % 64 || Gw <= 0 || ngw <= 0)
     return SQMP_EINVAL;
@@ -989,6 +1028,31 @@ extern "C" int sqmp_gemm_fq7_group(const sqmp_fq7_problem* probs, int nprob, int
   return fq7::dispatch_group<BF16>(g, M, Kp, S_pad, Gw, ngw, nt, s);
 }
 
+// Which kernel variant sqmp_gemm_fq7 (nprob = 0: N[0] alone) or sqmp_gemm_fq7_group (nprob
+// problems of N[0 .. nprob)) launches for these shapes: row-tile height and the OPT bits of
+// gemm_fq7_kernel (bit 4 = the K split inside the workgroup, whose fp32 partial sums add in
+// another order).  Test and tool use: which launches must agree bit for bit.
+extern "C" int sqmp_fq7_plan(int dtype, int M, const int* N, int nprob, int Kp, int Gw, int J,
+                             int* tm, int* opt) {
+  if (!N || !tm || !opt || M <= 0 || Kp <= 0 || nprob < 0 || nprob > fq7::FQ7_GRP_MAX)
+    return SQMP_EINVAL;
+  if (dtype != SQMP_F16 && dtype != SQMP_BF16) return SQMP_EUNSUPPORTED;
+  const bool bf16 = dtype == SQMP_BF16;
+  if (nprob == 0) {
+    const int t = fq7::tm_standalone(bf16, M, N[0], J);
+    *tm = t;
+    *opt = fq7::eff_opt_pk(!bf16 && J == 2 && Gw % 64 == 0, t, (long)cdiv(M, t) * cdiv(N[0], 128 * J), Kp);
+    return SQMP_OK;
+  }
+  if (J != 2 || Gw % 64) return SQMP_EUNSUPPORTED;
+  const int t = fq7::tm_group(bf16, M, N, nprob);
+  long tiles = 0;
+  for (int p = 0; p < nprob; ++p) tiles += (long)cdiv(M, t) * cdiv(N[p], 256);
+  *tm = t;
+  *opt = fq7::group_opt(!bf16, t, tiles, Kp);
+  return SQMP_OK;
+}
+
 // sqmp_gemm_fqt7: the activation-order GEMM (sqmp_gemm_fqt) on fq7's register-operand
 // structure, its activation operands in the tile-major layout (J = 2) that sqmp_quant_act_c4
 // writes when called with the SQMP_QA_TILED flag
@@ -1014,6 +1078,7 @@ static int gemm_fqt7_impl(const void* codes_t, const void* scale_t, const void* 
 extern "C" int sqmp_gemm_fqt7(const void* codes_t, const void* scale_t, const void* sal_t,
                               const void* wp, const void* bias, void* y, int dtype, int M, int N,
                               int Kq, int S_pad, int G, int ngq, void* stream) {
+  SQMP_DEVICE_GUARD(stream);
   return gemm_fqt7_impl(codes_t, scale_t, sal_t, wp, bias, y, dtype, M, N, Kq, S_pad, G, ngq,
                         2, nullptr, stream);
 }
@@ -1024,6 +1089,7 @@ extern "C" int sqmp_gemm_fqt7_colmax(const void* codes_t, const void* scale_t, c
                                      const void* wp, const void* bias, void* y, int dtype, int M,
                                      int N, int Kq, int S_pad, int G, int ngq, uint32_t* colmax,
                                      void* stream) {
+  SQMP_DEVICE_GUARD(stream);
   if (!colmax) return SQMP_EINVAL;
   return gemm_fqt7_impl(codes_t, scale_t, sal_t, wp, bias, y, dtype, M, N, Kq, S_pad, G, ngq,
                         2, colmax, stream);
@@ -1034,6 +1100,7 @@ extern "C" int sqmp_gemm_fqt7j(const void* codes_t, const void* scale_t, const v
                                const void* wp, const void* bias, void* y, int dtype, int M, int N,
                                int Kq, int S_pad, int G, int ngq, int J, uint32_t* colmax,
                                void* stream) {
+  SQMP_DEVICE_GUARD(stream);
   return gemm_fqt7_impl(codes_t, scale_t, sal_t, wp, bias, y, dtype, M, N, Kq, S_pad, G, ngq, J,
                         colmax, stream);
 }

@@ -329,6 +329,7 @@ __global__ __launch_bounds__(256) void pack_h2d_kernel(const uint16_t* __restric
 using namespace sqmp;
 
 extern "C" int sqmp_pack_h2d(const void* planes, int Np, int L, void* wt, void* stream) {
+  SQMP_DEVICE_GUARD(stream);
   if (!planes || !wt || Np <= 0 || Np % 256 != 0 || L <= 0 || L % 64 != 0) return SQMP_EINVAL;
   const long chunks = 2L * Np * L / 8;
   h2d::pack_h2d_kernel<<<cdiv(chunks, 256), 256, 0, (hipStream_t)stream>>>(
@@ -340,6 +341,7 @@ extern "C" int sqmp_pack_h2d(const void* planes, int Np, int L, void* wt, void* 
 extern "C" int sqmp_gemm_h2d(const void* a2, int ldr, const int* aexp, const void* wt,
                              const int* bexp, const float* bias, float* y, int M, int N, int L,
                              uint32_t* colmax, void* stream) {
+  SQMP_DEVICE_GUARD(stream);
   if (!a2 || !aexp || !wt || !bexp || !y || M < 0 || N <= 0 || L <= 0) return SQMP_EINVAL;
   if (L % 64 != 0 || N % 4 != 0 || ldr < 128 * cdiv(M, 128)) return SQMP_EINVAL;
   if (M == 0) return SQMP_OK;

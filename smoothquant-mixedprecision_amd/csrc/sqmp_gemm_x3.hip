@@ -328,6 +328,7 @@ using namespace sqmp;
 
 extern "C" int sqmp_split2_f16(const float* src, int R, int L, int ldr, void* dst, int* rexp,
                                void* stream) {
+  SQMP_DEVICE_GUARD(stream);
   if (!src || !dst || !rexp || R <= 0 || L <= 0 || ldr < R) return SQMP_EINVAL;
   split2h_kernel<<<cdiv(ldr, 4), 256, 0, (hipStream_t)stream>>>(src, R, L, ldr, (uint16_t*)dst, rexp);
   SQMP_LAUNCH_CHECK();
@@ -335,6 +336,7 @@ extern "C" int sqmp_split2_f16(const float* src, int R, int L, int ldr, void* ds
 }
 
 extern "C" int sqmp_row_exp(const float* src, int R, int L, int* rexp, void* stream) {
+  SQMP_DEVICE_GUARD(stream);
   if (!src || !rexp || R < 0 || L <= 0) return SQMP_EINVAL;
   if (R == 0) return SQMP_OK;
   row_exp_kernel<<<cdiv(R, 4), 256, 0, (hipStream_t)stream>>>(src, R, L, rexp);
@@ -345,6 +347,7 @@ extern "C" int sqmp_row_exp(const float* src, int R, int L, int* rexp, void* str
 extern "C" int sqmp_gemm_h2(const float* a, const int* aexp, const void* b2, const int* bexp,
                             const float* bias, float* y, int M, int N, int L, uint32_t* colmax,
                             void* stream) {
+  SQMP_DEVICE_GUARD(stream);
   if (!a || !aexp || !b2 || !bexp || !y || M < 0 || N <= 0 || L <= 0) return SQMP_EINVAL;
   if (L % X3_BK != 0) return SQMP_EINVAL;
   if (M == 0) return SQMP_OK;
@@ -354,15 +357,11 @@ extern "C" int sqmp_gemm_h2(const float* a, const int* aexp, const void* b2, con
   // 128 x 256 tiles (8 waves of 64 x 64: half the A re-fetch and A split work per MFMA of
   // 128 x 128 tiles) wherever they still give every CU a workgroup
   const int tiles_n2 = cdiv(N, 256);
-  static const bool wide_ok = [] {  // SQMP_H2_WIDE=0: 128 x 128 tiles only (A/B knob)
-    const char* e = knob("SQMP_H2_WIDE");
-    return !e || atoi(e) != 0;
-  }();
+  const char* we = knob("SQMP_H2_WIDE");  // SQMP_H2_WIDE=0: 128 x 128 tiles only (A/B knob)
+  const bool wide_ok = !we || atoi(we) != 0;
   const bool wide = wide_ok && (long)tiles_m * tiles_n2 >= 256;
-  static const bool bk64 = [] {  // SQMP_H2_BK64=0: K stages of 32 (A/B knob)
-    const char* e = knob("SQMP_H2_BK64");
-    return !e || atoi(e) != 0;
-  }();
+  const char* be = knob("SQMP_H2_BK64");  // SQMP_H2_BK64=0: K stages of 32 (A/B knob)
+  const bool bk64 = !be || atoi(be) != 0;
   const bool k64 = bk64 && L % 64 == 0;
   const int nt = nt_output((size_t)M * N * sizeof(float)) ? 1 : 0;
   // row tiles per raster group: 4 (same box, config-2 fp32 step: 1 / 2 / 4 / 8 / 16 / 32 ->

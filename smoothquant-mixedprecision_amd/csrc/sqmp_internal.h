@@ -125,9 +125,8 @@ struct C4Weight {
   const void* codes;   // bpack [pad_n(N)][Kp/2]
   const void* wscale;  // D [ngw][pad_n(N)]
   const void* wsal;    // D [N][S_pad]
-  void* wp;            // D [pad_n(N)][Kq + S_pad], or sqmp_gemm_fqa's layout (wpt)
+  void* wp;            // D [pad_n(N)][Kq + S_pad]
   int N, Kp, Gw, ngw;
-  int wpt;             // SQMP_QA_WPT
 };
 int launch_quant_lc_c4(int dtype, const void* x, int M, int K, int q_max, int G,
                        const uint32_t* lctab, int Kn, int P, const int32_t* sal, int S,

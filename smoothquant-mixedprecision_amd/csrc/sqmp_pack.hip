@@ -246,6 +246,7 @@ extern "C" int sqmp_pack_weight(const void* w, int dtype, int N, int K, int wmod
                                 void* codes, void* wscale, void* wsal, int32_t* perm,
                                 int32_t* amap, int32_t* amap_fq, int32_t* nonsal,
                                 void* workspace, size_t ws_bytes, void* stream) {
+  SQMP_DEVICE_GUARD(stream);
   hipStream_t s = (hipStream_t)stream;
   if (dtype < SQMP_F32 || dtype > SQMP_BF16 || N <= 0) return SQMP_EINVAL;
   if (wmode == SQMP_W_NONE) n_bits = 0;
@@ -292,6 +293,7 @@ extern "C" int sqmp_dequant_weight(const void* codes, const void* wscale, const 
                                    const int32_t* amap, const int32_t* salient, int dtype,
                                    int N, int K, int S, int n_bits, int Kp, int Gw, int ngw,
                                    int S_pad, void* w_hat, void* stream) {
+  SQMP_DEVICE_GUARD(stream);
   hipStream_t s = (hipStream_t)stream;
   if (dtype < SQMP_F32 || dtype > SQMP_BF16 || N <= 0 || K <= 0 || Kp < K || Gw <= 0)
     return SQMP_EINVAL;
@@ -311,6 +313,7 @@ extern "C" int sqmp_dequant_weight(const void* codes, const void* wscale, const 
 extern "C" int sqmp_dequant_weight_packed(const void* codes, const void* wscale, int dtype,
                                           int N, int Kp, int Gw, int ngw, int n_bits,
                                           void* out, void* stream) {
+  SQMP_DEVICE_GUARD(stream);
   hipStream_t s = (hipStream_t)stream;
   if (dtype < SQMP_F32 || dtype > SQMP_BF16 || N <= 0 || Kp <= 0 || Gw <= 0 || ngw <= 0)
     return SQMP_EINVAL;
@@ -328,6 +331,7 @@ extern "C" int sqmp_dequant_weight_packed(const void* codes, const void* wscale,
 extern "C" int sqmp_build_maps(int K, const int32_t* salient, int S, int32_t* perm,
                                int32_t* amap, int32_t* amap_fq, int32_t* nonsal, int Kp,
                                void* stream) {
+  SQMP_DEVICE_GUARD(stream);
   if (K <= 0 || K > 65000 || S < 0 || S > K || Kp < K) return SQMP_EINVAL;
   if (!perm || !amap || !amap_fq || (K - S > 0 && !nonsal) || (S > 0 && !salient))
     return SQMP_EINVAL;

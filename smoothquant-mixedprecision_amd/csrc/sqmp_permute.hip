@@ -120,6 +120,7 @@ using namespace sqmp;
 
 extern "C" int sqmp_permute_act(const void* src, void* dst, const int32_t* map, int dtype, int M,
                                 int P, int S_pad, void* stream) {
+  SQMP_DEVICE_GUARD(stream);
   if (!src || !dst || !map || M < 0 || P <= 0 || P % 8 || S_pad < 0 || S_pad % 8)
     return SQMP_EINVAL;
   if (dtype != SQMP_F16 && dtype != SQMP_BF16) return SQMP_EUNSUPPORTED;
@@ -136,21 +137,17 @@ extern "C" int sqmp_permute_act(const void* src, void* dst, const int32_t* map, 
   // the dynamic-LDS limit raised once to the largest row this entry accepts (256 PR_CH chunks
   // of 8 positions), not per launch
   constexpr int kMaxLds = (int)sizeof(uint32_t) * 8 * 256 * PR_CH;
-  static bool attr_h = false, attr_b = false;
+  static uint64_t attr_h = 0, attr_b = 0;  // (per device)
   if (dtype == SQMP_F16) {
-    if (!attr_h) {
+    if (first_on_device(attr_h))
       SQMP_HIP_CHECK(hipFuncSetAttribute((const void*)permute_rows_kernel<_Float16>,
                                          hipFuncAttributeMaxDynamicSharedMemorySize, kMaxLds));
-      attr_h = true;
-    }
     permute_rows_kernel<_Float16><<<grid, dim3(256), lds, s>>>(
         (const _Float16*)src, (_Float16*)dst, map, M, P, S_pad, ppw);
   } else {
-    if (!attr_b) {
+    if (first_on_device(attr_b))
       SQMP_HIP_CHECK(hipFuncSetAttribute((const void*)permute_rows_kernel<__bf16>,
                                          hipFuncAttributeMaxDynamicSharedMemorySize, kMaxLds));
-      attr_b = true;
-    }
     permute_rows_kernel<__bf16><<<grid, dim3(256), lds, s>>>(
         (const __bf16*)src, (__bf16*)dst, map, M, P, S_pad, ppw);
   }

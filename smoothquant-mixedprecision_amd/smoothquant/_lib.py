@@ -27,7 +27,6 @@ W_PER_CHANNEL, W_PER_TENSOR, W_PER_GROUP, W_PER_GROUP_UNSORTED, W_NONE = 0, 1, 2
 W_PER_GROUP_MEAN3STD = 5
 OUT_FP, OUT_I8, OUT_INPLACE, OUT_F8, OUT_C4, OUT_H2 = 0, 1, 2, 3, 5, 6
 QA_CLEAN_WS, QA_REUSE_STATS, QA_STATS_GIVEN, QA_TILED, QA_TILED4 = 1, 2, 4, 8, 16
-QA_WPT = 64
 
 _vp, _i, _sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t
 _ip = ctypes.POINTER(ctypes.c_int)
@@ -88,11 +87,8 @@ SIGNATURES = {
                                   _i, _i, _vp, _vp, _sz, _vp]),
     "sqmp_gemm_fq7_group": (_i, [ctypes.POINTER(Fq7Problem), _i, _i, _i, _i, _i, _i, _i, _i,
                                  _vp]),
-    "sqmp_gemm_fqa": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _vp,
-                           _vp]),
-    "sqmp_fqa_wpt_elems": (_sz, [_i, _i, _i]),
+    "sqmp_fq7_plan": (_i, [_i, _i, _ip, _i, _i, _i, _i, _ip, _ip]),
     "sqmp_reload_knobs": (_i, []),
-    "sqmp_pack_wpt": (_i, [_vp, _i, _i, _i, _vp, _vp]),
     "sqmp_split2_f16": (_i, [_vp, _i, _i, _i, _vp, _vp, _vp]),
     "sqmp_row_exp": (_i, [_vp, _i, _i, _vp, _vp]),
     "sqmp_gemm_h2": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _vp, _vp]),
@@ -145,8 +141,19 @@ def version() -> str:
     return load().sqmp_version().decode()
 
 
+_reload_hooks = []
+
+
+def on_reload(fn):
+    """Register a Python-side mirror of a library knob, refreshed by reload_knobs()."""
+    _reload_hooks.append(fn)
+
+
 def reload_knobs():
-    """Re-read the library's SQMP_* launch knobs (read once at load) after os.environ changed:
-    the in-process A/B tools and the tests that switch a launch variant call this."""
+    """Re-read the library's SQMP_* launch knobs (read once at load) and their Python-side
+    mirrors after os.environ changed: the in-process A/B tools and the tests that switch a
+    launch variant call this."""
     if _lib is not None:
         _lib.sqmp_reload_knobs()
+    for fn in _reload_hooks:
+        fn()

@@ -550,8 +550,7 @@ class W4A4Linear(nn.Module):
         fuse = (ospec is not None and ospec[0] in ("per_group", "per_tensor") and _OQ_FUSE
                 and not use_i8
                 and (not use_f8 or ops.f8_colmax_ok(pw))       # the 16x16x128 FP8 kernel
-                and (not use_fqt or c4[1].dim() == 3           # the tile-major fqt7 GEMM
-                     or c4[3].dim() == 3)                        # or the fqa GEMM
+                and (not use_fqt or c4[1].dim() == 3)          # the tile-major fqt7 GEMM
                 and (self.salient_indices is None or pw.K - pw.S > 0))
         colmax = ops.out_quant_workspace(x2.shape[0], pw.N, x2.device)["buf"] if fuse else None
         if use_f8:
@@ -625,8 +624,11 @@ class SiblingGroup:
     (ops.gemm_fq7_group).  The other members' outputs are kept for their own call on the same
     input object (identity, storage, shape and version must match -- an input changed in
     place, or another tensor, is computed as usual) and handed out once.  Each output is
-    bit-identical to the member's own forward; layers that the grouped kernels do not cover
-    (other act modes, output quantization, the activation-order path, ...) compute alone."""
+    bit-identical to the member's own forward unless exactly one of the two launches takes the
+    K split inside the workgroup (ops.fq7_plan, OPT bit 16: a member alone on a grid of at most
+    one 128-row tile per CU) -- then equal within fp32 rounding of the partial sums; layers that
+    the grouped kernels do not cover (other act modes, output quantization, the
+    activation-order path, ...) compute alone."""
 
     def __init__(self, members):
         self.members = list(members)

@@ -413,6 +413,19 @@ def gemm_fq7_group(As, pws, biases):
     return ys
 
 
+def fq7_plan(pws, M: int, group: bool):
+    """(row-tile height, OPT bits) of the packed-order launch sqmp_gemm_fq7 would take for
+    pws[0] alone (group False) or sqmp_gemm_fq7_group for all of pws: OPT bit 16 (the K split
+    inside the workgroup) adds the fp32 partial sums in another order."""
+    p0 = pws[0]
+    n = len(pws) if group else 1
+    Ns = (ctypes.c_int * n)(*[pw.N for pw in pws[:n]])
+    tm, opt = ctypes.c_int(), ctypes.c_int()
+    check(load().sqmp_fq7_plan(_dtype_code(p0.dtype), M, Ns, n if group else 0, p0.Kp, p0.Gw,
+                               FQ7_J, ctypes.byref(tm), ctypes.byref(opt)), "fq7_plan")
+    return tm.value, opt.value
+
+
 def group_eligible(pws, act_quant: str, act_bits: int, group_size: int, M: int) -> bool:
     """Whether quant_act_fp_group + gemm_fq7_group compute these sibling layers: sorted
     per_group activations of <= 8 bits in power-of-two groups of 16 .. 1024 on the
@@ -436,7 +449,7 @@ def group_eligible(pws, act_quant: str, act_bits: int, group_size: int, M: int) 
     if not FQ7_AUTO or p0.dtype not in (torch.float16, torch.bfloat16) or p0.K - p0.S <= 0:
         return False
     # the quantizer holds one LDS region of Kp + S_pad + 8 words per member + the salient list / masks
-    if 4 * ((p0.Kp + p0.S_pad + 8) * len(pws) + p0.S_pad + 2 * ((p0.Kp + 63) // 64)) > 150 * 1024:
+    if not lc_lds_ok(p0.Kp, p0.S_pad, len(pws)):
         return False
     return all(fq7_eligible(pw) and pw.Gw % 64 == 0 and pw.K == p0.K and pw.Kp == p0.Kp
                and pw.S_pad == p0.S_pad and pw.S == p0.S and pw.Gw == p0.Gw
@@ -459,14 +472,21 @@ FQT7 = os.environ.get("SQMP_FQT7", "1") == "1"
 # its register operand's row tiles per wave: 2 (256 weight rows x 256 tokens per tile) or 4
 # (128 x 512: half the permuted-weight LDS traffic per MFMA, twice the act-code decode)
 FQT7_J = int(os.environ.get("SQMP_FQT7_J", "2"))
-# the activation-order GEMM with the act codes decoded once per workgroup into LDS and the
-# permuted weight in registers (sqmp_gemm_fqa on the row-major act operands + SQMP_QA_WPT)
-FQA = os.environ.get("SQMP_FQA", "0") == "1"
 
 
 def _fqt_j() -> int:
     """Tile-major operand layout of the activation-order path (FQT7_J: 2 or 4)."""
     return FQT7_J if FQT7_J in (2, 4) else 2
+
+
+def lc_lds_ok(P: int, S_pad: int, nout: int = 1) -> bool:
+    """The lane-contiguous quantizer's LDS budget (quant_lc_supported / lc_lds_words in
+    sqmp_actquant_lc.hip): nout regions of P + S_pad + 8 words, the salient list and two mask
+    words per 64-position chunk, within 150 KiB; P + S_pad < 65536 (16-bit table positions).
+    Every Python-side eligibility check that leads to that kernel applies it, so that a layer
+    the library would refuse (EUNSUPPORTED) takes another path instead of raising."""
+    return (4 * ((P + S_pad + 8) * nout + S_pad + 2 * ((P + 63) // 64)) <= 150 * 1024
+            and P + S_pad < 65536)
 
 
 def fqt_eligible(pw: PackedWeight, act_quant: str, act_bits: int, group_size: int,
@@ -480,7 +500,8 @@ def fqt_eligible(pw: PackedWeight, act_quant: str, act_bits: int, group_size: in
     return (act_quant in _SORTED or act_quant == "per_group_unsorted") and act_bits <= 4 \
         and pw.n_bits == 4 and pw.dense is None and pw.dtype != torch.float32 \
         and 64 <= group_size <= 1024 and group_size & (group_size - 1) == 0 \
-        and pw.N % 8 == 0 and pw.K % 8 == 0 and pw.K <= 16384 and pw.K - pw.S > 0
+        and pw.N % 8 == 0 and pw.K % 8 == 0 and pw.K <= 16384 and pw.K - pw.S > 0 \
+        and lc_lds_ok(pw.Kp, pw.S_pad)
 
 
 def quant_act_c4(x2: torch.Tensor, pw: PackedWeight, act_quant: str, n_bits: int,
@@ -499,8 +520,7 @@ def quant_act_c4(x2: torch.Tensor, pw: PackedWeight, act_quant: str, n_bits: int
     Kq = (Kn + 63) // 64 * 64
     ngq = (Kn + group_size - 1) // group_size
     dev = x2.device
-    fqa = FQA
-    tiled = FQT7 and Kq % 128 == 0 and not fqa
+    tiled = FQT7 and Kq % 128 == 0
     tj = _fqt_j()
     if tiled:
         R = max(128 * tj, (M + 128 * tj - 1) // (128 * tj) * (128 * tj))
@@ -525,14 +545,7 @@ def quant_act_c4(x2: torch.Tensor, pw: PackedWeight, act_quant: str, n_bits: int
         flags |= _lib.QA_REUSE_STATS
     if pw.posmap is None:
         pw.posmap = build_posmap(pw.perm, K)
-    if fqa:
-        # sqmp_gemm_fqa's tile-major weight: [roundup(N, 512) / 64][(Kq + S_pad) / 64][4096]
-        # (3-d marks the layout)
-        nt_rows = (pw.N + 511) // 512 * 512
-        wp = torch.empty((nt_rows // 64, (Kq + pw.S_pad) // 64, 4096), dtype=pw.dtype, device=dev)
-        flags |= _lib.QA_WPT
-    else:
-        wp = torch.empty((pad_n(pw.N), Kq + pw.S_pad), dtype=pw.dtype, device=dev)
+    wp = torch.empty((pad_n(pw.N), Kq + pw.S_pad), dtype=pw.dtype, device=dev)
     # one call: quantizer + weight permutation in the same launch
     status = lib.sqmp_quant_act_c4(_p(x2), _dtype_code(x2.dtype), M, K, ACT_MODES[act_quant],
                                    n_bits, group_size, _p(pw.amap), pw.Kp, _p(pw.nonsal),
@@ -557,12 +570,6 @@ def gemm_fqt(codes: torch.Tensor, scales: torch.Tensor, xs: torch.Tensor, wp: to
     M = xs.shape[0]
     y = torch.empty((M, pw.N), dtype=pw.dtype, device=codes.device)
     Kq = codes.shape[1] * 2
-    if wp.dim() == 3:       # SQMP_QA_WPT: sqmp_gemm_fqa on the row-major act operands
-        check(load().sqmp_gemm_fqa(_p(codes), _p(scales), _p(xs) if pw.S_pad else None, _p(wp),
-                                   _p(bias), _p(y), _dtype_code(pw.dtype), M, pw.N, Kq,
-                                   pw.S_pad, group_size, scales.shape[1], _p(colmax),
-                                   _stream(codes)), "gemm_fqa")
-        return y
     if scales.dim() == 3:   # tile-major (SQMP_QA_TILED: 32-row blocks, TILED4: 64-row)
         check(load().sqmp_gemm_fqt7j(_p(codes), _p(scales), _p(xs), _p(wp), _p(bias), _p(y),
                                      _dtype_code(pw.dtype), M, pw.N, Kq, pw.S_pad, group_size,
@@ -727,7 +734,16 @@ def _h2d_rows_ok(M: int, L: int, N: int = 0) -> bool:
             and 4 * ((N + 255) // 256 * 256) * L < (1 << 32))
 
 
-_LC_OFF = os.environ.get("SQMP_DISABLE_LC") is not None  # (the library reads it once too)
+_LC_OFF = False  # SQMP_DISABLE_LC: the library's knob, mirrored here (refreshed by reload_knobs)
+
+
+def _read_lc_off():
+    global _LC_OFF
+    _LC_OFF = os.environ.get("SQMP_DISABLE_LC") is not None
+
+
+_read_lc_off()
+_lib.on_reload(_read_lc_off)
 
 
 def h2_planes_ok(pw: PackedWeight, act_quant: str, M: int = 0, group_size: int = 0) -> bool:
@@ -896,12 +912,12 @@ def gemm_f8(a8: torch.Tensor, sa: torch.Tensor, xs: torch.Tensor, pw: PackedWeig
 def f8_eligible(pw: PackedWeight, act_quant: str, act_bits: int) -> bool:
     """Whether the block-scaled FP8 MFMA path computes this layer: one act scale per row,
     4-bit codes on both sides (exact in e4m3), weight groups of whole 64-blocks, and the
-    lane-contiguous quantizer's shape limits (K % 8 == 0, K <= 16384; quant_lc_supported in
-    sqmp_actquant.hip).  The input pointer's 16-B alignment is checked per call
-    (f8_input_ok)."""
+    lane-contiguous quantizer's shape and LDS limits (K % 8 == 0, K <= 16384, lc_lds_ok;
+    quant_lc_supported in sqmp_actquant_lc.hip).  The input pointer's 16-B alignment is
+    checked per call (f8_input_ok)."""
     return (act_quant in ("per_token", "per_tensor") and pw.dtype != torch.float32
             and pw.n_bits == 4 and pw.dense is None and pw.Gw % 64 == 0 and act_bits <= 4
-            and pw.K <= 16384 and pw.K % 8 == 0)
+            and pw.K <= 16384 and pw.K % 8 == 0 and lc_lds_ok(pw.Kp, pw.S_pad))
 
 
 def f8_input_ok(x2: torch.Tensor) -> bool:

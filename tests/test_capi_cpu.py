@@ -137,3 +137,58 @@ def test_model_size_formula():
     assert get_model_size(lin) == 64 * 32 * 16
     assert get_model_size(lin, data_width=4, salient_prop=0.1, group_size=64) == pytest.approx(
         64 * 32 * ((4 + 20 / 64) * 0.9 + (16 + 20 / 64) * 0.1))
+
+
+def _c_entries():
+    """(name, parameter list, body start) of every extern "C" definition in csrc/."""
+    import glob
+    out = []
+    for f in sorted(glob.glob(os.path.join(ROOT, "smoothquant-mixedprecision_amd", "csrc", "*.hip"))):
+        src = open(f).read()
+        for m in re.finditer(r'extern "C" [^;{]*?\b(sqmp_[a-z0-9_]+)\s*\(([^)]*)\)\s*\{', src):
+            out.append((m.group(1), m.group(2), src[m.end():m.end() + 200]))
+    return out
+
+
+def test_every_launching_entry_runs_on_its_streams_device():
+    """Every C entry that takes a stream (i.e. launches work) makes the stream's device
+    current first (SQMP_DEVICE_GUARD, sqmp_common.h): the reference's callers place layers on
+    several GPUs (accelerate device_map="auto", run_experiments.py:146-148,
+    examples/ppl_eval.sh:17-18), so the caller's current device need not be the tensors'."""
+    entries = _c_entries()
+    declared = set(_declared_functions())
+    launching = [(n, body) for n, params, body in entries if re.search(r"void\s*\*\s*stream\b", params)]
+    assert len(launching) >= 25
+    for n, body in launching:
+        first = body.strip().split("\n", 1)[0].strip()
+        assert first == "SQMP_DEVICE_GUARD(stream);", f"{n}: first statement is {first!r}"
+    # every declared entry that takes a stream is among them
+    for n, params, _ in entries:
+        if n in declared and "stream" in params:
+            assert n in dict(launching), n
+
+
+def test_lc_lds_budget_in_every_eligibility_check(lib):
+    """The lane-contiguous quantizer refuses rows whose LDS image exceeds 150 KiB
+    (quant_lc_supported); fqt_eligible, f8_eligible and group_eligible apply the same limit
+    (ops.lc_lds_ok), so such a layer takes another path instead of raising EUNSUPPORTED.
+    K = 16384, G = 128: half salient fits, two thirds does not."""
+    from types import SimpleNamespace
+    from smoothquant import ops
+
+    def pw(S):
+        g = [ctypes.c_int() for _ in range(4)]
+        assert lib.sqmp_weight_geometry(16384, S, 2, 128, *[ctypes.byref(v) for v in g]) == 0
+        Kp, Gw, ngw, S_pad = (v.value for v in g)
+        return SimpleNamespace(K=16384, S=S, Kp=Kp, S_pad=S_pad, Gw=Gw, ngw=ngw, N=4096,
+                               n_bits=4, dense=None, dtype=torch.float16)
+
+    ok, big = pw(8192), pw(11000)
+    assert ops.lc_lds_ok(ok.Kp, ok.S_pad) and not ops.lc_lds_ok(big.Kp, big.S_pad)
+    # the boundary itself: 4 * lc_lds_words(P, S_pad, 1) <= 150 KiB
+    P = 16384
+    S_max = (150 * 1024 // 4 - P - 8 - 2 * (P // 64)) // 2
+    assert ops.lc_lds_ok(P, S_max) and not ops.lc_lds_ok(P, S_max + 1)
+    assert ops.fqt_eligible(ok, "per_group", 4, 128, 16384, force=True)
+    assert not ops.fqt_eligible(big, "per_group", 4, 128, 16384, force=True)
+    assert ops.f8_eligible(ok, "per_token", 4) and not ops.f8_eligible(big, "per_token", 4)

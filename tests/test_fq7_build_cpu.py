@@ -88,7 +88,7 @@ def test_asm_sgpr_hazard_other_kernels(tmp_path):
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     import check_asm_sgpr_hazard as H
     csrc = os.path.dirname(SRC)
-    names = ["sqmp_gemm_f8", "sqmp_gemm_h2d", "sqmp_actquant_lc", "sqmp_gemm_fqa", "sqmp_gemm_fast",
+    names = ["sqmp_gemm_f8", "sqmp_gemm_h2d", "sqmp_actquant_lc", "sqmp_gemm_fast",
              "sqmp_gemm_x3"]
 
     def asm(n):
@@ -105,3 +105,36 @@ def test_asm_sgpr_hazard_other_kernels(tmp_path):
     for n, rc, out in results:
         assert rc == 0, n
         assert H.main(out) == 0, n
+
+
+_FIXTURE = """_Z6kernelv:
+{body}
+.Lfunc_end0:
+"""
+
+
+@pytest.mark.parametrize("body,want", [
+    # straight line: a v_readlane restore 2 wait states before an asm buffer_load reading it
+    ("  v_readlane_b32 s12, v3, 4\n  s_nop 0\n  ;;#ASMSTART\n"
+     "  buffer_load_dword v5, v6, s[8:11], s12 offen\n  ;;#ASMEND", 1),
+    # the same padded by s_nop 4 (5 wait states): clean
+    ("  v_readlane_b32 s12, v3, 4\n  s_nop 4\n  ;;#ASMSTART\n"
+     "  buffer_load_dword v5, v6, s[8:11], s12 offen\n  ;;#ASMEND", 0),
+    # the write at the end of a loop body reaches the load at the loop head by the back edge
+    (".LBB0_1:\n  ;;#ASMSTART\n  buffer_load_dword v5, v6, s[8:11], s12 offen\n  ;;#ASMEND\n"
+     "  s_nop 7\n  s_nop 7\n  v_readfirstlane_b32 s12, v7\n  s_cbranch_scc1 .LBB0_1", 1),
+    # a VOP3b carry-out (the second operand) into the load's soffset
+    ("  v_add_co_u32 v1, s[12:13], v2, v3\n  ;;#ASMSTART\n"
+     "  buffer_load_dword v5, v6, s[8:11], s12 offen\n  ;;#ASMEND", 1),
+    # a VGPR-destination VALU op and an SALU write of the register: no hazard
+    ("  v_add_co_u32 v1, vcc, v2, v3\n  s_mov_b32 s12, 0\n  ;;#ASMSTART\n"
+     "  buffer_load_dword v5, v6, s[8:11], s12 offen\n  ;;#ASMEND", 0),
+])
+def test_asm_hazard_scan_fixtures(tmp_path, body, want):
+    """tools/check_asm_sgpr_hazard.py on synthetic assembly: straight-line and back-edge
+    paths, VOP3b carry-out destinations, and the clean cases."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import check_asm_sgpr_hazard as H
+    p = tmp_path / "k.s"
+    p.write_text(_FIXTURE.format(body=body))
+    assert H.main(str(p)) == want

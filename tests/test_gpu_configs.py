@@ -160,13 +160,23 @@ def test_config_workload_matches_reference(case):
         ospec = resolve_quantizer(m.output_quant)
         if ospec is None:
             # forward = this GEMM: bit for bit, except where the forward ran a sibling group's
-            # launch and this layer alone takes the K-split kernel (one 128-row tile per CU,
-            # SQMP_FQ7_KS; fp32 partial sums in another order) -- then within the pair
-            # tolerance of it, and the forward itself within tol of the fp64 product
+            # launch and exactly one of that launch and this layer's own takes the K split
+            # inside the workgroup (ops.fq7_plan, OPT bit 16; fp32 partial sums in another
+            # order) -- then within the pair tolerance of it, and the forward itself within
+            # tol of the fp64 product
             yf = y.reshape(y_pre.shape)
-            if not torch.equal(yf, y_pre):
+            grp = m.__dict__.get("_sqmp_group")
+            split_differs = False
+            if grp is not None and grp._plan(x2) is not None and ops.fq7_eligible(pw):
+                pws = [g.packed() for g in grp.members]
+                own = ops.fq7_plan([pw], x2.shape[0], group=False)[1]
+                grouped = ops.fq7_plan(pws, x2.shape[0], group=True)[1]
+                split_differs = bool((own ^ grouped) & 16)
+            if split_differs:
                 assert _rel(yf.float().cpu().numpy(), y_pre.float().cpu().numpy()) < 1e-3, n
                 assert _rel(yf.float().cpu().numpy(), yr.cpu().numpy()) < tol, n
+            else:
+                assert torch.equal(yf, y_pre), f"{n}: forward differs from its own GEMM"
         else:
             # output quantization (fake_quant.py:308-316) is discontinuous in the GEMM
             # output, so it is checked on OUR pre-quant output: the forward's y must be

@@ -144,15 +144,7 @@ def same_values(a, b):
     return bool(ok.all())
 
 
-def untile_wpt(wpt, N):
-    """sqmp_gemm_fqa's weight [Nt/64][L/64][4096] ([rb][h][lane = 16 q + r16][8] per stage)
-    -> row-major [N, L]."""
-    nb, nkt = wpt.shape[0], wpt.shape[1]
-    t = wpt.reshape(nb, nkt, 4, 2, 4, 16, 8)                       # nb kt rb h q r e
-    return t.permute(0, 2, 5, 1, 3, 4, 6).reshape(nb * 64, nkt * 64)[:N]
-
-
-@pytest.mark.parametrize("tiled", [0, 2, 4, -1], ids=["rowmajor", "tiled", "tiled4", "fqa"])
+@pytest.mark.parametrize("tiled", [0, 2, 4], ids=["rowmajor", "tiled", "tiled4"])
 @pytest.mark.parametrize("M,K,N,Gs,p,dt,aq", CASES)
 def test_fqt_operands_exact_and_y(M, K, N, Gs, p, dt, aq, tiled):
     """Column for column against the ORACLE (oracle/fake_quant_oracle.py, pinned to the
@@ -169,24 +161,18 @@ def test_fqt_operands_exact_and_y(M, K, N, Gs, p, dt, aq, tiled):
     if tiled and Kq % 128:
         pytest.skip("tile-major operands need Kq % 128 == 0 (the dispatcher then takes "
                     "the row-major layout, covered by the rowmajor case)")
-    fqt7, fqt7_j, fqa = ops.FQT7, ops.FQT7_J, ops.FQA
-    ops.FQT7, ops.FQT7_J, ops.FQA = tiled > 0, max(tiled, 2), tiled < 0
+    fqt7, fqt7_j = ops.FQT7, ops.FQT7_J
+    ops.FQT7, ops.FQT7_J = tiled > 0, max(tiled, 2)
     try:
         codes, scales, xs, wp = ops.quant_act_c4(x, pw, aq, 4, Gs)
     finally:
-        ops.FQT7, ops.FQT7_J, ops.FQA = fqt7, fqt7_j, fqa
+        ops.FQT7, ops.FQT7_J = fqt7, fqt7_j
     assert (scales.dim() == 3) == (tiled > 0)
-    assert (wp.dim() == 3) == (tiled < 0)
     if tiled > 0:
         assert scales.shape[2] == 16 * tiled
     y = ops.gemm_fqt(codes, scales, xs, wp, pw, lin.bias, Gs)
     if tiled > 0:
         codes, scales, xs = untile_c4(codes, scales, xs, M, Kq, pw.S_pad)
-    if tiled < 0:
-        # the fqa weight layout; rows past N hold zeros
-        full = untile_wpt(wp, wp.shape[0] * 64)
-        assert (full[pw.N:] == 0).all()
-        wp = full[: pw.N]
     # ---- the oracle's operands (CPU, numpy)
     Dn = {torch.float16: "fp16", torch.bfloat16: "bf16"}[dt]
     D = O.DT(Dn)
@@ -268,66 +254,6 @@ def test_fqt_forward_dispatch_and_full_size_config2():
     q.kernel = "fq"
     y_f = q(x)
     assert rel(y_t, y_f) < 1e-3
-
-
-@pytest.mark.parametrize("M,K,N,Gs,p,dt,aq", [CASES[1], CASES[5], CASES[6],
-                                                (16384, 4096, 4096, 128, 0.10, torch.float16, "per_group")])
-def test_fqa_matches_fqt7_and_colmax(M, K, N, Gs, p, dt, aq):
-    """sqmp_gemm_fqa (act codes decoded once per workgroup into LDS, wp in registers) against
-    fqt7 on the same batch: the permuted weight equal element for element (untiled), y within the
-    accumulation-order tolerance, the fused column statistics equal max |y| per column, and the
-    output without bias equal up to the bias."""
-    dev = _dev()
-    from smoothquant import ops
-    q, lin, x = _layer(dev, M, K, N, Gs, p, dt, aq=aq)
-    pw = q.packed()
-    saved = ops.FQT7, ops.FQT7_J, ops.FQA
-    try:
-        ops.FQT7, ops.FQT7_J, ops.FQA = True, 2, False
-        c7 = ops.quant_act_c4(x, pw, aq, 4, Gs)
-        y7 = ops.gemm_fqt(*c7, pw, lin.bias, Gs)
-        ops.FQA = True
-        ca = ops.quant_act_c4(x, pw, aq, 4, Gs)
-        cm = torch.zeros(pw.N, dtype=torch.int32, device=dev)
-        ya = ops.gemm_fqt(*ca, pw, lin.bias, Gs, colmax=cm)
-        yn = ops.gemm_fqt(*ca, pw, None, Gs)
-    finally:
-        ops.FQT7, ops.FQT7_J, ops.FQA = saved
-    wp7 = c7[3] if c7[3].dim() == 2 else None
-    wpa = untile_wpt(ca[3], pw.N)
-    if wp7 is not None:
-        assert torch.equal(wp7[: pw.N].view(torch.int16), wpa.view(torch.int16))
-    assert rel(ya, y7) < (1e-3 if dt == torch.float16 else 8e-3)
-    ref_cm = ya.float().abs().amax(0)
-    assert torch.equal(cm.view(torch.float32), ref_cm)
-    b = lin.bias.detach().float()
-    assert rel(yn.float() + b, ya.float()) < 2e-2
-
-
-@pytest.mark.parametrize("M,L,N,dt", [(128, 64, 512, torch.float16), (300, 448, 1000, torch.float16),
-                                      (2048, 4160, 4096, torch.float16),
-                                      (257, 1024, 520, torch.bfloat16)])
-def test_fqa_dense_core(M, L, N, dt):
-    """sqmp_gemm_fqa with Kq = 0 is a plain dense GEMM y = x . W^T on the same core (the
-    dense-core measurement of tools/dense_core.py): against the fp64 product."""
-    dev = _dev()
-    from smoothquant import ops
-    from smoothquant._lib import load, check
-    g = torch.Generator(device=dev).manual_seed(1)
-    R = (M + 255) // 256 * 256
-    xs = torch.randn(R, L, generator=g, device=dev).to(dt)
-    W = (torch.randn(N, L, generator=g, device=dev) * 0.05).to(dt)
-    bias = (torch.randn(N, generator=g, device=dev) * 0.1).to(dt)
-    lib = load()
-    wpt = torch.empty(lib.sqmp_fqa_wpt_elems(N, L, 0), dtype=dt, device=dev)
-    check(lib.sqmp_pack_wpt(ops._p(W), ops._dtype_code(dt), N, L, ops._p(wpt), ops._stream(W)), "pack_wpt")
-    y = torch.empty(M, N, dtype=dt, device=dev)
-    check(lib.sqmp_gemm_fqa(None, None, ops._p(xs), ops._p(wpt), ops._p(bias), ops._p(y),
-                            ops._dtype_code(dt), M, N, 0, L, 64, R, None, ops._stream(W)), "gemm_fqa")
-    ref = xs[:M].double() @ W.double().t() + bias.double()
-    assert rel(y, ref) < (2e-3 if dt == torch.float16 else 1e-2)
-    wr = untile_wpt(wpt.view(-1, L // 64, 4096), N)
-    assert torch.equal(wr.view(torch.int16), W.view(torch.int16))
 
 
 def test_standalone_perm_matches_fused():

@@ -4,9 +4,9 @@ variants.  python tools/ab_fqt7.py [variants, "+"- or comma-separated] [rounds] 
 ENV (default SQMP_FQT7_OPT) names the per-launch variable; SQMP_FQ7_DIAG selects the timing
 diagnostics of a SQMP_DIAG=1 build (wrong results by design: no equality check then).  A
 variant "J4:3" runs the 64-row-block operands (ops.FQT7_J = 4) with value 3; "P..." times the
-prepass (quant_act_c4) of that variant instead of the GEMM; "A" runs sqmp_gemm_fqa (act codes
-decoded once per workgroup into LDS) on its own operands.  (The one-wave-per-SIMD fqt8 / fqt9
-variants were removed in round 5: profiles/r04_ab_fqt8.txt, r04_ab_fqt9.txt.)"""
+prepass (quant_act_c4) of that variant instead of the GEMM.  (The one-wave-per-SIMD fqt8 /
+fqt9 variants were removed in round 5, profiles/r04_ab_fqt8.txt, r04_ab_fqt9.txt; the fqa
+variant in round 6, profiles/r05_ab_fqa_dense_core.txt.)"""
 import os
 import sys
 
@@ -30,14 +30,11 @@ stream = torch.cuda.current_stream(dev)
 def parse(v):
     pre = v.startswith("P")
     v = v[1:] if pre else v
-    if v.startswith("A"):
-        return pre, 0, v[2:] or "0"
     j, val = (int(v[1:v.index(":")]), v[v.index(":") + 1:]) if v.startswith("J") else (2, v)
     return pre, j, val
 
 
 def use(j):
-    ops.FQA = j == 0
     ops.FQT7_J = j if j in (2, 4) else 2
 
 
@@ -73,10 +70,7 @@ for v in variants:
     torch.cuda.synchronize()
     if ref is None:
         ref = y.clone()
-    if parse(v)[1] == 0:  # fqa: another accumulation order -- tolerance, not bits
-        assert float((y.float() - ref.float()).norm() / ref.float().norm()) < 1e-3, f"variant {v} changed y"
-    else:
-        assert ENV.endswith("_DIAG") or torch.equal(y.view(torch.int16), ref.view(torch.int16)), f"variant {v} changed y"
+    assert ENV.endswith("_DIAG") or torch.equal(y.view(torch.int16), ref.view(torch.int16)), f"variant {v} changed y"
 t_end = __import__("time").perf_counter() + 2.0
 while __import__("time").perf_counter() < t_end:
     for _ in range(10):
