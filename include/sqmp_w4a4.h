@@ -86,9 +86,7 @@ enum sqmp_weight_mode {
 enum sqmp_act_out {
   SQMP_OUT_FP = 0,      /* out: D [M][Kp + S_pad]: x_hat at packed positions, exact
                            salient x in the tail (operand of sqmp_gemm_fq) */
-  SQMP_OUT_I8 = 1,      /* out: int8 codes [M][roundup(Kp,256)] in the i8 GEMM's K order
-                           (sqmp_actquant.hip); out_scale: fp32 [M] (the D scale);
-                           out_xs: D [M][S_pad] exact salient x (operand of sqmp_gemm_i8) */
+  /* 1: reserved (the int8-code output of the removed integer GEMM, ABI < 0.6) */
   SQMP_OUT_INPLACE = 2, /* fake-quantize `x` in place through amap_fq (output quant,
                            fake_quant.py:308-316) */
   SQMP_OUT_F8 = 3,      /* per_token / per_tensor, n_bits <= 4, sqmp_quant_act_v2 with
@@ -213,14 +211,6 @@ int sqmp_gemm_fq_colmax(const void* a, const void* codes, const void* wscale,
                         const void* wsal, const void* bias, void* y, int dtype, int M, int N,
                         int Kp, int S_pad, int Gw, int ngw, int n_bits, uint32_t* colmax,
                         void* stream);
-
-/* Integer GEMM (per_token / per_tensor activations): int8 act codes x int4 weight codes
- * on the i8 MFMA, per-weight-group fp32 fold, per-row act scale, salient tail on the D
- * MFMA, bias, one rounding to D.  Needs Gw % 64 == 0 and dtype fp16/bf16. */
-int sqmp_gemm_i8(const int8_t* a8, const float* ascale, const void* xs,
-                 const void* codes, const void* wscale, const void* wsal,
-                 const void* bias, void* y, int dtype, int M, int N, int Kp, int S_pad,
-                 int Gw, int ngw, int n_bits, void* stream);
 
 /* e4m3 operands of sqmp_gemm_f8 from a packed 4-bit weight: w8 = the int4 codes as OCP
  * e4m3 bytes [Np][Kp] in packed order, ws32 = the D group scales as fp32 [ngw][Np]

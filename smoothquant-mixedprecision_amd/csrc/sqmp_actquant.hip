@@ -142,40 +142,7 @@ __global__ __launch_bounds__(256) void quant_act_kernel(
       __syncthreads();
     }
     // ---- outputs, in output order
-    if (OUT == SQMP_OUT_I8) {
-      // int8 codes in the K order of the i8 GEMM's fragments (sqmp_mfma.h unpack_i8):
-      // 16-byte chunk c of a row -> 64-code block c>>2, chunk cb=c&3 within it, byte idx ->
-      // packed position blk*64 + 16*(2*(cb>>1) + (idx>>3)) + 8*(cb&1) + E[idx&7],
-      // E = (0,4,1,5,2,6,3,7): the codes of bpack dwords (cb&1)*4 + 2*(cb>>1) + {0,1}.
-      // Rows are padded to a multiple of 256 codes.
-      const int P8 = (int)round_up_dev(P, 256);
-      int8_t* o = (int8_t*)out + (size_t)m * P8;
-      for (int c = tid; c < P8 / 16; c += 256) {
-        const int base = (c >> 2) * 64 + 32 * ((c & 3) >> 1) + 8 * (c & 1);
-        uint32_t wv[4];
-#pragma unroll
-        for (int w4 = 0; w4 < 4; ++w4) {
-          uint32_t word = 0;
-#pragma unroll
-          for (int e4 = 0; e4 < 4; ++e4) {
-            const int idx = w4 * 4 + e4;
-            const int ee = ((idx & 1) << 2) | ((idx & 7) >> 1);
-            const int p = base + 16 * (idx >> 3) + ee;
-            int code = 0;
-            if (p < P) {
-              const uint32_t e = ent[p];
-              if ((e >> 16) != G_ZERO) code = (int)quant_code<DT>(DT::to_f(row[e & 0xFFFFu]), s_row);
-            }
-            word |= ((uint32_t)code & 0xFFu) << (8 * e4);
-          }
-          wv[w4] = word;
-        }
-        ((u32x4*)o)[c] = u32x4{wv[0], wv[1], wv[2], wv[3]};
-      }
-      if (tid == 0) out_scale[m] = s_row;
-      T* xs = out_xs + (size_t)m * S_pad;
-      for (int j = tid; j < S_pad; j += 256) xs[j] = j < S ? row[sal[j]] : DT::from_f(0.f);
-    } else if (OUT == SQMP_OUT_FP) {
+    if (OUT == SQMP_OUT_FP) {
       const int W = P + S_pad;
       T* o = (T*)out + (size_t)m * W;
       for (int c = tid; c < W / VEC; c += 256) {
@@ -482,20 +449,34 @@ __global__ __launch_bounds__(256) void ent_from_lctab_kernel(
   if (key_clear && t < clear_words) key_clear[t] = 0u;
 }
 
+// ---------------------------------------------------------------- table padding
+// Ranks [Kn, lc_len) of the lane-contiguous table.  With the salient list and a per-weight
+// posmap, the first S of them are (zero word, packed position of salient column j) entries:
+// the quantizer gathers the zero word and scatters it to the salient positions itself, so it
+// needs no salient-position mask (the amap loads and ballots it used to make per workgroup).
+// The rest, and every pad rank without a posmap (in-place output quantization: salient
+// columns pass through), are the (zero word, sink word) entry lc_none.
+__device__ inline uint32_t pad_entry(int r, int Kn, uint32_t lc_none,
+                                     const int32_t* __restrict__ sal, int S,
+                                     const int32_t* __restrict__ posmap) {
+  const int j = r - Kn;
+  return (posmap && j < S) ? (lc_none & 0xFFFFu) | ((uint32_t)posmap[sal[j]] << 16) : lc_none;
+}
+
 // ---------------------------------------------------------------- lane-contiguous table
 // Per call, one thread per non-salient list entry i (column nonsal[i]):
 //   TAB_COUNTS  r = counts[col] (the stable rank), counts[col] = 0 afterwards, and the
 //               sorted column list colsorted[r] = col is kept for sibling layers;
 //   TAB_SORTED  col = colsorted[i], r = i (statistics reused from a previous call);
 //   TAB_LIST    r = i (unsorted groups / per_token / per_tensor).
-// lctab[r] = col | posmap[col] << 16, ranks [Kn, lc_len) get the (zero word, sink word)
-// entry, and key[0..K) is cleared when given (clean-workspace protocol).
+// lctab[r] = col | posmap[col] << 16, ranks [Kn, lc_len) the padding entries (pad_entry),
+// and key[0..K) is cleared when given (clean-workspace protocol).
 enum { TAB_COUNTS = 0, TAB_SORTED = 1, TAB_LIST = 2 };
 __global__ __launch_bounds__(256) void lc_table_kernel(
     int mode, const int32_t* __restrict__ nonsal, int Kn, int K,
     const int32_t* __restrict__ posmap, int32_t* __restrict__ counts,
     int32_t* __restrict__ colsorted, uint32_t* __restrict__ key, uint32_t* __restrict__ lctab,
-    int lc_len, uint32_t lc_none) {
+    int lc_len, uint32_t lc_none, const int32_t* __restrict__ sal, int S) {
   const int t = blockIdx.x * 256 + threadIdx.x;
   const int nt = gridDim.x * 256;
   if (t < Kn) {
@@ -515,7 +496,7 @@ __global__ __launch_bounds__(256) void lc_table_kernel(
     lctab[r] = (uint32_t)col | ((uint32_t)(posmap ? posmap[col] : col) << 16);
   }
   if (key && t < K) key[t] = 0u;
-  for (int r = Kn + t; r < lc_len; r += nt) lctab[r] = lc_none;
+  for (int r = Kn + t; r < lc_len; r += nt) lctab[r] = pad_entry(r, Kn, lc_none, sal, S, posmap);
 }
 
 // The F8 quantizer's table in packed-POSITION order: lctab[p] = amap[p] | p << 16 for the
@@ -617,15 +598,19 @@ struct RankOwnerEnt {
   int col[R];
 };
 
-template <int R>
-__device__ inline RankOwnerEnt<R> rank_owner_ents(int g0, int sub, int L,
+// BYCOL (the dense stagings): owner g is COLUMN g (< n = K) -- no list lookup in front of the
+// posmap load; a salient column's staged key is the sentinel, and it ranks nothing.  Else
+// owner g is list entry g (< n = L), column nonsal[g].
+template <int R, bool BYCOL = false>
+__device__ inline RankOwnerEnt<R> rank_owner_ents(int g0, int sub, int n,
                                                   const int32_t* __restrict__ nonsal,
                                                   const int32_t* __restrict__ posmap,
                                                   const SibTables& sib) {
   RankOwnerEnt<R> e;
   int pm[R][3];
 #pragma unroll
-  for (int o = 0; o < R; ++o) e.col[o] = sub == 0 && g0 + o < L ? nonsal[g0 + o] : -1;
+  for (int o = 0; o < R; ++o)
+    e.col[o] = sub == 0 && g0 + o < n ? (BYCOL ? g0 + o : nonsal[g0 + o]) : -1;
 #pragma unroll
   for (int o = 0; o < R; ++o) {
     const int c = e.col[o] < 0 ? 0 : e.col[o];
@@ -653,7 +638,7 @@ __device__ inline void rank_owner_group(const uint32_t* rt_kv, int L, int L4, in
     // (DENSE: the staged array is column-indexed -- the owner sits at its column, which the
     // group's sub 0 lane loaded; owners past the list rank column 0 and discard)
     int oi = li;
-    if constexpr (DENSE) {
+    if constexpr (DENSE) {  // (owner = column: rank_owner_ents<R, true>)
       const int c = __shfl(oe.col[o], (int)(threadIdx.x & 63) & ~(TPO - 1), 64);
       oi = c >= 0 ? c : 0;
     }
@@ -680,7 +665,8 @@ __device__ inline void rank_owner_group(const uint32_t* rt_kv, int L, int L4, in
       for (int e = 0; e < (oi & 3); ++e) cnt[o] += rt_kv[4 * ochunk[o] + e] == mine[o] ? 1u : 0u;
 #pragma unroll
     for (int w = 1; w < TPO; w <<= 1) cnt[o] += (uint32_t)__shfl_xor((int)cnt[o], w, 64);
-    if (sub == 0 && g0 + o < L) {
+    // (DENSE: a salient column's owner -- sentinel key -- writes nothing)
+    if (sub == 0 && (DENSE ? (oe.col[o] >= 0 && mine[o] != 0xFFFFFFFFu) : g0 + o < L)) {
       colsorted[cnt[o]] = oe.col[o];
       lctab[cnt[o]] = oe.ent[o][0];
       if (sib.n > 0) sib.lctab[0][cnt[o]] = oe.ent[o][1];
@@ -777,7 +763,8 @@ __device__ inline void rank_owner_group16(const uint16_t* kv, int L, int K8, int
       for (int e = 0; e < (oi & 7); ++e) cnt[o] += kv[8 * ochunk[o] + e] == mine[o] ? 1u : 0u;
 #pragma unroll
     for (int w = 1; w < TPO; w <<= 1) cnt[o] += (uint32_t)__shfl_xor((int)cnt[o], w, 64);
-    if (sub == 0 && g0 + o < L) {
+    // (owner = column; a salient column's sentinel key writes nothing)
+    if (sub == 0 && oe.col[o] >= 0 && mine[o] != 0xFFFFu) {
       colsorted[cnt[o]] = oe.col[o];
       lctab[cnt[o]] = oe.ent[o][0];
       if (sib.n > 0) sib.lctab[0][cnt[o]] = oe.ent[o][1];
@@ -796,7 +783,8 @@ __global__ __launch_bounds__(256) void rank_table_kernel(
   const int tid = threadIdx.x;
   const int L4 = (int)round_up_dev(DENSE ? K : L, (KW ? 8 : 4) * TPO) >> 2;  // u32x4 words: L4 / (KW ? 2 : 1) chunks
   const int g0 = (blockIdx.x * (256 / TPO) + tid / TPO) * R;  // this lane group's first owner
-  const RankOwnerEnt<R> oe = rank_owner_ents<R>(g0, tid % TPO, L, nonsal, posmap, sib);
+  // (DENSE: owners are the K columns, else the L list entries)
+  const RankOwnerEnt<R> oe = rank_owner_ents<R, DENSE>(g0, tid % TPO, DENSE ? K : L, nonsal, posmap, sib);
   if constexpr (KW != 0)
     rank_stage_dense16<KW, 12>(key, K, L4 >> 1, sal, S, (uint16_t*)rt_kv);
   else if constexpr (DENSE)
@@ -805,8 +793,8 @@ __global__ __launch_bounds__(256) void rank_table_kernel(
     rank_stage_keys<SB>(key, nonsal, L, L4, rt_kv);
   const int nt = gridDim.x * 256;
   for (int r = L + blockIdx.x * 256 + tid; r < lc_len; r += nt) {
-    lctab[r] = lc_none;
-    for (int o = 0; o < sib.n; ++o) sib.lctab[o][r] = lc_none;
+    lctab[r] = pad_entry(r, L, lc_none, sal, S, posmap);
+    for (int o = 0; o < sib.n; ++o) sib.lctab[o][r] = pad_entry(r, L, lc_none, sal, S, sib.posmap[o]);
   }
   __syncthreads();
   if constexpr (KW != 0)
@@ -832,7 +820,8 @@ template <int TPO, int SB>
 __global__ __launch_bounds__(256) void rank_bucket_kernel(
     const uint32_t* __restrict__ key, const int32_t* __restrict__ nonsal, int L,
     const int32_t* __restrict__ posmap, int32_t* __restrict__ colsorted,
-    uint32_t* __restrict__ lctab, int lc_len, uint32_t lc_none, SibTables sib) {
+    uint32_t* __restrict__ lctab, int lc_len, uint32_t lc_none, SibTables sib,
+    const int32_t* __restrict__ sal, int S) {
   extern __shared__ __attribute__((aligned(16))) uint32_t rb_lds[];
   const int tid = threadIdx.x;
   const int L4 = (int)round_up_dev(L, 4) >> 2;
@@ -846,8 +835,8 @@ __global__ __launch_bounds__(256) void rank_bucket_kernel(
   rank_stage_keys<SB>(key, nonsal, L, L4, keys);
   const int nt = gridDim.x * 256;
   for (int r = L + blockIdx.x * 256 + tid; r < lc_len; r += nt) {
-    lctab[r] = lc_none;
-    for (int o = 0; o < sib.n; ++o) sib.lctab[o][r] = lc_none;
+    lctab[r] = pad_entry(r, L, lc_none, sal, S, posmap);
+    for (int o = 0; o < sib.n; ++o) sib.lctab[o][r] = pad_entry(r, L, lc_none, sal, S, sib.posmap[o]);
   }
   __syncthreads();
   // ---- the key range (bucket = its position in [kmin, kmax], monotone in the key: column
@@ -1019,7 +1008,7 @@ static int launch_rank_table(const uint32_t* key, const int32_t* nonsal, int L,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);     \
     rank_bucket_kernel<T, 24><<<dim3(bgrid), dim3(256), blds, s>>>(key, nonsal, L, posmap,   \
                                                                   colsorted, lctab, lc_len,  \
-                                                                  lc_none, sib);             \
+                                                                  lc_none, sib, sal, S);     \
   } while (0)
     switch (btpo) {
       case 1: SQMP_RB(1); break;
@@ -1038,6 +1027,8 @@ static int launch_rank_table(const uint32_t* key, const int32_t* nonsal, int L,
   // 72.0 us, profiles/r05_ab_rank_dense.txt); SQMP_RT_DENSE=0: the list gather (A/B)
   const char* de = knob("SQMP_RT_DENSE");
   if (!(de && atoi(de) == 0) && K > 0 && K <= RT_MAX && K % 4 == 0 && (S == 0 || sal)) {
+    // owners are the K columns (rank_owner_ents<R, true>)
+    const int grid = cdiv((long)K * tpo, 256L * r);
     // 16-bit keys (f16 / bf16 column maxima; down_proj prepass 47.5 -> 45.2 us,
     // profiles/r05_ab_rank_k16.txt) unless SQMP_RT_K16=0 (A/B)
     const char* k16 = knob("SQMP_RT_K16");
@@ -1061,13 +1052,13 @@ static int launch_rank_table(const uint32_t* key, const int32_t* nonsal, int L,
   const size_t lds = sizeof(uint32_t) * (size_t)round_up(L, 4 * tpo);
   if (sb == 8)
     rank_table_go<8>(tpo, r, grid, lds, s, key, nonsal, L, posmap, colsorted, lctab, lc_len,
-                     lc_none, sib);
+                     lc_none, sib, 0, sal, S);
   else if (sb == 16)
     rank_table_go<16>(tpo, r, grid, lds, s, key, nonsal, L, posmap, colsorted, lctab, lc_len,
-                      lc_none, sib);
+                     lc_none, sib, 0, sal, S);
   else
     rank_table_go<24>(tpo, r, grid, lds, s, key, nonsal, L, posmap, colsorted, lctab, lc_len,
-                      lc_none, sib);
+                     lc_none, sib, 0, sal, S);
   SQMP_LAUNCH_CHECK();
   return SQMP_OK;
 }
@@ -1616,11 +1607,6 @@ static int quant_dispatch(void* x, int M, int K, int amode, int q_max, int G, in
     if (mode == MODE_TENSOR) return SQMP_Q(MODE_TENSOR, SQMP_OUT_FP);
     return SQMP_Q(MODE_GROUP, SQMP_OUT_FP);
   }
-  if (out_kind == SQMP_OUT_I8) {
-    if (mode == MODE_TOKEN) return SQMP_Q(MODE_TOKEN, SQMP_OUT_I8);
-    if (mode == MODE_TENSOR) return SQMP_Q(MODE_TENSOR, SQMP_OUT_I8);
-    return SQMP_EUNSUPPORTED;  // per-group act scales do not factor out of an int GEMM
-  }
   if (mode == MODE_TOKEN) return SQMP_Q(MODE_TOKEN, SQMP_OUT_INPLACE);
   if (mode == MODE_TENSOR) return SQMP_Q(MODE_TENSOR, SQMP_OUT_INPLACE);
   return SQMP_Q(MODE_GROUP, SQMP_OUT_INPLACE);
@@ -1697,7 +1683,7 @@ static int quant_act_impl(void* x, int dtype, int M, int K, int amode, int n_bit
                        amode != SQMP_ACT_PER_GROUP_MEAN3STD) ||
         group_size % 64 != 0)
       return SQMP_EUNSUPPORTED;
-  } else if (out_kind == SQMP_OUT_FP || out_kind == SQMP_OUT_I8 || out_kind == SQMP_OUT_F8 ||
+  } else if (out_kind == SQMP_OUT_FP || out_kind == SQMP_OUT_F8 ||
              out_kind == SQMP_OUT_H2) {
     if (Kp < K || Kp % 128 != 0 || S_pad < S || S_pad % 64 != 0 || !out) return SQMP_EINVAL;
     if (out_kind == SQMP_OUT_H2 && (dtype != SQMP_F32 || !out_scale)) return SQMP_EINVAL;
@@ -1708,8 +1694,6 @@ static int quant_act_impl(void* x, int dtype, int M, int K, int amode, int n_bit
         return SQMP_EUNSUPPORTED;
     }
     if (S > 0 && !salient) return SQMP_EINVAL;
-    if (out_kind == SQMP_OUT_I8 && (!out_scale || (S_pad > 0 && !out_xs))) return SQMP_EINVAL;
-    if (out_kind == SQMP_OUT_I8 && n_bits > 8) return SQMP_EUNSUPPORTED;
   } else {
     return SQMP_EINVAL;
   }
@@ -1781,7 +1765,7 @@ static int quant_act_impl(void* x, int dtype, int M, int K, int amode, int n_bit
     const int nthr = K > Kn ? K : (Kn > 0 ? Kn : 1);
     lc_table_kernel<<<dim3(cdiv(nthr, 256)), dim3(256), 0, s>>>(
         tmode, nonsal, Kn, K, pm, counts, colsorted, tmode == TAB_COUNTS ? cmax : nullptr,
-        lctab, lc_len, none);
+        lctab, lc_len, none, salient, S);
     SQMP_LAUNCH_CHECK();
     return SQMP_OK;
   };
@@ -1831,7 +1815,8 @@ static int quant_act_impl(void* x, int dtype, int M, int K, int amode, int n_bit
     uint32_t* kc;
     st = lc_prepare(posmap, lc_none, (flags & SQMP_QA_REUSE_STATS) != 0, kc);
     if (st) return st;
-    return launch_quant_lc(dtype, lmode, x, M, K, q_max, group_size, lctab, Kn, amap, Kp,
+    // (amap NULL: the table's pad entries zero the salient positions, pad_entry)
+    return launch_quant_lc(dtype, lmode, x, M, K, q_max, group_size, lctab, Kn, nullptr, Kp,
                            salient, S, S_pad, cmax, nonsal, out, kc, (int)k64, s);
   }
 
@@ -2054,7 +2039,8 @@ extern "C" int sqmp_quant_act_group(void* x, int dtype, int M, int K, int amode,
   r = launch_rank_table(cmax, nonsal, Kn, posmaps[0], colsorted, lctab, lc_len, lc_none, s, st, K,
                         salient, S, rank_key_kind(amode, dtype));
   if (r) return r;
+  // (amap NULL: the tables' pad entries zero the salient positions, pad_entry)
   return launch_quant_lc_group(dtype, x, M, K, (1 << (n_bits - 1)) - 1, group_size, lctab, Kn,
-                               amaps[0], Kp, salient, S, S_pad, cmax, nonsal, outs[0], cmax,
+                               nullptr, Kp, salient, S, S_pad, cmax, nonsal, outs[0], cmax,
                                (int)k64, ls, s);
 }

@@ -289,23 +289,48 @@ __device__ __forceinline__ void quant_lc_body(
   const int rp_end = (int)((long)(wg + 1) * npair / nblk);
   int rp = (int)((long)wg * npair / nblk);
 
-  // ---- once per workgroup: salient-position mask, zeroed buffer (+ two spare words: W =
-  // a zero read by padding table entries, W + 1 = a write-only sink for their scatter).
-  // Issue order: the mask's and the salient list's loads first, the first row pair's x
-  // after them, so that the mask's wait (vmcnt counts in issue order) does not wait for x and
-  // the prologue runs under x's latency.
+  // ---- this thread's RPL table entries (L1/L2-resident, padded to whole rounds with pad
+  // entries), the same for every row pair: the first pair's are loaded here, first, so that
+  // their round trip overlaps x's instead of following the prologue
+  uint32_t tab[RPL];
+  uint32_t tabs[NOUT > 1 ? NOUT - 1 : 1][RPL];  // the siblings' tables (same ranks, their positions)
+  auto load_tab = [&]() {
+    int toff = rb;
+    asm volatile("" : "+v"(toff));  // re-read per pair (no loop-invariant hoisting)
+#pragma unroll
+    for (int i = 0; i < RPL / 4; ++i) {
+      const u32x4 e = ((const u32x4*)(lctab + toff))[i];
+      tab[4 * i] = e[0]; tab[4 * i + 1] = e[1]; tab[4 * i + 2] = e[2]; tab[4 * i + 3] = e[3];
+    }
+#pragma unroll
+    for (int o = 0; o + 1 < NOUT; ++o)
+#pragma unroll
+      for (int i = 0; i < RPL / 4; ++i) {
+        const u32x4 e = ((const u32x4*)(sib.tab[o] + toff))[i];
+        tabs[o][4 * i] = e[0]; tabs[o][4 * i + 1] = e[1];
+        tabs[o][4 * i + 2] = e[2]; tabs[o][4 * i + 3] = e[3];
+      }
+  };
+  load_tab();
+
+  // ---- once per workgroup: zeroed buffer (+ two spare words: W = a zero read by padding
+  // table entries, W + 1 = a write-only sink for their scatter).  The salient positions of
+  // the output are zeroed by the table itself where its producer wrote (zero word, salient
+  // position) pad entries (pad_entry, sqmp_actquant.hip; amap NULL here); with amap, by a
+  // mask built here.  Issue order: the mask's and the salient list's loads, then the first
+  // row pair's x, so that the mask's wait (vmcnt counts in issue order) does not wait for x
+  // and the prologue runs under x's latency.
   const int zp0 = 64 * tid;
   // the salient mask of 64-position chunk c (bit i: amap[64 c + i] < 0, positions < K) is one
   // wave ballot over a coalesced dword per lane; wave w takes chunks w, w + NW, ... (at most
   // 16: K <= 16384, NW >= K / 1024) and parks the masks in LDS for their owner, thread c
   const int nzc = F8 == 0 && amap ? (K + 63) >> 6 : 0;
   uint32_t zraw[F8 == 0 ? 16 : 1];
-  if (F8 == 0) {
-    const int32_t* const am = amap ? amap : (const int32_t*)lctab;  // (NULL: loads unused)
+  if (F8 == 0 && amap) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const int p = 64 * (wave + NW * i) + lane;  // (clamped: an unconditional load)
-      zraw[i] = (uint32_t)am[min(p, K - 1)];
+      zraw[i] = (uint32_t)amap[min(p, K - 1)];
     }
   }
   // the salient list in two registers per thread (unconditional loads from a clamped index --
@@ -320,7 +345,7 @@ __device__ __forceinline__ void quant_lc_body(
   __builtin_amdgcn_sched_barrier(0);
   // (amap NULL: in-place output quantization, salient columns pass through: no mask)
   uint32_t* const zm_l = lc_buf + NOUT * (W + 8) + S_pad;  // [nzc] u64 masks
-  if (F8 == 0) {
+  if (F8 == 0 && amap) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const int c = wave + NW * i;
@@ -333,7 +358,7 @@ __device__ __forceinline__ void quant_lc_body(
     }
   }
 #ifdef SQMP_DIAG_BUILD
-  if (F8 == 0 && zraw[0] == 0x5A5A5A5Au) lc_buf[0] = 1u;  // (keeps the stamp behind the mask's loads)
+  if (F8 == 0 && amap && zraw[0] == 0x5A5A5A5Au) lc_buf[0] = 1u;  // (keeps the stamp behind the mask's loads)
 #endif
   LC_STAMP(7);
   const int RW = W + 8;  // LDS region stride (words; a multiple of 8)
@@ -375,26 +400,9 @@ __device__ __forceinline__ void quant_lc_body(
   for (; rp < rp_end; ++rp) {
     const int m0 = 2 * rp;
     const bool has1 = m0 + 1 < M;
-    // ---- this thread's RPL table entries (L1/L2-resident, padded to whole rounds with
-    // (W, W + 1) entries), issued first so their latency overlaps the interleave
-    uint32_t tab[RPL];
-    int toff = rb;
-    asm volatile("" : "+v"(toff));  // re-read per pair (no loop-invariant hoisting)
-#pragma unroll
-    for (int i = 0; i < RPL / 4; ++i) {
-      const u32x4 e = ((const u32x4*)(lctab + toff))[i];
-      tab[4 * i] = e[0]; tab[4 * i + 1] = e[1]; tab[4 * i + 2] = e[2]; tab[4 * i + 3] = e[3];
-    }
-    // the siblings' tables (same ranks, their packed positions)
-    uint32_t tabs[NOUT > 1 ? NOUT - 1 : 1][RPL];
-#pragma unroll
-    for (int o = 0; o + 1 < NOUT; ++o)
-#pragma unroll
-      for (int i = 0; i < RPL / 4; ++i) {
-        const u32x4 e = ((const u32x4*)(sib.tab[o] + toff))[i];
-        tabs[o][4 * i] = e[0]; tabs[o][4 * i + 1] = e[1];
-        tabs[o][4 * i + 2] = e[2]; tabs[o][4 * i + 3] = e[3];
-      }
+    // the table entries again for every later pair (the registers are not kept across
+    // pairs), issued first so their latency overlaps the interleave
+    if (rp != rp0) load_tab();
     // ---- interleave the two rows into LDS: word k = (x[m0][k], x[m0+1][k])
 #pragma unroll
     for (int i = 0; i < LC_CH; ++i) {
@@ -580,7 +588,7 @@ __device__ __forceinline__ void quant_lc_body(
     }
     // salient columns' own packed positions hold 0 (their weight codes are 0 too; the F8
     // position-order table gathers the zero word for them)
-    if (F8 == 0)
+    if (F8 == 0 && amap)
       for (uint64_t zm = zmask; zm; zm &= zm - 1) lc_buf[zp0 + __builtin_ctzll(zm)] = 0u;
     __syncthreads();
     if (rp == rp0) LC_STAMP(4);

@@ -4,7 +4,6 @@
 //                   group sizes that are a multiple of 32, or dense weights;
 //                   gemm_generic below for everything else (fp32, 8-bit codes, groups
 //                   of 8 / 16 elements): the round-1 register-staged 128 x 128 kernel.
-//   sqmp_gemm_i8 -> gemm_i8v2 (sqmp_gemm_fast.hip).
 #include <stdlib.h>
 
 #include <type_traits>
@@ -277,21 +276,6 @@ extern "C" int sqmp_gemm_fq_colmax(const void* a, const void* codes, const void*
     default: return n_bits == 4 ? SQMP_G(BF16, 4) : n_bits == 8 ? SQMP_G(BF16, 8) : SQMP_G(BF16, 0);
   }
 #undef SQMP_G
-}
-
-extern "C" int sqmp_gemm_i8(const int8_t* a8, const float* ascale, const void* xs,
-                            const void* codes, const void* wscale, const void* wsal,
-                            const void* bias, void* y, int dtype, int M, int N, int Kp,
-                            int S_pad, int Gw, int ngw, int n_bits, void* stream) {
-  SQMP_DEVICE_GUARD(stream);
-  int st = check_gemm_geometry(dtype, M, N, Kp, S_pad, Gw, ngw, n_bits);
-  if (st) return st;
-  if (dtype == SQMP_F32 || n_bits != 4 || Gw % 64 != 0) return SQMP_EUNSUPPORTED;
-  if (!a8 || !ascale || !codes || !wscale || !y || (S_pad > 0 && (!wsal || !xs)))
-    return SQMP_EINVAL;
-  if (M == 0) return SQMP_OK;
-  return launch_gemm_i8_fast(dtype, a8, ascale, xs, codes, wscale, wsal, bias, y, M, N, Kp,
-                             S_pad, Gw, ngw, (hipStream_t)stream);
 }
 
 extern "C" int sqmp_gemm_fqt(const void* acodes, const void* ascale, const void* xs,

@@ -8,7 +8,6 @@
 //   fp32 accumulation, one rounding to D.  Layout and schedule: the comment above the
 //   kernel; measurements: DESIGN.md §4.
 //
-// gemm_i8v2 -- per_token / per_tensor activations on the integer MFMA (see below).
 #include <stdlib.h>
 #include <string.h>
 
@@ -511,213 +510,6 @@ __global__ __launch_bounds__(512, 1) void gemm_fq6_kernel(
   }
 }
 
-// ================================================================= gemm_i8v2
-// per_token / per_tensor activations: int8 act codes x int4 weight codes on
-// v_mfma_i32_16x16x64_i8, per-weight-group fp32 fold, per-row act scale, salient tail on
-// the D MFMA into the same accumulators.  128 x 128 tile, 4 waves as 2 (M) x 2 (N), each
-// 64 x 64.  A stages hold 256 int8 codes (4 bpack blocks) per row: i8 sub-step t (one
-// 64-code block) reads chunk 4 t + q; the activation codes were written in the K order
-// that matches unpack_i8 of the bpack dword pair of lane group q.
-struct StageA256 {
-  uint32_t off, off_half, stride16;
-  __device__ inline void init(int m0, size_t lda_b, int wave, int lane) {
-    const int rin = 4 * wave + (lane >> 4);
-    const int c = (lane & 15) ^ (rin & 15);
-    off = (uint32_t)((size_t)(m0 + rin) * lda_b + (c << 4));
-    // a half stage (the last 64 salient columns when S_pad % 128 == 64): the upper 8
-    // chunks re-read the lower ones (in bounds; those sub-steps are skipped)
-    off_half = (uint32_t)((size_t)(m0 + rin) * lda_b + ((c & 7) << 4));
-    stride16 = (uint32_t)(16 * lda_b);
-  }
-  __device__ inline void issue(const unsigned char* base, unsigned char* st, int wave,
-                               bool half = false) const {
-    const uint32_t o = half ? off_half : off;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) glds16(base + (size_t)i * stride16 + o, st + (i * 4 + wave) * 1024);
-  }
-};
-
-__device__ inline const u32x4* a256_frag(const unsigned char* st, int row, int chunk) {
-  return (const u32x4*)(st + row * 256 + ((chunk ^ (row & 15)) << 4));
-}
-
-template <class DT>
-__global__ __launch_bounds__(256, 1) void gemm_i8v2_kernel(
-    const int8_t* __restrict__ A8, const float* __restrict__ ascale,
-    const typename DT::T* __restrict__ XS, const uint32_t* __restrict__ B4,
-    const typename DT::T* __restrict__ wscale, const typename DT::T* __restrict__ wsal,
-    const typename DT::T* __restrict__ bias, typename DT::T* __restrict__ Y, int M, int N,
-    int Kp, int S_pad, int Gw, int ngw, int tiles_m, int tiles_n) {
-  typedef typename DT::T T;
-  constexpr int ST = 32768;
-  __shared__ __attribute__((aligned(16))) unsigned char lds[2 * ST];
-
-  int tm, tn;
-  tile_coords(tiles_m, tiles_n, 8, tm, tn);
-  const int m0 = tm * 128, n0 = tn * 128;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 1, wn = wave & 1;
-  const int r16 = lane & 15, q = lane >> 4;
-  const int nkm = (Kp + 255) / 256;    // 256-code stages (the last may be partial)
-  const int nks = (S_pad + 127) / 128;  // 128-element salient stages (the last may be 64)
-  const bool tail_half = (S_pad & 127) != 0;
-  const int nblk = Kp / 64;
-  const int Np = pad_n(N);
-
-  int nrow[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) nrow[j] = min(n0 + wn * 64 + j * 16 + r16, N - 1);
-
-  f32x4 tot[4][4];
-  i32x4 acc[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      tot[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-      acc[i][j] = i32x4{0, 0, 0, 0};
-    }
-
-  const size_t brow_dw = (size_t)Kp / 8;
-  uint2 bc[4][4], bn[4][4];
-  auto load_codes = [&](int ks, uint2 (&b)[4][4]) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const int blk = min(ks * 4 + t, nblk - 1);
-        b[j][t] = *(const uint2*)(B4 + (size_t)nrow[j] * brow_dw + (size_t)blk * 8 + 4 * (q & 1) + 2 * (q >> 1));
-      }
-  };
-  auto fold = [&](int g) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int nb = n0 + wn * 64 + j * 16 + q * 4;
-      float s[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) s[r] = DT::to_f(wscale[(size_t)g * Np + min(nb + r, N - 1)]);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) tot[i][j][r] += (float)acc[i][j][r] * s[r];
-        acc[i][j] = i32x4{0, 0, 0, 0};
-      }
-    }
-  };
-  auto compute_codes = [&](int ks, const unsigned char* st, const uint2 (&b)[4][4]) {
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const int p_end = ks * 256 + (t + 1) * 64;
-      if (p_end > Kp) break;  // partial last stage
-      u32x4 bf[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        uint32_t l0, h0, l1, h1;
-        unpack_i8(b[j][t].x, l0, h0);
-        unpack_i8(b[j][t].y, l1, h1);
-        bf[j] = u32x4{l0, h0, l1, h1};
-      }
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const u32x4 af = *a256_frag(st, wm * 64 + i * 16 + r16, 4 * t + q);
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(*(const i32x4*)&bf[j], *(const i32x4*)&af, acc[i][j], 0, 0, 0);
-      }
-      if (p_end % Gw == 0 && p_end / Gw <= ngw) fold(p_end / Gw - 1);
-    }
-  };
-
-  const int lda8 = nkm * 256;
-  StageA256 sa;
-  sa.init(m0, (size_t)lda8, wave, lane);
-  const unsigned char* Ab = (const unsigned char*)A8;
-  if (nkm > 0) {
-    sa.issue(Ab, lds, wave);
-    load_codes(0, bc);
-    __syncthreads();
-    for (int ks = 0; ks < nkm; ++ks) {
-      const int cur = ks & 1;
-      if (ks + 1 < nkm) {
-        sa.issue(Ab + (size_t)(ks + 1) * 256, lds + (cur ^ 1) * ST, wave);
-        load_codes(ks + 1, bn);
-      }
-      compute_codes(ks, lds + cur * ST, bc);
-      if (ks + 1 < nkm) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-          for (int t = 0; t < 4; ++t) bc[j][t] = bn[j][t];
-      }
-      __syncthreads();
-    }
-  }
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int gm = min(m0 + wm * 64 + i * 16 + r16, M - 1);
-    const float s = ascale[gm];
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) tot[i][j][r] *= s;
-  }
-  if (nks > 0) {
-    StageA256 sx;
-    sx.init(m0, (size_t)S_pad * sizeof(T), wave, lane);
-    const unsigned char* Xb = (const unsigned char*)XS;
-    sx.issue(Xb, lds, wave, tail_half && nks == 1);
-    __syncthreads();
-    for (int ks = 0; ks < nks; ++ks) {
-      const int cur = ks & 1;
-      if (ks + 1 < nks)
-        sx.issue(Xb + (size_t)(ks + 1) * 128 * sizeof(T), lds + (cur ^ 1) * ST, wave,
-                 tail_half && ks + 2 == nks);
-      const unsigned char* st = lds + cur * ST;
-      const int nsub = tail_half && ks + 1 == nks ? 2 : 4;
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        if (s >= nsub) break;
-        u32x4 bf[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          bf[j] = *(const u32x4*)(wsal + (size_t)nrow[j] * S_pad + ks * 128 + 32 * s + 8 * q);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const u32x4 af = *a256_frag(st, wm * 64 + i * 16 + r16, 4 * s + q);
-#pragma unroll
-          for (int j = 0; j < 4; ++j) Mfma<DT>::run(tot[i][j], bf[j], af);
-        }
-      }
-      __syncthreads();
-    }
-  }
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int nb = n0 + wn * 64 + j * 16 + q * 4;
-    if (nb >= N) continue;
-    float bv[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) bv[r] = (bias && nb + r < N) ? DT::to_f(bias[nb + r]) : 0.f;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int gm = m0 + wm * 64 + i * 16 + r16;
-      if (gm >= M) continue;
-      T v[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = DT::from_f(tot[i][j][r] + bv[r]);
-      T* dst = Y + (size_t)gm * N + nb;
-      if (nb + 4 <= N && (N & 3) == 0) {
-        *(uint2*)dst = *(const uint2*)v;
-      } else {
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          if (nb + r < N) dst[r] = v[r];
-      }
-    }
-  }
-}
-
 // ================================================================= launchers
 // M-tiles per raster group (tile_coords): SQMP_GROUP_M overrides (A/B tuning knob; 4 and
 // 8 measured equal at config 2, 1 and 2 0.5-1 % slower)
@@ -793,28 +585,6 @@ int launch_gemm_fqt(int dtype, const void* acodes, const void* ascale, const voi
   if (dtype == SQMP_BF16)
     return fqt_dispatch<BF16>(acodes, ascale, xs, wp, bias, y, M, N, Kq, S_pad, G, ngq, s);
   return SQMP_EUNSUPPORTED;
-}
-
-int launch_gemm_i8_fast(int dtype, const int8_t* a8, const float* ascale, const void* xs,
-                        const void* codes, const void* wscale, const void* wsal,
-                        const void* bias, void* y, int M, int N, int Kp, int S_pad, int Gw,
-                        int ngw, hipStream_t s) {
-  const int tiles_m = cdiv(M, 128), tiles_n = cdiv(N, 128);
-  if (dtype == SQMP_F16) {
-    gemm_i8v2_kernel<F16><<<dim3(tiles_m * tiles_n), dim3(256), 0, s>>>(
-        a8, ascale, (const _Float16*)xs, (const uint32_t*)codes, (const _Float16*)wscale,
-        (const _Float16*)wsal, (const _Float16*)bias, (_Float16*)y, M, N, Kp, S_pad, Gw, ngw,
-        tiles_m, tiles_n);
-  } else if (dtype == SQMP_BF16) {
-    gemm_i8v2_kernel<BF16><<<dim3(tiles_m * tiles_n), dim3(256), 0, s>>>(
-        a8, ascale, (const __bf16*)xs, (const uint32_t*)codes, (const __bf16*)wscale,
-        (const __bf16*)wsal, (const __bf16*)bias, (__bf16*)y, M, N, Kp, S_pad, Gw, ngw,
-        tiles_m, tiles_n);
-  } else {
-    return SQMP_EUNSUPPORTED;
-  }
-  SQMP_LAUNCH_CHECK();
-  return SQMP_OK;
 }
 
 }  // namespace sqmp

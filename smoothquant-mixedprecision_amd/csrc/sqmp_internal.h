@@ -147,9 +147,5 @@ int launch_gemm_fq_fast(int dtype, const void* a, const void* codes, const void*
 int launch_gemm_fqt(int dtype, const void* acodes, const void* ascale, const void* xs,
                     const void* wp, const void* bias, void* y, int M, int N, int Kq, int S_pad,
                     int G, int ngq, hipStream_t s);
-int launch_gemm_i8_fast(int dtype, const int8_t* a8, const float* ascale, const void* xs,
-                        const void* codes, const void* wscale, const void* wsal,
-                        const void* bias, void* y, int M, int N, int Kp, int S_pad, int Gw,
-                        int ngw, hipStream_t s);
 
 }  // namespace sqmp

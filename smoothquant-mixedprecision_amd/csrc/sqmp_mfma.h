@@ -115,13 +115,6 @@ template <> struct Dec<BF16> {
   }
 };
 
-// int4 bpack dword -> two int8 dwords, byte order (e0,e4,e1,e5) and (e2,e6,e3,e7); the
-// i8 activation operand is written in the matching K order (sqmp_actquant.hip).
-__device__ inline void unpack_i8(uint32_t w, uint32_t& lo, uint32_t& hi) {
-  lo = ((w & 0x0F0F0F0Fu) + 0x78787878u) ^ 0x80808080u;
-  hi = (((w >> 4) & 0x0F0F0F0Fu) + 0x78787878u) ^ 0x80808080u;
-}
-
 // 16-B non-temporal (streaming) global store.  From inline asm: hipcc merges the two arms of
 // `if (nt) __builtin_nontemporal_store(v, p); else *p = v;` into one plain store.
 __device__ inline void store16_nt(void* p, const u32x4& v) {

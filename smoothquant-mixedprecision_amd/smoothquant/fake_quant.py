@@ -203,11 +203,9 @@ class W4A4Linear(nn.Module):
     """Mixed-precision W4A4 linear: salient input channels in D, the rest int4/int8.
 
     Forward kernels (chosen per layer, see `kernel`; "auto" = "f8" where ops.f8_auto (fp16),
-    "fqt" for large sorted per_group batches, else "fq" unless ops.I8_AUTO):
+    "fqt" for large sorted per_group batches, else "fq"):
       "f8"  per_token / per_tensor 4-bit activations: e4m3 act codes x e4m3 weight codes on
             the block-scaled FP8 MFMA (exact integer block sums), per-group fp32 folds.
-      "i8"  per_token / per_tensor activations: int8 act codes x int4 weight codes on the
-            i8 MFMA with per-group fp32 folds (exact scale factorisation).
       "fq"  every act mode: dequantized activations x in-kernel-decoded weights on the D
             MFMA (bit-exact operands; the reference's numerics up to accumulation order).
       "fqt" per_group activations (auto from ops.FQT_MIN_ROWS rows, ops.fqt_eligible): "fq"
@@ -518,20 +516,15 @@ class W4A4Linear(nn.Module):
                                "to the input's device")
         use_f8 = self.kernel == "f8" or (
             self.kernel == "auto" and ops.f8_auto(pw, amode, bits) and ops.f8_input_ok(xc))
-        use_i8 = not use_f8 and (
-            self.kernel == "i8" or
-            (self.kernel == "auto" and ops.I8_AUTO and ops.i8_eligible(pw, amode, bits)))
-        use_fqt = (not use_f8 and not use_i8 and self.kernel in ("auto", "fqt")
+        use_fqt = (not use_f8 and self.kernel in ("auto", "fqt")
                    and ops.fqt_eligible(pw, amode, bits, ag, x2.shape[0],
                                         force=self.kernel == "fqt")
                    and ops.f8_input_ok(xc))
         # fp32 layers: the quantizer writes sqmp_gemm_h2d's two f16 planes itself
-        use_h2 = (not use_f8 and not use_i8 and not use_fqt and self.kernel == "auto"
+        use_h2 = (not use_f8 and not use_fqt and self.kernel == "auto"
                   and ops.h2_planes_ok(pw, amode, x2.shape[0], ag))
         if use_f8:
             a8, sa, xs = ops.quant_act_f8(xc, pw, amode, bits)
-        elif use_i8:
-            a8, sa, xs = ops.quant_act_i8(xc, pw, amode, bits)
         elif use_fqt:
             c4 = ops.quant_act_c4(xc, pw, amode, bits, ag, stats_of=x)
         elif use_h2:
@@ -548,15 +541,12 @@ class W4A4Linear(nn.Module):
         # per_group (sorted) / per_tensor the faithful GEMM also writes the column maxima of
         # y into the output quantizer's workspace, which then skips its statistics pass
         fuse = (ospec is not None and ospec[0] in ("per_group", "per_tensor") and _OQ_FUSE
-                and not use_i8
                 and (not use_f8 or ops.f8_colmax_ok(pw))       # the 16x16x128 FP8 kernel
                 and (not use_fqt or c4[1].dim() == 3)          # the tile-major fqt7 GEMM
                 and (self.salient_indices is None or pw.K - pw.S > 0))
         colmax = ops.out_quant_workspace(x2.shape[0], pw.N, x2.device)["buf"] if fuse else None
         if use_f8:
             y = ops.gemm_f8(a8, sa, xs, pw, bias, colmax=colmax)
-        elif use_i8:
-            y = ops.gemm_i8(a8, sa, xs, pw, bias)
         elif use_fqt:
             y = ops.gemm_fqt(*c4, pw, bias, ag, colmax=colmax)
         elif use_h2:

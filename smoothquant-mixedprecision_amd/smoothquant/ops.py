@@ -584,23 +584,6 @@ def gemm_fqt(codes: torch.Tensor, scales: torch.Tensor, xs: torch.Tensor, wp: to
     return y
 
 
-def quant_act_i8(x2: torch.Tensor, pw: PackedWeight, act_quant: str, n_bits: int):
-    """x [M, K] -> (int8 codes [M, roundup(Kp, 256)] in the i8 GEMM's K order, fp32
-    scales [M], exact salient x [M, S_pad])."""
-    _require_gpu(x2, "quant_act")
-    M, K = x2.shape
-    Mp = _pad_rows(M)
-    a8 = torch.empty((Mp, (pw.Kp + 255) // 256 * 256), dtype=torch.int8, device=x2.device)[:M]
-    sa = torch.empty((M,), dtype=torch.float32, device=x2.device)
-    xs = torch.empty((Mp, pw.S_pad), dtype=x2.dtype, device=x2.device)[:M]
-    ws, nb = _act_workspace(M, K, pw.Kp, x2.device)
-    check(load().sqmp_quant_act(_p(x2), _dtype_code(x2.dtype), M, K, ACT_MODES[act_quant], n_bits,
-                                0, _p(pw.amap), pw.Kp, _p(pw.nonsal), _p(pw.salient), pw.S,
-                                pw.S_pad, _lib.OUT_I8, _p(a8), _p(sa), _p(xs) if pw.S_pad else None,
-                                _p(ws), nb, _stream(x2)), "quant_act")
-    return a8, sa, xs
-
-
 def out_quant_workspace(M: int, C: int, device):
     """The persistent workspace fake_quant_inplace uses for an [M, C] tensor on the current
     stream (its first C words: the column-maximum region sqmp_gemm_fq_colmax fills)."""
@@ -827,17 +810,6 @@ def gemm_fq(a: torch.Tensor, pw: PackedWeight, bias: Optional[torch.Tensor],
     return y
 
 
-def gemm_i8(a8: torch.Tensor, sa: torch.Tensor, xs: torch.Tensor, pw: PackedWeight,
-            bias: Optional[torch.Tensor]) -> torch.Tensor:
-    M = a8.shape[0]
-    y = torch.empty((M, pw.N), dtype=pw.dtype, device=a8.device)
-    check(load().sqmp_gemm_i8(_p(a8), _p(sa), _p(xs) if pw.S_pad else None, _p(pw.codes),
-                              _p(pw.wscale), _p(pw.wsal) if pw.S_pad else None, _p(bias), _p(y),
-                              _dtype_code(pw.dtype), M, pw.N, pw.Kp, pw.S_pad, pw.Gw, pw.ngw,
-                              pw.n_bits, _stream(a8)), "gemm_i8")
-    return y
-
-
 def _ws32(pw: PackedWeight) -> torch.Tensor:
     """fp32 [ngw, Np] weight scales of the f8 GEMM, built once per packed weight."""
     if pw.ws32 is None:
@@ -925,9 +897,6 @@ def f8_input_ok(x2: torch.Tensor) -> bool:
     return x2.is_contiguous() and x2.data_ptr() % 16 == 0
 
 
-# Whether W4A4Linear(kernel="auto") takes the integer path for eligible layers.  Off: on
-# gfx950 the faithful fq GEMM is currently faster than gemm_i8 (perf log).
-I8_AUTO = False
 # Whether kernel="auto" takes the FP8 path for eligible layers (f8_eligible): on gfx950
 # it is 1.4x the fq GEMM at config 2.
 F8_AUTO = True
@@ -945,7 +914,3 @@ def f8_auto(pw: PackedWeight, act_quant: str, act_bits: int) -> bool:
     return F8_AUTO and pw.dtype == torch.float16 and f8_eligible(pw, act_quant, act_bits)
 
 
-def i8_eligible(pw: PackedWeight, act_quant: str, act_bits: int) -> bool:
-    """Whether the integer MFMA path computes this layer (exact-scale factorisation)."""
-    return (act_quant in ("per_token", "per_tensor") and pw.dtype != torch.float32
-            and pw.n_bits == 4 and pw.dense is None and pw.Gw % 64 == 0 and act_bits <= 8)

@@ -73,7 +73,7 @@ def test_workspace_queries(lib):
 def test_invalid_arguments_rejected_without_gpu(lib):
     # argument validation happens before any HIP call
     assert lib.sqmp_gemm_fq(None, None, None, None, None, None, 1, 16, 16, 100, 0, 32, 4, 4, None) == -1
-    assert lib.sqmp_gemm_i8(None, None, None, None, None, None, None, None, 0, 16, 16, 128, 0, 64, 2, 4, None) == -2
+    assert lib.sqmp_gemm_f8(None, None, None, None, None, None, None, None, 0, 16, 16, 128, 0, 64, 2, None) == -1
     assert lib.sqmp_quant_act(None, 1, 4, 64, 9, 4, 32, None, 128, None, None, 0, 0, 0, None, None, None, None, 0, None) == -1
     assert lib.sqmp_pack_weight(None, 1, 4, 64, 2, 3, 32, None, 0, None, None, None, None, None, None, None, None, 0, None) == -2
 

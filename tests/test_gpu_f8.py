@@ -4,7 +4,7 @@
   the oracle's q_x BIT-EXACT at every non-salient column, 0 at salient and padding
   positions; the exact salient columns land in xs unchanged.
 * y: relative Frobenius error vs the oracle product within the integer-path tolerance of
-  test_gpu_parity (TOL_I8: the scales are factored out of the sum)."""
+  test_gpu_parity (TOL_F8: the scales are factored out of the sum)."""
 import zlib
 
 import numpy as np
@@ -12,7 +12,7 @@ import pytest
 import torch
 
 from oracle import fake_quant_oracle as O
-from test_gpu_parity import TOL_I8, TORCH_DT, _dev, _rand_inputs, bits_equal, make_layer, rel, to_np, to_t
+from test_gpu_parity import TOL_F8, TORCH_DT, _dev, _rand_inputs, bits_equal, make_layer, rel, to_np, to_t
 
 pytestmark = pytest.mark.gpu
 
@@ -92,7 +92,7 @@ def test_f8_gemm_vs_oracle(case):
     want = D.f32(O.linear(qx, w_hat, b, D))
     q.kernel = "f8"
     y = to_np(q(to_t(x, dt, dev)))
-    assert rel(y, want) < TOL_I8[dt], rel(y, want)
+    assert rel(y, want) < TOL_F8[dt], rel(y, want)
 
 
 @torch.no_grad()
@@ -124,7 +124,7 @@ def test_f8_full_size_config2_per_token():
     b_full = torch.cat([ops.dequant_weight_packed(pw), pw.wsal], dim=1)
     ref = torch.addmm(lin.bias.double(), a.double(), b_full.double().t())
     r = float((y.double() - ref).norm() / ref.norm())
-    assert r < TOL_I8["fp16"], r
+    assert r < TOL_F8["fp16"], r
     a8, sa, _ = ops.quant_act_f8(x, pw, "per_token", 4)
     rows = torch.arange(0, M, 509, device=dev)
     codes = torch.from_numpy(e4m3_to_float(a8[rows].cpu().numpy()))

@@ -5,7 +5,7 @@ Tolerances (stated once, used everywhere):
   * y: relative Frobenius error vs the oracle's fp64-accumulated product, which differs
     from any fp32-accumulating GEMM only by accumulation order:
         fp32 1e-5, fp16 2e-3, bf16 1e-2            (faithful "fq" kernel)
-    The integer "i8" and "f8" kernels factor the scales out of the sum, so each product
+    The "f8" kernel (e4m3 codes) factors the scales out of the sum, so each product
     differs by the D rounding of x_hat and W_hat (<= 2^-11 rel for fp16, 2^-8 for bf16):
         fp16 3e-3, bf16 2e-2.
 """
@@ -22,7 +22,7 @@ pytestmark = pytest.mark.gpu
 
 TORCH_DT = {"fp32": torch.float32, "fp16": torch.float16, "bf16": torch.bfloat16}
 TOL_FQ = {"fp32": 1e-5, "fp16": 2e-3, "bf16": 1e-2}
-TOL_I8 = {"fp16": 3e-3, "bf16": 2e-2}
+TOL_F8 = {"fp16": 3e-3, "bf16": 2e-2}
 
 G = Golden()
 
@@ -123,14 +123,14 @@ def test_golden_layer(m):
     assert bits_equal(a_operand_to_original(q, a, K), G.arr(key + "_qx", dt))
     # forward
     kernels = ["fq"]
-    if ops.i8_eligible(q.packed(), m["act_quant"], m["n_bits"]):
-        kernels.append("i8")
+    if ops.f8_eligible(q.packed(), m["act_quant"], m["n_bits"]):
+        kernels.append("f8")
     want = G.arr(key + "_y", dt)
     for kern in kernels:
         q.kernel = kern
         y = q(xt.clone())
         assert tuple(y.shape) == tuple(want.shape)
-        tol = TOL_FQ[dt] if kern == "fq" else TOL_I8[dt]
+        tol = TOL_FQ[dt] if kern == "fq" else TOL_F8[dt]
         if m["quantize_output"]:
             tol = tol * 10 + 1e-6
         assert rel(to_np(y), want) < tol, (kern, rel(to_np(y), want))
@@ -190,12 +190,11 @@ def test_oracle_parity(case):
     a = ops.quant_act_fp(xt, q.packed(), aq, bits, Gs)
     assert bits_equal(a_operand_to_original(q, a, K), D.f32(qx))
     want = O.linear(qx, w_hat, b, D)
-    kernels = (["fq"] + (["i8"] if ops.i8_eligible(q.packed(), aq, bits) else [])
-               + (["f8"] if ops.f8_eligible(q.packed(), aq, bits) else []))
+    kernels = ["fq"] + (["f8"] if ops.f8_eligible(q.packed(), aq, bits) else [])
     for kern in kernels:
         q.kernel = kern
         y = q(xt.clone())
-        tol = TOL_FQ[dt] if kern == "fq" else TOL_I8[dt]
+        tol = TOL_FQ[dt] if kern == "fq" else TOL_F8[dt]
         assert rel(to_np(y), D.f32(want)) < tol, (kern, rel(to_np(y), D.f32(want)))
 
 

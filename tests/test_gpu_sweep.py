@@ -120,7 +120,8 @@ def test_mean3std_sort_vs_oracle(dtn, G):
 
 
 def test_w4a8_per_token_both_kernels():
-    """W4A8 with per-token activations: rebinding reaches the integer path too."""
+    """W4A8 with per-token activations: the rebinding reaches the faithful kernel (forced
+    and auto; 8-bit codes are not exact in e4m3, so auto never takes the FP8 path)."""
     dev = _dev()
     from smoothquant import fake_quant as FQ
     dt = O.DT("fp16")
@@ -136,7 +137,7 @@ def test_w4a8_per_token_both_kernels():
     sal = O.select_salient(imp, 0.1)
     w_hat = O.w4a4_from_float(W, "per_group", 4, G, sal, dt)
     want = O.w4a4_forward(x, w_hat, None, "per_token", 4, G, sal, False, dt, act_bits=8)
-    for kern, tol in (("fq", 2e-3), ("i8", 3e-3)):
+    for kern, tol in (("fq", 2e-3), ("auto", 2e-3)):
         q.kernel = kern
         y = to_np(q(to_t(x, "fp16", dev)))
         assert rel(y, want) < tol, kern

@@ -1,5 +1,5 @@
 """Run only the W4A4 GEMM (and optionally the prepass) of BASELINE config 2 -- a target
-for rocprofv3 counter passes.  python tools/gemm_only.py [fq|fqt|i8|f8|h2|c4] [iters] [per_group|per_token] [prepass]
+for rocprofv3 counter passes.  python tools/gemm_only.py [fq|fqt|f8|h2|c4] [iters] [per_group|per_token] [prepass]
 (c4: the activation-order prepass alone -- column max, rank table, fused quantizer + permutation)"""
 import os
 import sys
@@ -50,10 +50,6 @@ elif kind == "f8":
             ops.quant_act_f8(x, pw, act, 4)
         ops.gemm_f8(a8, sa, xs, pw, lin.bias)
 else:
-    a8, sa, xs = ops.quant_act_i8(x, pw, act, 4)
-    for _ in range(iters):
-        if prepass:
-            ops.quant_act_i8(x, pw, act, 4)
-        ops.gemm_i8(a8, sa, xs, pw, lin.bias)
+    raise SystemExit(f"unknown kind {kind}")
 torch.cuda.synchronize()
 print("done", kind, iters)

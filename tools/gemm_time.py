@@ -1,5 +1,5 @@
 """Time the W4A4 GEMM alone on BASELINE config 2 (HIP events, GEMM on torch's current
-stream).  python tools/gemm_time.py [fq|fq7|fqt|i8|f8] [iters]  -> one line: kind, avg ms, TFLOP/s."""
+stream).  python tools/gemm_time.py [fq|fq7|fqt|f8] [iters]  -> one line: kind, avg ms, TFLOP/s."""
 import os
 import sys
 
@@ -30,8 +30,7 @@ elif kind == "f8":
     a8, sa, xs = ops.quant_act_f8(x, pw, act, 4)
     run = lambda: ops.gemm_f8(a8, sa, xs, pw, lin.bias)  # noqa: E731
 else:
-    a8, sa, xs = ops.quant_act_i8(x, pw, act, 4)
-    run = lambda: ops.gemm_i8(a8, sa, xs, pw, lin.bias)  # noqa: E731
+    raise SystemExit(f"unknown kind {kind}")
 t_end = __import__("time").perf_counter() + 2.0  # settle the clock
 while __import__("time").perf_counter() < t_end:
     for _ in range(10):
