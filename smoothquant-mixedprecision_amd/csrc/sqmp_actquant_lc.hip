@@ -290,8 +290,10 @@ __device__ __forceinline__ void quant_lc_body(
   int rp = (int)((long)wg * npair / nblk);
 
   // ---- this thread's RPL table entries (L1/L2-resident, padded to whole rounds with pad
-  // entries), the same for every row pair: the first pair's are loaded here, first, so that
-  // their round trip overlaps x's instead of following the prologue
+  // entries), the same for every row pair: for the OUT_FP outputs the first pair's are loaded
+  // here, first, so that their round trip overlaps x's instead of following the prologue
+  // (the F8 / C4 outputs load them per pair: held through the prologue they cost those
+  // kernels 16 VGPRs and a wave per SIMD)
   uint32_t tab[RPL];
   uint32_t tabs[NOUT > 1 ? NOUT - 1 : 1][RPL];  // the siblings' tables (same ranks, their positions)
   auto load_tab = [&]() {
@@ -311,7 +313,7 @@ __device__ __forceinline__ void quant_lc_body(
         tabs[o][4 * i + 2] = e[2]; tabs[o][4 * i + 3] = e[3];
       }
   };
-  load_tab();
+  if (F8 == 0) load_tab();
 
   // ---- once per workgroup: zeroed buffer (+ two spare words: W = a zero read by padding
   // table entries, W + 1 = a write-only sink for their scatter).  The salient positions of
@@ -402,7 +404,7 @@ __device__ __forceinline__ void quant_lc_body(
     const bool has1 = m0 + 1 < M;
     // the table entries again for every later pair (the registers are not kept across
     // pairs), issued first so their latency overlaps the interleave
-    if (rp != rp0) load_tab();
+    if (F8 != 0 || rp != rp0) load_tab();
     // ---- interleave the two rows into LDS: word k = (x[m0][k], x[m0+1][k])
 #pragma unroll
     for (int i = 0; i < LC_CH; ++i) {

@@ -33,12 +33,20 @@ def parse(path):
     passes = [p for p in passes if p]
     last = passes[-1]
     t0, prev_end, busy = last[0][0], last[0][0], 0
-    for s, e, n in last:
+    # the median duration of each launch position over the passes of the same shape (the
+    # first few passes warm the clock and the caches: the second half only)
+    full = [p for p in passes if len(p) == len(last)]
+    full = full[len(full) // 2:]
+    med = [sorted((p[i][1] - p[i][0]) for p in full)[len(full) // 2] for i in range(len(last))]
+    for i, (s, e, n) in enumerate(last):
         short = n.split("(")[0].replace("void ", "")[:70]
-        print(f"{(s - t0) / 1e3:8.1f} us  gap {(s - prev_end) / 1e3:5.1f}  dur {(e - s) / 1e3:6.1f}  {short}")
+        print(f"{(s - t0) / 1e3:8.1f} us  gap {(s - prev_end) / 1e3:5.1f}  dur {(e - s) / 1e3:6.1f}  "
+              f"median {med[i] / 1e3:6.1f}  {short}")
         prev_end, busy = e, busy + (e - s)
+    nongemm = sum(m for m, (_, _, n) in zip(med, last) if "gemm" not in n)
     print(f"pass: {(last[-1][1] - t0) / 1e3:.1f} us, kernels {busy / 1e3:.1f} us, "
-          f"{len(last)} launches ({len(passes)} passes in the trace)")
+          f"{len(last)} launches ({len(passes)} passes in the trace); medians over {len(full)} "
+          f"passes: kernels {sum(med) / 1e3:.1f} us, non-GEMM {nongemm / 1e3:.1f} us")
 
 
 def run(passes):
