@@ -1024,7 +1024,7 @@ static int launch_rank_table(const uint32_t* key, const int32_t* nonsal, int L,
   const int grid = cdiv((long)L * tpo, 256L * r);
   // every column's key staged by coalesced loads, the salient ones masked (rank_stage_dense;
   // default: down_proj's packed-order prepass 49.9 -> 47.7 us, config-2 C4 prepass 73.0 ->
-  // 72.0 us, profiles/r05_ab_rank_dense.txt); SQMP_RT_DENSE=0: the list gather (A/B)
+  // 72.0 us, profiles/r06_ab_rank_dense.txt); SQMP_RT_DENSE=0: the list gather (A/B)
   const char* de = knob("SQMP_RT_DENSE");
   if (!(de && atoi(de) == 0) && K > 0 && K <= RT_MAX && K % 4 == 0 && (S == 0 || sal)) {
     // owners are the K columns (rank_owner_ents<R, true>)

@@ -131,30 +131,52 @@ struct Fq7Grp {
   int n;
 };
 
-// Stream-K schedule (OPT bit 5, value 32; packed order, 256-row tiles): a persistent grid of
-// `nwg` workgroups (one per CU) walks the tiles in raster order, the K loop of every tile cut
-// into 64-position stage PAIRS (the unit of the unrolled codes loop) with the salient tail on
-// the tile's last pair.  Workgroup w takes the pair range [total w / nwg, total (w + 1) / nwg),
-// each end moved to a pair boundary with at least one codes pair on either side (a cut in the
-// tail moves to the tile's end): every workgroup does the same work up to one pair, so a grid
-// of tiles that is not a whole number of rounds of the CUs (Llama-2-7B gate/up at 2048 tokens:
-// 688 tiles = 2.69 rounds) no longer idles most CUs through a last partial round.  A tile cut
-// at boundary b is finished by whichever of its two workgroups arrives second: workgroup b + 1
-// runs the tile's SECOND part first (its range starts there) and workgroup b the FIRST part
-// last, so the second part normally stores its fp32 partial tile (write-through, sc1) into slot
-// A of boundary b and counts itself on the boundary's flag; the first part polls the flag, adds
-// the partial, runs the epilogue and clears the flag.  Should the first part arrive before the
-// partial (never waiting), it stores its own partial into slot B and counts itself instead, and
-// the second part's add then finds it and finishes the tile (MI355X_MICROARCH.md hand-off rule:
-// sc1 stores, every storing wave's vmcnt(0), a workgroup barrier, one lane's agent-scope add;
-// the workgroup whose add or poll saw the other's count loads with sc1 loads after a barrier).
-// A cut tile's output adds two fp32 partial sums: within fp32 rounding of the unsplit kernel's.
+// Stream-K schedule (OPT bit 5, value 32; packed order, 256-row tiles): data-parallel rounds
+// plus a stream-K stretch over the rest (the Stream-K paper's hybrid).  A persistent grid of
+// `nwg` workgroups (one per CU): with T = q nwg + r tiles (0 < r < nwg, q >= 1), workgroup w
+// (XCD-contiguous logical index) first runs the whole tiles k nwg + w, k < q - 1 -- round by
+// round, so the workgroups of one XCD work on neighbouring raster tiles as in the plain grid --
+// then an equal share of the last nwg + r tiles' K loops: those tiles' 64-position stage PAIRS
+// (the unit of the unrolled codes loop; the salient tail rides on the tile's last pair) in
+// raster order, workgroup w taking [R P w / nwg, R P (w + 1) / nwg), R = nwg + r, each end moved
+// to a pair boundary with at least one codes pair on either side (a cut in the tail moves to
+// the tile's end).  A share of at least one tile cuts every tile into at most two parts.  A grid that is not a whole number of rounds of the CUs (Llama-2-7B gate/up at 2048
+// tokens: 688 tiles = 2.69 rounds) then no longer idles most CUs through a last partial round.
+// A remainder tile cut at boundary b is finished by whichever of its two workgroups arrives
+// second: workgroup b + 1 runs the tile's SECOND part first (its share starts there) and
+// workgroup b the FIRST part last, so the second part normally stores its fp32 partial tile
+// (write-through, sc1) into slot A of boundary b and counts itself on the boundary's flag; the
+// first part polls the flag, adds the partial in its epilogue and clears the flag.  Should the
+// first part arrive before the partial (never waiting), it stores its own partial into slot B
+// and counts itself instead, and the second part's add then finds it and finishes the tile
+// (MI355X_MICROARCH.md hand-off rule: sc1 stores, every storing wave's vmcnt(0), a workgroup
+// barrier, one lane's agent-scope add; the workgroup whose add or poll saw the other's count
+// loads with sc1 loads after a barrier).  A cut tile's output adds two fp32 partial sums:
+// within fp32 rounding of the unsplit kernel's.
 struct Fq7Sk {
   float* part;      // 2 slots of TM x TN fp32 per boundary (A: second part, B: first part)
   uint32_t* flag;   // one arrival count per boundary, zero between launches
   int nwg;          // the persistent grid
   int tiles;        // tiles in the flattened raster order
 };
+
+// Timing stamps of the stream-K kernel (SQMP_DIAG_BUILD only): per logical workgroup and
+// segment s < 4, the 100-MHz real-time counter at the segment's start, after its K loop, after
+// the hand-off and at its end ([4 s + 0..3]); the segment's role in sqmp_sk_roles
+// (tools/sk_stamps.py)
+#ifdef SQMP_DIAG_BUILD
+__device__ unsigned long long sqmp_sk_stamps[512][16];
+__device__ int sqmp_sk_roles[512][4];
+#define SK_STAMP(k)                                                                     \
+  do {                                                                                  \
+    if (SK && threadIdx.x == 0 && sk_seg < 4 && sk_w < 512)                             \
+      sqmp_sk_stamps[sk_w][4 * sk_seg + (k)] = __builtin_amdgcn_s_memrealtime();        \
+  } while (0)
+#else
+#define SK_STAMP(k) \
+  do {              \
+  } while (0)
+#endif
 
 // a pair index moved to the nearest legal cut: inside a tile only after >= 1 and before >= 1
 // codes pair; a cut at or past the last codes pair's end (in the salient tail) moves to the
@@ -255,18 +277,27 @@ __global__ __launch_bounds__((OPT & 16) ? 1024 : 512, ((OPT & 8) && !(OPT & 16))
     const int bid = blockIdx.x, xcd = bid & 7, q8 = n >> 3, r8 = n & 7;
     return (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
   };
-  // stream-K: this workgroup's pair range [sk_u, sk_end) of the flattened (tile, pair) order
+  // stream-K: this workgroup's whole tiles k nwg + w (k < sk_q), then its pair range
+  // [sk_u, sk_end) of the remainder tiles' flattened (tile, pair) order
   const int sk_pc = Kp / 128, sk_pt = sk_pc + (S_pad / 64 + 1) / 2;
-  int sk_w = 0, sk_u = 0, sk_end = 0;
+  int sk_w = 0, sk_u = 0, sk_end = 0, sk_k = 0, sk_q = 0, sk_seg = -1;
   if constexpr (SK) {
     sk_w = xcd_remap(sk.nwg);
-    const long total = (long)sk.tiles * sk_pt;
-    sk_u = sk_snap(total * sk_w / sk.nwg, sk_pc, sk_pt);
-    sk_end = sk_snap(total * (sk_w + 1) / sk.nwg, sk_pc, sk_pt);
+    sk_q = sk.tiles / sk.nwg - 1;  // (the launcher guarantees tiles >= nwg)
+    const int rem = sk.tiles - sk_q * sk.nwg;
+    const long total = (long)rem * sk_pt, base = (long)sk_q * sk.nwg * sk_pt;
+    sk_u = (int)base + sk_snap(total * sk_w / sk.nwg, sk_pc, sk_pt);
+    sk_end = (int)base + sk_snap(total * (sk_w + 1) / sk.nwg, sk_pc, sk_pt);
   }
-  for (;;) {  // (one pass unless SK: one per segment of the workgroup's range)
+  for (;;) {  // (one pass unless SK: one per segment of the workgroup's work)
   int tm, tn, sk_role = 0, sk_lo = 0, sk_hi = 0;  // role 0: whole tile, 1: second part, 2: first part
   if constexpr (SK) {
+    if (sk_k < sk_q) {  // a whole tile of the data-parallel rounds
+      raster(sk_k * sk.nwg + sk_w, tm, tn);
+      ++sk_k;
+      sk_lo = 0;
+      sk_hi = Kp / 64 + S_pad / 64;
+    } else {
     if (sk_u >= sk_end) break;
     const int t = sk_u / sk_pt, q0 = sk_u - t * sk_pt;
     const int e = min(sk_end, (t + 1) * sk_pt), q1 = e - t * sk_pt;
@@ -275,11 +306,17 @@ __global__ __launch_bounds__((OPT & 16) ? 1024 : 512, ((OPT & 8) && !(OPT & 16))
     sk_hi = q1 == sk_pt ? Kp / 64 + S_pad / 64 : 2 * q1;
     sk_role = (q0 == 0 && q1 == sk_pt) ? 0 : q0 > 0 ? 1 : 2;
     raster(t, tm, tn);
+    }
   } else if constexpr (GRP) {
     raster(xcd_remap(grp.tile_end[grp.n - 1]), tm, tn);
   } else {
     tile_coords(tiles_m, tiles_n, group_m, tm, tn);
   }
+  ++sk_seg;
+  SK_STAMP(0);
+#ifdef SQMP_DIAG_BUILD
+  if (SK && threadIdx.x == 0 && sk_seg < 4 && sk_w < 512) sqmp_sk_roles[sk_w][sk_seg] = sk_role;
+#endif
   const int m0 = tm * TM, n0 = tn * TN;
   const int lane = threadIdx.x & 63;
   const int wave_wg = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
@@ -542,6 +579,7 @@ __global__ __launch_bounds__((OPT & 16) ? 1024 : 512, ((OPT & 8) && !(OPT & 16))
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   barrier();  // every wave is past its last read of the ring
+  SK_STAMP(1);
   // (SK) the other part's fp32 partial tile, added in the epilogue: a buffer resource over
   // its slot, or of zero records (loads return 0) for a whole tile
   __amdgpu_buffer_rsrc_t sk_src = __builtin_amdgcn_make_buffer_rsrc((void*)sk.part, 0, 0, 0x00020000);
@@ -569,7 +607,7 @@ __global__ __launch_bounds__((OPT & 16) ? 1024 : 512, ((OPT & 8) && !(OPT & 16))
         __syncthreads();
         if (threadIdx.x == 0) sk_word = (int)atomicAdd(flag, 1u);  // returns the old count
         __syncthreads();
-        return sk_word;
+        return __builtin_amdgcn_readfirstlane(sk_word);  // (uniform: scalar branches below)
       };
       unsigned char* src = nullptr;  // the other part's partial, when this part finishes the tile
       if (sk_role == 1) {
@@ -577,14 +615,25 @@ __global__ __launch_bounds__((OPT & 16) ? 1024 : 512, ((OPT & 8) && !(OPT & 16))
       } else {
         if (threadIdx.x == 0) sk_word = (int)__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __syncthreads();
-        if (sk_word == 1) src = slot_a;
+        if (__builtin_amdgcn_readfirstlane(sk_word) == 1) src = slot_a;
         else if (put(slot_b) == 1) src = slot_a;
       }
-      if (!src) continue;  // the other workgroup finishes this tile
-      sk_src = __builtin_amdgcn_make_buffer_rsrc(src, 0, SLOT, 0x00020000);
+      if (!src) {  // the other workgroup finishes this tile
+        SK_STAMP(2);
+        SK_STAMP(3);
+        continue;
+      }
+      // (a uniform descriptor: a divergent one turns every load into a waterfall loop)
+      const uint64_t sa = (uint64_t)(size_t)src;
+      // (readfirstlane returns int: through uint32_t, or bit 31 of the low word would be
+      // sign-extended into the high word)
+      const uint64_t su = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)sa) |
+                          ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(sa >> 32)) << 32);
+      sk_src = __builtin_amdgcn_make_buffer_rsrc((void*)(size_t)su, 0, SLOT, 0x00020000);
       if (threadIdx.x == 0) __hip_atomic_store(flag, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
+  SK_STAMP(2);
   if constexpr (KS2) {
     // half 1's accumulators to half 0 through LDS (lane-contiguous f32x4: conflict-free)
     f32x4* part = (f32x4*)lds;
@@ -664,13 +713,21 @@ __global__ __launch_bounds__((OPT & 16) ? 1024 : 512, ((OPT & 8) && !(OPT & 16))
 #pragma unroll
     for (int r = 0; r < 4; ++r)
       bv[r] = bias && n0 + nl + r < N ? DT::to_f(bias[n0 + nl + r]) : 0.f;
+    // (SK) the other part's partial for this column block, all I loads in flight at once, after
+    // the bias (vmcnt counts in issue order); sc1, after the hand-off barrier; zeros from a
+    // zero-record descriptor for a whole tile
+    f32x4 pv[SK ? I : 1];
+    if constexpr (SK) {
+#pragma unroll
+      for (int i = 0; i < I; ++i)
+        pv[i] = __builtin_amdgcn_raw_buffer_load_b128(
+            sk_src, (uint32_t)((wave * (I * J * 64) + el) * 16 + (i * J + j) * 1024), 0, 16);
+    }
 #pragma unroll
     for (int i = 0; i < I; ++i) {
       const int ml = 16 * i + er16;
       f32x4 a4 = acc[i][j];
-      if constexpr (SK)  // (sc1 loads of the other part's partial, after the hand-off barrier)
-        a4 += __builtin_amdgcn_raw_buffer_load_b128(
-            sk_src, (uint32_t)((wave * (I * J * 64) + el) * 16 + (i * J + j) * 1024), 0, 16);
+      if constexpr (SK) a4 += pv[i];
       T v[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) v[r] = DT::from_f(a4[r] + bv[r]);
@@ -718,6 +775,7 @@ __global__ __launch_bounds__((OPT & 16) ? 1024 : 512, ((OPT & 8) && !(OPT & 16))
   if constexpr (!SK) break;
   // (SK) the next segment's DMA reuses the LDS the staged tile was read from
   __syncthreads();
+  SK_STAMP(3);
   }  // segment loop
 }
 
@@ -941,13 +999,17 @@ static int num_cus() {
 
 // The stream-K schedule (Fq7Sk) for a grouped launch of t256 256 x 256 tiles: with a
 // workspace, fp16, when the tiles are not a whole number of rounds of the CUs and there are
-// at least as many as CUs (every cut tile then has exactly two parts).  SQMP_FQ7_SK=0 turns
-// it off (A/B knob).
+// at least as many as CUs (every cut tile then has at most two parts).  Opt-in
+// (SQMP_FQ7_SK=1; 2 also cuts whole rounds): measured slower than the 256-row data-parallel
+// grid at the Llama sibling shapes -- the K loop of a stretch runs 10-35 % longer per tile than
+// in the data-parallel kernel, more than the last round's idle CUs cost
+// (profiles/r06_stream_k.txt).
 static bool sk_wanted(bool f16, long t256, bool have_ws) {
   const char* e = knob("SQMP_FQ7_SK");
-  if (e && atoi(e) == 0) return false;
+  if (!e || atoi(e) == 0) return false;
   const int ncu = num_cus();
-  return f16 && have_ws && t256 >= ncu && t256 % ncu != 0;
+  const bool force = e && atoi(e) == 2;  // (A/B diagnostics: whole rounds too)
+  return f16 && have_ws && t256 >= ncu && (t256 % ncu != 0 || force);
 }
 
 static int tm_group(bool bf16, int M, const int* Ns, int n, bool have_ws = false) {
@@ -1233,6 +1295,23 @@ extern "C" int sqmp_fq7_plan(int dtype, int M, const int* N, int nprob, int Kp, 
 
 // the stream-K workspace of sqmp_gemm_fq7_group_ws on the current device
 extern "C" size_t sqmp_fq7_workspace_bytes(void) { return fq7::sk_ws_bytes(); }
+
+#ifdef SQMP_DIAG_BUILD
+// the stream-K kernel's stamps (host NULL: clear them): stamps [512][16], roles [512][4]
+extern "C" int sqmp_diag_sk_stamps(unsigned long long* host, int* roles) {
+  if (!host) {
+    void* d = nullptr;
+    if (hipGetSymbolAddress(&d, HIP_SYMBOL(fq7::sqmp_sk_stamps)) != hipSuccess) return -3;
+    if (hipMemset(d, 0, sizeof(unsigned long long) * 512 * 16) != hipSuccess) return -3;
+    if (hipGetSymbolAddress(&d, HIP_SYMBOL(fq7::sqmp_sk_roles)) != hipSuccess) return -3;
+    return hipMemset(d, 0xFF, sizeof(int) * 512 * 4) == hipSuccess ? 0 : -3;
+  }
+  if (hipMemcpyFromSymbol(host, HIP_SYMBOL(fq7::sqmp_sk_stamps), sizeof(unsigned long long) * 512 * 16, 0,
+                          hipMemcpyDeviceToHost) != hipSuccess) return -3;
+  return hipMemcpyFromSymbol(roles, HIP_SYMBOL(fq7::sqmp_sk_roles), sizeof(int) * 512 * 4, 0,
+                             hipMemcpyDeviceToHost) == hipSuccess ? 0 : -3;
+}
+#endif
 
 // sqmp_gemm_fqt7: the activation-order GEMM (sqmp_gemm_fqt) on fq7's register-operand
 // structure, its activation operands in the tile-major layout (J = 2) that sqmp_quant_act_c4

@@ -68,7 +68,7 @@ def test_group_gemm_equals_own(tm, M, K, Ns, G, p, dt, monkeypatch):
     dev = _dev()
     from smoothquant import ops
     monkeypatch.setenv("SQMP_FQ7_KS", "0")
-    monkeypatch.setenv("SQMP_FQ7_SK", "0")  # (the stream-K schedule: test_group_gemm_stream_k)
+    monkeypatch.setenv("SQMP_FQ7_SK", "0")  # (the opt-in stream-K schedule: test_group_gemm_stream_k)
     monkeypatch.setenv("SQMP_FQ7G_TM", tm)
     __import__("smoothquant._lib", fromlist=["_lib"]).reload_knobs()  # (knobs are read once at load)
     layers, x = _siblings(dev, M, K, Ns, G, p, dt, seed=5)
@@ -88,13 +88,14 @@ def _sk_split_tiles(M, Kp, S_pad, Ns, ncu, group_m=4):
     tiles_m = (M + 255) // 256
     tn = [(n + 255) // 256 for n in Ns]
     T = sum(tiles_m * t for t in tn)
-    total = T * pt
+    q = T // ncu - 1               # whole rounds, then a stream-K stretch over ncu + r tiles
+    total, base = (T - q * ncu) * pt, q * ncu * pt
 
     def snap(u):
-        t, q = divmod(u, pt)
-        return (t + 1) * pt if q >= pc else u
+        t, qq = divmod(u, pt)
+        return (t + 1) * pt if qq >= pc else u
 
-    cuts = {snap(total * w // ncu) for w in range(1, ncu)}
+    cuts = {base + snap(total * w // ncu) for w in range(1, ncu)}
     out = set()
     for c in cuts:
         t, q = divmod(c, pt)
@@ -126,6 +127,8 @@ def test_group_gemm_stream_k(M, K, Ns, G, p, monkeypatch):
     the same bits (the arrival flags are left zero)."""
     dev = _dev()
     from smoothquant import ops
+    monkeypatch.setenv("SQMP_FQ7_SK", "1")  # (opt-in: measured slower than the 256-row DP grid)
+    __import__("smoothquant._lib", fromlist=["_lib"]).reload_knobs()
     layers, x = _siblings(dev, M, K, Ns, G, p, torch.float16, seed=21)
     pws = [q.packed() for q in layers]
     a = ops.quant_act_fp_group(x, pws, "per_group", 4, G)
