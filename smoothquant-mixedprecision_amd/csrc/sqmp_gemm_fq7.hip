@@ -158,6 +158,7 @@ struct Fq7Sk {
   uint32_t* flag;   // one arrival count per boundary, zero between launches
   int nwg;          // the persistent grid
   int tiles;        // tiles in the flattened raster order
+  int q;            // whole data-parallel rounds before the stretch (sk_rounds)
 };
 
 // Timing stamps of the stream-K kernel (SQMP_DIAG_BUILD only): per logical workgroup and
@@ -283,7 +284,7 @@ __global__ __launch_bounds__((OPT & 16) ? 1024 : 512, ((OPT & 8) && !(OPT & 16))
   int sk_w = 0, sk_u = 0, sk_end = 0, sk_k = 0, sk_q = 0, sk_seg = -1;
   if constexpr (SK) {
     sk_w = xcd_remap(sk.nwg);
-    sk_q = sk.tiles / sk.nwg - 1;  // (the launcher guarantees tiles >= nwg)
+    sk_q = sk.q;
     const int rem = sk.tiles - sk_q * sk.nwg;
     const long total = (long)rem * sk_pt, base = (long)sk_q * sk.nwg * sk_pt;
     sk_u = (int)base + sk_snap(total * sk_w / sk.nwg, sk_pc, sk_pt);
@@ -999,7 +1000,8 @@ static int num_cus() {
 
 // The stream-K schedule (Fq7Sk) for a grouped launch of t256 256 x 256 tiles: with a
 // workspace, fp16, when the tiles are not a whole number of rounds of the CUs and there are
-// at least as many as CUs (every cut tile then has at most two parts).  Opt-in
+// at least as many as CUs, or exactly half as many beyond whole rounds (every cut tile then
+// has at most two parts; sk_rounds).  Opt-in
 // (SQMP_FQ7_SK=1; 2 also cuts whole rounds): measured slower than the 256-row data-parallel
 // grid at the Llama sibling shapes -- the K loop of a stretch runs 10-35 % longer per tile than
 // in the data-parallel kernel, more than the last round's idle CUs cost
@@ -1009,7 +1011,21 @@ static bool sk_wanted(bool f16, long t256, bool have_ws) {
   if (!e || atoi(e) == 0) return false;
   const int ncu = num_cus();
   const bool force = e && atoi(e) == 2;  // (A/B diagnostics: whole rounds too)
-  return f16 && have_ws && t256 >= ncu && (t256 % ncu != 0 || force);
+  return f16 && have_ws && ((t256 >= ncu && (t256 % ncu != 0 || force)) || 2 * (t256 % ncu) == ncu);
+}
+
+// Whole data-parallel rounds before the stream-K stretch.  The stretch covers the last
+// nwg + r tiles (r = tiles mod nwg), 1 + r / nwg tiles per workgroup: no workgroup range is
+// shorter than a tile, so a tile is cut at most once.  A remainder of exactly nwg / 2 tiles
+// is instead cut in half, every workgroup taking one K half of a tile: the two halves of a
+// tile start together at K 0 and K / 2 (aligned phases: the workgroups sharing an operand
+// row block stream it at two K positions, not at as many as there are cut offsets).
+// SQMP_FQ7_SK=3 takes the halves for such a remainder; otherwise the stretch.
+static int sk_rounds(long tiles, int nwg) {
+  const long r = tiles % nwg;
+  const char* e = knob("SQMP_FQ7_SK");
+  if (2 * r == nwg && (tiles < nwg || (e && atoi(e) == 3))) return (int)(tiles / nwg);
+  return (int)(tiles / nwg) - 1;
 }
 
 static int tm_group(bool bf16, int M, const int* Ns, int n, bool have_ws = false) {
@@ -1057,7 +1073,7 @@ static int dispatch_group(Fq7Grp& g, int M, int Kp, int S_pad, int Gw, int ngw, 
         // stream-K over the union of the problems' tiles, one persistent workgroup per CU
         const int ncu = num_cus();
         Fq7Sk sk{(float*)((unsigned char*)ws + round_up((size_t)ncu * sizeof(uint32_t), 256)),
-                 (uint32_t*)ws, ncu, end};
+                 (uint32_t*)ws, ncu, end, sk_rounds(end, ncu)};
         gemm_fq7_kernel<DT, 1, 256, 2, 0, false, 3 | 32, true><<<dim3(ncu), dim3(512), 0, s>>>(
             (const T*)nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, M, 0, Kp, S_pad, Gw,
             ngw, tiles_m, 0, group_m_env(), nullptr, nt, g, sk);
