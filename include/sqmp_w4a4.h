@@ -361,24 +361,12 @@ typedef struct sqmp_fq7_problem {
 int sqmp_gemm_fq7_group(const sqmp_fq7_problem* probs, int nprob, int dtype, int M, int Kp,
                         int S_pad, int Gw, int ngw, int J, void* stream);
 
-/* sqmp_gemm_fq7_group with a workspace of sqmp_fq7_workspace_bytes() (zero-initialised once by
- * the caller; every launch leaves it reusable; one per stream): a launch whose 256 x 256 tiles
- * are not a whole number of rounds of the CUs runs a stream-K schedule -- one persistent
- * workgroup per CU walking an equal share of the tiles' 128-position K stages; a tile cut
- * between two workgroups adds their fp32 partial sums (y within fp32 rounding of the unsplit
- * kernel's; sqmp_fq7_plan reports OPT bit 32).  Refuses a smaller workspace (EWORKSPACE). */
-int sqmp_gemm_fq7_group_ws(const sqmp_fq7_problem* probs, int nprob, int dtype, int M, int Kp,
-                           int S_pad, int Gw, int ngw, int J, void* workspace, size_t ws_bytes,
-                           void* stream);
-size_t sqmp_fq7_workspace_bytes(void);
-
 /* The kernel variant sqmp_gemm_fq7 (nprob = 0: the problem N[0] alone) or sqmp_gemm_fq7_group
  * (nprob problems of N[0 .. nprob)) launches for these shapes: *tm = the row-tile height, *opt =
- * the OPT bits of the packed-order kernel (bit 16 = the K split inside the workgroup, bit 32 =
- * the stream-K schedule of sqmp_gemm_fq7_group_ws: fp32 partial sums added in another order,
- * so y equals the unsplit kernel's only within fp32 rounding; every other bit gives
- * bit-identical y).  The group plan is that of sqmp_gemm_fq7_group_ws.  Tests and tools use it
- * to know which launches must agree bit for bit. */
+ * the OPT bits of the packed-order kernel (bit 16 = the K split inside the workgroup: its fp32
+ * partial sums add in another order, so its y equals the unsplit kernel's only within fp32
+ * rounding; every other bit gives bit-identical y).  Tests and tools use it to know which
+ * launches must agree bit for bit. */
 int sqmp_fq7_plan(int dtype, int M, const int* N, int nprob, int Kp, int Gw, int J, int* tm,
                   int* opt);
 

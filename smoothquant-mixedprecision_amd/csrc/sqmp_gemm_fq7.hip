@@ -131,62 +131,6 @@ struct Fq7Grp {
   int n;
 };
 
-// Stream-K schedule (OPT bit 5, value 32; packed order, 256-row tiles): data-parallel rounds
-// plus a stream-K stretch over the rest (the Stream-K paper's hybrid).  A persistent grid of
-// `nwg` workgroups (one per CU): with T = q nwg + r tiles (0 < r < nwg, q >= 1), workgroup w
-// (XCD-contiguous logical index) first runs the whole tiles k nwg + w, k < q - 1 -- round by
-// round, so the workgroups of one XCD work on neighbouring raster tiles as in the plain grid --
-// then an equal share of the last nwg + r tiles' K loops: those tiles' 64-position stage PAIRS
-// (the unit of the unrolled codes loop; the salient tail rides on the tile's last pair) in
-// raster order, workgroup w taking [R P w / nwg, R P (w + 1) / nwg), R = nwg + r, each end moved
-// to a pair boundary with at least one codes pair on either side (a cut in the tail moves to
-// the tile's end).  A share of at least one tile cuts every tile into at most two parts.  A grid that is not a whole number of rounds of the CUs (Llama-2-7B gate/up at 2048
-// tokens: 688 tiles = 2.69 rounds) then no longer idles most CUs through a last partial round.
-// A remainder tile cut at boundary b is finished by whichever of its two workgroups arrives
-// second: workgroup b + 1 runs the tile's SECOND part first (its share starts there) and
-// workgroup b the FIRST part last, so the second part normally stores its fp32 partial tile
-// (write-through, sc1) into slot A of boundary b and counts itself on the boundary's flag; the
-// first part polls the flag, adds the partial in its epilogue and clears the flag.  Should the
-// first part arrive before the partial (never waiting), it stores its own partial into slot B
-// and counts itself instead, and the second part's add then finds it and finishes the tile
-// (MI355X_MICROARCH.md hand-off rule: sc1 stores, every storing wave's vmcnt(0), a workgroup
-// barrier, one lane's agent-scope add; the workgroup whose add or poll saw the other's count
-// loads with sc1 loads after a barrier).  A cut tile's output adds two fp32 partial sums:
-// within fp32 rounding of the unsplit kernel's.
-struct Fq7Sk {
-  float* part;      // 2 slots of TM x TN fp32 per boundary (A: second part, B: first part)
-  uint32_t* flag;   // one arrival count per boundary, zero between launches
-  int nwg;          // the persistent grid
-  int tiles;        // tiles in the flattened raster order
-  int q;            // whole data-parallel rounds before the stretch (sk_rounds)
-};
-
-// Timing stamps of the stream-K kernel (SQMP_DIAG_BUILD only): per logical workgroup and
-// segment s < 4, the 100-MHz real-time counter at the segment's start, after its K loop, after
-// the hand-off and at its end ([4 s + 0..3]); the segment's role in sqmp_sk_roles
-// (tools/sk_stamps.py)
-#ifdef SQMP_DIAG_BUILD
-__device__ unsigned long long sqmp_sk_stamps[512][16];
-__device__ int sqmp_sk_roles[512][4];
-#define SK_STAMP(k)                                                                     \
-  do {                                                                                  \
-    if (SK && threadIdx.x == 0 && sk_seg < 4 && sk_w < 512)                             \
-      sqmp_sk_stamps[sk_w][4 * sk_seg + (k)] = __builtin_amdgcn_s_memrealtime();        \
-  } while (0)
-#else
-#define SK_STAMP(k) \
-  do {              \
-  } while (0)
-#endif
-
-// a pair index moved to the nearest legal cut: inside a tile only after >= 1 and before >= 1
-// codes pair; a cut at or past the last codes pair's end (in the salient tail) moves to the
-// tile's end
-__host__ __device__ inline int sk_snap(long u, int pc, int pt) {
-  const long t = u / pt, q = u - t * pt;
-  return (int)(q >= pc ? (t + 1) * pt : u);
-}
-
 // DIAG (timing diagnostics, wrong results by design, instantiated only in a SQMP_DIAG_BUILD;
 // 0 = the product kernel): 1 no weight
 // register loads after the prologue, 2 no A DMA after the prologue, 3 no int4 decode, 4 no
@@ -226,7 +170,7 @@ __global__ __launch_bounds__((OPT & 16) ? 1024 : 512, ((OPT & 8) && !(OPT & 16))
     const typename DT::T* __restrict__ St, const typename DT::T* __restrict__ Salt,
     const typename DT::T* __restrict__ bias, typename DT::T* __restrict__ Y, int M, int N,
     int Kp, int S_pad, int Gw, int ngw, int tiles_m, int tiles_n, int group_m,
-    uint32_t* __restrict__ colmax, int nt, const Fq7Grp grp, const Fq7Sk sk) {
+    uint32_t* __restrict__ colmax, int nt, const Fq7Grp grp) {
   typedef typename DT::T T;
   constexpr int I = TM / 16;            // 16 x 16 tiles per wave: TM rows x 16 J weight rows
   constexpr int TN = 128 * J, WR = 16 * J;  // tile width, weight rows per wave
@@ -244,80 +188,36 @@ __global__ __launch_bounds__((OPT & 16) ? 1024 : 512, ((OPT & 8) && !(OPT & 16))
   constexpr int LDS0 = NH * NS * SLOT > EPI ? NH * NS * SLOT : EPI;
   constexpr int LDS_BYTES = LDS0 > PART ? LDS0 : PART;
   static_assert(J <= I, "sub-step 1 decode must finish before block I");
-  constexpr bool SK = (OPT & 32) != 0;  // stream-K schedule (Fq7Sk)
-  static_assert(!SK || (!KS2 && !TR), "stream-K: packed order, one 8-wave ring");
   __shared__ __attribute__((aligned(16))) unsigned char lds[LDS_BYTES];
-  __shared__ int sk_word;  // (SK) a flag value broadcast to the workgroup
 
-  // tile wg of the raster: GRP -- the problem and its own grouped raster (as tile_coords)
-  auto raster = [&](int wg, int& tm_, int& tn_) {
-    if constexpr (GRP) {
-      int p = 0;
+  int tm, tn;
+  if constexpr (GRP) {
+    // XCD-aware bijective remap over every problem's tiles, then the problem and its own
+    // grouped raster (as tile_coords)
+    const int nwg = grp.tile_end[grp.n - 1];
+    const int bid = blockIdx.x, xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+    int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+    int p = 0;
 #pragma unroll
-      for (int i = 1; i < FQ7_GRP_MAX; ++i)
-        if (i < grp.n && wg >= grp.tile_end[i - 1]) p = i;
-      wg -= p > 0 ? grp.tile_end[p - 1] : 0;
-      A = (const T*)grp.A[p];
-      Bt = grp.Bt[p];
-      St = (const T*)grp.St[p];
-      Salt = (const T*)grp.Salt[p];
-      bias = (const T*)grp.bias[p];
-      Y = (T*)grp.Y[p];
-      colmax = grp.colmax[p];
-      N = grp.N[p];
-      tiles_n = grp.tiles_n[p];
-    }
+    for (int i = 1; i < FQ7_GRP_MAX; ++i)
+      if (i < grp.n && wg >= grp.tile_end[i - 1]) p = i;
+    wg -= p > 0 ? grp.tile_end[p - 1] : 0;
+    A = (const T*)grp.A[p];
+    Bt = grp.Bt[p];
+    St = (const T*)grp.St[p];
+    Salt = (const T*)grp.Salt[p];
+    bias = (const T*)grp.bias[p];
+    Y = (T*)grp.Y[p];
+    colmax = grp.colmax[p];
+    N = grp.N[p];
+    tiles_n = grp.tiles_n[p];
     const int per_group = group_m * tiles_n, gid = wg / per_group, first_m = gid * group_m;
     const int gsz = min(tiles_m - first_m, group_m), in_g = wg - gid * per_group;
-    tm_ = first_m + in_g % gsz;
-    tn_ = in_g / gsz;
-  };
-  // XCD-aware bijective remap of the block index over n workgroups (consecutive logical
-  // indices on one XCD: blocks are dealt round-robin over the 8 XCDs)
-  auto xcd_remap = [&](int n) {
-    const int bid = blockIdx.x, xcd = bid & 7, q8 = n >> 3, r8 = n & 7;
-    return (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
-  };
-  // stream-K: this workgroup's whole tiles k nwg + w (k < sk_q), then its pair range
-  // [sk_u, sk_end) of the remainder tiles' flattened (tile, pair) order
-  const int sk_pc = Kp / 128, sk_pt = sk_pc + (S_pad / 64 + 1) / 2;
-  int sk_w = 0, sk_u = 0, sk_end = 0, sk_k = 0, sk_q = 0, sk_seg = -1;
-  if constexpr (SK) {
-    sk_w = xcd_remap(sk.nwg);
-    sk_q = sk.q;
-    const int rem = sk.tiles - sk_q * sk.nwg;
-    const long total = (long)rem * sk_pt, base = (long)sk_q * sk.nwg * sk_pt;
-    sk_u = (int)base + sk_snap(total * sk_w / sk.nwg, sk_pc, sk_pt);
-    sk_end = (int)base + sk_snap(total * (sk_w + 1) / sk.nwg, sk_pc, sk_pt);
-  }
-  for (;;) {  // (one pass unless SK: one per segment of the workgroup's work)
-  int tm, tn, sk_role = 0, sk_lo = 0, sk_hi = 0;  // role 0: whole tile, 1: second part, 2: first part
-  if constexpr (SK) {
-    if (sk_k < sk_q) {  // a whole tile of the data-parallel rounds
-      raster(sk_k * sk.nwg + sk_w, tm, tn);
-      ++sk_k;
-      sk_lo = 0;
-      sk_hi = Kp / 64 + S_pad / 64;
-    } else {
-    if (sk_u >= sk_end) break;
-    const int t = sk_u / sk_pt, q0 = sk_u - t * sk_pt;
-    const int e = min(sk_end, (t + 1) * sk_pt), q1 = e - t * sk_pt;
-    sk_u = e;
-    sk_lo = 2 * q0;
-    sk_hi = q1 == sk_pt ? Kp / 64 + S_pad / 64 : 2 * q1;
-    sk_role = (q0 == 0 && q1 == sk_pt) ? 0 : q0 > 0 ? 1 : 2;
-    raster(t, tm, tn);
-    }
-  } else if constexpr (GRP) {
-    raster(xcd_remap(grp.tile_end[grp.n - 1]), tm, tn);
+    tm = first_m + in_g % gsz;
+    tn = in_g / gsz;
   } else {
     tile_coords(tiles_m, tiles_n, group_m, tm, tn);
   }
-  ++sk_seg;
-  SK_STAMP(0);
-#ifdef SQMP_DIAG_BUILD
-  if (SK && threadIdx.x == 0 && sk_seg < 4 && sk_w < 512) sqmp_sk_roles[sk_w][sk_seg] = sk_role;
-#endif
   const int m0 = tm * TM, n0 = tn * TN;
   const int lane = threadIdx.x & 63;
   const int wave_wg = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
@@ -330,11 +230,9 @@ __global__ __launch_bounds__((OPT & 16) ? 1024 : 512, ((OPT & 8) && !(OPT & 16))
   // this half's stages [k_lo, k_hi): bit 4 splits at an even h <= nkm - 2 near nkt / 2 (both
   // halves' codes stage counts stay even); the salient tail is half 1's
   const int hsplit = KS2 ? min(nkm - 2, (nkt / 2 + 1) & ~1) : nkt;
-  // (SK: the segment's stages [sk_lo, sk_hi), the salient tail with the tile's last pair)
-  const int k_lo = SK ? sk_lo : half == 1 ? hsplit : 0;
-  const int k_hi = SK ? sk_hi : (KS2 && half == 0) ? hsplit : nkt;
-  const int kc_hi = (KS2 || SK) ? min(k_hi, nkm) : nkm;   // end of this half's codes stages
-  const bool has_tail = (KS2 || SK) ? k_hi > nkm : nks > 0;
+  const int k_lo = half == 1 ? hsplit : 0, k_hi = (KS2 && half == 0) ? hsplit : nkt;
+  const int kc_hi = KS2 ? min(k_hi, nkm) : nkm;   // end of this half's codes stages
+  const bool has_tail = KS2 ? k_hi > nkm : nks > 0;
   unsigned char* const ring = lds + half * (NS * SLOT);
   const int nb = tn * 8 + wave;  // this wave's WR-row weight block
 
@@ -541,7 +439,7 @@ __global__ __launch_bounds__((OPT & 16) ? 1024 : 512, ((OPT & 8) && !(OPT & 16))
   // after block I - 1, sub-step 1 of kd + 1 at the end; so at the top of stage kd the ops
   // younger than its sub-step 0 are its sub-step 1 (4), and at block I those younger
   // than its sub-step 1 are A(k + PA).
-  for (int kd = 0; kd < ((KS2 || SK) ? (has_tail ? nks : 0) : nks); ++kd) {
+  for (int kd = 0; kd < (KS2 ? (has_tail ? nks : 0) : nks); ++kd) {
     const int k = nkm + kd;
     vmwait<J>();
 #pragma unroll
@@ -580,61 +478,6 @@ __global__ __launch_bounds__((OPT & 16) ? 1024 : 512, ((OPT & 8) && !(OPT & 16))
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   barrier();  // every wave is past its last read of the ring
-  SK_STAMP(1);
-  // (SK) the other part's fp32 partial tile, added in the epilogue: a buffer resource over
-  // its slot, or of zero records (loads return 0) for a whole tile
-  __amdgpu_buffer_rsrc_t sk_src = __builtin_amdgcn_make_buffer_rsrc((void*)sk.part, 0, 0, 0x00020000);
-  if constexpr (SK) {
-    if (sk_role != 0) {
-      // boundary b: the cut between workgroups b and b + 1 (the second part runs first in
-      // workgroup b + 1, the first part last in workgroup b)
-      const int b = sk_role == 1 ? sk_w - 1 : sk_w;
-      constexpr int SLOT = TM * TN * 4;  // bytes per slot
-      unsigned char* const slot_a = (unsigned char*)sk.part + (size_t)(2 * b) * SLOT;
-      unsigned char* const slot_b = slot_a + SLOT;
-      uint32_t* const flag = sk.flag + b;
-      // lane-contiguous: 1 KiB per wave store (the lane index computed again here: a value
-      // derived from the kernel-entry lane would be hoisted out of the segment loop and held
-      // through the K loop)
-      const uint32_t pbase = (uint32_t)(wave * (I * J * 64) + lane_now()) * 16u;
-      auto put = [&](unsigned char* dst) {
-        const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(dst, 0, SLOT, 0x00020000);
-#pragma unroll
-        for (int i = 0; i < I; ++i)
-#pragma unroll
-          for (int j = 0; j < J; ++j)  // write-through (sc1)
-            __builtin_amdgcn_raw_buffer_store_b128(acc[i][j], r, pbase + (uint32_t)((i * J + j) * 1024), 0, 16);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave, before the add
-        __syncthreads();
-        if (threadIdx.x == 0) sk_word = (int)atomicAdd(flag, 1u);  // returns the old count
-        __syncthreads();
-        return __builtin_amdgcn_readfirstlane(sk_word);  // (uniform: scalar branches below)
-      };
-      unsigned char* src = nullptr;  // the other part's partial, when this part finishes the tile
-      if (sk_role == 1) {
-        if (put(slot_a) == 1) src = slot_b;  // the first part was there first
-      } else {
-        if (threadIdx.x == 0) sk_word = (int)__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __syncthreads();
-        if (__builtin_amdgcn_readfirstlane(sk_word) == 1) src = slot_a;
-        else if (put(slot_b) == 1) src = slot_a;
-      }
-      if (!src) {  // the other workgroup finishes this tile
-        SK_STAMP(2);
-        SK_STAMP(3);
-        continue;
-      }
-      // (a uniform descriptor: a divergent one turns every load into a waterfall loop)
-      const uint64_t sa = (uint64_t)(size_t)src;
-      // (readfirstlane returns int: through uint32_t, or bit 31 of the low word would be
-      // sign-extended into the high word)
-      const uint64_t su = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)sa) |
-                          ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(sa >> 32)) << 32);
-      sk_src = __builtin_amdgcn_make_buffer_rsrc((void*)(size_t)su, 0, SLOT, 0x00020000);
-      if (threadIdx.x == 0) __hip_atomic_store(flag, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-  SK_STAMP(2);
   if constexpr (KS2) {
     // half 1's accumulators to half 0 through LDS (lane-contiguous f32x4: conflict-free)
     f32x4* part = (f32x4*)lds;
@@ -702,9 +545,8 @@ __global__ __launch_bounds__((OPT & 16) ? 1024 : 512, ((OPT & 8) && !(OPT & 16))
     }
     return;
   }
-  // (OPT bit 3: the lane index computed again here rather than kept live from the entry; SK:
-  // so that nothing the epilogue derives from it is hoisted out of the segment loop)
-  const int el = ((OPT & 8) || SK) ? lane_now() : lane;
+  // (OPT bit 3: the lane index computed again here rather than kept live from the entry)
+  const int el = (OPT & 8) ? lane_now() : lane;
   const int etid = wave * 64 + el, er16 = el & 15, eq = el >> 4;
   float cmx[J][4] = {};
 #pragma unroll
@@ -714,24 +556,12 @@ __global__ __launch_bounds__((OPT & 16) ? 1024 : 512, ((OPT & 8) && !(OPT & 16))
 #pragma unroll
     for (int r = 0; r < 4; ++r)
       bv[r] = bias && n0 + nl + r < N ? DT::to_f(bias[n0 + nl + r]) : 0.f;
-    // (SK) the other part's partial for this column block, all I loads in flight at once, after
-    // the bias (vmcnt counts in issue order); sc1, after the hand-off barrier; zeros from a
-    // zero-record descriptor for a whole tile
-    f32x4 pv[SK ? I : 1];
-    if constexpr (SK) {
-#pragma unroll
-      for (int i = 0; i < I; ++i)
-        pv[i] = __builtin_amdgcn_raw_buffer_load_b128(
-            sk_src, (uint32_t)((wave * (I * J * 64) + el) * 16 + (i * J + j) * 1024), 0, 16);
-    }
 #pragma unroll
     for (int i = 0; i < I; ++i) {
       const int ml = 16 * i + er16;
-      f32x4 a4 = acc[i][j];
-      if constexpr (SK) a4 += pv[i];
       T v[4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = DT::from_f(a4[r] + bv[r]);
+      for (int r = 0; r < 4; ++r) v[r] = DT::from_f(acc[i][j][r] + bv[r]);
       if (colmax && m0 + ml < M) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) cmx[j][r] = fmaxf(cmx[j][r], fabsf(DT::to_f(v[r])));
@@ -773,11 +603,6 @@ __global__ __launch_bounds__((OPT & 16) ? 1024 : 512, ((OPT & 8) && !(OPT & 16))
         *dst = val;
     }
   }
-  if constexpr (!SK) break;
-  // (SK) the next segment's DMA reuses the LDS the staged tile was read from
-  __syncthreads();
-  SK_STAMP(3);
-  }  // segment loop
 }
 
 // ---- tile-major copies of the packed weight (once per layer), blocks of WR = 16 J rows
@@ -909,7 +734,7 @@ static int launch_k(const void* a, const void* bt, const void* st, const void* s
 #define SQMP_PK(O)                                                                              \
   gemm_fq7_kernel<DT, GB, TM, J, DIAG, false, O><<<dim3(tiles_m * tiles_n), dim3((O) & 16 ? 1024 : 512), 0, s>>>( \
       (const T*)a, (const uint32_t*)bt, (const T*)st, (const T*)salt, (const T*)bias, (T*)y, M,  \
-      N, Kp, S_pad, Gw, ngw, tiles_m, tiles_n, group_m_env(), colmax, nt, Fq7Grp{}, Fq7Sk{})
+      N, Kp, S_pad, Gw, ngw, tiles_m, tiles_n, group_m_env(), colmax, nt, Fq7Grp{})
   // OPT variants (setprio for waves 4-7, loader split) for the fp16 J = 2 kernels, the
   // 2048-token Llama GEMMs (A/B knob SQMP_FQ7_OPT, read per launch)
   if constexpr (std::is_same<DT, F16>::value && J == 2 && GB == 1 && DIAG == 0) {
@@ -983,69 +808,16 @@ static int dispatch(const void* a, const void* bt, const void* st, const void* s
 // group.  Row tiles of 256 where the problems' 256 x 256 tiles fill two rounds of the CUs, else
 // of 128 (two workgroups per CU where that gives more than one tile per CU), as dispatch();
 // SQMP_FQ7G_TM = 128 / 256 overrides (A/B, read per launch).
-// CUs of the current device (the stream-K grid), cached per device
-static int num_cus() {
-  static int cus[64] = {0};
-  int d = 0;
-  (void)hipGetDevice(&d);
-  d &= 63;
-  if (cus[d] <= 0) {
-    int n = 0;
-    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, d) != hipSuccess || n <= 0)
-      n = 256;
-    cus[d] = n;
-  }
-  return cus[d];
-}
-
-// The stream-K schedule (Fq7Sk) for a grouped launch of t256 256 x 256 tiles: with a
-// workspace, fp16, when the tiles are not a whole number of rounds of the CUs and there are
-// at least as many as CUs, or exactly half as many beyond whole rounds (every cut tile then
-// has at most two parts; sk_rounds).  Opt-in
-// (SQMP_FQ7_SK=1; 2 also cuts whole rounds): measured slower than the 256-row data-parallel
-// grid at the Llama sibling shapes -- the K loop of a stretch runs 10-35 % longer per tile than
-// in the data-parallel kernel, more than the last round's idle CUs cost
-// (profiles/r06_stream_k.txt).
-static bool sk_wanted(bool f16, long t256, bool have_ws) {
-  const char* e = knob("SQMP_FQ7_SK");
-  if (!e || atoi(e) == 0) return false;
-  const int ncu = num_cus();
-  const bool force = e && atoi(e) == 2;  // (A/B diagnostics: whole rounds too)
-  return f16 && have_ws && ((t256 >= ncu && (t256 % ncu != 0 || force)) || 2 * (t256 % ncu) == ncu);
-}
-
-// Whole data-parallel rounds before the stream-K stretch.  The stretch covers the last
-// nwg + r tiles (r = tiles mod nwg), 1 + r / nwg tiles per workgroup: no workgroup range is
-// shorter than a tile, so a tile is cut at most once.  A remainder of exactly nwg / 2 tiles
-// is instead cut in half, every workgroup taking one K half of a tile: the two halves of a
-// tile start together at K 0 and K / 2 (aligned phases: the workgroups sharing an operand
-// row block stream it at two K positions, not at as many as there are cut offsets).
-// SQMP_FQ7_SK=3 takes the halves for such a remainder; otherwise the stretch.
-static int sk_rounds(long tiles, int nwg) {
-  const long r = tiles % nwg;
-  const char* e = knob("SQMP_FQ7_SK");
-  if (2 * r == nwg && (tiles < nwg || (e && atoi(e) == 3))) return (int)(tiles / nwg);
-  return (int)(tiles / nwg) - 1;
-}
-
-static int tm_group(bool bf16, int M, const int* Ns, int n, bool have_ws = false) {
+static int tm_group(bool bf16, int M, const int* Ns, int n) {
   long t256 = 0;
   for (int p = 0; p < n; ++p) t256 += (long)cdiv(M, 256) * cdiv(Ns[p], 256);
-  int tm = (t256 >= 512 && ks_env() < 3) || sk_wanted(!bf16, t256, have_ws) ? 256 : 128;
+  int tm = t256 >= 512 && ks_env() < 3 ? 256 : 128;
   if (const char* e = knob("SQMP_FQ7G_TM")) tm = atoi(e) == 256 ? 256 : 128;
   return bf16 ? 128 : tm;  // (bf16 at 256 x 256 puts an array in scratch)
 }
-
-// Bytes of the stream-K workspace on the current device: the arrival flags (one per boundary,
-// zero-initialised by the caller and left zero by every launch), then two 256 x 256 fp32
-// partial slots per boundary.
-static size_t sk_ws_bytes() {
-  const size_t nb = (size_t)num_cus();
-  return round_up(nb * sizeof(uint32_t), 256) + 2 * nb * 256 * 256 * sizeof(float);
-}
 // the OPT variant dispatch_group launches
-static int group_opt(bool f16, int tm, long tiles, int kp, bool have_ws = false) {
-  if (tm == 256) return f16 ? (sk_wanted(true, tiles, have_ws) ? 3 | 32 : 3) : -1;
+static int group_opt(bool f16, int tm, long tiles, int kp) {
+  if (tm == 256) return f16 ? 3 : -1;
   const int o = opt_pk_env(128, tiles, kp);
   if (o == 24 && f16) return 24;
   return o == 8 ? 8 : 3;
@@ -1053,9 +825,9 @@ static int group_opt(bool f16, int tm, long tiles, int kp, bool have_ws = false)
 
 template <class DT>
 static int dispatch_group(Fq7Grp& g, int M, int Kp, int S_pad, int Gw, int ngw, int nt,
-                          hipStream_t s, void* ws = nullptr) {
+                          hipStream_t s) {
   typedef typename DT::T T;
-  const int tm = tm_group(std::is_same<DT, BF16>::value, M, g.N, g.n, ws != nullptr);
+  const int tm = tm_group(std::is_same<DT, BF16>::value, M, g.N, g.n);
   const int tiles_m = cdiv(M, tm);
   int end = 0;
   for (int p = 0; p < g.n; ++p) {
@@ -1066,19 +838,8 @@ static int dispatch_group(Fq7Grp& g, int M, int Kp, int S_pad, int Gw, int ngw, 
 #define SQMP_G(TMV, O)                                                                          \
   gemm_fq7_kernel<DT, 1, TMV, 2, 0, false, O, true><<<dim3(end), dim3((O) & 16 ? 1024 : 512), 0, s>>>( \
       (const T*)nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, M, 0, Kp, S_pad, Gw, ngw, \
-      tiles_m, 0, group_m_env(), nullptr, nt, g, Fq7Sk{})
-  switch (group_opt(std::is_same<DT, F16>::value, tm, end, Kp, ws != nullptr)) {
-    case 3 | 32:
-      if constexpr (std::is_same<DT, F16>::value) {
-        // stream-K over the union of the problems' tiles, one persistent workgroup per CU
-        const int ncu = num_cus();
-        Fq7Sk sk{(float*)((unsigned char*)ws + round_up((size_t)ncu * sizeof(uint32_t), 256)),
-                 (uint32_t*)ws, ncu, end, sk_rounds(end, ncu)};
-        gemm_fq7_kernel<DT, 1, 256, 2, 0, false, 3 | 32, true><<<dim3(ncu), dim3(512), 0, s>>>(
-            (const T*)nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, M, 0, Kp, S_pad, Gw,
-            ngw, tiles_m, 0, group_m_env(), nullptr, nt, g, sk);
-      }
-      break;
+      tiles_m, 0, group_m_env(), nullptr, nt, g)
+  switch (group_opt(std::is_same<DT, F16>::value, tm, end, Kp)) {
     case 3:
       if (tm == 256) {
         if constexpr (std::is_same<DT, F16>::value) SQMP_G(256, 3);
@@ -1111,13 +872,13 @@ static int dispatch_tr(const void* wp, const void* codes_t, const void* scale_t,
 #define SQMP_TR(O)                                                                              \
   gemm_fq7_kernel<DT, 1, TM, J, 0, true, O><<<dim3(tiles_m * tiles_n), dim3(512), 0, s>>>(      \
       (const T*)wp, (const uint32_t*)codes_t, (const T*)scale_t, (const T*)sal_t, (const T*)bias, \
-      (T*)y, N, M, Kq, S_pad, G, ngq, tiles_m, tiles_n, group_m_tr_env(), colmax, nt, Fq7Grp{}, Fq7Sk{})
+      (T*)y, N, M, Kq, S_pad, G, ngq, tiles_m, tiles_n, group_m_tr_env(), colmax, nt, Fq7Grp{})
   const int nt = nt_output((size_t)M * N * sizeof(T)) ? 1 : 0;
 #ifdef SQMP_DIAG_BUILD
 #define SQMP_TRD(D)                                                                             \
   gemm_fq7_kernel<DT, 1, TM, 2, D, true, 3><<<dim3(tiles_m * tiles_n), dim3(512), 0, s>>>(      \
       (const T*)wp, (const uint32_t*)codes_t, (const T*)scale_t, (const T*)sal_t, (const T*)bias, \
-      (T*)y, N, M, Kq, S_pad, G, ngq, tiles_m, tiles_n, group_m_tr_env(), colmax, nt, Fq7Grp{}, Fq7Sk{})
+      (T*)y, N, M, Kq, S_pad, G, ngq, tiles_m, tiles_n, group_m_tr_env(), colmax, nt, Fq7Grp{})
   if (std::is_same<DT, F16>::value && J == 2 && diag_env() > 0) {
     switch (diag_env()) {
       case 1: SQMP_TRD(1); break;
@@ -1151,7 +912,7 @@ static int dispatch_tr(const void* wp, const void* codes_t, const void* scale_t,
 #define SQMP_TR128(O)                                                                           \
   gemm_fq7_kernel<DT, 1, 128, 2, 0, true, O><<<dim3(cdiv(N, 128) * tiles_n), dim3(512), 0, s>>>( \
       (const T*)wp, (const uint32_t*)codes_t, (const T*)scale_t, (const T*)sal_t, (const T*)bias, \
-      (T*)y, N, M, Kq, S_pad, G, ngq, cdiv(N, 128), tiles_n, group_m_tr_env(), colmax, nt, Fq7Grp{}, Fq7Sk{})
+      (T*)y, N, M, Kq, S_pad, G, ngq, cdiv(N, 128), tiles_n, group_m_tr_env(), colmax, nt, Fq7Grp{})
       // 128-row tiles at two workgroups per CU (OPT bit 3; 8, 9 spill at 128 VGPRs)
       case 10: if constexpr (TM == 256) { SQMP_TR128(10); } else { SQMP_TR(0); } break;
       case 11: if constexpr (TM == 256) { SQMP_TR128(11); } else { SQMP_TR(0); } break;
@@ -1234,9 +995,9 @@ extern "C" int sqmp_gemm_fq7(const void* a, const void* codes_t, const void* sca
   return fq7::dispatch<BF16>(a, codes_t, scale_t, sal_t, bias, y, M, N, Kp, S_pad, Gw, ngw, J, colmax, s);
 }
 
-static int gemm_fq7_group_impl(const sqmp_fq7_problem* probs, int nprob, int dtype, int M,
-                               int Kp, int S_pad, int Gw, int ngw, int J, void* ws,
-                               void* stream) {
+extern "C" int sqmp_gemm_fq7_group(const sqmp_fq7_problem* probs, int nprob, int dtype, int M,
+                                   int Kp, int S_pad, int Gw, int ngw, int J, void* stream) {
+  SQMP_DEVICE_GUARD(stream);
   if (!probs || nprob < 1 || nprob > fq7::FQ7_GRP_MAX) return SQMP_EINVAL;
   if (M < 0 || Kp <= 0 || Kp % 128 || S_pad < 0 || S_pad % 64 || Gw <= 0 || ngw <= 0)
     return SQMP_EINVAL;
@@ -1263,25 +1024,8 @@ static int gemm_fq7_group_impl(const sqmp_fq7_problem* probs, int nprob, int dty
   if (M == 0) return SQMP_OK;
   const int nt = nt_output(ybytes) ? 1 : 0;
   hipStream_t s = (hipStream_t)stream;
-  if (dtype == SQMP_F16) return fq7::dispatch_group<F16>(g, M, Kp, S_pad, Gw, ngw, nt, s, ws);
-  return fq7::dispatch_group<BF16>(g, M, Kp, S_pad, Gw, ngw, nt, s, ws);
-}
-
-extern "C" int sqmp_gemm_fq7_group(const sqmp_fq7_problem* probs, int nprob, int dtype, int M,
-                                   int Kp, int S_pad, int Gw, int ngw, int J, void* stream) {
-  SQMP_DEVICE_GUARD(stream);
-  return gemm_fq7_group_impl(probs, nprob, dtype, M, Kp, S_pad, Gw, ngw, J, nullptr, stream);
-}
-
-// the same with the stream-K workspace (sqmp_fq7_workspace_bytes, zero-initialised once;
-// every launch leaves it reusable): grids that are not whole rounds of the CUs run the
-// stream-K schedule
-extern "C" int sqmp_gemm_fq7_group_ws(const sqmp_fq7_problem* probs, int nprob, int dtype, int M,
-                                      int Kp, int S_pad, int Gw, int ngw, int J, void* workspace,
-                                      size_t ws_bytes, void* stream) {
-  SQMP_DEVICE_GUARD(stream);
-  if (!workspace || ws_bytes < fq7::sk_ws_bytes()) return SQMP_EWORKSPACE;
-  return gemm_fq7_group_impl(probs, nprob, dtype, M, Kp, S_pad, Gw, ngw, J, workspace, stream);
+  if (dtype == SQMP_F16) return fq7::dispatch_group<F16>(g, M, Kp, S_pad, Gw, ngw, nt, s);
+  return fq7::dispatch_group<BF16>(g, M, Kp, S_pad, Gw, ngw, nt, s);
 }
 
 // Which kernel variant sqmp_gemm_fq7 (nprob = 0: N[0] alone) or sqmp_gemm_fq7_group (nprob
@@ -1301,33 +1045,13 @@ extern "C" int sqmp_fq7_plan(int dtype, int M, const int* N, int nprob, int Kp, 
     return SQMP_OK;
   }
   if (J != 2 || Gw % 64) return SQMP_EUNSUPPORTED;
-  const int t = fq7::tm_group(bf16, M, N, nprob, true);
+  const int t = fq7::tm_group(bf16, M, N, nprob);
   long tiles = 0;
   for (int p = 0; p < nprob; ++p) tiles += (long)cdiv(M, t) * cdiv(N[p], 256);
   *tm = t;
-  *opt = fq7::group_opt(!bf16, t, tiles, Kp, true);
+  *opt = fq7::group_opt(!bf16, t, tiles, Kp);
   return SQMP_OK;
 }
-
-// the stream-K workspace of sqmp_gemm_fq7_group_ws on the current device
-extern "C" size_t sqmp_fq7_workspace_bytes(void) { return fq7::sk_ws_bytes(); }
-
-#ifdef SQMP_DIAG_BUILD
-// the stream-K kernel's stamps (host NULL: clear them): stamps [512][16], roles [512][4]
-extern "C" int sqmp_diag_sk_stamps(unsigned long long* host, int* roles) {
-  if (!host) {
-    void* d = nullptr;
-    if (hipGetSymbolAddress(&d, HIP_SYMBOL(fq7::sqmp_sk_stamps)) != hipSuccess) return -3;
-    if (hipMemset(d, 0, sizeof(unsigned long long) * 512 * 16) != hipSuccess) return -3;
-    if (hipGetSymbolAddress(&d, HIP_SYMBOL(fq7::sqmp_sk_roles)) != hipSuccess) return -3;
-    return hipMemset(d, 0xFF, sizeof(int) * 512 * 4) == hipSuccess ? 0 : -3;
-  }
-  if (hipMemcpyFromSymbol(host, HIP_SYMBOL(fq7::sqmp_sk_stamps), sizeof(unsigned long long) * 512 * 16, 0,
-                          hipMemcpyDeviceToHost) != hipSuccess) return -3;
-  return hipMemcpyFromSymbol(roles, HIP_SYMBOL(fq7::sqmp_sk_roles), sizeof(int) * 512 * 4, 0,
-                             hipMemcpyDeviceToHost) == hipSuccess ? 0 : -3;
-}
-#endif
 
 // sqmp_gemm_fqt7: the activation-order GEMM (sqmp_gemm_fqt) on fq7's register-operand
 // structure, its activation operands in the tile-major layout (J = 2) that sqmp_quant_act_c4

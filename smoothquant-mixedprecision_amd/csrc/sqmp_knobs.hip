@@ -19,7 +19,7 @@ static const char* const kKnobs[] = {
     "SQMP_LC_PERCU",    "SQMP_PW_RB",          "SQMP_C4_QPERCU",   "SQMP_F32_WN2",
     "SQMP_F8_V1",       "SQMP_GROUP_M",        "SQMP_F8_OPT",      "SQMP_F8_DIAG",
     "SQMP_FQ7_GROUP_M", "SQMP_FQT7_GROUP_M",   "SQMP_FQ7_OPT",     "SQMP_FQT7_OPT",
-    "SQMP_FQ7_DIAG",    "SQMP_FQ7G_TM", "SQMP_FQ7_KS", "SQMP_FQ7_SK",        "SQMP_H2D_GROUP_M", "SQMP_H2_WIDE",
+    "SQMP_FQ7_DIAG",    "SQMP_FQ7G_TM", "SQMP_FQ7_KS",        "SQMP_H2D_GROUP_M", "SQMP_H2_WIDE",
     "SQMP_H2_BK64",     "SQMP_H2_GROUP_M",     "SQMP_COLMAX_RPB",  "SQMP_LC_PPW",
 };
 constexpr int NKNOBS = (int)(sizeof(kKnobs) / sizeof(kKnobs[0]));

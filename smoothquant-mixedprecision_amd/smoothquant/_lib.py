@@ -86,9 +86,6 @@ SIGNATURES = {
     "sqmp_gemm_fq7_group": (_i, [ctypes.POINTER(Fq7Problem), _i, _i, _i, _i, _i, _i, _i, _i,
                                  _vp]),
     "sqmp_fq7_plan": (_i, [_i, _i, _ip, _i, _i, _i, _i, _ip, _ip]),
-    "sqmp_gemm_fq7_group_ws": (_i, [ctypes.POINTER(Fq7Problem), _i, _i, _i, _i, _i, _i, _i, _i,
-                                    _vp, _sz, _vp]),
-    "sqmp_fq7_workspace_bytes": (_sz, []),
     "sqmp_reload_knobs": (_i, []),
     "sqmp_split2_f16": (_i, [_vp, _i, _i, _i, _vp, _vp, _vp]),
     "sqmp_row_exp": (_i, [_vp, _i, _i, _vp, _vp]),

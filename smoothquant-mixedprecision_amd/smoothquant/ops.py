@@ -392,25 +392,10 @@ def quant_act_fp_group(x2: torch.Tensor, pws, act_quant: str, n_bits: int,
     return outs
 
 
-_SKWS = {}
-
-
-def _fq7_sk_ws(device, stream_ptr: int) -> torch.Tensor:
-    """The stream-K workspace of sqmp_gemm_fq7_group_ws (arrival flags + partial tiles), one
-    per (device, stream): zero-initialised once, every launch leaves it reusable."""
-    key = (device.index, stream_ptr)
-    w = _SKWS.get(key)
-    if w is None:
-        w = torch.zeros(int(load().sqmp_fq7_workspace_bytes()), dtype=torch.uint8, device=device)
-        _SKWS[key] = w
-    return w
-
-
 def gemm_fq7_group(As, pws, biases):
     """[y_0, ..., y_{n-1}] with y_o = gemm_fq7(As[o], pws[o], biases[o]) in one launch
-    (sqmp_gemm_fq7_group_ws): bit for bit, except where the launch runs the stream-K schedule
-    (fq7_plan, OPT bit 32) or only one of the two takes the K split (bit 16) -- then within
-    fp32 rounding of the partial sums."""
+    (sqmp_gemm_fq7_group): bit for bit, unless only one of the two takes the K split inside the
+    workgroup (fq7_plan, OPT bit 16) -- then within fp32 rounding of the partial sums."""
     M = As[0].shape[0]
     p0 = pws[0]
     n = len(pws)
@@ -424,11 +409,8 @@ def gemm_fq7_group(As, pws, biases):
         probs[o] = _lib.Fq7Problem(a.data_ptr(), bt.data_ptr(), st.data_ptr(), salt.data_ptr(),
                                    None if b is None else b.data_ptr(), y.data_ptr(), None,
                                    pw.N)
-    stream = _stream(As[0])
-    ws = _fq7_sk_ws(As[0].device, stream.value if hasattr(stream, "value") else int(stream or 0))
-    check(load().sqmp_gemm_fq7_group_ws(probs, n, _dtype_code(p0.dtype), M, p0.Kp, p0.S_pad,
-                                        p0.Gw, p0.ngw, FQ7_J, _p(ws), ws.numel(), stream),
-          "gemm_fq7_group")
+    check(load().sqmp_gemm_fq7_group(probs, n, _dtype_code(p0.dtype), M, p0.Kp, p0.S_pad, p0.Gw,
+                                     p0.ngw, FQ7_J, _stream(As[0])), "gemm_fq7_group")
     return ys
 
 

@@ -68,7 +68,6 @@ def test_group_gemm_equals_own(tm, M, K, Ns, G, p, dt, monkeypatch):
     dev = _dev()
     from smoothquant import ops
     monkeypatch.setenv("SQMP_FQ7_KS", "0")
-    monkeypatch.setenv("SQMP_FQ7_SK", "0")  # (the opt-in stream-K schedule: test_group_gemm_stream_k)
     monkeypatch.setenv("SQMP_FQ7G_TM", tm)
     __import__("smoothquant._lib", fromlist=["_lib"]).reload_knobs()  # (knobs are read once at load)
     layers, x = _siblings(dev, M, K, Ns, G, p, dt, seed=5)
@@ -79,100 +78,6 @@ def test_group_gemm_equals_own(tm, M, K, Ns, G, p, dt, monkeypatch):
     for ai, pw, b, y in zip(a, pws, biases, ys):
         ref = ops.gemm_fq7(ai, pw, b)
         assert torch.equal(_bits(y), _bits(ref))
-
-
-def _sk_split_tiles(M, Kp, S_pad, Ns, ncu, halves=False, group_m=4):
-    """The (problem, row tile, column tile) of every 256 x 256 tile the stream-K schedule cuts
-    (a restatement of gemm_fq7_kernel's Fq7Sk partition, sk_rounds and the grouped raster, for
-    the test)."""
-    pc, pt = Kp // 128, Kp // 128 + (S_pad // 64 + 1) // 2
-    tiles_m = (M + 255) // 256
-    tn = [(n + 255) // 256 for n in Ns]
-    T = sum(tiles_m * t for t in tn)
-    # whole rounds, then a stream-K stretch over ncu + r tiles -- or, for a remainder of half
-    # a round (always when there is no whole round), the remainder cut into K halves
-    q = T // ncu if 2 * (T % ncu) == ncu and (halves or T < ncu) else T // ncu - 1
-    total, base = (T - q * ncu) * pt, q * ncu * pt
-
-    def snap(u):
-        t, qq = divmod(u, pt)
-        return (t + 1) * pt if qq >= pc else u
-
-    cuts = {base + snap(total * w // ncu) for w in range(1, ncu)}
-    out = set()
-    for c in cuts:
-        t, q = divmod(c, pt)
-        if q == 0:
-            continue
-        p, wg = 0, t
-        while wg >= tiles_m * tn[p]:
-            wg -= tiles_m * tn[p]
-            p += 1
-        per_group = group_m * tn[p]
-        gid = wg // per_group
-        first_m = gid * group_m
-        gsz = min(tiles_m - first_m, group_m)
-        in_g = wg - gid * per_group
-        out.add((p, first_m + in_g % gsz, in_g // gsz))
-    return out
-
-
-@pytest.mark.parametrize("M,K,Ns,G,p,mode", [
-    (2048, 4096, (4096, 4096, 4096), 64, 0.05, 1),   # Llama q/k/v: 384 tiles = 1.5 rounds
-    (2048, 4096, (4096, 4096, 4096), 64, 0.05, 3),   # the same, the last 128 tiles in K halves
-    (2048, 4096, (11008, 11008), 64, 0.05, 1),       # Llama gate/up: 688 tiles = 2.69 rounds
-    (1792, 2048, (8192, 3072), 128, 0.10, 1),        # 7 x 44 = 308 tiles, Kp = 2048
-    (2048, 11008, (4096,), 64, 0.05, 1),             # down_proj alone: 128 tiles in K halves
-])
-def test_group_gemm_stream_k(M, K, Ns, G, p, mode, monkeypatch):
-    """The stream-K schedule of the grouped launch (sqmp_gemm_fq7_group_ws, OPT bit 32) against
-    the same launch without it: every tile that no workgroup boundary cuts is bit-identical,
-    the cut tiles (two fp32 partial sums) within 1e-3 of it per tile, and the whole output
-    within the pair tolerance of the fp64 product; a second launch on the same workspace gives
-    the same bits (the arrival flags are left zero)."""
-    dev = _dev()
-    from smoothquant import ops
-    monkeypatch.setenv("SQMP_FQ7_SK", str(mode))  # (opt-in: see profiles/r06_stream_k.txt)
-    __import__("smoothquant._lib", fromlist=["_lib"]).reload_knobs()
-    layers, x = _siblings(dev, M, K, Ns, G, p, torch.float16, seed=21)
-    pws = [q.packed() for q in layers]
-    a = (ops.quant_act_fp_group(x, pws, "per_group", 4, G) if len(pws) > 1
-         else [ops.quant_act_fp(x, pws[0], "per_group", 4, G)])
-    biases = [q.bias.reshape(-1) for q in layers]
-    tm, opt = ops.fq7_plan(pws, M, group=True)
-    assert tm == 256 and opt & 32, (tm, opt)
-    ys = ops.gemm_fq7_group(a, pws, biases)
-    ys2 = ops.gemm_fq7_group(a, pws, biases)
-    for y, y2 in zip(ys, ys2):
-        assert torch.equal(_bits(y), _bits(y2))
-    monkeypatch.setenv("SQMP_FQ7_SK", "0")
-    monkeypatch.setenv("SQMP_FQ7G_TM", "256")
-    __import__("smoothquant._lib", fromlist=["_lib"]).reload_knobs()
-    assert not ops.fq7_plan(pws, M, group=True)[1] & 32
-    ref = ops.gemm_fq7_group(a, pws, biases)
-    ncu = torch.cuda.get_device_properties(dev).multi_processor_count
-    if 2 * (sum((M + 255) // 256 * ((pw.N + 255) // 256) for pw in pws) % ncu) != ncu and mode == 3:
-        pytest.skip("the remainder is not half a round on this device")
-    cut = _sk_split_tiles(M, pws[0].Kp, pws[0].S_pad, [pw.N for pw in pws], ncu, mode == 3)
-    assert cut, "no tile cut: the shape does not exercise the partial hand-off"
-    ncut = 0
-    for pi, (y, r) in enumerate(zip(ys, ref)):
-        for tmi in range((M + 255) // 256):
-            for tni in range((y.shape[1] + 255) // 256):
-                ys_ = y[256 * tmi:256 * (tmi + 1), 256 * tni:256 * (tni + 1)]
-                rs_ = r[256 * tmi:256 * (tmi + 1), 256 * tni:256 * (tni + 1)]
-                if (pi, tmi, tni) in cut:
-                    ncut += 1
-                    d = (ys_.float() - rs_.float()).norm() / rs_.float().norm()
-                    assert d < 1e-3, (pi, tmi, tni, float(d))
-                else:
-                    assert torch.equal(_bits(ys_), _bits(rs_)), (pi, tmi, tni)
-        pw, ai = pws[pi], a[pi][:M].double()
-        yr = ai[:, :pw.Kp] @ ops.dequant_weight_packed(pw).double().t() + biases[pi].double()
-        if pw.S_pad:
-            yr += ai[:, pw.Kp:pw.Kp + pw.S_pad] @ pw.wsal.double().t()
-        assert float((y.double() - yr).norm() / yr.norm()) < 2e-3
-    assert ncut == len(cut)
 
 
 def test_linked_modules_forward():
