@@ -63,15 +63,19 @@ step() {
       f=$(ls "$O"/prof/*/run_kernel_stats.csv "$O"/prof/run_kernel_stats.csv 2>/dev/null | head -1)
       [ -n "$f" ] && cp "$f" "$O/kernel_stats.csv" && head -6 "$O/kernel_stats.csv" | cut -c1-160 ;;
     pmc:*)
+      # PMC_TAG (env): a suffix of the pass directories (knob sweeps: SQMP_...=v PMC_TAG=v);
+      # PMC_PASSES (env, default "a b c d"): the passes to run
       local kind=${s#pmc:}
       local pa="SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT"
       local pb="SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_WAIT_ANY SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE"
       local pc="FETCH_SIZE"
       local pd="WRITE_SIZE TCC_HIT_sum TCC_MISS_sum"
-      for p in a b c d; do
+      for p in ${PMC_PASSES:-a b c d}; do
         local C; eval C=\$p$p
-        (cd /tmp && timeout -s KILL 120 rocprofv3 --pmc $C --output-format csv -d "$O/pmc/${kind}_$p" -o run \
-          -- python "$R/tools/gemm_only.py" $kind 20 > "$O/pmc_${kind}_$p.log" 2>&1) || fail "pmc $kind $p" "$O/pmc_${kind}_$p.log"
+        local D="$O/pmc${PMC_TAG:+_$PMC_TAG}/${kind}_$p"
+        mkdir -p "$(dirname "$D")"
+        (cd /tmp && timeout -s KILL 120 rocprofv3 --pmc $C --output-format csv -d "$D" -o run \
+          -- python "$R/tools/gemm_only.py" $kind 20 > "$D.log" 2>&1) || fail "pmc $kind $p" "$D.log"
       done
       echo "pmc $kind ok" ;;
     e2e)
