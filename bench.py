@@ -66,7 +66,7 @@ import torch  # noqa: E402
 M, K, N, G, P = 16384, 4096, 4096, 128, 0.10
 # dense MFMA peaks (MI355X_MICROARCH.md: 256 CU @ 2.4 GHz): f16/bf16 2.5 PF, i8/fp8 5 PF,
 # (fp6/fp4 10 PF: no kernel here)
-PEAK_TFLOPS = {"f16": 2516.6, "bf16": 2516.6, "i8": 5033.2, "f8": 5033.2, "f6": 10066.3,
+PEAK_TFLOPS = {"f16": 2516.6, "bf16": 2516.6, "i8": 5033.2, "f8": 5033.2,
                "f32": 157.3}
 HBM_PEAK_GBS = 8000.0
 
@@ -388,10 +388,8 @@ def llama_layer(dev, iters=40):
 def per_token_leg(dev, iters=200):
     """The per_token act mode of the same config-2 layer (BASELINE configs' per_token rows; the
     reference's per_token path, fake_quant.py:64-90): W4A4Linear.forward on the auto kernel
-    (the 4-bit codes as e2m3 on the block-scaled MFMA's FP6 form, sqmp_gemm_f6 -- e4m3 /
-    sqmp_gemm_f8 with SQMP_F8_FMT=8), step and GEMM timed with HIP events on the launch
-    stream; frac against the dense peak of the operand format (FP6 10066, FP8 5033 TFLOP/s),
-    frac_fp8_peak against the FP8 one either way."""
+    (e4m3 codes on the block-scaled FP8 MFMA, sqmp_gemm_f8), step and GEMM timed with HIP
+    events on the launch stream; frac against the dense FP8 MFMA peak."""
     from smoothquant import ops
     q, x, lin = make_layer(dev, "per_token", seed=4321)
     pw = q.packed()
@@ -399,10 +397,10 @@ def per_token_leg(dev, iters=200):
     flops = 2.0 * M * N * K
     use_f8 = ops.f8_auto(pw, "per_token", 4)
     if use_f8:
-        a8, sa, xs = ops.quant_act_f8(x, pw, "per_token", 4, ops.f8_fmt(pw))
+        a8, sa, xs = ops.quant_act_f8(x, pw, "per_token", 4)
         gemm = lambda: ops.gemm_f8(a8, sa, xs, pw, lin.bias)  # noqa: E731
-        quant = lambda: ops.quant_act_f8(x, pw, "per_token", 4, ops.f8_fmt(pw))  # noqa: E731
-        kdt = "f6" if ops.f8_fmt(pw) == 6 else "f8"
+        quant = lambda: ops.quant_act_f8(x, pw, "per_token", 4)  # noqa: E731
+        kdt = "f8"
     else:
         a = ops.quant_act_fp(x, pw, "per_token", 4, G)
         gemm = lambda: ops.gemm_fq(a, pw, lin.bias)  # noqa: E731
@@ -419,9 +417,7 @@ def per_token_leg(dev, iters=200):
     return {
         "workload": "the config-2 layer with act per_token (4-bit, per-row absmax), weight "
                     "per_group(sorted), 10% salient",
-        "kernel": ("sqmp_gemm_f6 (e2m3 codes, block-scaled MFMA in its FP6 form) + fp16 salient "
-                   "tail" if kdt == "f6" else
-                   "sqmp_gemm_f8 (e4m3 codes, block-scaled FP8 MFMA) + fp16 salient tail"
+        "kernel": ("sqmp_gemm_f8 (e4m3 codes, block-scaled FP8 MFMA) + fp16 salient tail"
                    if use_f8 else "sqmp_gemm_fq (fp16 D values)"),
         "ms_per_step": round(step_ms, 4),
         "TFLOP_per_s": round(flops / (step_ms * 1e-3) / 1e12, 1),
@@ -429,11 +425,9 @@ def per_token_leg(dev, iters=200):
         "gemm_TFLOP_per_s": round(achieved, 1),
         "peak": PEAK_TFLOPS[kdt],
         "frac": round(achieved / PEAK_TFLOPS[kdt], 4),
-        "frac_fp8_peak": round(achieved / PEAK_TFLOPS["f8"], 4),
         "prepass_avg_ms": round(quant_ms, 4),
         "note": "HIP events, 200 back-to-back calls each after 20 warm-up; frac = GEMM "
-                "achieved / dense peak of the kernel's MFMA operand format (FP6 10066, FP8 "
-                "5033 TFLOP/s); frac_fp8_peak against the FP8 peak (the round-5 figure)",
+                "achieved / dense peak of the kernel's MFMA dtype (FP8 5033 TFLOP/s)",
     }
 
 
@@ -598,13 +592,11 @@ def main(argv=None):
     dense_ms = time_events(dense, sec_iters, stream)
     # dominant kernel: the GEMM, timed alone on the stream it is launched on
     if use_f8:
-        a8, sa, xs = ops.quant_act_f8(x, pw, args.act, 4, ops.f8_fmt(pw))
+        a8, sa, xs = ops.quant_act_f8(x, pw, args.act, 4)
         gemm = lambda: ops.gemm_f8(a8, sa, xs, pw, lin.bias)  # noqa: E731
-        quant = lambda: ops.quant_act_f8(x, pw, args.act, 4, ops.f8_fmt(pw))  # noqa: E731
-        kdt = "f6" if ops.f8_fmt(pw) == 6 else "f8"
-        kname = ("sqmp::gemm_f8v2_kernel<F16,2,0,6> (e2m3 on v_mfma_scale_f32_16x16x128_f8f6f4)"
-                 if kdt == "f6" else
-                 "sqmp::gemm_f8v2_kernel<F16> (e4m3 on v_mfma_scale_f32_16x16x128_f8f6f4)"
+        quant = lambda: ops.quant_act_f8(x, pw, args.act, 4)  # noqa: E731
+        kdt = "f8"
+        kname = ("sqmp::gemm_f8v2_kernel<F16> (e4m3 on v_mfma_scale_f32_16x16x128_f8f6f4)"
                  if pw.Gw % 128 == 0 else
                  "sqmp::gemm_f8_kernel<F16> (e4m3 on v_mfma_scale_f32_32x32x64_f8f6f4)")
     elif use_fqt:
@@ -668,7 +660,7 @@ def main(argv=None):
     esz = 4 if fp32 else 2
     xbytes = M * K * esz
     if use_f8:
-        wbytes = M * (pw.Kp // 4 * 3 if kdt == "f6" else pw.Kp) + M * 4 + M * pw.S_pad * 2
+        wbytes = M * pw.Kp + M * 4 + M * pw.S_pad * 2
         reads = 2 if args.act == "per_tensor" else 1
     elif use_fqt:
         Kq = (K - pw.S + 63) // 64 * 64
@@ -683,7 +675,6 @@ def main(argv=None):
     prepass_bytes = reads * xbytes + wbytes
 
     pname = ("pmc_gemm_f8v2_per_token.json" if kdt == "f8"
-             else "pmc_gemm_f6_per_token.json" if kdt == "f6"
              else "pmc_gemm_h2d_fp32.json" if fp32 and "h2d" in kname
              else "pmc_gemm_h2_fp32.json" if fp32
              else "pmc_gemm_fqt7_per_group.json" if use_fqt and "fqt7" in kname
@@ -702,8 +693,7 @@ def main(argv=None):
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": ("e2m3 codes (fp32 accumulate) + fp16 salient tail" if kdt == "f6" else
-                  "e4m3 codes (fp32 accumulate) + fp16 salient tail" if use_f8 else
+        "dtype": ("e4m3 codes (fp32 accumulate) + fp16 salient tail" if use_f8 else
                   "fp32 (fp32-accurate products from fp16 pieces on the f16 MFMA)" if fp32
                   else "fp16"),
         "data": "synthetic (random-init weights N(0,0.02^2), x N(0,1) with 1% outlier channels x30)",

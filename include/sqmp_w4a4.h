@@ -94,11 +94,7 @@ enum sqmp_act_out {
                            packed order (0 at salient / padding positions); out_scale: fp32
                            [M] (the D scale); out_xs: D [M][S_pad] exact salient x
                            (operands of sqmp_gemm_f8) */
-  SQMP_OUT_F6 = 4,      /* as SQMP_OUT_F8 with the codes as packed e2m3 (FP6): out = [M][3 Kp / 4]
-                           bytes, per 128 positions a 96-B block -- four 24-B lane chunks of
-                           32 positions (position 32 q + e at bits [6 e, 6 e + 6)), chunk q's
-                           bytes 0-15 at block offset 16 q, bytes 16-23 at 64 + 8 q (operands
-                           of sqmp_gemm_f6).  Value 4 held a different FP6 output before 0.6. */
+  /* 4: reserved (the removed FP6 code output) */
   SQMP_OUT_C4 = 5,      /* per_group activations in ACTIVATION order (operands of
                            sqmp_gemm_fqt): out = int4 codes [roundup(M, 256)][Kq / 2] bytes,
                            Kq = roundup(K - S, 64), bpack rows whose position j is the
@@ -236,21 +232,6 @@ int sqmp_gemm_f8(const void* a8, const float* ascale, const void* xs, const void
  * (fake_quant.py:308-316 then skips its statistics pass: SQMP_QA_STATS_GIVEN).
  * Gw % 128 == 0 (the 16x16x128 kernel). */
 int sqmp_gemm_f8_colmax(const void* a8, const float* ascale, const void* xs, const void* w8,
-                        const float* ws32, const void* wsal, const void* bias, void* y,
-                        int dtype, int M, int N, int Kp, int S_pad, int Gw, int ngw,
-                        uint32_t* colmax, void* stream);
-
-/* FP6 weight operand: w8 of sqmp_pack_f8 ([Np][Kp] e4m3 codes) repacked as e2m3 rows
- * [Np][3 Kp / 4] in SQMP_OUT_F6's block layout.  Once per layer. */
-int sqmp_pack_f6(const void* w8, int N, int Kp, void* w6, void* stream);
-
-/* sqmp_gemm_f8 / _colmax on FP6 operands (a6 from SQMP_OUT_F6, w6 from sqmp_pack_f6): the same
- * exact integer block sums on the e2m3 form of the scaled MFMA, which issues at ~1.8x the e4m3
- * rate; y bit-identical to sqmp_gemm_f8 on the same codes.  Gw % 128 == 0. */
-int sqmp_gemm_f6(const void* a6, const float* ascale, const void* xs, const void* w6,
-                 const float* ws32, const void* wsal, const void* bias, void* y, int dtype,
-                 int M, int N, int Kp, int S_pad, int Gw, int ngw, void* stream);
-int sqmp_gemm_f6_colmax(const void* a6, const float* ascale, const void* xs, const void* w6,
                         const float* ws32, const void* wsal, const void* bias, void* y,
                         int dtype, int M, int N, int Kp, int S_pad, int Gw, int ngw,
                         uint32_t* colmax, void* stream);

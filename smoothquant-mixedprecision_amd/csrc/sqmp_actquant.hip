@@ -1683,11 +1683,11 @@ static int quant_act_impl(void* x, int dtype, int M, int K, int amode, int n_bit
                        amode != SQMP_ACT_PER_GROUP_MEAN3STD) ||
         group_size % 64 != 0)
       return SQMP_EUNSUPPORTED;
-  } else if (out_kind == SQMP_OUT_FP || out_kind == SQMP_OUT_F8 || out_kind == SQMP_OUT_F6 ||
+  } else if (out_kind == SQMP_OUT_FP || out_kind == SQMP_OUT_F8 ||
              out_kind == SQMP_OUT_H2) {
     if (Kp < K || Kp % 128 != 0 || S_pad < S || S_pad % 64 != 0 || !out) return SQMP_EINVAL;
     if (out_kind == SQMP_OUT_H2 && (dtype != SQMP_F32 || !out_scale)) return SQMP_EINVAL;
-    if (out_kind == SQMP_OUT_F8 || out_kind == SQMP_OUT_F6) {
+    if (out_kind == SQMP_OUT_F8) {
       if (!out_scale || (S_pad > 0 && !out_xs)) return SQMP_EINVAL;
       // e4m3 holds every integer code up to 16 exactly, e2m3 up to 7; one scale per row
       if (n_bits > 4 || (amode != SQMP_ACT_PER_TOKEN && amode != SQMP_ACT_PER_TENSOR))
@@ -1770,9 +1770,9 @@ static int quant_act_impl(void* x, int dtype, int M, int K, int amode, int n_bit
     return SQMP_OK;
   };
 
-  // e4m3 (f6: packed e2m3) codes for the f8 / f6 GEMM (token / tensor scales): list-order
-  // table, lc quantizer
-  if (out_kind == SQMP_OUT_F8 || out_kind == SQMP_OUT_F6) {
+  // e4m3 codes for the f8 GEMM (token / tensor scales): list-order table, lc
+  // quantizer
+  if (out_kind == SQMP_OUT_F8) {
     if (!posmap || lc_off || !quant_lc_supported(dtype, M, K, false, 0, Kn, Kp, S_pad, x, out) ||
         ((uintptr_t)out_xs) % 16 != 0)
       return SQMP_EUNSUPPORTED;
@@ -1785,7 +1785,7 @@ static int quant_act_impl(void* x, int dtype, int M, int K, int amode, int n_bit
     SQMP_LAUNCH_CHECK();
     st = launch_quant_lc(dtype, amode == SQMP_ACT_PER_TENSOR ? 1 : 0, x, M, K, q_max, 1, lctab,
                          Kn, amap, Kp, salient, S, S_pad, cmax, nonsal, out, nullptr, 0, s,
-                         (float*)out_scale, out_xs, out_kind == SQMP_OUT_F6);
+                         (float*)out_scale, out_xs);
     if (st) return st;
     // the per-tensor maximum was read by every workgroup: clear it after the launch
     if (clean && amode == SQMP_ACT_PER_TENSOR)

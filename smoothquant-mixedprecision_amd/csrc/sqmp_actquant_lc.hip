@@ -546,7 +546,7 @@ __device__ __forceinline__ void quant_lc_body(
           }
         }
       } else if (F8) {
-        // F8 = 1 / 2: the table is in packed-POSITION order (pos_table_kernel), so this thread's
+        // F8 = 1: the table is in packed-POSITION order (pos_table_kernel), so this thread's
         // RPL codes are positions rb .. rb + RPL - 1 of both rows: packed in registers and
         // stored straight to global memory (no LDS scatter, no second pass)
         if (rb < P) {
@@ -563,21 +563,6 @@ __device__ __forceinline__ void quant_lc_body(
             w0[d] = lo0 | hi0;
             w1[d] = lo1 | hi1;
           }
-          if constexpr (F8 == 2) {
-            // F8 = 2 (SQMP_OUT_F6): the same codes as packed e2m3 rows of 3 P / 4 bytes
-            // (f6_store16's block layout)
-            const size_t pitch = (size_t)(P / 4) * 3;
-            uint32_t pk[3];
-#pragma unroll
-            for (int d = 0; d < RPL / 16; ++d) {
-              f6_pack16(&w0[4 * d], pk);
-              f6_store16((unsigned char*)out + (size_t)m0 * pitch, rb + 16 * d, pk);
-              if (has1) {
-                f6_pack16(&w1[4 * d], pk);
-                f6_store16((unsigned char*)out + (size_t)(m0 + 1) * pitch, rb + 16 * d, pk);
-              }
-            }
-          } else {
           unsigned char* b0p = (unsigned char*)out + (size_t)m0 * P + rb;
 #pragma unroll
           for (int d = 0; d < RPL / 16; ++d)
@@ -587,7 +572,6 @@ __device__ __forceinline__ void quant_lc_body(
 #pragma unroll
             for (int d = 0; d < RPL / 16; ++d)
               ((u32x4*)b1p)[d] = u32x4{w1[4 * d], w1[4 * d + 1], w1[4 * d + 2], w1[4 * d + 3]};
-          }
           }
         }
         if (tid == 0) {
@@ -953,7 +937,7 @@ static int quant_lc_launch(const void* x, int M, int K, int q_max, int G, const 
   const void* kf = (const void*)quant_lc_kernel<DT, MODE, LC_RPL, GS, F8, NOUT>;
   int nw = lc_waves(K, Kn);
   // F8: every packed position is some thread's (position-order table)
-  if ((F8 == 1 || F8 == 2) && cdiv(P, 64 * LC_RPL) > nw) nw = cdiv(P, 64 * LC_RPL);
+  if (F8 == 1 && cdiv(P, 64 * LC_RPL) > nw) nw = cdiv(P, 64 * LC_RPL);
   if (nw > LC_MAXW) return SQMP_EUNSUPPORTED;
   const size_t lds = sizeof(uint32_t) * lc_lds_words(P, S_pad, NOUT);
   SQMP_HIP_CHECK(hipFuncSetAttribute(kf, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
@@ -965,7 +949,7 @@ static int quant_lc_launch(const void* x, int M, int K, int q_max, int G, const 
   // the e4m3 output (row-major, no 32-row blocks to keep together): runs of 3 pairs where the
   // pairs exceed one round of slots -- config 2 per_token 46.4 -> 43.3 us against runs of 8
   // (1 / 2 / 4 / 5 / 6 pairs: 46.5 / 47.5 / 43.9 / 44.3 / 45.7 us; profiles/r05_ab_lc_ppw.txt)
-  if ((F8 == 1 || F8 == 2) && npair > 256 * per_cu) grid = cdiv(npair, 3);
+  if (F8 == 1 && npair > 256 * per_cu) grid = cdiv(npair, 3);
   if (const char* e = knob("SQMP_LC_PPW"))  // (A/B: exact row pairs per workgroup)
     if (atoi(e) > 0) grid = cdiv(npair, atoi(e));
   quant_lc_kernel<DT, MODE, LC_RPL, GS, F8, NOUT><<<dim3(grid), dim3(64 * nw), lds, s>>>(
@@ -993,17 +977,15 @@ int launch_quant_lc(int dtype, int mode, const void* x, int M, int K, int q_max,
                     const uint32_t* lctab, int Kn, const int32_t* amap, int P,
                     const int32_t* sal, int S, int S_pad, const uint32_t* cmax,
                     const int32_t* nonsal, void* out, uint32_t* key_clear, int clear_words,
-                    hipStream_t s, float* out_scale, void* out_xs, bool f6) {
+                    hipStream_t s, float* out_scale, void* out_xs) {
 #define SQMP_LC(DTT, MD, GSV, F8V)                                                           \
   quant_lc_launch<DTT, MD, GSV, F8V>(x, M, K, q_max, G, lctab, Kn, amap, P, sal, S, S_pad,   \
                                      cmax, nonsal, out, key_clear, clear_words, out_scale,  \
                                      out_xs, s)
 #define SQMP_LC_MODE(DTT)                                                                  \
-  (out_scale ? (mode == LC_MODE_TOKEN && f6   ? SQMP_LC(DTT, LC_MODE_TOKEN, 0, 2)          \
-                : mode == LC_MODE_TENSOR && f6 ? SQMP_LC(DTT, LC_MODE_TENSOR, 0, 2)         \
-                : mode == LC_MODE_TOKEN        ? SQMP_LC(DTT, LC_MODE_TOKEN, 0, 1)          \
-                : mode == LC_MODE_TENSOR       ? SQMP_LC(DTT, LC_MODE_TENSOR, 0, 1)         \
-                                               : SQMP_EUNSUPPORTED)                         \
+  (out_scale ? (mode == LC_MODE_TOKEN    ? SQMP_LC(DTT, LC_MODE_TOKEN, 0, 1)               \
+                : mode == LC_MODE_TENSOR ? SQMP_LC(DTT, LC_MODE_TENSOR, 0, 1)              \
+                                         : SQMP_EUNSUPPORTED)                              \
    : mode == LC_MODE_TOKEN ? SQMP_LC(DTT, LC_MODE_TOKEN, 0, 0)                             \
    : mode == LC_MODE_TENSOR ? SQMP_LC(DTT, LC_MODE_TENSOR, 0, 0)                           \
    : G < LC_RPL ? SQMP_LC(DTT, LC_MODE_GROUP, 8, 0) : SQMP_LC(DTT, LC_MODE_GROUP, 0, 0))

@@ -297,14 +297,7 @@ __device__ inline i32x8b cat8(const u32x4& a, const u32x4& b) {
 // DIAG (timing diagnostics, wrong results by design, only in a SQMP_DIAG_BUILD): 1 the code
 // stages' DMA from two L2-hot stages, 2 no code-stage DMA after the first two stages, 3 no
 // per-group fold (the MFMA accumulates straight into the totals)
-// FMT 6 (sqmp_gemm_f6): both code operands as packed e2m3 rows (f6_store16's layout, 96 B per
-// 128 positions) -- the same exact integer block sums at the FP6 rate of the scaled MFMA.  A
-// code stage's images are 256 rows x 96 B, dense (24 one-KiB DMA pieces per operand, three
-// per wave); in row r the two tail chunks trade places when bit 3 of r is set, which makes the
-// fragment reads (a ds_read_b128 of the head, a ds_read_b64 of the tail) conflict-free for
-// both lane-group patterns of the LDS (MI355X_MICROARCH.md §LDS; the dense 96-B pitch alone
-// leaves the b64 reads two-way).  Same fold, tail and epilogue: y is bit-identical to FMT 8.
-template <class DT, int OPT = 0, int DIAG = 0, int FMT = 8>
+template <class DT, int OPT = 0, int DIAG = 0>
 __global__ __launch_bounds__(512, 1) void gemm_f8v2_kernel(
     const unsigned char* __restrict__ A8, const float* __restrict__ ascale,
     const typename DT::T* __restrict__ XS, const unsigned char* __restrict__ W8,
@@ -313,13 +306,11 @@ __global__ __launch_bounds__(512, 1) void gemm_f8v2_kernel(
     int Kp, int S_pad, int Gw, int ngw, int tiles_m, int tiles_n, int group_m,
     uint32_t* __restrict__ colmax, int nt) {
   typedef typename DT::T T;
-  static_assert(FMT == 8 || (FMT == 6 && DIAG == 0), "FMT: 8 (e4m3) or 6 (e2m3)");
   __shared__ __attribute__((aligned(16))) unsigned char lds[V2_NSLOT * V2_SLOT];
 
   int tm, tn;
   tile_coords(tiles_m, tiles_n, group_m, tm, tn);
   const int m0 = tm * 256, n0 = tn * 256;
-  const int ldc = FMT == 6 ? Kp / 4 * 3 : Kp;  // code row pitch (bytes)
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 2, wn = wave & 3;
@@ -330,8 +321,8 @@ __global__ __launch_bounds__(512, 1) void gemm_f8v2_kernel(
   // ---- DMA geometry: piece p = 4 w + j moves rows 8p .. 8p + 7 of a 256 x 128 B image;
   // lane L writes row 8p + (L >> 3), physical chunk L & 7 = logical chunk (L & 7) ^ v2_sw
   // (offsets recomputed per stage: a few VALU ops instead of 12 live VGPRs)
-  const i32x4b rA = rsrc_of(A8 + (size_t)m0 * ldc, 0xFFFFFFFFu);
-  const i32x4b rW = rsrc_of(W8 + (size_t)n0 * ldc, 0xFFFFFFFFu);
+  const i32x4b rA = rsrc_of(A8 + (size_t)m0 * Kp, 0xFFFFFFFFu);
+  const i32x4b rW = rsrc_of(W8 + (size_t)n0 * Kp, 0xFFFFFFFFu);
   const i32x4b rX = rsrc_of(XS + (size_t)m0 * S_pad, 0xFFFFFFFFu);
   const i32x4b rL = rsrc_of(wsal, 0xFFFFFFFFu);
   const i32x4b rS = rsrc_of(ws32 + n0, 0xFFFFFFFFu);
@@ -347,20 +338,7 @@ __global__ __launch_bounds__(512, 1) void gemm_f8v2_kernel(
       const int r0 = 32 * w + (lane >> 3);
       auto row = [&](int j) { return r0 + 8 * j; };
       auto ch = [&](int j) { return (uint32_t)(((lane & 7) ^ v2_sw(row(j))) << 4); };
-      if (FMT == 6 && kt < nk8) {
-        // image chunk o = 64 p + lane of the 24 pieces: row o / 6, physical chunk o % 6
-        const uint32_t so = (uint32_t)kt * 96;
-#pragma unroll
-        for (int j = 0; j < 3; ++j) {
-          const int p = 3 * w + j, o = 64 * p + lane;
-          const int r = (o * 10923) >> 16;  // o / 6 (exact for o < 1536)
-          const int pc = o - 6 * r;
-          const int lc = pc < 4 ? pc : 4 + ((pc - 4) ^ ((r >> 3) & 1));
-          const uint32_t v = (uint32_t)r * ldc + lc * 16;
-          dma16(rA, v, so, slot + V2_A + p * 1024);
-          dma16(rW, v, so, slot + V2_B + p * 1024);
-        }
-      } else if (kt < nk8) {
+      if (kt < nk8) {
         if (DIAG == 2 && kt >= 2) continue;
         const uint32_t so = (uint32_t)(DIAG == 1 && kt >= 2 ? (kt & 1) : kt) * 128;
 #pragma unroll
@@ -398,31 +376,18 @@ __global__ __launch_bounds__(512, 1) void gemm_f8v2_kernel(
 
   const int wcol0 = wn * 64 + r16;   // + 16 j: the lane's weight row in the B image
   const int xrow0 = wm * 128 + r16;  // + 16 i: the lane's activation row in the A image
-  // (FMT 6) lane q's fragment of image row r: its head chunk q and half q & 1 of tail chunk
-  // 4 + ((q >> 1) ^ (r >> 3 & 1)); rows r and r + 16 k share the swizzle
-  const int f6_tail = 16 * (4 + ((q >> 1) ^ ((r16 >> 3) & 1))) + 8 * (q & 1);
-  auto frag6 = [&](const unsigned char* img, int r) {
-    const u32x4 h = *(const u32x4*)(img + r * 96 + 16 * q);
-    const uint2 t = *(const uint2*)(img + r * 96 + f6_tail);
-    return i32x8b{(int)h[0], (int)h[1], (int)h[2], (int)h[3], (int)t.x, (int)t.y, 0, 0};
-  };
-  constexpr int MF = FMT == 6 ? 2 : 0;  // the scaled MFMA's operand format (cbsz / blgp)
   auto compute_f8 = [&](const unsigned char* __restrict__ slot) {
     i32x8b bw[4];
     f32x4 sv[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int c = wcol0 + 16 * j;
-      if constexpr (FMT == 6)
-        bw[j] = frag6(slot + V2_B, c);
-      else
-        bw[j] = cat8(*(const u32x4*)(slot + V2_B + v2_off(c, 2 * q)),
-                     *(const u32x4*)(slot + V2_B + v2_off(c, 2 * q + 1)));
+      bw[j] = cat8(*(const u32x4*)(slot + V2_B + v2_off(c, 2 * q)),
+                   *(const u32x4*)(slot + V2_B + v2_off(c, 2 * q + 1)));
       sv[j] = *(const f32x4*)(slot + V2_S + (wn * 64 + 16 * j + 4 * q) * 4);
     }
     auto ald = [&](int i) {
       const int r = xrow0 + 16 * i;
-      if constexpr (FMT == 6) return frag6(slot + V2_A, r);
       return cat8(*(const u32x4*)(slot + V2_A + v2_off(r, 2 * q)),
                   *(const u32x4*)(slot + V2_A + v2_off(r, 2 * q + 1)));
     };
@@ -451,7 +416,7 @@ __global__ __launch_bounds__(512, 1) void gemm_f8v2_kernel(
       const int i = u >> 2, j = u & 3;
       if (u < 32) {
         if (j == 0 && i + 1 < 8) ax[(i + 1) & 1] = ald(i + 1);
-        t[u % 3] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(bw[j], ax[i & 1], zero, MF, MF, 0, 127, 0, 127);
+        t[u % 3] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(bw[j], ax[i & 1], zero, 0, 0, 0, 127, 0, 127);
         __builtin_amdgcn_sched_barrier(0);
       }
       if (u >= 2) {
@@ -647,35 +612,9 @@ __global__ __launch_bounds__(256) void pack_f8_kernel(const uint32_t* __restrict
   if (t < (size_t)ngw * Np) ws32[t] = DT::to_f(wscale[t]);
 }
 
-// e4m3 code rows [Np][Kp] -> packed e2m3 rows [Np][3 Kp / 4] (f6_store16's layout): one
-// thread per 16 positions
-__global__ __launch_bounds__(256) void pack_f6_kernel(const uint32_t* __restrict__ w8, int Np,
-                                                      int Kp, unsigned char* __restrict__ w6) {
-  const size_t t = (size_t)blockIdx.x * 256 + threadIdx.x;
-  const int per_row = Kp / 16;
-  if (t >= (size_t)Np * per_row) return;
-  const int n = (int)(t / per_row), pos = (int)(t % per_row) * 16;
-  const u32x4 v = *(const u32x4*)(w8 + ((size_t)n * Kp + pos) / 4);
-  const uint32_t w[4] = {v[0], v[1], v[2], v[3]};
-  uint32_t p[3];
-  f6_pack16(w, p);
-  f6_store16(w6 + (size_t)n * (Kp / 4 * 3), pos, p);
-}
-
 }  // namespace sqmp
 
 using namespace sqmp;
-
-extern "C" int sqmp_pack_f6(const void* w8, int N, int Kp, void* w6, void* stream) {
-  SQMP_DEVICE_GUARD(stream);
-  if (!w8 || !w6 || N <= 0 || Kp <= 0 || Kp % 128 != 0) return SQMP_EINVAL;
-  const int Np = pad_n(N);
-  const size_t n = (size_t)Np * (Kp / 16);
-  pack_f6_kernel<<<dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream>>>(
-      (const uint32_t*)w8, Np, Kp, (unsigned char*)w6);
-  SQMP_LAUNCH_CHECK();
-  return SQMP_OK;
-}
 
 extern "C" int sqmp_pack_f8(const void* codes, const void* wscale, int dtype, int N, int Kp,
                             int ngw, void* w8, float* ws32, void* stream) {
@@ -703,7 +642,7 @@ extern "C" int sqmp_pack_f8(const void* codes, const void* wscale, int dtype, in
 static int gemm_f8_impl(const void* a8, const float* ascale, const void* xs, const void* w8,
                         const float* ws32, const void* wsal, const void* bias, void* y,
                         int dtype, int M, int N, int Kp, int S_pad, int Gw, int ngw,
-                        uint32_t* colmax, void* stream, int fmt = 8) {
+                        uint32_t* colmax, void* stream) {
   if (M < 0 || N <= 0 || Kp <= 0 || Kp % 128 != 0 || S_pad < 0 || S_pad % 64 != 0)
     return SQMP_EINVAL;
   if (!a8 || !ascale || !w8 || !ws32 || !y || (S_pad > 0 && (!xs || !wsal))) return SQMP_EINVAL;
@@ -716,9 +655,8 @@ static int gemm_f8_impl(const void* a8, const float* ascale, const void* xs, con
   // Gw % 128 == 0 runs the 16x16x128 kernel (SQMP_F8_V1=1 keeps the 32x32x64 one, A/B)
   const char* v1e = knob("SQMP_F8_V1");
   const bool v1_only = v1e && atoi(v1e) != 0;
-  const bool v2 = Gw % 128 == 0 && (!v1_only || fmt == 6);
+  const bool v2 = Gw % 128 == 0 && !v1_only;
   if (colmax && !v2) return SQMP_EUNSUPPORTED;  // fused statistics: the 16x16x128 kernel only
-  if (fmt == 6 && Gw % 128 != 0) return SQMP_EUNSUPPORTED;  // FP6: the 16x16x128 kernel only
   // M-tiles per raster group (SQMP_GROUP_M: A/B knob, read per launch)
   const char* ge = knob("SQMP_GROUP_M");
   const int group_m = ge && atoi(ge) > 0 ? atoi(ge) : 4;
@@ -728,11 +666,7 @@ static int gemm_f8_impl(const void* a8, const float* ascale, const void* xs, con
   const char* oe = knob("SQMP_F8_OPT");
   const int opt = oe ? atoi(oe) & 3 : 2;
 #define SQMP_F8V2(DTT, O)                                                                    \
-  if (fmt == 6) gemm_f8v2_kernel<DTT, O, 0, 6><<<grid, block, 0, s>>>(                       \
-      (const unsigned char*)a8, ascale, (const DTT::T*)xs, (const unsigned char*)w8, ws32,   \
-      (const DTT::T*)wsal, (const DTT::T*)bias, (DTT::T*)y, M, N, Kp, S_pad, Gw, ngw, tiles_m, \
-      tiles_n, group_m, colmax, nt ? 1 : 0);                                                 \
-  else gemm_f8v2_kernel<DTT, O><<<grid, block, 0, s>>>(                                      \
+  gemm_f8v2_kernel<DTT, O><<<grid, block, 0, s>>>(                                           \
       (const unsigned char*)a8, ascale, (const DTT::T*)xs, (const unsigned char*)w8, ws32,   \
       (const DTT::T*)wsal, (const DTT::T*)bias, (DTT::T*)y, M, N, Kp, S_pad, Gw, ngw, tiles_m, \
       tiles_n, group_m, colmax, nt ? 1 : 0)
@@ -744,7 +678,7 @@ static int gemm_f8_impl(const void* a8, const float* ascale, const void* xs, con
       (const unsigned char*)a8, ascale, (const DTT::T*)xs, (const unsigned char*)w8, ws32,   \
       (const DTT::T*)wsal, (const DTT::T*)bias, (DTT::T*)y, M, N, Kp, S_pad, Gw, ngw, tiles_m, \
       tiles_n, group_m, colmax, nt ? 1 : 0)
-  if (v2 && fmt == 8 && dtype == SQMP_F16 && diag > 0) {
+  if (v2 && dtype == SQMP_F16 && diag > 0) {
     if (diag == 1) SQMP_F8D(F16, 1); else if (diag == 2) SQMP_F8D(F16, 2); else SQMP_F8D(F16, 3);
     SQMP_LAUNCH_CHECK();
     return SQMP_OK;
@@ -782,26 +716,6 @@ extern "C" int sqmp_gemm_f8(const void* a8, const float* ascale, const void* xs,
   SQMP_DEVICE_GUARD(stream);
   return gemm_f8_impl(a8, ascale, xs, w8, ws32, wsal, bias, y, dtype, M, N, Kp, S_pad, Gw, ngw,
                       nullptr, stream);
-}
-
-// sqmp_gemm_f8 on packed e2m3 operands (SQMP_OUT_F6 + sqmp_pack_f6); Gw % 128 == 0
-extern "C" int sqmp_gemm_f6(const void* a6, const float* ascale, const void* xs, const void* w6,
-                            const float* ws32, const void* wsal, const void* bias, void* y,
-                            int dtype, int M, int N, int Kp, int S_pad, int Gw, int ngw,
-                            void* stream) {
-  SQMP_DEVICE_GUARD(stream);
-  return gemm_f8_impl(a6, ascale, xs, w6, ws32, wsal, bias, y, dtype, M, N, Kp, S_pad, Gw, ngw,
-                      nullptr, stream, 6);
-}
-
-extern "C" int sqmp_gemm_f6_colmax(const void* a6, const float* ascale, const void* xs,
-                                   const void* w6, const float* ws32, const void* wsal,
-                                   const void* bias, void* y, int dtype, int M, int N, int Kp,
-                                   int S_pad, int Gw, int ngw, uint32_t* colmax, void* stream) {
-  SQMP_DEVICE_GUARD(stream);
-  if (!colmax) return SQMP_EINVAL;
-  return gemm_f8_impl(a6, ascale, xs, w6, ws32, wsal, bias, y, dtype, M, N, Kp, S_pad, Gw, ngw,
-                      colmax, stream, 6);
 }
 
 // sqmp_gemm_f8 with the fused output-quant statistics (as sqmp_gemm_fq_colmax); Gw % 128 == 0

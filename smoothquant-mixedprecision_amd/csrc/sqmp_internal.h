@@ -52,52 +52,6 @@ __device__ inline void store_h2x8(uint16_t* p, size_t hplane, const float* r, in
       u32x4{l[0] | (l[1] << 16), l[2] | (l[3] << 16), l[4] | (l[5] << 16), l[6] | (l[7] << 16)};
 }
 
-// ---- FP6 (e2m3) code operands of the block-scaled MFMA (SQMP_OUT_F6, sqmp_pack_f6,
-// sqmp_gemm_f6).  Every 4-bit code |c| <= 7 is exact in e2m3, and the 16x16x128 scaled MFMA
-// takes e2m3 operands at 1.7-1.8x its e4m3 rate (profiles/r06_mfma_rate_asm_probe.txt).
-// A row of P codes (P % 128 == 0) is P / 128 blocks of 96 B; block b holds positions
-// 128 b .. 128 b + 127 as four 32-position lane chunks q (the MFMA's K slice of lane group q):
-// chunk q is 24 B, position 32 q + e at bits [6 e, 6 e + 6) of its 192-bit little-endian
-// value; its bytes 0-15 (the head) sit at block bytes 16 q, its bytes 16-23 (the tail) at
-// 64 + 8 q -- one ds_read_b128 and one ds_read_b64 per MFMA fragment.
-
-// 4 e4m3 code bytes (|c| <= 7) -> 4 e2m3 codes, one per byte: the magnitude's exponent
-// rebias (e4m3 0x38 = 1.0, e2m3 0x08 = 1.0: minus 0x30 for every nonzero magnitude), the
-// sign from bit 7 to bit 5
-__device__ inline uint32_t e4m3x4_to_e2m3x4(uint32_t w) {
-  const uint32_t m = w & 0x7F7F7F7Fu;
-  const uint32_t nz = ((m + 0x7F7F7F7Fu) & 0x80808080u) >> 7;  // 1 per nonzero byte (m <= 0x4E)
-  return (m - nz * 0x30u) | ((w & 0x80808080u) >> 2);
-}
-// 4 six-bit values (one per byte) -> 24 bits, value i at bits [6 i, 6 i + 6)
-__device__ inline uint32_t pack6x4(uint32_t x) {
-  return (x & 0x3Fu) | ((x >> 2) & 0xFC0u) | ((x >> 4) & 0x3F000u) | ((x >> 6) & 0xFC0000u);
-}
-// 16 consecutive e4m3 codes (4 dwords, position order) -> their 12 packed e2m3 bytes
-__device__ inline void f6_pack16(const uint32_t w[4], uint32_t p[3]) {
-  const uint32_t y0 = pack6x4(e4m3x4_to_e2m3x4(w[0])), y1 = pack6x4(e4m3x4_to_e2m3x4(w[1]));
-  const uint32_t y2 = pack6x4(e4m3x4_to_e2m3x4(w[2])), y3 = pack6x4(e4m3x4_to_e2m3x4(w[3]));
-  p[0] = y0 | (y1 << 24);
-  p[1] = (y1 >> 8) | (y2 << 16);
-  p[2] = (y2 >> 16) | (y3 << 8);
-}
-// store the packed 16 codes of positions pos .. pos + 15 (pos % 16 == 0) of an F6 row
-__device__ inline void f6_store16(unsigned char* row, int pos, const uint32_t p[3]) {
-  unsigned char* blk = row + (size_t)(pos >> 7) * 96;
-  const int q = (pos >> 5) & 3;
-  if ((pos & 16) == 0) {  // chunk bytes 0-11: head dwords 0-2
-    uint32_t* h = (uint32_t*)(blk + 16 * q);
-    h[0] = p[0];
-    h[1] = p[1];
-    h[2] = p[2];
-  } else {  // chunk bytes 12-23: head dword 3, then the 8-B tail
-    *(uint32_t*)(blk + 16 * q + 12) = p[0];
-    uint32_t* t = (uint32_t*)(blk + 64 + 8 * q);
-    t[0] = p[1];
-    t[1] = p[2];
-  }
-}
-
 // cmax[c] = bits(max_r |x[r][c]|) over a contiguous D matrix [R][C] (fp32 bits of the
 // D value; non-negative floats order like their bit patterns).  Zeroes cmax first.
 int launch_colmax(const void* x, int dtype, int R, int C, uint32_t* cmax, hipStream_t s,
@@ -154,8 +108,7 @@ int launch_quant_lc(int dtype, int mode, const void* x, int M, int K, int q_max,
                     const uint32_t* lctab, int Kn, const int32_t* amap, int P,
                     const int32_t* sal, int S, int S_pad, const uint32_t* cmax,
                     const int32_t* nonsal, void* out, uint32_t* key_clear, int clear_words,
-                    hipStream_t s, float* out_scale = nullptr, void* out_xs = nullptr,
-                    bool f6 = false);  // out_scale: the e4m3 (f6: packed e2m3) code output
+                    hipStream_t s, float* out_scale = nullptr, void* out_xs = nullptr);
 // key_clear: zeroed (clear_words % 4 == 0), may be NULL.  out_scale != NULL selects the
 // e4m3 code output (token / tensor modes): out = codes [M][P], out_xs = D [M][S_pad].
 // group mode with up to two sibling outputs (sib.n), fp16 / bf16, G >= 16

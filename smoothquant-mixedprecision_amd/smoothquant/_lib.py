@@ -25,7 +25,7 @@ ACT_PER_TOKEN, ACT_PER_TENSOR, ACT_PER_GROUP, ACT_PER_GROUP_UNSORTED = 0, 1, 2, 
 ACT_PER_GROUP_MEAN3STD = 4
 W_PER_CHANNEL, W_PER_TENSOR, W_PER_GROUP, W_PER_GROUP_UNSORTED, W_NONE = 0, 1, 2, 3, 4
 W_PER_GROUP_MEAN3STD = 5
-OUT_FP, OUT_INPLACE, OUT_F8, OUT_F6, OUT_C4, OUT_H2 = 0, 2, 3, 4, 5, 6
+OUT_FP, OUT_INPLACE, OUT_F8, OUT_C4, OUT_H2 = 0, 2, 3, 5, 6
 QA_CLEAN_WS, QA_REUSE_STATS, QA_STATS_GIVEN, QA_TILED, QA_TILED4 = 1, 2, 4, 8, 16
 
 _vp, _i, _sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t
@@ -66,11 +66,6 @@ SIGNATURES = {
                           _vp]),
     "sqmp_gemm_f8_colmax": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i,
                                  _i, _vp, _vp]),
-    "sqmp_gemm_f6": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i,
-                          _vp]),
-    "sqmp_gemm_f6_colmax": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i,
-                                 _i, _vp, _vp]),
-    "sqmp_pack_f6": (_i, [_vp, _i, _i, _vp, _vp]),
     "sqmp_quant_act_c4": (_i, [_vp, _i, _i, _i, _i, _i, _i, _vp, _i, _vp, _vp, _i, _i, _vp, _i,
                                _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _vp, _vp, _sz, _vp]),
     "sqmp_perm_weight_c4": (_i, [_vp, _i, _i, _i, _i, _vp, _vp, _vp, _i, _i, _i, _i, _vp, _vp]),

@@ -524,7 +524,7 @@ class W4A4Linear(nn.Module):
         use_h2 = (not use_f8 and not use_fqt and self.kernel == "auto"
                   and ops.h2_planes_ok(pw, amode, x2.shape[0], ag))
         if use_f8:
-            a8, sa, xs = ops.quant_act_f8(xc, pw, amode, bits, ops.f8_fmt(pw))
+            a8, sa, xs = ops.quant_act_f8(xc, pw, amode, bits)
         elif use_fqt:
             c4 = ops.quant_act_c4(xc, pw, amode, bits, ag, stats_of=x)
         elif use_h2:

@@ -91,7 +91,6 @@ class PackedWeight:
     sal_key: Optional[tuple] = field(default=None)        # identity of the salient set (host)
     w8: Optional[torch.Tensor] = field(default=None)     # uint8 [Np, Kp] e4m3 codes (f8 GEMM)
     ws32: Optional[torch.Tensor] = field(default=None)   # fp32 [ngw, Np] scales (f8 GEMM)
-    w6: Optional[torch.Tensor] = field(default=None)     # uint8 [Np, 3 Kp / 4] e2m3 (f6 GEMM)
     fq7: Optional[tuple] = field(default=None)           # (codes_t, scale_t, sal_t, J) of gemm_fq7
     h2: Optional[tuple] = field(default=None)            # (f16 [2, Np, L], int32 [Np]) (gemm_h2)
     h2d: Optional[torch.Tensor] = field(default=None)    # f16 tile-major planes (gemm_h2d)
@@ -833,38 +832,13 @@ def f8_operands(pw: PackedWeight):
     return pw.w8, _ws32(pw)
 
 
-def f6_operand(pw: PackedWeight) -> torch.Tensor:
-    """The weight codes as packed e2m3 rows [Np, 3 Kp / 4] (sqmp_pack_f6 of the e4m3 codes),
-    built once per packed weight."""
-    if pw.w6 is None:
-        w8, _ = f8_operands(pw)
-        w6 = torch.empty((pad_n(pw.N), pw.Kp // 4 * 3), dtype=torch.uint8, device=w8.device)
-        check(load().sqmp_pack_f6(_p(w8), pw.N, pw.Kp, _p(w6), _stream(w8)), "pack_f6")
-        pw.w6 = w6
-    return pw.w6
-
-
-def f8_fmt(pw: PackedWeight) -> int:
-    """The code format of the low-precision per_token / per_tensor path: 6 -- e2m3 operands
-    (SQMP_OUT_F6 + sqmp_gemm_f6, the scaled MFMA at its FP6 rate; y bit-identical to the e4m3
-    kernel) wherever the 16x16x128 kernel runs (Gw % 128 == 0); else 8 (e4m3).
-    SQMP_F8_FMT=8 keeps e4m3 (A/B), read per call."""
-    if pw.Gw % 128 != 0 or os.environ.get("SQMP_F8_V1") == "1":
-        return 8
-    return 8 if os.environ.get("SQMP_F8_FMT") == "8" else 6
-
-
-def quant_act_f8(x2: torch.Tensor, pw: PackedWeight, act_quant: str, n_bits: int,
-                 fmt: int = 8):
-    """x [M, K] -> (codes in packed order, fp32 row scales [M], exact salient x [M, S_pad])
-    for gemm_f8 (per_token / per_tensor, n_bits <= 4): fmt 8 -- e4m3 bytes [M, Kp]; fmt 6 --
-    packed e2m3 rows [M, 3 Kp / 4] (SQMP_OUT_F6's block layout; f8_fmt)."""
+def quant_act_f8(x2: torch.Tensor, pw: PackedWeight, act_quant: str, n_bits: int):
+    """x [M, K] -> (e4m3 codes [M, Kp] in packed order, fp32 row scales [M], exact salient
+    x [M, S_pad]) for gemm_f8 (per_token / per_tensor, n_bits <= 4)."""
     _require_gpu(x2, "quant_act")
-    if fmt not in (6, 8):
-        raise ValueError(f"fmt must be 6 or 8, got {fmt}")
     M, K = x2.shape
     Mp = _pad_rows(M)
-    width = pw.Kp if fmt == 8 else pw.Kp // 4 * 3
+    width = pw.Kp
     a8 = torch.empty((Mp, width), dtype=torch.uint8, device=x2.device)[:M]
     sa = torch.empty((M,), dtype=torch.float32, device=x2.device)
     xs = torch.empty((Mp, max(pw.S_pad, 8)), dtype=x2.dtype, device=x2.device)[:M]
@@ -876,8 +850,7 @@ def quant_act_f8(x2: torch.Tensor, pw: PackedWeight, act_quant: str, n_bits: int
         pw.posmap = build_posmap(pw.perm, K)
     status = lib.sqmp_quant_act_v2(_p(x2), _dtype_code(x2.dtype), M, K, ACT_MODES[act_quant],
                                    n_bits, 0, _p(pw.amap), pw.Kp, _p(pw.nonsal), _p(pw.salient),
-                                   pw.S, pw.S_pad, _p(pw.posmap), _lib.QA_CLEAN_WS,
-                                   _lib.OUT_F8 if fmt == 8 else _lib.OUT_F6,
+                                   pw.S, pw.S_pad, _p(pw.posmap), _lib.QA_CLEAN_WS, _lib.OUT_F8,
                                    _p(a8), _p(sa), _p(xs), _p(e["buf"]), e["buf"].numel(),
                                    ctypes.c_void_p(stream))
     if status != _lib.SQMP_OK:
@@ -895,23 +868,17 @@ def f8_colmax_ok(pw: PackedWeight) -> bool:
 
 def gemm_f8(a8: torch.Tensor, sa: torch.Tensor, xs: torch.Tensor, pw: PackedWeight,
             bias: Optional[torch.Tensor], colmax: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """a8: quant_act_f8's codes, e4m3 ([M, Kp]: sqmp_gemm_f8) or packed e2m3 ([M, 3 Kp / 4]:
-    sqmp_gemm_f6, bit-identical y).  colmax (Gw % 128 == 0): as gemm_fq's fused output-quant
-    statistics."""
+    """colmax (Gw % 128 == 0): as gemm_fq's fused output-quant statistics."""
     M = a8.shape[0]
-    f6 = a8.shape[1] != pw.Kp
     w8, ws32 = f8_operands(pw)
-    wc = f6_operand(pw) if f6 else w8
     y = torch.empty((M, pw.N), dtype=pw.dtype, device=a8.device)
-    args = (_p(a8), _p(sa), _p(xs) if pw.S_pad else None, _p(wc), _p(ws32),
+    args = (_p(a8), _p(sa), _p(xs) if pw.S_pad else None, _p(w8), _p(ws32),
             _p(pw.wsal) if pw.S_pad else None, _p(bias), _p(y), _dtype_code(pw.dtype), M, pw.N,
             pw.Kp, pw.S_pad, pw.Gw, pw.ngw)
-    lib = load()
     if colmax is None:
-        check((lib.sqmp_gemm_f6 if f6 else lib.sqmp_gemm_f8)(*args, _stream(a8)), "gemm_f8")
+        check(load().sqmp_gemm_f8(*args, _stream(a8)), "gemm_f8")
     else:
-        check((lib.sqmp_gemm_f6_colmax if f6 else lib.sqmp_gemm_f8_colmax)(
-            *args, _p(colmax), _stream(a8)), "gemm_f8")
+        check(load().sqmp_gemm_f8_colmax(*args, _p(colmax), _stream(a8)), "gemm_f8")
     return y
 
 

@@ -154,115 +154,3 @@ def test_per_token_k_not_multiple_of_8_falls_back():
         want = D.f32(O.w4a4_forward(x, w_hat, b, "per_token", 4, 128, sal, False, D))
         y = to_np(q(to_t(x, "fp16", dev)))
         assert rel(y, want) < 2e-3
-
-
-def e2m3_rows_to_float(b, P):
-    """Packed e2m3 rows [R][3 P / 4] (SQMP_OUT_F6 / sqmp_pack_f6 block layout) -> values [R][P]:
-    per 128 positions a 96-B block, lane chunk q's 24 bytes = head at 16 q + tail at 64 + 8 q,
-    position 32 q + e at bits [6 e, 6 e + 6)."""
-    b = np.asarray(b, np.uint8)
-    R = b.shape[0]
-    blk = b[:, :P // 128 * 96].reshape(R, P // 128, 96)
-    out = np.zeros((R, P // 128, 4, 32), np.float64)
-    for q in range(4):
-        chunk = np.concatenate([blk[:, :, 16 * q:16 * q + 16], blk[:, :, 64 + 8 * q:72 + 8 * q]], axis=2)
-        bits = np.unpackbits(chunk, axis=2, bitorder="little")  # [R, nb, 192]
-        code = np.zeros(bits.shape[:2] + (32,), np.int64)
-        for k in range(6):
-            code |= bits[:, :, k::6][:, :, :32].astype(np.int64) << k
-        s = np.where(code >> 5, -1.0, 1.0)
-        e = (code >> 3) & 3
-        m = code & 7
-        out[:, :, q, :] = s * np.where(e == 0, m / 8.0, (1 + m / 8.0) * 2.0 ** (e - 1))
-    return out.reshape(R, P)
-
-
-F6_CASES = [c for c in OPERAND_CASES if c[3] % 128 == 0]
-
-
-@pytest.mark.parametrize("case", F6_CASES, ids=[f"{c[0]}-{c[1]}-p{c[2]}-G{c[3]}-{c[4]}x{c[5]}" for c in F6_CASES])
-def test_f6_operands_equal_f8(case):
-    """SQMP_OUT_F6: the packed e2m3 codes decode to the e4m3 output's codes exactly, with the
-    same row scales and salient columns; sqmp_pack_f6's weight rows likewise."""
-    dev = _dev()
-    from smoothquant import ops
-    dt, aq, p, Gs, M, K, N = case
-    D = O.DT(dt)
-    W, x, imp, _ = _rand_inputs(zlib.crc32(repr(case).encode()), M, K, N, False)
-    W, x = D.rnd(W), D.rnd(x)
-    q = make_layer(W, None, dt, dev, weight_quant="per_group", act_quant=aq,
-                   importance=torch.from_numpy(imp), salient_prop=p, quant_bits=4, group_size=Gs)
-    pw = q.packed()
-    xt = to_t(x, dt, dev)
-    a8, sa8, xs8 = ops.quant_act_f8(xt, pw, aq, 4, 8)
-    a6, sa6, xs6 = ops.quant_act_f8(xt, pw, aq, 4, 6)
-    assert a6.shape == (M, pw.Kp // 4 * 3)
-    c8 = e4m3_to_float(a8.cpu().numpy())
-    c6 = e2m3_rows_to_float(a6.cpu().numpy(), pw.Kp)
-    assert np.array_equal(c6, c8)
-    assert torch.equal(sa6, sa8) and torch.equal(xs6[:, :pw.S_pad], xs8[:, :pw.S_pad])
-    w8, _ = ops.f8_operands(pw)
-    w6 = ops.f6_operand(pw)
-    assert np.array_equal(e2m3_rows_to_float(w6.cpu().numpy(), pw.Kp),
-                          e4m3_to_float(w8.cpu().numpy()))
-
-
-F6_GEMM_CASES = [c for c in GEMM_CASES if c[3] % 128 == 0]
-
-
-@pytest.mark.parametrize("case", F6_GEMM_CASES, ids=[f"{c[0]}-{c[1]}-p{c[2]}-G{c[3]}-{c[4]}x{c[5]}x{c[6]}" for c in F6_GEMM_CASES])
-def test_f6_gemm_bit_identical_to_f8(case):
-    """sqmp_gemm_f6 (e2m3 operands) gives y bit-identical to sqmp_gemm_f8 on the same codes
-    (exact integer block sums either way, same fold / tail / epilogue), with and without the
-    fused output statistics; and within TOL_F8 of the oracle through the forward."""
-    dev = _dev()
-    from smoothquant import ops
-    dt, aq, p, Gs, M, K, N, bias = case
-    D = O.DT(dt)
-    W, x, imp, b = _rand_inputs(zlib.crc32(repr(case).encode()), M, K, N, bias)
-    W, x = D.rnd(W), D.rnd(x)
-    b = D.rnd(b) if b is not None else None
-    q = make_layer(W, b, dt, dev, weight_quant="per_group", act_quant=aq,
-                   importance=torch.from_numpy(imp), salient_prop=p, quant_bits=4, group_size=Gs)
-    pw = q.packed()
-    assert ops.f8_fmt(pw) == 6
-    xt = to_t(x, dt, dev)
-    bt = q.bias.reshape(-1) if q.bias is not None else None
-    y8 = ops.gemm_f8(*ops.quant_act_f8(xt, pw, aq, 4, 8), pw, bt)
-    y6 = ops.gemm_f8(*ops.quant_act_f8(xt, pw, aq, 4, 6), pw, bt)
-    assert torch.equal(y6.view(torch.int16), y8.view(torch.int16))
-    cm8 = torch.zeros(N, dtype=torch.int32, device=dev)
-    cm6 = torch.zeros(N, dtype=torch.int32, device=dev)
-    z8 = ops.gemm_f8(*ops.quant_act_f8(xt, pw, aq, 4, 8), pw, bt, colmax=cm8)
-    z6 = ops.gemm_f8(*ops.quant_act_f8(xt, pw, aq, 4, 6), pw, bt, colmax=cm6)
-    assert torch.equal(z6.view(torch.int16), z8.view(torch.int16)) and torch.equal(cm6, cm8)
-    sal = O.select_salient(imp, p)
-    w_hat = O.w4a4_from_float(W, "per_group", 4, Gs, sal, D)
-    want = D.f32(O.linear(O.quantize_input(x, aq, 4, Gs, sal, D), w_hat, b, D))
-    q.kernel = "f8"
-    assert rel(to_np(q(xt)), want) < TOL_F8[dt]
-
-
-@torch.no_grad()
-def test_f6_full_size_config2_bit_identical():
-    """Config 2 per_token (M = 16384, K = N = 4096, G = 128, 10 % salient) on the FP6 kernel
-    against the FP8 kernel: the same bits."""
-    dev = _dev()
-    from smoothquant import ops
-    from smoothquant.fake_quant import W4A4Linear
-    M, K, N, Gs, p = 16384, 4096, 4096, 128, 0.10
-    gen = torch.Generator(device=dev).manual_seed(7)
-    lin = torch.nn.Linear(K, N, bias=True).to(dev, torch.float16)
-    with torch.no_grad():
-        lin.weight.copy_((torch.randn(N, K, generator=gen, device=dev) * 0.02).half())
-        lin.bias.copy_((torch.randn(N, generator=gen, device=dev) * 0.01).half())
-    x = torch.randn(M, K, generator=gen, device=dev)
-    x[:, torch.randperm(K, generator=gen, device=dev)[:41]] *= 30
-    x = x.half()
-    imp = x[:2048].float().abs().mean(0).cpu()
-    q = W4A4Linear.from_float(lin, weight_quant="per_group", act_quant="per_token",
-                              importance=imp, salient_prop=p, group_size=Gs)
-    pw = q.packed()
-    y8 = ops.gemm_f8(*ops.quant_act_f8(x, pw, "per_token", 4, 8), pw, lin.bias)
-    y6 = ops.gemm_f8(*ops.quant_act_f8(x, pw, "per_token", 4, 6), pw, lin.bias)
-    assert torch.equal(y6.view(torch.int16), y8.view(torch.int16))
