@@ -2005,9 +2005,11 @@ extern "C" int sqmp_quant_act_group(void* x, int dtype, int M, int K, int amode,
     if (!quant_lc_supported(dtype, M, K, true, group_size, Kn, Kp, S_pad, x, outs[o]))
       return SQMP_EUNSUPPORTED;
   if (group_size < 16) return SQMP_EUNSUPPORTED;
-  // the quantizer's LDS: one region of Kp + S_pad + 8 words per output + the salient list and masks (checked before any
-  // launch: a refusal after the statistics pass would leave the workspace dirty)
-  if ((size_t)4 * ((Kp + S_pad + 8) * nout + S_pad + 2 * ((Kp + 63) / 64)) > 150 * 1024) return SQMP_EUNSUPPORTED;
+  // the quantizer's LDS: one region of Kp + S_pad + 8 words per output, at most two (a third
+  // output reuses the second) + the salient list and masks (checked before any launch: a
+  // refusal after the statistics pass would leave the workspace dirty)
+  if ((size_t)4 * ((Kp + S_pad + 8) * (nout < 2 ? nout : 2) + S_pad + 2 * ((Kp + 63) / 64)) > 150 * 1024)
+    return SQMP_EUNSUPPORTED;
   if (M == 0) return SQMP_OK;
   if (ws_bytes < sqmp_act_workspace_bytes(M, K, Kp) || !workspace) return SQMP_EWORKSPACE;
   hipStream_t s = (hipStream_t)stream;

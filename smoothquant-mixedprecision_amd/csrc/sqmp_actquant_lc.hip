@@ -242,8 +242,13 @@ __device__ __forceinline__ void quant_lc_body(
   // x and out alias for in-place output quantization (every row is read before it is
   // written: a workgroup stores a pair only after loading it)
   typedef typename DT::T T;
-  // [NOUT][W + 8] column pairs: region 0 = the interleaved input, then output 0; region o =
-  // sibling output o - 1 (written by the scatter only, so its salient positions stay zero)
+  // [NR][W + 8] column pairs: region 0 = the interleaved input, then output 0; region 1 =
+  // the sibling outputs, one after another (NOUT = 3: output 1, stored, then output 2 over
+  // it -- every position < P of a sibling output is rewritten by its scatter, the values at
+  // its non-salient positions and zeros at its salient ones from the table's pad entries,
+  // pad_entry in sqmp_actquant.hip; padding positions >= K are never written and stay zero).
+  // Two regions instead of three keep the q/k/v quantizer at four workgroups per CU.
+  constexpr int NR = NOUT < 2 ? NOUT : 2;
   extern __shared__ __attribute__((aligned(16))) uint32_t lc_buf[];
   __shared__ float lc_red[2][LC_MAXW];
   const int nthr = blockDim.x;
@@ -346,7 +351,7 @@ __device__ __forceinline__ void quant_lc_body(
   load_pair(rp);
   __builtin_amdgcn_sched_barrier(0);
   // (amap NULL: in-place output quantization, salient columns pass through: no mask)
-  uint32_t* const zm_l = lc_buf + NOUT * (W + 8) + S_pad;  // [nzc] u64 masks
+  uint32_t* const zm_l = lc_buf + NR * (W + 8) + S_pad;  // [nzc] u64 masks
   if (F8 == 0 && amap) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
@@ -364,10 +369,10 @@ __device__ __forceinline__ void quant_lc_body(
 #endif
   LC_STAMP(7);
   const int RW = W + 8;  // LDS region stride (words; a multiple of 8)
-  for (int c = tid; c < (NOUT > 1 ? NOUT * RW : W + 2); c += nthr) lc_buf[c] = 0u;
+  for (int c = tid; c < (NOUT > 1 ? NR * RW : W + 2); c += nthr) lc_buf[c] = 0u;
   // the salient columns' input positions, once per workgroup (every row pair gathers them:
   // an LDS read instead of a dependent global load per pair)
-  uint32_t* const sal_l = lc_buf + NOUT * RW;
+  uint32_t* const sal_l = lc_buf + NR * RW;
   if (sal_reg) {
 #pragma unroll
     for (int k = 0; k < 2; ++k)
@@ -439,8 +444,7 @@ __device__ __forceinline__ void quant_lc_body(
     for (int j = tid; j < S; j += nthr) {
       const uint32_t xs = lc_buf[sal_l[j]];
       lc_buf[P + j] = xs;
-#pragma unroll
-      for (int o = 1; o < NOUT; ++o) lc_buf[o * RW + P + j] = xs;  // the shared salient tail
+      if (NOUT > 1) lc_buf[RW + P + j] = xs;  // the siblings' shared salient tail
     }
 
     // ---- scales, then quantize + scatter
@@ -583,8 +587,8 @@ __device__ __forceinline__ void quant_lc_body(
         for (int i = 0; i < RPL; ++i) {
           const uint32_t y = quant_pair<DT>(v[i], c);
           lc_buf[tab[i] >> 16] = y;
-#pragma unroll
-          for (int o = 1; o < NOUT; ++o) lc_buf[o * RW + (tabs[o - 1][i] >> 16)] = y;
+          if (NOUT > 1) lc_buf[RW + (tabs[0][i] >> 16)] = y;
+          if (NOUT > 2) v[i] = y;  // (kept for output 2's scatter)
         }
       }
     }
@@ -629,15 +633,15 @@ __device__ __forceinline__ void quant_lc_body(
       continue;
     }
     // ---- de-interleave 16-B chunks and store both rows of every output
-    for (int c = tid; c < ochk; c += nthr) {
-      // ds_read_b128 groups {0-3,12-15,20-27}, {4-11,16-19,28-31} (+32), banks (a/4) mod 64:
-      // at a 32-B stride lanes l and l ^ 24 (l ^ 8 ...) collide; reading the second half first
-      // where lane bit 3 is set separates every such pair
-      const bool sw = (c >> 3) & 1;
-#pragma unroll
-      for (int o = 0; o < NOUT; ++o) {
-        const u32x4 f = ((const u32x4*)(lc_buf + o * RW))[2 * c + (sw ? 1 : 0)];
-        const u32x4 g = ((const u32x4*)(lc_buf + o * RW))[2 * c + (sw ? 0 : 1)];
+    // (region r of the LDS as output ob)
+    auto store_region = [&](int r, T* ob) {
+      for (int c = tid; c < ochk; c += nthr) {
+        // ds_read_b128 groups {0-3,12-15,20-27}, {4-11,16-19,28-31} (+32), banks (a/4) mod 64:
+        // at a 32-B stride lanes l and l ^ 24 (l ^ 8 ...) collide; reading the second half first
+        // where lane bit 3 is set separates every such pair
+        const bool sw = (c >> 3) & 1;
+        const u32x4 f = ((const u32x4*)(lc_buf + r * RW))[2 * c + (sw ? 1 : 0)];
+        const u32x4 g = ((const u32x4*)(lc_buf + r * RW))[2 * c + (sw ? 0 : 1)];
         const u32x4 a = sw ? g : f, b = sw ? f : g;
         u32x4 y0, y1;
         y0[0] = __builtin_amdgcn_perm(a[1], a[0], 0x05040100u);
@@ -648,10 +652,44 @@ __device__ __forceinline__ void quant_lc_body(
         y1[1] = __builtin_amdgcn_perm(a[3], a[2], 0x07060302u);
         y1[2] = __builtin_amdgcn_perm(b[1], b[0], 0x07060302u);
         y1[3] = __builtin_amdgcn_perm(b[3], b[2], 0x07060302u);
-        T* ob = o == 0 ? out : (T*)sib.out[o - 1];
         ((u32x4*)(ob + (size_t)m0 * W))[c] = y0;
         if (has1) ((u32x4*)(ob + (size_t)(m0 + 1) * W))[c] = y1;
       }
+    };
+    if constexpr (NR == 2) {
+      // both regions in one pass (their loads interleave)
+      for (int c = tid; c < ochk; c += nthr) {
+        const bool sw = (c >> 3) & 1;
+#pragma unroll
+        for (int o = 0; o < 2; ++o) {
+          const u32x4 f = ((const u32x4*)(lc_buf + o * RW))[2 * c + (sw ? 1 : 0)];
+          const u32x4 g = ((const u32x4*)(lc_buf + o * RW))[2 * c + (sw ? 0 : 1)];
+          const u32x4 a = sw ? g : f, b = sw ? f : g;
+          u32x4 y0, y1;
+          y0[0] = __builtin_amdgcn_perm(a[1], a[0], 0x05040100u);
+          y0[1] = __builtin_amdgcn_perm(a[3], a[2], 0x05040100u);
+          y0[2] = __builtin_amdgcn_perm(b[1], b[0], 0x05040100u);
+          y0[3] = __builtin_amdgcn_perm(b[3], b[2], 0x05040100u);
+          y1[0] = __builtin_amdgcn_perm(a[1], a[0], 0x07060302u);
+          y1[1] = __builtin_amdgcn_perm(a[3], a[2], 0x07060302u);
+          y1[2] = __builtin_amdgcn_perm(b[1], b[0], 0x07060302u);
+          y1[3] = __builtin_amdgcn_perm(b[3], b[2], 0x07060302u);
+          T* ob = o == 0 ? out : (T*)sib.out[0];
+          ((u32x4*)(ob + (size_t)m0 * W))[c] = y0;
+          if (has1) ((u32x4*)(ob + (size_t)(m0 + 1) * W))[c] = y1;
+        }
+      }
+    } else {
+      store_region(0, out);
+    }
+    if constexpr (NOUT > 2) {
+      // output 2 over region 1 (every position < P rewritten: its values and its pad
+      // entries' zeros), then stored
+      __syncthreads();  // region 1 is read before it is rewritten
+#pragma unroll
+      for (int i = 0; i < RPL; ++i) lc_buf[RW + (tabs[1][i] >> 16)] = v[i];
+      __syncthreads();
+      store_region(1, (T*)sib.out[1]);
     }
     __syncthreads();  // the buffer is rewritten by the next pair
     if (rp == rp0) LC_STAMP(5);
@@ -889,10 +927,11 @@ __global__ __launch_bounds__(1024) void quant_c4_fused_kernel(
 
 constexpr int LC_RPL = 16;
 
-// dynamic LDS words of quant_lc_body: NOUT regions of P + S_pad + 8 words, the salient list
+// dynamic LDS words of quant_lc_body: min(NOUT, 2) regions of P + S_pad + 8 words, the salient list
 // and the salient masks of the 64-position chunks (2 words each, K <= P)
 static size_t lc_lds_words(int P, int S_pad, int nout) {
-  return (size_t)(P + S_pad + 8) * nout + S_pad + 2 * (size_t)((P + 63) / 64);
+  const int nr = nout < 2 ? nout : 2;  // (a third output reuses region 1)
+  return (size_t)(P + S_pad + 8) * nr + S_pad + 2 * (size_t)((P + 63) / 64);
 }
 
 // Workgroups of `block` threads and `lds` dynamic LDS bytes a CU holds at once for kernel f

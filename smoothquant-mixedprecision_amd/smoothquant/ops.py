@@ -482,11 +482,13 @@ def _fqt_j() -> int:
 
 def lc_lds_ok(P: int, S_pad: int, nout: int = 1) -> bool:
     """The lane-contiguous quantizer's LDS budget (quant_lc_supported / lc_lds_words in
-    sqmp_actquant_lc.hip): nout regions of P + S_pad + 8 words, the salient list and two mask
-    words per 64-position chunk, within 150 KiB; P + S_pad < 65536 (16-bit table positions).
-    Every Python-side eligibility check that leads to that kernel applies it, so that a layer
-    the library would refuse (EUNSUPPORTED) takes another path instead of raising."""
-    return (4 * ((P + S_pad + 8) * nout + S_pad + 2 * ((P + 63) // 64)) <= 150 * 1024
+    sqmp_actquant_lc.hip): min(nout, 2) regions of P + S_pad + 8 words (a third sibling
+    output reuses the second region), the salient list and two mask words per 64-position
+    chunk, within 150 KiB; P + S_pad < 65536 (16-bit table positions).  Every Python-side
+    eligibility check that leads to that kernel applies it, so that a layer the library would
+    refuse (EUNSUPPORTED) takes another path instead of raising."""
+    nr = min(nout, 2)
+    return (4 * ((P + S_pad + 8) * nr + S_pad + 2 * ((P + 63) // 64)) <= 150 * 1024
             and P + S_pad < 65536)
 
 
