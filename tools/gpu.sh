@@ -61,7 +61,7 @@ step() {
       (cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof" -o run \
         -- python "$R/bench.py" --no-cpu > "$O/prof.log" 2>&1) || fail prof "$O/prof.log"
       f=$(ls "$O"/prof/*/run_kernel_stats.csv "$O"/prof/run_kernel_stats.csv 2>/dev/null | head -1)
-      [ -n "$f" ] && cp "$f" "$O/kernel_stats.csv" && head -6 "$O/kernel_stats.csv" | cut -c1-160 ;;
+      [ -n "$f" ] && cp "$f" "$O/kernel_stats.csv" && rm -rf "$O/prof" && head -6 "$O/kernel_stats.csv" | cut -c1-160 ;;
     pmc:*)
       # PMC_TAG (env): a suffix of the pass directories (knob sweeps: SQMP_...=v PMC_TAG=v);
       # PMC_PASSES (env, default "a b c d"): the passes to run
@@ -97,7 +97,7 @@ step() {
       (cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof_$name" -o run \
         -- python "$R/$script" $args > "$O/prof_$name.log" 2>&1) || fail "$s" "$O/prof_$name.log"
       f=$(ls "$O"/prof_$name/*/run_kernel_stats.csv "$O"/prof_$name/run_kernel_stats.csv 2>/dev/null | head -1)
-      [ -n "$f" ] && cp "$f" "$O/kernel_stats_$name.csv" && cut -d, -f1-4 "$O/kernel_stats_$name.csv" | cut -c1-150 ;;
+      [ -n "$f" ] && cp "$f" "$O/kernel_stats_$name.csv" && rm -rf "$O/prof_$name" && cut -d, -f1-4 "$O/kernel_stats_$name.csv" | cut -c1-150 ;;
     trace:*)
       local rest=${s#trace:}; local script=${rest%%:*}; local args=""
       [ "$rest" != "$script" ] && args=$(echo "${rest#*:}" | tr ',' ' ')
