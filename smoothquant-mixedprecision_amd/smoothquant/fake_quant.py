@@ -199,6 +199,10 @@ _PW_KEY = ("w_codes", "w_scale", "w_salient", "w_perm", "w_amap", "w_amap_fq", "
 # ----------------------------------------------------------------------------------------
 # W4A4Linear (fake_quant.py:209-374)
 # ----------------------------------------------------------------------------------------
+# the forward kernels a module's `kernel` attribute selects (W4A4Linear docstring)
+KERNELS = ("auto", "fq", "f8", "fqt")
+
+
 class W4A4Linear(nn.Module):
     """Mixed-precision W4A4 linear: salient input channels in D, the rest int4/int8.
 
@@ -475,6 +479,8 @@ class W4A4Linear(nn.Module):
     # ------------------------------------------------------------------ forward
     @torch.no_grad()
     def forward(self, x):
+        if self.kernel not in KERNELS:
+            raise ValueError(f"kernel must be one of {KERNELS}, got {self.kernel!r}")
         x_shape = x.shape
         if len(x_shape) == 3:
             x2 = x.reshape(-1, x_shape[-1])

@@ -121,6 +121,12 @@ def test_module_host_logic():
         m(torch.zeros(2, 8, dtype=torch.float16))
     with pytest.raises(ValueError, match="Unsupported input shape"):
         m(torch.zeros(1, 1, 2, 8))
+    # a kernel name outside the documented set (e.g. the removed "i8") is refused, not
+    # silently run on another kernel
+    m.kernel = "i8"
+    with pytest.raises(ValueError, match="kernel must be one of"):
+        m(torch.zeros(2, 8, dtype=torch.float16))
+    m.kernel = "auto"
     with pytest.raises(AssertionError):
         W4A4Linear.from_float(torch.nn.Conv1d(2, 2, 1))
 
