@@ -803,6 +803,118 @@ __global__ __launch_bounds__(256) void rank_table_kernel(
     rank_owner_group<TPO, R, DENSE>(rt_kv, L, L4, g0, tid % TPO, oe, colsorted, lctab, sib);
 }
 
+// ---------------------------------------------------------------- 16-bit histogram rank
+// The same stable ranks and table as rank_table_kernel's 16-bit dense path, from a histogram
+// of the 15-bit f16 / bf16 key patterns instead of all-pairs compares.  Every workgroup (1024
+// threads) stages all K keys (salient and padding: the 0xFFFF sentinel, never counted), counts
+// them into 32768 bins (two u16 counts per LDS word, atomic adds that cannot carry across the
+// halves: counts <= K <= 16384), turns the counts into exclusive bin starts (one block scan),
+// scatters the columns into bin order (the same atomics return each column's slot, leaving
+// every bin's END behind, so bin k starts where bin k - 1 ends), and ranks its owners:
+//   rank(c) = start(key_c) + #{j in bin(key_c) : j < c}
+// -- #{j : key_j < key_c} + #{j < c : key_j == key_c}, the reference's stable argsort
+// (fake_quant.py:113, ties by list index = column order).  An owner's bin is scanned by TPO
+// lanes; a bin holding many equal keys costs compares, never correctness.
+constexpr int RH_BINS = 32768, RH_THREADS = 1024, RH_TPO = 4, RH_OWNERS = RH_THREADS / RH_TPO;
+
+template <int KW>
+__global__ __launch_bounds__(RH_THREADS) void rank_hist16_kernel(
+    const uint32_t* __restrict__ key, int K, int L, const int32_t* __restrict__ posmap,
+    int32_t* __restrict__ colsorted, uint32_t* __restrict__ lctab, int lc_len,
+    uint32_t lc_none, SibTables sib, const int32_t* __restrict__ sal, int S) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t rh_lds[];
+  uint32_t* hist = rh_lds;                                  // [RH_BINS / 2] u16 pairs
+  uint16_t* kv = (uint16_t*)(hist + RH_BINS / 2);           // [K8] 16-bit keys
+  const int K8 = (int)round_up_dev(K, 8);
+  uint16_t* order = kv + K8;                                // [K8] columns in bin order
+  __shared__ uint32_t wsum[RH_THREADS / 64];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int sub = tid % RH_TPO;
+  const int owner = blockIdx.x * RH_OWNERS + tid / RH_TPO;  // a column
+  const RankOwnerEnt<1> oe = rank_owner_ents<1, true>(owner, sub, K, nullptr, posmap, sib);
+  // ---- bins zeroed, keys staged (coalesced 16-B loads: 4 keys per load)
+  for (int i = tid; i < RH_BINS / 8; i += RH_THREADS) ((u32x4*)hist)[i] = u32x4{0u, 0u, 0u, 0u};
+  const int Kq = K >> 2;  // K % 4 == 0 (the launcher)
+  for (int c = tid; c < K8 / 4; c += RH_THREADS) {
+    const u32x4 v = c < Kq ? ((const u32x4*)key)[c] : u32x4{0u, 0u, 0u, 0u};
+    uint32_t h[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      h[e] = c < Kq ? (KW == 2 ? v[e] >> 16
+                               : (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)__uint_as_float(v[e])))
+                    : 0xFFFFu;
+    ((uint2*)kv)[c] = uint2{h[0] | h[1] << 16, h[2] | h[3] << 16};
+  }
+  for (int r = L + blockIdx.x * RH_THREADS + tid; r < lc_len; r += gridDim.x * RH_THREADS) {
+    lctab[r] = pad_entry(r, L, lc_none, sal, S, posmap);
+    for (int o = 0; o < sib.n; ++o) sib.lctab[o][r] = pad_entry(r, L, lc_none, sal, S, sib.posmap[o]);
+  }
+  __syncthreads();
+  for (int j = tid; j < S; j += RH_THREADS) kv[sal[j]] = 0xFFFFu;  // salient: never counted
+  __syncthreads();
+  // ---- counts
+  for (int c = tid; c < K; c += RH_THREADS) {
+    const uint32_t k = kv[c];
+    if (k < (uint32_t)RH_BINS) atomicAdd(&hist[k >> 1], 1u << ((k & 1u) * 16u));
+  }
+  __syncthreads();
+  // ---- exclusive bin starts: 32 bins (16 words) per thread, then across the block
+  constexpr int PW = RH_BINS / 2 / RH_THREADS;  // words per thread
+  uint32_t w[PW], run = 0u;
+#pragma unroll
+  for (int i = 0; i < PW; ++i) {
+    w[i] = hist[PW * tid + i];
+    run += (w[i] & 0xFFFFu) + (w[i] >> 16);
+  }
+  uint32_t inc = run;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t v = (uint32_t)__shfl_up((int)inc, o, 64);
+    if (lane >= o) inc += v;
+  }
+  if (lane == 63) wsum[wave] = inc;
+  __syncthreads();
+  uint32_t base = inc - run;
+  for (int i = 0; i < wave; ++i) base += wsum[i];
+#pragma unroll
+  for (int i = 0; i < PW; ++i) {
+    const uint32_t lo = base, hi = base + (w[i] & 0xFFFFu);
+    hist[PW * tid + i] = lo | (hi << 16);
+    base = hi + (w[i] >> 16);
+  }
+  __syncthreads();
+  // ---- columns into bin order; each bin's word half ends at the bin's end
+  for (int c = tid; c < K; c += RH_THREADS) {
+    const uint32_t k = kv[c];
+    if (k < (uint32_t)RH_BINS) {
+      const uint32_t sh = (k & 1u) * 16u;
+      const uint32_t old = atomicAdd(&hist[k >> 1], 1u << sh);
+      order[(old >> sh) & 0xFFFFu] = (uint16_t)c;
+    }
+  }
+  __syncthreads();
+  // ---- ranks of this workgroup's owners (TPO lanes each)
+  const int c = owner < K ? owner : K - 1;
+  const uint32_t mine = kv[c];
+  const bool real = owner < K && mine < (uint32_t)RH_BINS;
+  uint32_t cnt = 0u, lo = 0u;
+  if (real) {
+    auto end_of = [&](uint32_t k) { return (hist[k >> 1] >> ((k & 1u) * 16u)) & 0xFFFFu; };
+    lo = mine > 0u ? end_of(mine - 1u) : 0u;
+    const uint32_t hi = end_of(mine);
+    for (uint32_t e = lo + sub; e < hi; e += RH_TPO) cnt += order[e] < c ? 1u : 0u;
+  }
+#pragma unroll
+  for (int o = 1; o < RH_TPO; o <<= 1) cnt += (uint32_t)__shfl_xor((int)cnt, o, 64);
+  if (sub == 0 && real) {
+    const uint32_t rk = lo + cnt;
+    colsorted[rk] = oe.col[0];
+    lctab[rk] = oe.ent[0][0];
+    if (sib.n > 0) sib.lctab[0][rk] = oe.ent[0][1];
+    if (sib.n > 1) sib.lctab[1][rk] = oe.ent[0][2];
+  }
+}
+
 // ---------------------------------------------------------------- bucketed rank + table
 // The same stable ranks and table as rank_table_kernel with O(L * bucket) compares instead of
 // O(L^2): every workgroup stages the L keys (as above), counts them into 4096 buckets by the
@@ -1032,6 +1144,29 @@ static int launch_rank_table(const uint32_t* key, const int32_t* nonsal, int L,
     // 16-bit keys (f16 / bf16 column maxima; down_proj prepass 47.5 -> 45.2 us,
     // profiles/r05_ab_rank_k16.txt) unless SQMP_RT_K16=0 (A/B)
     const char* k16 = knob("SQMP_RT_K16");
+    // the histogram rank (rank_hist16_kernel) above 8192 columns: Llama down_proj's 10458-rank
+    // table 14.8 -> 10.2 us, while at 4096 columns its fixed chain (32768 bins zeroed and
+    // scanned per workgroup) is slower than the all-pairs compares, 5.2-7.8 -> 7.6-9.2 us
+    // (profiles/r06_ab_rank_hist.txt).  SQMP_RT_HIST=0 / 1 forces it off / on (A/B).
+    const char* he = knob("SQMP_RT_HIST");
+    const bool hist = he ? atoi(he) != 0 : K > 8192;
+    if (kw != 0 && !(k16 && atoi(k16) == 0) && hist && K <= 16384) {
+      const size_t hl = sizeof(uint32_t) * (RH_BINS / 2) + 2 * sizeof(uint16_t) * (size_t)round_up(K, 8);
+      const int hgrid = cdiv(K, RH_OWNERS);
+#define SQMP_RH(KWV)                                                                            \
+  do {                                                                                         \
+    static uint64_t hattr = 0;                                                                 \
+    if (first_on_device(hattr))                                                                \
+      (void)hipFuncSetAttribute((const void*)rank_hist16_kernel<KWV>,                          \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);       \
+    rank_hist16_kernel<KWV><<<dim3(hgrid), dim3(RH_THREADS), hl, s>>>(                         \
+        key, K, L, posmap, colsorted, lctab, lc_len, lc_none, sib, sal, S);                    \
+  } while (0)
+      if (kw == 2) SQMP_RH(2); else SQMP_RH(1);
+#undef SQMP_RH
+      SQMP_LAUNCH_CHECK();
+      return SQMP_OK;
+    }
     if (kw != 0 && !(k16 && atoi(k16) == 0)) {
       const size_t hlds = sizeof(uint16_t) * (size_t)round_up(K, 8 * tpo);
       if (kw == 2)

@@ -66,8 +66,9 @@ def test_bucketed_rank_bit_identical(M, K, Ns, G, p, dt, kind, btpo, monkeypatch
 ])
 def test_dense_rank_staging_bit_identical(M, K, Ns, G, p, dt, kind, monkeypatch):
     """The rank table with every column's key staged by coalesced loads and the salient
-    columns masked (the default: ties broken by column order = list order; 16-bit f16 / bf16
-    key patterns compared two per packed op, and the 32-bit variant SQMP_RT_K16=0) against
+    columns masked (ties broken by column order = list order): the default 16-bit f16 / bf16
+    key patterns ranked by a histogram of the keys (rank_hist16_kernel), the same keys compared
+    two per packed op (SQMP_RT_HIST=0), and the 32-bit variant SQMP_RT_K16=0, against
     the list gather (SQMP_RT_DENSE=0): bit-identical operands, ragged K, a salient list longer than
     the first staging batch (30 % of 16384 columns)."""
     dev = _dev()
@@ -77,15 +78,18 @@ def test_dense_rank_staging_bit_identical(M, K, Ns, G, p, dt, kind, monkeypatch)
     x = _inputs(kind, x).contiguous()
     pws = [q.packed() for q in layers]
     outs = {}
-    for on in ("0", "1", "k32"):  # gather | dense 16-bit keys (default) | dense 32-bit keys
+    # gather | dense 16-bit keys, histogram rank (default) | dense 16-bit keys, all-pairs
+    # compares | dense 32-bit keys
+    for on in ("0", "1", "a16", "k32"):
         monkeypatch.setenv("SQMP_RT_DENSE", "0" if on == "0" else "1")
         monkeypatch.setenv("SQMP_RT_K16", "0" if on == "k32" else "1")
+        monkeypatch.setenv("SQMP_RT_HIST", "0" if on == "a16" else "1")
         lib.reload_knobs()
         if len(pws) > 1:
             outs[on] = [a.clone() for a in ops.quant_act_fp_group(x, pws, "per_group", 4, G)]
         else:
             outs[on] = [ops.quant_act_fp(x, pws[0], "per_group", 4, G).clone()]
         torch.cuda.synchronize()
-    for v in ("1", "k32"):
+    for v in ("1", "a16", "k32"):
         for a, b in zip(outs["0"], outs[v]):
             assert torch.equal(a.view(torch.int16), b.view(torch.int16))
