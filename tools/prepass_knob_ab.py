@@ -3,7 +3,8 @@ shape: interleaved rounds, HIP events, outputs checked bit-identical across the 
 
     python tools/prepass_knob_ab.py KIND KNOB v1/v2/... [rounds] [iters]
     KIND: f8 (per_token e4m3 quantizer, config 2) | c4 (act-order quantizer + permutation,
-          config 2) | fp (packed-order per_group quantizer, 2048 x 11008 Llama down_proj)
+          config 2) | fp (packed-order per_group quantizer, 2048 x 11008 Llama down_proj) |
+          fp4k (the same at 2048 x 4096, Llama o_proj)
 """
 import os
 import sys
@@ -20,13 +21,14 @@ kind, knob, vals = sys.argv[1], sys.argv[2], sys.argv[3].split("/")
 rounds = int(sys.argv[4]) if len(sys.argv) > 4 else 4
 iters = int(sys.argv[5]) if len(sys.argv) > 5 else 100
 dev = torch.device("cuda")
-if kind == "fp":
+if kind in ("fp", "fp4k"):
     from smoothquant.fake_quant import W4A4Linear
+    KK = 11008 if kind == "fp" else 4096
     g = torch.Generator(device=dev).manual_seed(0)
-    x = torch.randn(2048, 11008, generator=g, device=dev)
-    x[:, torch.randperm(11008, generator=g, device=dev)[:110]] *= 30.0
+    x = torch.randn(2048, KK, generator=g, device=dev)
+    x[:, torch.randperm(KK, generator=g, device=dev)[:KK // 100]] *= 30.0
     x = x.half()
-    lin = torch.nn.Linear(11008, 4096, bias=False).to(dev, torch.float16)
+    lin = torch.nn.Linear(KK, 4096, bias=False).to(dev, torch.float16)
     q = W4A4Linear.from_float(lin, weight_quant="per_group", act_quant="per_group",
                               importance=x[:512].float().abs().mean(0).cpu(), salient_prop=0.05,
                               group_size=64)
