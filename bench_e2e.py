@@ -14,9 +14,10 @@ quantize_opt, fake_quant.py:377-561) with every nn.Linear of the decoder becomin
 W4A4Linear.  Timing: Evaluator-style prefill (run_experiments.py:86-123), batch 1, wall
 clock around the whole window loop after one warm-up window, for (1) the unquantized model,
 (2) the W4A4 model (1 and 2 in interleaved rounds, best of each), (3) the reference's fake-quant forward restated in PyTorch ops
-(tools/torch_fakequant.py) on the same W_hat and salient sets, with the fp16 GEMM, and
-(4) the same with an fp32 GEMM -- (3) vs (4) is the reference's own sensitivity to GEMM
-accumulation order, the noise floor against which the W4A4 kernel's PPL delta reads.
+(tools/torch_fakequant.py) on the same W_hat and salient sets, with the model-dtype GEMM,
+and (4) the same with a higher-precision GEMM (fp32 for fp16 / bf16 models, fp64 for fp32
+models) -- (3) vs (4) is the reference's own sensitivity to GEMM accumulation, the noise
+floor against which the W4A4 kernel's PPL delta reads.
 Perplexities are of a random model: only differences are meaningful.
 
 CPU baseline (north star: e2e tokens/s "next to the CPU baseline"): the same architecture
@@ -285,6 +286,7 @@ def run(args):
             "ppl_reference_fakequant_fp32_gemm": round(pplr32, 4),
             "ppl_delta_vs_reference": round(ppl4 - pplr, 4),
             "reference_gemm_order_noise": round(pplr32 - pplr, 4),
+            "noise_gemm_dtype": "fp64" if dtn == "fp32" else "fp32",
         })
     out.update({
         "data": f"synthetic: random-init {dtn} weights of the named architecture, random tokens; "

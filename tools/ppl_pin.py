@@ -4,8 +4,9 @@ One e2e run gives one PPL delta, and on a random-init model one delta cannot be 
 from the reference's own sensitivity to GEMM accumulation order (bench_e2e.py's
 `reference_gemm_order_noise`).  This tool repeats the comparison over S random models and
 token streams and reports, per seed and as mean / spread over seeds, four views of
-"ours vs the reference" beside the same four of "the reference with an fp32 GEMM vs the
-reference" (the noise floor: identical operands, another accumulation):
+"ours vs the reference" beside the same four of "the reference with a higher-precision GEMM
+vs the reference" (the noise floor: identical operands, another accumulation -- fp32 for the
+fp16 Llama, fp64 for the fp32 OPT):
 
   * the PPL delta, and its share of the reference PPL;
   * the mean |ΔNLL| per token;
@@ -14,7 +15,8 @@ reference" (the noise floor: identical operands, another accumulation):
     0), which shows how the two forwards part from layer to layer beside how the noise
     floor's do.
 
-The W4A4 model is quantize_llama_like's (fake_quant.py:377-421) with the HIP W4A4Linear;
+The W4A4 model is quantize_llama_like's / quantize_opt's (fake_quant.py:377-561, OPT with
+its default bmm-input output quantization) with the HIP W4A4Linear;
 the reference legs are tools/torch_fakequant.py's restatement of the reference forward
 (fake_quant.py:280-375) on the same W_hat, salient sets and bound quantizers
 (bench_e2e.swap_reference).  Random-init weights of the named architecture (no checkpoints
@@ -83,15 +85,15 @@ def one_seed(args, seed):
     dev = torch.device("cuda")
     torch.manual_seed(seed)
     family, cfg, model = E.build(args.model, args.layers, E.TDT[E.MODELS[args.model][3]])
+    qfn = FQ.quantize_llama_like if family == "llama" else FQ.quantize_opt
     G = E.MODELS[args.model][2]
     g = torch.Generator(device=dev).manual_seed(1000 + seed)
     ids = torch.randint(0, cfg.vocab_size, (1, args.windows * args.seq), generator=g, device=dev)
     cal = [torch.randint(0, cfg.vocab_size, (1, 512), generator=g, device=dev) for _ in range(4)]
     feat = get_calib_feat(model, None, samples=cal, device=dev)
     fp16 = forward_stats(model, ids, args.seq, args.windows)
-    qmodel = FQ.quantize_llama_like(copy.deepcopy(model), weight_quant="per_group",
-                                    act_quant="per_group", input_feat=feat,
-                                    salient_prop=args.salient, quant_bits=4, group_size=G)
+    qmodel = qfn(copy.deepcopy(model), weight_quant="per_group", act_quant="per_group",
+                 input_feat=feat, salient_prop=args.salient, quant_bits=4, group_size=G)
     if args.act_bits != 4:
         # W4A8: rebind the bound activation quantizer, as bench_e2e.py --act-bits does
         fn = FQ._ACT_FNS["per_group"]
@@ -131,7 +133,7 @@ def summarize(rows):
 
 def main(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--model", default="llama2-7b", choices=["llama2-7b"])
+    ap.add_argument("--model", default="llama2-7b", choices=sorted(E.MODELS))
     ap.add_argument("--seeds", type=int, default=6)
     ap.add_argument("--windows", type=int, default=2)
     ap.add_argument("--seq", type=int, default=2048)
@@ -152,7 +154,8 @@ def main(argv=None):
               f"top1 {n['top1_agree']:.4f})  {time.perf_counter() - t0:.0f} s", flush=True)
     res = {"model": args.model, "act_bits": args.act_bits, "seeds": args.seeds, "windows": args.windows, "seq": args.seq,
            "layers": args.layers or E.MODELS[args.model][1]["num_hidden_layers"],
-           "data": "random-init fp16 weights of the named architecture, random tokens, "
+           "dtype": E.MODELS[args.model][3],
+           "data": "random-init weights of the named architecture, random tokens, "
                    "4 x 512-token random calibration blocks per seed",
            "summary": summarize(rows), "per_seed": rows}
     text = json.dumps(res, indent=1)

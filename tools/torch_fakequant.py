@@ -11,8 +11,9 @@ Follows /root/reference/smoothquant/fake_quant.py:
   per_token / tensor   :56-75
   output quantization  :308-316 (OPT q/k/v with quantize_bmm_input)
 plus the config-5 variants (unsorted groups :77-101, the mean+3sigma sort key).
-`accum32` runs F.linear on fp32 copies: the same fake-quant math with a different GEMM
-accumulation order (the noise floor of PPL comparisons).
+`accum32` runs F.linear at a higher precision than the model's -- fp32 copies for fp16 / bf16
+models, fp64 for fp32 models -- : the same fake-quant math with another GEMM accumulation
+(the noise floor of PPL comparisons).
 """
 import torch
 import torch.nn.functional as F
@@ -104,8 +105,9 @@ class TorchFakeQuantLinear:
         else:
             q_x = self._aq(x2)
         if self.accum32:
-            y = F.linear(q_x.float(), self.w.float(),
-                         None if self.b is None else self.b.float()).to(q_x.dtype)
+            hi = torch.float64 if q_x.dtype == torch.float32 else torch.float32
+            y = F.linear(q_x.to(hi), self.w.to(hi),
+                         None if self.b is None else self.b.to(hi)).to(q_x.dtype)
         else:
             y = F.linear(q_x, self.w, self.b)
         if self.out_spec is not None:
