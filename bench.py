@@ -310,12 +310,17 @@ LLAMA_LINEARS = [  # name, K, N, input
 LLAMA_T, LLAMA_G, LLAMA_P = 2048, 64, 0.05
 
 
-def llama_layer(dev, iters=40):
-    """Per-linear and whole-layer time of the W4A4 layer against the same 7 unquantized fp16
-    F.linear calls (hipBLASLt), HIP events on the launch stream."""
+def llama_layer(dev, iters=40, flow="experiments"):
+    """Per-linear and whole-layer time of the W4A4 layer against the same 7 unquantized
+    F.linear calls (hipBLASLt), HIP events on the launch stream.  flow "experiments": config 4
+    (fp16, per_group sorted W and A, G 64, 5 % salient; run_experiments.py); "ppl_eval": the
+    reference's SmoothQuant baseline evaluation (smoothquant/ppl_eval.py:69-83: bf16,
+    quantize_model with per_channel W, per_token A, quantize_bmm_input=True, no salient
+    channels -- each linear quantizes its input in place, q/k/v their outputs)."""
     from smoothquant.fake_quant import W4A4Linear, link_siblings
     gen = torch.Generator(device=dev).manual_seed(7)
-    dt = torch.float16
+    ppl = flow == "ppl_eval"
+    dt = torch.bfloat16 if ppl else torch.float16
     xs = {}
     for name, K in (("attn", 4096), ("o", 4096), ("mlp", 4096), ("down", 11008)):
         x = torch.randn(LLAMA_T, K, generator=gen, device=dev)
@@ -326,9 +331,13 @@ def llama_layer(dev, iters=40):
         lin = torch.nn.Linear(K, N, bias=False).to(dev, dt)
         with torch.no_grad():
             lin.weight.copy_((torch.randn(N, K, generator=gen, device=dev) * 0.02).to(dt))
-        imp = xs[src][:512].float().abs().mean(0).cpu()
-        q = W4A4Linear.from_float(lin, weight_quant="per_group", act_quant="per_group",
-                                  importance=imp, salient_prop=LLAMA_P, group_size=LLAMA_G)
+        if ppl:
+            q = W4A4Linear.from_float(lin, weight_quant="per_channel", act_quant="per_token",
+                                      quantize_output=name in ("q_proj", "k_proj", "v_proj"))
+        else:
+            imp = xs[src][:512].float().abs().mean(0).cpu()
+            q = W4A4Linear.from_float(lin, weight_quant="per_group", act_quant="per_group",
+                                      importance=imp, salient_prop=LLAMA_P, group_size=LLAMA_G)
         layers.append((name, q, lin.weight.detach(), xs[src]))
     # the sibling groups quantize_llama_like links (q/k/v, gate/up: fake_quant.SiblingGroup)
     link_siblings(*[layers[i][1] for i in (0, 1, 2)])
@@ -357,11 +366,26 @@ def llama_layer(dev, iters=40):
         per = [sorted(ev[i].elapsed_time(ev[i + 1]) for ev in evs)[iters // 2]
                for i in range(len(layers))]
         tot = sorted(ev[0].elapsed_time(ev[-1]) for ev in evs)[iters // 2]
-        key = "fp16" if kind else "w4a4"
+        key = "fp16" if kind else "w4a4"  # ("fp16": the unquantized model dtype)
         if key not in out or tot < out[key][1]:
             out[key] = (per, tot)
     flops = sum(2.0 * LLAMA_T * K * N for _, K, N, _ in LLAMA_LINEARS)
     (pw4, tw4), (pf16, tf16) = out["w4a4"], out["fp16"]
+    if ppl:
+        return {
+            "workload": (f"Llama-2-7B decoder layer linears, {LLAMA_T} tokens, the reference's "
+                         "ppl_eval flow: bf16, W4 per_channel, A4 per_token (in place), q/k/v "
+                         "outputs quantized per_token, no salient channels"),
+            "w4a4_ms": round(tw4, 4), "bf16_linear_ms": round(tf16, 4),
+            "w4a4_over_bf16_speed": round(tf16 / tw4, 4),
+            "w4a4_TFLOP_per_s": round(flops / (tw4 * 1e-3) / 1e12, 1),
+            "per_linear": {name: {"w4a4_ms": round(a, 4), "bf16_ms": round(b, 4),
+                                  "bf16_over_w4a4": round(b / a, 3)}
+                           for (name, _, _, _), a, b in zip(LLAMA_LINEARS, pw4, pf16)},
+            "note": "median of 40 layer passes, best of 2 interleaved rounds; every input is "
+                    "quantized in place by its layer, as in the reference (the passes re-run "
+                    "on the quantized inputs)",
+        }
     return {
         "workload": (f"Llama-2-7B decoder layer linears, {LLAMA_T} tokens, W4A4 G={LLAMA_G}, "
                      f"{int(LLAMA_P * 100)}% salient, per_group(sorted) W and A, fp16; "
@@ -757,6 +781,7 @@ def main(argv=None):
         out["per_token"] = per_token_leg(dev)
     if not fp32 and not args.no_layer:
         out["llama_layer"] = llama_layer(dev)
+        out["llama_layer_pplflow"] = llama_layer(dev, flow="ppl_eval")
         out["fp32"] = fp32_leg(dev)
     if not fp32 and not args.no_layer and not args.no_e2e and world == 1:
         out["e2e"] = e2e_leg(args.e2e_windows, cpu=rank == 0 and not args.no_cpu)

@@ -4,6 +4,10 @@
                         [--salient 0.05] [--act per_group] [--weight per_group] [--cal-blocks 4]
     python bench_e2e.py --model opt-1.3b   (config 3: G=128, 5 % salient, quantize_opt with
                                             its default bmm-input output quantization)
+    python bench_e2e.py --model llama2-7b --flow ppl_eval   (the reference's SmoothQuant
+        baseline evaluation, smoothquant/ppl_eval.py:69-83 / examples/ppl_eval.sh: bf16 model,
+        quantize_model(weight_quant="per_channel", act_quant="per_token",
+        quantize_bmm_input=True), no calibration features, so no salient channels)
 
 The architecture of the named model with random-init weights built directly on the GPU
 (there are no checkpoints offline), random token windows, in the reference's dtype for that
@@ -72,9 +76,19 @@ def parse(argv=None):
     ap.add_argument("--dtype", default=None, choices=["fp16", "bf16", "fp32"],
                     help="model dtype (default: the reference's for this model)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--flow", default="experiments", choices=["experiments", "ppl_eval"],
+                    help="experiments: run_experiments.py's quantize_llama_like / quantize_opt "
+                         "flow (configs 3-5); ppl_eval: smoothquant/ppl_eval.py's quantize_model "
+                         "flow (bf16, per_channel W, per_token A, bmm-input output quant)")
     ap.add_argument("--rounds", type=int, default=2,
                     help="interleaved (unquantized, W4A4) timing rounds; the best of each")
-    return ap.parse_args(argv)
+    args = ap.parse_args(argv)
+    if args.flow == "ppl_eval":
+        # ppl_eval.py:69-83: torch_dtype=torch.bfloat16, quantize_model(...) with its
+        # input_feat / salient_prop defaults (no importance -> no salient channels)
+        args.dtype = args.dtype or "bf16"
+        args.weight, args.act, args.salient = "per_channel", "per_token", 0.0
+    return args
 
 
 @torch.no_grad()
@@ -151,7 +165,8 @@ def cpu_baseline(args, G):
         for name, mod in list(m.named_modules()):
             for attr, child in list(mod.named_children()):
                 if isinstance(child, nn.Linear) and "lm_head" not in f"{name}.{attr}":
-                    outq = family == "opt" and attr in ("q_proj", "k_proj", "v_proj")
+                    outq = ((family == "opt" or args.flow == "ppl_eval")
+                            and attr in ("q_proj", "k_proj", "v_proj"))
                     setattr(mod, attr, CPURefLinear(child, args.weight, args.act, G,
                                                     args.salient, outq))
         ids = torch.randint(0, m.config.vocab_size, (1, seq),
@@ -233,12 +248,17 @@ def run(args):
     flops_tok = linear_flops_per_token(model)
 
     t_q = time.perf_counter()
-    feat = get_calib_feat(model, None, samples=cal, device=dev)
-    qfn = FQ.quantize_llama_like if family == "llama" else FQ.quantize_opt
     # the unquantized model stays alive beside its quantized copy, so the two are timed in
     # interleaved rounds on the same warmed-up chip (separate runs drifted by up to 25 %)
-    qmodel = qfn(copy.deepcopy(model), weight_quant=args.weight, act_quant=args.act,
-                 input_feat=feat, salient_prop=args.salient, quant_bits=4, group_size=G)
+    if args.flow == "ppl_eval":
+        qfn = FQ.quantize_model
+        qmodel = qfn(copy.deepcopy(model), weight_quant="per_channel", act_quant="per_token",
+                     quantize_bmm_input=True)
+    else:
+        feat = get_calib_feat(model, None, samples=cal, device=dev)
+        qfn = FQ.quantize_llama_like if family == "llama" else FQ.quantize_opt
+        qmodel = qfn(copy.deepcopy(model), weight_quant=args.weight, act_quant=args.act,
+                     input_feat=feat, salient_prop=args.salient, quant_bits=4, group_size=G)
     if args.act_bits != 4:
         # W4A8 (config 5): rebind the bound activation quantizer, as a reference user would
         fn = FQ._ACT_FNS[args.act]
@@ -295,7 +315,7 @@ def run(args):
                    "seq_len": args.seq, "windows": args.windows, "group_size": G,
                    "salient_prop": args.salient, "weight_quant": args.weight,
                    "act_quant": args.act, "act_bits": args.act_bits, "w4a4_linears": n_w4,
-                   "quantizer": qfn.__name__,
+                   "quantizer": qfn.__name__, "flow": args.flow,
                    "calibration": f"{args.cal_blocks} x 512 random tokens"},
         "setup_s": {"calibrate_and_quantize": round(t_q, 1)},
     })

@@ -178,6 +178,13 @@ int sqmp_quant_act(void* x, int dtype, int M, int K, int amode, int n_bits,
                                  J = 2 and N = M gives their sizes) instead of row-major */
 #define SQMP_QA_TILED4 16     /* as SQMP_QA_TILED with 64-row blocks (J = 4), the operands of
                                  sqmp_gemm_fqt7j with J = 4 */
+#define SQMP_QA_TABLE_READY 32 /* unsorted act modes (per_token, per_group_unsorted) on the
+                                 lane-contiguous quantizer: the workspace's rank table already
+                                 holds exactly the list table this call would build (a previous
+                                 call on this workspace with the same K, non-salient list,
+                                 salient set and position map, e.g. the in-place quantizers of
+                                 consecutive layers without salient channels): its build launch
+                                 is skipped.  Ignored by the sorted modes. */
 
 /* sqmp_quant_act with the per-weight map posmap (int32 [K]: packed position of column k,
  * the inverse of perm; NULL = derive it per call) and flags.  With posmap, OUT_FP on

@@ -1800,7 +1800,7 @@ static int quant_act_impl(void* x, int dtype, int M, int K, int amode, int n_bit
   if (n_bits < 2 || n_bits > 8) return SQMP_EUNSUPPORTED;
   if (S < 0 || S > K || !x || !amap || (K - S > 0 && !nonsal)) return SQMP_EINVAL;
   if (flags & ~(SQMP_QA_CLEAN_WS | SQMP_QA_REUSE_STATS | SQMP_QA_STATS_GIVEN | SQMP_QA_TILED |
-                SQMP_QA_TILED4))
+                SQMP_QA_TILED4 | SQMP_QA_TABLE_READY))
     return SQMP_EINVAL;
   if ((flags & (SQMP_QA_TILED | SQMP_QA_TILED4)) && out_kind != SQMP_OUT_C4)
     return SQMP_EINVAL;
@@ -1897,6 +1897,8 @@ static int quant_act_impl(void* x, int dtype, int M, int K, int amode, int n_bit
         if (st2) return st2;
       }
     }
+    // (SQMP_QA_TABLE_READY: the list table of a previous call is still in place)
+    if (tmode == TAB_LIST && (flags & SQMP_QA_TABLE_READY)) return SQMP_OK;
     const int nthr = K > Kn ? K : (Kn > 0 ? Kn : 1);
     lc_table_kernel<<<dim3(cdiv(nthr, 256)), dim3(256), 0, s>>>(
         tmode, nonsal, Kn, K, pm, counts, colsorted, tmode == TAB_COUNTS ? cmax : nullptr,
@@ -1955,6 +1957,20 @@ static int quant_act_impl(void* x, int dtype, int M, int K, int amode, int n_bit
                            salient, S, S_pad, cmax, nonsal, out, kc, (int)k64, s);
   }
 
+  // ---- in-place per-token quantization without salient columns: one row-pair pass, no
+  // table (launch_token_rows).  The list table is still left in the workspace (unless it is
+  // there already: SQMP_QA_TABLE_READY), so that a later unsorted in-place call may skip it.
+  if (out_kind == SQMP_OUT_INPLACE && amode == SQMP_ACT_PER_TOKEN && S == 0 && !lc_off &&
+      (dtype == SQMP_F16 || dtype == SQMP_BF16) && K % 8 == 0 && ((uintptr_t)x) % 16 == 0) {
+    if (!(flags & SQMP_QA_TABLE_READY)) {
+      lc_table_kernel<<<dim3(cdiv(K, 256)), dim3(256), 0, s>>>(
+          TAB_LIST, nonsal, Kn, K, nullptr, counts, colsorted, nullptr, lctab, lc_len,
+          (uint32_t)K | ((uint32_t)(K + 1) << 16), salient, S);
+      SQMP_LAUNCH_CHECK();
+    }
+    return launch_token_rows(dtype, x, M, K, q_max, s);
+  }
+
   // ---- in-place output quantization (fake_quant.py:308-316) on the same kernels: the
   // "packed" order is the identity, salient columns keep their values (no zeroing, no
   // tail), and the row is written back over itself.
@@ -1998,6 +2014,18 @@ static int quant_act_impl(void* x, int dtype, int M, int K, int amode, int n_bit
   }
 
   if (h2) return SQMP_EUNSUPPORTED;  // the two-plane output: the fp32 wave kernels only
+
+  // (the in-place list table is left in the workspace by every in-place call of an unsorted
+  // per-row / per-group mode, whichever path quantizes, so that a caller's
+  // SQMP_QA_TABLE_READY on the next such call never finds a stale table)
+  if (out_kind == SQMP_OUT_INPLACE && !sorted && amode != SQMP_ACT_PER_TENSOR &&
+      !(flags & SQMP_QA_TABLE_READY)) {
+    const int nthr = K > Kn ? K : (Kn > 0 ? Kn : 1);
+    lc_table_kernel<<<dim3(cdiv(nthr, 256)), dim3(256), 0, s>>>(
+        TAB_LIST, nonsal, Kn, K, nullptr, counts, colsorted, nullptr, lctab, lc_len,
+        (uint32_t)K | ((uint32_t)(K + 1) << 16), salient, S);
+    SQMP_LAUNCH_CHECK();
+  }
 
   // ---- general path (fp32, 8-bit int output, large rows, other group sizes)
   // SQMP_QA_REUSE_STATS: the rank partials of the previous call on this workspace (a

@@ -1035,6 +1035,101 @@ int launch_quant_lc(int dtype, int mode, const void* x, int M, int K, int q_max,
 #undef SQMP_LC
 }
 
+// ---- in-place per-token quantization without salient columns (fake_quant.py:56-64 on the
+// caller's x: the reference's ppl_eval flow quantizes every linear's input and the q/k/v
+// outputs this way): no table, no gather, no LDS row -- a workgroup takes two rows, each thread
+// CH 16-B chunks of both, interleaved in registers into (row m0, row m0 + 1) pairs, one
+// workgroup-wide packed absmax, then pair_scale / quant_pair (the lane-contiguous quantizer's
+// arithmetic, so bit for bit its values) and the chunks stored back over the rows.
+// (rows longer than CH chunks per thread: the chunks are streamed twice, max then quantize)
+template <class DT, int CH>
+__global__ __launch_bounds__(1024) void token_rows_kernel(typename DT::T* __restrict__ x, int M,
+                                                          int K, float qmf, float rqf) {
+  __shared__ uint32_t red[LC_MAXW];
+  const int nthr = blockDim.x, tid = threadIdx.x, lane = tid & 63, NW = nthr >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nchk = K >> 3, npair = (M + 1) >> 1;
+  const bool cached = nchk <= CH * nthr;
+  auto pk_lo = [](uint32_t b, uint32_t a) { return __builtin_amdgcn_perm(b, a, 0x05040100u); };
+  auto pk_hi = [](uint32_t b, uint32_t a) { return __builtin_amdgcn_perm(b, a, 0x07060302u); };
+  for (int rp = blockIdx.x; rp < npair; rp += gridDim.x) {
+    const int m0 = 2 * rp;
+    const bool has1 = m0 + 1 < M;
+    u32x4* r0 = (u32x4*)(x + (size_t)m0 * K);
+    u32x4* r1 = (u32x4*)(x + (size_t)(has1 ? m0 + 1 : m0) * K);
+    u32x4 a[CH], b[CH];
+    uint32_t mx = 0u;
+    for (int c0 = 0; c0 < nchk; c0 += CH * nthr) {
+#pragma unroll
+      for (int i = 0; i < CH; ++i) {
+        const int c = min(c0 + tid + nthr * i, nchk - 1);  // (clamped: unconditional loads)
+        a[i] = r0[c];
+        b[i] = r1[c];
+      }
+#pragma unroll
+      for (int i = 0; i < CH; ++i)
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          mx = pk_absmax(pk_absmax(mx, pk_lo(b[i][k], a[i][k])), pk_hi(b[i][k], a[i][k]));
+    }
+    mx = xor_max(mx, 64);
+    if (lane == 0) red[wave] = mx;
+    __syncthreads();
+    mx = 0u;
+    for (int w = 0; w < NW; ++w) mx = pk_absmax(mx, red[w]);
+    __syncthreads();  // (red is rewritten by the next pair)
+    const PairScale sc = pair_scale<DT>(mx, qmf, rqf);
+    for (int c0 = 0; c0 < nchk; c0 += CH * nthr) {
+      if (!cached) {
+#pragma unroll
+        for (int i = 0; i < CH; ++i) {
+          const int c = min(c0 + tid + nthr * i, nchk - 1);
+          a[i] = r0[c];
+          b[i] = r1[c];
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < CH; ++i) {
+        const int c = c0 + tid + nthr * i;
+        if (c >= nchk) continue;
+        u32x4 o0, o1;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const uint32_t lo = quant_pair<DT>(pk_lo(b[i][k], a[i][k]), sc);
+          const uint32_t hi = quant_pair<DT>(pk_hi(b[i][k], a[i][k]), sc);
+          o0[k] = pk_lo(hi, lo);
+          o1[k] = pk_hi(hi, lo);
+        }
+        r0[c] = o0;
+        if (has1) r1[c] = o1;
+      }
+    }
+  }
+}
+
+template <class DT>
+static int token_rows_launch(void* x, int M, int K, int q_max, hipStream_t s) {
+  const int nchk = K / 8;
+  const int ch = nchk <= 2048 ? 2 : 4;
+  const int nthr = (int)min(1024L, round_up(cdiv(nchk, ch), 64));
+  const int npair = (M + 1) / 2;
+  const dim3 grid(npair < 65536 ? npair : 65536), block(nthr < 64 ? 64 : nthr);
+  const float qmf = (float)q_max, rqf = 1.0f / qmf;
+  if (ch == 2)
+    token_rows_kernel<DT, 2><<<grid, block, 0, s>>>((typename DT::T*)x, M, K, qmf, rqf);
+  else
+    token_rows_kernel<DT, 4><<<grid, block, 0, s>>>((typename DT::T*)x, M, K, qmf, rqf);
+  SQMP_LAUNCH_CHECK();
+  return SQMP_OK;
+}
+
+int launch_token_rows(int dtype, void* x, int M, int K, int q_max, hipStream_t s) {
+  if (M <= 0 || K <= 0 || K % 8 != 0 || ((uintptr_t)x) % 16 != 0) return SQMP_EUNSUPPORTED;
+  if (dtype == SQMP_F16) return token_rows_launch<F16>(x, M, K, q_max, s);
+  if (dtype == SQMP_BF16) return token_rows_launch<BF16>(x, M, K, q_max, s);
+  return SQMP_EUNSUPPORTED;
+}
+
 // The OUT_FP quantizer for a layer and up to two siblings (sqmp_quant_act_group): group mode,
 // groups of >= LC_RPL ranks; out[0] in the packed order of lctab, sib.out[o] in sib.tab[o]'s.
 int launch_quant_lc_group(int dtype, const void* x, int M, int K, int q_max, int G,

@@ -378,11 +378,13 @@ __global__ __launch_bounds__((OPT & 16) ? 1024 : 512, ((OPT & 8) && !(OPT & 16))
 #pragma unroll
     for (int j = 0; j < J; ++j)
       bf[0][j] = DIAG == 3 ? u32x4{cd.w[j >> 1][(j & 1) * 2], sp[j], sp[j], sp[j]}
-                           : Dec<DT>::run(cd.w[j >> 1][(j & 1) * 2], sp[j], dk);
+                           : (J == 4 ? Dec<DT>::run_lean(cd.w[j >> 1][(j & 1) * 2], sp[j], dk)
+                                     : Dec<DT>::run(cd.w[j >> 1][(j & 1) * 2], sp[j], dk));
 #define SQMP_BF7(s, j) bf[s][j]
     SQMP_FQ7_BLOCKS(SQMP_BF7, ald,
                     if (t < J) bf[1][t] = DIAG == 3 ? u32x4{cd.w[t >> 1][(t & 1) * 2 + 1], sp[t], sp[t], sp[t]}
-                                                    : Dec<DT>::run(cd.w[t >> 1][(t & 1) * 2 + 1], sp[t], dk));
+                                                    : (J == 4 ? Dec<DT>::run_lean(cd.w[t >> 1][(t & 1) * 2 + 1], sp[t], dk)
+                                                              : Dec<DT>::run(cd.w[t >> 1][(t & 1) * 2 + 1], sp[t], dk)));
 #undef SQMP_BF7
   };
   // hook(t) runs after the MFMAs of block t (the mid-stage wait / issue at t = I - 1)
@@ -735,9 +737,11 @@ static int launch_k(const void* a, const void* bt, const void* st, const void* s
   gemm_fq7_kernel<DT, GB, TM, J, DIAG, false, O><<<dim3(tiles_m * tiles_n), dim3((O) & 16 ? 1024 : 512), 0, s>>>( \
       (const T*)a, (const uint32_t*)bt, (const T*)st, (const T*)salt, (const T*)bias, (T*)y, M,  \
       N, Kp, S_pad, Gw, ngw, tiles_m, tiles_n, group_m_env(), colmax, nt, Fq7Grp{})
-  // OPT variants (setprio for waves 4-7, loader split) for the fp16 J = 2 kernels, the
-  // 2048-token Llama GEMMs (A/B knob SQMP_FQ7_OPT, read per launch)
-  if constexpr (std::is_same<DT, F16>::value && J == 2 && GB == 1 && DIAG == 0) {
+  // OPT variants (setprio for waves 4-7, loader split, two workgroups per CU, K split) for the
+  // fp16 and bf16 J = 2 kernels, the 2048-token Llama GEMMs (A/B knob SQMP_FQ7_OPT, read per
+  // launch)
+  if constexpr ((std::is_same<DT, F16>::value || std::is_same<DT, BF16>::value) && J == 2 &&
+                GB == 1 && DIAG == 0) {
     switch (eff_opt_pk(true, TM, (long)tiles_m * tiles_n, Kp)) {
       case 1: SQMP_PK(1); break;
       case 2: SQMP_PK(2); break;
@@ -816,10 +820,11 @@ static int tm_group(bool bf16, int M, const int* Ns, int n) {
   return bf16 ? 128 : tm;  // (bf16 at 256 x 256 puts an array in scratch)
 }
 // the OPT variant dispatch_group launches
-static int group_opt(bool f16, int tm, long tiles, int kp) {
-  if (tm == 256) return f16 ? 3 : -1;
+// (fp16 and bf16 alike; bf16 groups always take 128-row tiles, tm_group)
+static int group_opt(int tm, long tiles, int kp) {
+  if (tm == 256) return 3;
   const int o = opt_pk_env(128, tiles, kp);
-  if (o == 24 && f16) return 24;
+  if (o == 24) return 24;
   return o == 8 ? 8 : 3;
 }
 
@@ -839,7 +844,7 @@ static int dispatch_group(Fq7Grp& g, int M, int Kp, int S_pad, int Gw, int ngw, 
   gemm_fq7_kernel<DT, 1, TMV, 2, 0, false, O, true><<<dim3(end), dim3((O) & 16 ? 1024 : 512), 0, s>>>( \
       (const T*)nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, M, 0, Kp, S_pad, Gw, ngw, \
       tiles_m, 0, group_m_env(), nullptr, nt, g)
-  switch (group_opt(std::is_same<DT, F16>::value, tm, end, Kp)) {
+  switch (group_opt(tm, end, Kp)) {
     case 3:
       if (tm == 256) {
         if constexpr (std::is_same<DT, F16>::value) SQMP_G(256, 3);
@@ -847,9 +852,7 @@ static int dispatch_group(Fq7Grp& g, int M, int Kp, int S_pad, int Gw, int ngw, 
         SQMP_G(128, 3);
       }
       break;
-    case 24:
-      if constexpr (std::is_same<DT, F16>::value) SQMP_G(128, 24);
-      break;
+    case 24: SQMP_G(128, 24); break;
     case 8: SQMP_G(128, 8); break;
     default: break;
   }
@@ -1041,7 +1044,7 @@ extern "C" int sqmp_fq7_plan(int dtype, int M, const int* N, int nprob, int Kp, 
   if (nprob == 0) {
     const int t = fq7::tm_standalone(bf16, M, N[0], J);
     *tm = t;
-    *opt = fq7::eff_opt_pk(!bf16 && J == 2 && Gw % 64 == 0, t, (long)cdiv(M, t) * cdiv(N[0], 128 * J), Kp);
+    *opt = fq7::eff_opt_pk(J == 2 && Gw % 64 == 0, t, (long)cdiv(M, t) * cdiv(N[0], 128 * J), Kp);
     return SQMP_OK;
   }
   if (J != 2 || Gw % 64) return SQMP_EUNSUPPORTED;
@@ -1049,7 +1052,7 @@ extern "C" int sqmp_fq7_plan(int dtype, int M, const int* N, int nprob, int Kp, 
   long tiles = 0;
   for (int p = 0; p < nprob; ++p) tiles += (long)cdiv(M, t) * cdiv(N[p], 256);
   *tm = t;
-  *opt = fq7::group_opt(!bf16, t, tiles, Kp);
+  *opt = fq7::group_opt(t, tiles, Kp);
   return SQMP_OK;
 }
 

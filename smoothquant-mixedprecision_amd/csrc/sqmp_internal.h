@@ -104,6 +104,9 @@ struct LcSib {
 // 2 group (any rank order: sorted / unsorted / mean3std -- lctab carries it).
 bool quant_lc_supported(int dtype, int M, int K, int amode_group, int G, int Kn, int P,
                         int S_pad, const void* x, const void* out);
+// in-place per-token quantization of [M][K] rows without salient columns (f16 / bf16, K % 8 == 0,
+// 16-B aligned; else SQMP_EUNSUPPORTED)
+int launch_token_rows(int dtype, void* x, int M, int K, int q_max, hipStream_t s);
 int launch_quant_lc(int dtype, int mode, const void* x, int M, int K, int q_max, int G,
                     const uint32_t* lctab, int Kn, const int32_t* amap, int P,
                     const int32_t* sal, int S, int S_pad, const uint32_t* cmax,

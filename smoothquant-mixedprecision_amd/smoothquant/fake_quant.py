@@ -529,16 +529,24 @@ class W4A4Linear(nn.Module):
         # fp32 layers: the quantizer writes sqmp_gemm_h2d's two f16 planes itself
         use_h2 = (not use_f8 and not use_fqt and self.kernel == "auto"
                   and ops.h2_planes_ok(pw, amode, x2.shape[0], ag))
+        # the in-place quantization of the caller's x is the GEMM operand itself when the
+        # packed order is the column order (ops.identity_layout): one quantizer pass, not two
+        # (the operand rows the GEMM over-reads up to its 256-row tiles exist only when M is a
+        # multiple of 256; else the quantized rows are copied into a padded operand)
+        inplace_op = (mutate_input and not (use_f8 or use_fqt or use_h2)
+                      and ops.identity_layout(pw) and ops.f8_input_ok(xc))
         if use_f8:
             a8, sa, xs = ops.quant_act_f8(xc, pw, amode, bits)
         elif use_fqt:
             c4 = ops.quant_act_c4(xc, pw, amode, bits, ag, stats_of=x)
         elif use_h2:
             a2 = ops.quant_act_fp(xc, pw, amode, bits, ag, stats_of=x, h2=True)
-        else:
+        elif not inplace_op:
             a = ops.quant_act_fp(xc, pw, amode, bits, ag, stats_of=x)
         if mutate_input:
             ops.fake_quant_inplace(xc, amode, bits, ag, pw.amap_fq, pw.nonsal, 0)
+        if inplace_op:
+            a = xc if xc.shape[0] % 256 == 0 else ops.padded_operand(xc)
         if ospec is not None and self.salient_indices is not None and pw.N != pw.K:
             raise IndexError(                                                # :311-314
                 f"The shape of the mask [{pw.K}] at index 0 does not match the shape "

@@ -95,6 +95,7 @@ class PackedWeight:
     h2: Optional[tuple] = field(default=None)            # (f16 [2, Np, L], int32 [Np]) (gemm_h2)
     h2d: Optional[torch.Tensor] = field(default=None)    # f16 tile-major planes (gemm_h2d)
     sib_maps: Optional[tuple] = field(default=None)      # sibling position map (sqmp_permute_act)
+    ident: Optional[bool] = field(default=None)          # packed order == column order (identity_layout)
 
     @property
     def gemm_operand(self):
@@ -159,11 +160,30 @@ def pack_weight(w: torch.Tensor, weight_quant: str, n_bits: int, group_size: int
                       Gw, ngw, n_bits_eff, wmode, w.dtype)
     pw.posmap = build_posmap(perm, K)
     pw.sal_key = salient_key(K, salient)
+    identity_layout(pw)
     epc = 4 if w.dtype == torch.float32 else 8
     if n_bits_eff and Gw % epc != 0:
         # groups finer than one 16-B chunk: keep a dense packed-order operand for the GEMM
         pw.dense = dequant_weight_packed(pw)
     return pw
+
+
+def identity_layout(pw: PackedWeight) -> bool:
+    """Whether the GEMM's activation operand [M, Kp + S_pad] is x_hat in the input's own column
+    order: no salient column, no padding position, the identity packed order (per_channel /
+    per_tensor / unsorted weights without salient channels, the reference's ppl_eval flow).
+    Then the in-place act quantizer's result (fake_quant.py:56-75 on the caller's x) IS the
+    operand.  Decided once per packed weight, at pack time or at the first forward outside a
+    HIP-graph capture (the check reads the order back); False while capturing."""
+    if pw.ident is None:
+        if pw.S != 0 or pw.S_pad != 0 or pw.Kp != pw.K:
+            pw.ident = False
+        elif torch.cuda.is_current_stream_capturing():
+            return False
+        else:
+            pw.ident = bool(torch.equal(pw.perm[:pw.K].long(),
+                                        torch.arange(pw.K, device=pw.perm.device)))
+    return pw.ident
 
 
 def build_posmap(perm: torch.Tensor, K: int) -> torch.Tensor:
@@ -205,6 +225,14 @@ def dequant_weight(pw: PackedWeight) -> torch.Tensor:
 def _pad_rows(M: int) -> int:
     """Activation operands are allocated with rows padded to the GEMM's 256-row tile."""
     return max(256, (M + 255) // 256 * 256)
+
+
+def padded_operand(t2: torch.Tensor) -> torch.Tensor:
+    """An M-row view of a copy of t [M, L] in an allocation of _pad_rows(M) rows (the row
+    padding the GEMMs' LDS-DMA tiles read past M)."""
+    a = torch.empty((_pad_rows(t2.shape[0]), t2.shape[1]), dtype=t2.dtype, device=t2.device)
+    a[:t2.shape[0]].copy_(t2)
+    return a[:t2.shape[0]]
 
 
 def _act_workspace(M: int, K: int, Kp: int, device):
@@ -608,6 +636,19 @@ def fake_quant_inplace(t2: torch.Tensor, act_quant: str, n_bits: int, group_size
     stream = torch.cuda.current_stream(t2.device).cuda_stream
     e = _act_ws(t2.device, stream, C, C, nb, "out")
     flags = _lib.QA_CLEAN_WS | (_lib.QA_STATS_GIVEN if stats_given else 0)
+    # the list table of the unsorted modes depends only on (C, the non-salient list, the
+    # salient set): with no salient column the list is 0 .. C-1 (build_maps / pack_weight), so
+    # every such call on this workspace builds the same table -- consecutive in-place
+    # quantizers (the ppl_eval flow's inputs and q/k/v outputs) skip its launch
+    # (SQMP_QA_TABLE_READY).  Never across a HIP-graph capture: a workspace a capture used is
+    # rewritten by every replay, behind this bookkeeping.
+    tab = (("list", C) if (S == 0 and M > 0 and act_quant in ("per_token", "per_group_unsorted"))
+           else None)
+    capturing = torch.cuda.is_current_stream_capturing()
+    if capturing:
+        e["captured"] = True
+    if tab is not None and not e.get("captured") and e.get("tab") == tab:
+        flags |= _lib.QA_TABLE_READY
     status = lib.sqmp_quant_act_v2(_p(t2), _dtype_code(t2.dtype), M, C, ACT_MODES[act_quant],
                                    n_bits, group_size, _p(amap_fq), C, _p(nonsal), None, S, 0,
                                    None, flags, _lib.OUT_INPLACE, None, None, None,
@@ -615,6 +656,7 @@ def fake_quant_inplace(t2: torch.Tensor, act_quant: str, n_bits: int, group_size
     if status != _lib.SQMP_OK:
         _WS.pop((t2.device.index, stream, C, C, "out"), None)
         check(status, "fake_quant")
+    e["tab"] = tab  # (any other mode rebuilt or overwrote the table region)
     e["stats"] = None  # the sorted-column list now describes t2, not a layer input
     # the kernel wrote t2 through a raw pointer: bump its version counter so statistics
     # another workspace recorded for this (now quantized) tensor are not reused
