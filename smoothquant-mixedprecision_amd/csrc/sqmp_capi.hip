@@ -2,7 +2,7 @@
 #include "sqmp_common.h"
 
 extern "C" const char* sqmp_version(void) {
-  return "sqmp_w4a4 0.6.0 (gfx950; W4A4 mixed-precision linear, smoothquant-mixedprecision)";
+  return "sqmp_w4a4 0.6.1 (gfx950; W4A4 mixed-precision linear, smoothquant-mixedprecision)";
 }
 
 extern "C" const char* sqmp_status_string(int status) {
