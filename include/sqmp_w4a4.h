@@ -185,6 +185,11 @@ int sqmp_quant_act(void* x, int dtype, int M, int K, int amode, int n_bits,
                                  salient set and position map, e.g. the in-place quantizers of
                                  consecutive layers without salient channels): its build launch
                                  is skipped.  Ignored by the sorted modes. */
+#define SQMP_QA_WRITE_X 64    /* SQMP_OUT_F8, per_token, no salient column, identity packed
+                                 order (Kp == K), f16 / bf16 rows with K % 8 == 0 and 16-B
+                                 alignment: x_hat is also written over x in the same pass (the
+                                 reference's in-place act quantization of the caller's input,
+                                 fake_quant.py:56-64 via :304); else SQMP_EUNSUPPORTED */
 
 /* sqmp_quant_act with the per-weight map posmap (int32 [K]: packed position of column k,
  * the inverse of perm; NULL = derive it per call) and flags.  With posmap, OUT_FP on

@@ -1800,8 +1800,9 @@ static int quant_act_impl(void* x, int dtype, int M, int K, int amode, int n_bit
   if (n_bits < 2 || n_bits > 8) return SQMP_EUNSUPPORTED;
   if (S < 0 || S > K || !x || !amap || (K - S > 0 && !nonsal)) return SQMP_EINVAL;
   if (flags & ~(SQMP_QA_CLEAN_WS | SQMP_QA_REUSE_STATS | SQMP_QA_STATS_GIVEN | SQMP_QA_TILED |
-                SQMP_QA_TILED4 | SQMP_QA_TABLE_READY))
+                SQMP_QA_TILED4 | SQMP_QA_TABLE_READY | SQMP_QA_WRITE_X))
     return SQMP_EINVAL;
+  if ((flags & SQMP_QA_WRITE_X) && out_kind != SQMP_OUT_F8) return SQMP_EINVAL;
   if ((flags & (SQMP_QA_TILED | SQMP_QA_TILED4)) && out_kind != SQMP_OUT_C4)
     return SQMP_EINVAL;
   // column maxima already in the workspace (written by sqmp_gemm_fq_colmax's epilogue)
@@ -1907,6 +1908,12 @@ static int quant_act_impl(void* x, int dtype, int M, int K, int amode, int n_bit
     return SQMP_OK;
   };
 
+  // e4m3 codes for the f8 GEMM and x_hat over x in one pass (SQMP_QA_WRITE_X: per_token, no
+  // salient column, identity packed order)
+  if (out_kind == SQMP_OUT_F8 && (flags & SQMP_QA_WRITE_X)) {
+    if (amode != SQMP_ACT_PER_TOKEN || S != 0 || Kp != K || lc_off) return SQMP_EUNSUPPORTED;
+    return launch_token_rows(dtype, x, M, K, q_max, s, (unsigned char*)out, (float*)out_scale);
+  }
   // e4m3 codes for the f8 GEMM (token / tensor scales): list-order table, lc
   // quantizer
   if (out_kind == SQMP_OUT_F8) {

@@ -41,6 +41,7 @@ typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef _Float16 h16x2 __attribute__((ext_vector_type(2)));
 typedef __bf16 b16x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x2v __attribute__((ext_vector_type(2)));
 
 __device__ inline uint32_t pk_absmax(uint32_t a, uint32_t b) {
   // both halves are D values; their magnitudes order like unsigned 16-bit integers
@@ -1042,9 +1043,13 @@ int launch_quant_lc(int dtype, int mode, const void* x, int M, int K, int q_max,
 // workgroup-wide packed absmax, then pair_scale / quant_pair (the lane-contiguous quantizer's
 // arithmetic, so bit for bit its values) and the chunks stored back over the rows.
 // (rows longer than CH chunks per thread: the chunks are streamed twice, max then quantize)
-template <class DT, int CH>
+// F8OUT (the FP8 GEMM's operand in the same pass, identity packed order): the e4m3 codes
+// [M][K] (bytes, row-major, the OUT_F8 layout) and the fp32 row scales as well.
+template <class DT, int CH, bool F8OUT = false>
 __global__ __launch_bounds__(1024) void token_rows_kernel(typename DT::T* __restrict__ x, int M,
-                                                          int K, float qmf, float rqf) {
+                                                          int K, float qmf, float rqf,
+                                                          unsigned char* __restrict__ codes = nullptr,
+                                                          float* __restrict__ oscale = nullptr) {
   __shared__ uint32_t red[LC_MAXW];
   const int nthr = blockDim.x, tid = threadIdx.x, lane = tid & 63, NW = nthr >> 6;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1079,6 +1084,10 @@ __global__ __launch_bounds__(1024) void token_rows_kernel(typename DT::T* __rest
     for (int w = 0; w < NW; ++w) mx = pk_absmax(mx, red[w]);
     __syncthreads();  // (red is rewritten by the next pair)
     const PairScale sc = pair_scale<DT>(mx, qmf, rqf);
+    if (F8OUT && tid == 0) {
+      oscale[m0] = sc.s[0];
+      if (has1) oscale[m0 + 1] = sc.s[1];
+    }
     for (int c0 = 0; c0 < nchk; c0 += CH * nthr) {
       if (!cached) {
 #pragma unroll
@@ -1093,40 +1102,69 @@ __global__ __launch_bounds__(1024) void token_rows_kernel(typename DT::T* __rest
         const int c = c0 + tid + nthr * i;
         if (c >= nchk) continue;
         u32x4 o0, o1;
+        uint32_t f[8];  // (F8OUT) the e4m3 code pairs of columns 8c .. 8c + 7
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-          const uint32_t lo = quant_pair<DT>(pk_lo(b[i][k], a[i][k]), sc);
-          const uint32_t hi = quant_pair<DT>(pk_hi(b[i][k], a[i][k]), sc);
+          const uint32_t wl = pk_lo(b[i][k], a[i][k]), wh = pk_hi(b[i][k], a[i][k]);
+          const uint32_t lo = quant_pair<DT>(wl, sc);
+          const uint32_t hi = quant_pair<DT>(wh, sc);
           o0[k] = pk_lo(hi, lo);
           o1[k] = pk_hi(hi, lo);
+          if (F8OUT) {
+            f[2 * k] = f8_pair<DT>(wl, sc);
+            f[2 * k + 1] = f8_pair<DT>(wh, sc);
+          }
         }
         r0[c] = o0;
         if (has1) r1[c] = o1;
+        if (F8OUT) {
+          // row m0's codes are byte 0 of each pair word, row m0 + 1's byte 2 (f8_pair)
+          u32x2v c0w, c1w;
+#pragma unroll
+          for (int d = 0; d < 2; ++d) {
+            c0w[d] = __builtin_amdgcn_perm(f[4 * d + 1], f[4 * d], 0x0c0c0400u) |
+                     __builtin_amdgcn_perm(f[4 * d + 3], f[4 * d + 2], 0x04000c0cu);
+            c1w[d] = __builtin_amdgcn_perm(f[4 * d + 1], f[4 * d], 0x0c0c0602u) |
+                     __builtin_amdgcn_perm(f[4 * d + 3], f[4 * d + 2], 0x06020c0cu);
+          }
+          *(u32x2v*)(codes + (size_t)m0 * K + 8 * c) = c0w;
+          if (has1) *(u32x2v*)(codes + (size_t)(m0 + 1) * K + 8 * c) = c1w;
+        }
       }
     }
   }
 }
 
 template <class DT>
-static int token_rows_launch(void* x, int M, int K, int q_max, hipStream_t s) {
+static int token_rows_launch(void* x, int M, int K, int q_max, hipStream_t s,
+                             unsigned char* codes = nullptr, float* oscale = nullptr) {
   const int nchk = K / 8;
   const int ch = nchk <= 2048 ? 2 : 4;
   const int nthr = (int)min(1024L, round_up(cdiv(nchk, ch), 64));
   const int npair = (M + 1) / 2;
   const dim3 grid(npair < 65536 ? npair : 65536), block(nthr < 64 ? 64 : nthr);
   const float qmf = (float)q_max, rqf = 1.0f / qmf;
-  if (ch == 2)
-    token_rows_kernel<DT, 2><<<grid, block, 0, s>>>((typename DT::T*)x, M, K, qmf, rqf);
-  else
-    token_rows_kernel<DT, 4><<<grid, block, 0, s>>>((typename DT::T*)x, M, K, qmf, rqf);
+  typedef typename DT::T T;
+  if (codes) {
+    if (ch == 2)
+      token_rows_kernel<DT, 2, true><<<grid, block, 0, s>>>((T*)x, M, K, qmf, rqf, codes, oscale);
+    else
+      token_rows_kernel<DT, 4, true><<<grid, block, 0, s>>>((T*)x, M, K, qmf, rqf, codes, oscale);
+  } else if (ch == 2) {
+    token_rows_kernel<DT, 2><<<grid, block, 0, s>>>((T*)x, M, K, qmf, rqf);
+  } else {
+    token_rows_kernel<DT, 4><<<grid, block, 0, s>>>((T*)x, M, K, qmf, rqf);
+  }
   SQMP_LAUNCH_CHECK();
   return SQMP_OK;
 }
 
-int launch_token_rows(int dtype, void* x, int M, int K, int q_max, hipStream_t s) {
+int launch_token_rows(int dtype, void* x, int M, int K, int q_max, hipStream_t s,
+                      unsigned char* codes, float* oscale) {
   if (M <= 0 || K <= 0 || K % 8 != 0 || ((uintptr_t)x) % 16 != 0) return SQMP_EUNSUPPORTED;
-  if (dtype == SQMP_F16) return token_rows_launch<F16>(x, M, K, q_max, s);
-  if (dtype == SQMP_BF16) return token_rows_launch<BF16>(x, M, K, q_max, s);
+  if (codes && (!oscale || ((uintptr_t)codes) % 8 != 0 || q_max > 7)) return SQMP_EUNSUPPORTED;
+  if (dtype == SQMP_F16) return token_rows_launch<F16>(x, M, K, q_max, s, codes, oscale);
+  if (dtype == SQMP_BF16) return token_rows_launch<BF16>(x, M, K, q_max, s, codes, oscale);
   return SQMP_EUNSUPPORTED;
 }
 

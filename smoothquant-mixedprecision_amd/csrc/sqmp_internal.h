@@ -106,7 +106,9 @@ bool quant_lc_supported(int dtype, int M, int K, int amode_group, int G, int Kn,
                         int S_pad, const void* x, const void* out);
 // in-place per-token quantization of [M][K] rows without salient columns (f16 / bf16, K % 8 == 0,
 // 16-B aligned; else SQMP_EUNSUPPORTED)
-int launch_token_rows(int dtype, void* x, int M, int K, int q_max, hipStream_t s);
+// codes / oscale (optional): also the e4m3 codes [M][K] and fp32 row scales of SQMP_OUT_F8
+int launch_token_rows(int dtype, void* x, int M, int K, int q_max, hipStream_t s,
+                      unsigned char* codes = nullptr, float* oscale = nullptr);
 int launch_quant_lc(int dtype, int mode, const void* x, int M, int K, int q_max, int G,
                     const uint32_t* lctab, int Kn, const int32_t* amap, int P,
                     const int32_t* sal, int S, int S_pad, const uint32_t* cmax,

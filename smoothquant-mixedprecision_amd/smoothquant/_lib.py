@@ -28,6 +28,7 @@ W_PER_GROUP_MEAN3STD = 5
 OUT_FP, OUT_INPLACE, OUT_F8, OUT_C4, OUT_H2 = 0, 2, 3, 5, 6
 QA_CLEAN_WS, QA_REUSE_STATS, QA_STATS_GIVEN, QA_TILED, QA_TILED4 = 1, 2, 4, 8, 16
 QA_TABLE_READY = 32
+QA_WRITE_X = 64
 
 _vp, _i, _sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t
 _ip = ctypes.POINTER(ctypes.c_int)

@@ -535,15 +535,17 @@ class W4A4Linear(nn.Module):
         # multiple of 256; else the quantized rows are copied into a padded operand)
         inplace_op = (mutate_input and not (use_f8 or use_fqt or use_h2)
                       and ops.identity_layout(pw) and ops.f8_input_ok(xc))
+        # on the FP8 path the same pass writes the codes and x_hat over x (SQMP_QA_WRITE_X)
+        f8_write_x = use_f8 and mutate_input and ops.f8_write_x_ok(xc, pw, amode, bits)
         if use_f8:
-            a8, sa, xs = ops.quant_act_f8(xc, pw, amode, bits)
+            a8, sa, xs = ops.quant_act_f8(xc, pw, amode, bits, write_x=f8_write_x)
         elif use_fqt:
             c4 = ops.quant_act_c4(xc, pw, amode, bits, ag, stats_of=x)
         elif use_h2:
             a2 = ops.quant_act_fp(xc, pw, amode, bits, ag, stats_of=x, h2=True)
         elif not inplace_op:
             a = ops.quant_act_fp(xc, pw, amode, bits, ag, stats_of=x)
-        if mutate_input:
+        if mutate_input and not f8_write_x:
             ops.fake_quant_inplace(xc, amode, bits, ag, pw.amap_fq, pw.nonsal, 0)
         if inplace_op:
             a = xc if xc.shape[0] % 256 == 0 else ops.padded_operand(xc)

@@ -876,7 +876,8 @@ def f8_operands(pw: PackedWeight):
     return pw.w8, _ws32(pw)
 
 
-def quant_act_f8(x2: torch.Tensor, pw: PackedWeight, act_quant: str, n_bits: int):
+def quant_act_f8(x2: torch.Tensor, pw: PackedWeight, act_quant: str, n_bits: int,
+                 write_x: bool = False):
     """x [M, K] -> (e4m3 codes [M, Kp] in packed order, fp32 row scales [M], exact salient
     x [M, S_pad]) for gemm_f8 (per_token / per_tensor, n_bits <= 4)."""
     _require_gpu(x2, "quant_act")
@@ -894,13 +895,24 @@ def quant_act_f8(x2: torch.Tensor, pw: PackedWeight, act_quant: str, n_bits: int
         pw.posmap = build_posmap(pw.perm, K)
     status = lib.sqmp_quant_act_v2(_p(x2), _dtype_code(x2.dtype), M, K, ACT_MODES[act_quant],
                                    n_bits, 0, _p(pw.amap), pw.Kp, _p(pw.nonsal), _p(pw.salient),
-                                   pw.S, pw.S_pad, _p(pw.posmap), _lib.QA_CLEAN_WS, _lib.OUT_F8,
+                                   pw.S, pw.S_pad, _p(pw.posmap),
+                                   _lib.QA_CLEAN_WS | (_lib.QA_WRITE_X if write_x else 0), _lib.OUT_F8,
                                    _p(a8), _p(sa), _p(xs), _p(e["buf"]), e["buf"].numel(),
                                    ctypes.c_void_p(stream))
     if status != _lib.SQMP_OK:
         _WS.pop((x2.device.index, stream, K, pw.Kp, "in"), None)
         check(status, "quant_act")
+    if write_x:
+        torch.autograd.graph.increment_version(x2)  # (x was rewritten through a raw pointer)
     return a8, sa, xs
+
+
+def f8_write_x_ok(x2: torch.Tensor, pw: PackedWeight, act_quant: str, n_bits: int) -> bool:
+    """Whether quant_act_f8(..., write_x=True) takes this call (SQMP_QA_WRITE_X): per_token
+    4-bit codes, the identity packed order, 16-B aligned contiguous f16 / bf16 rows, K % 8 == 0."""
+    return (act_quant == "per_token" and n_bits <= 4 and pw.K % 8 == 0 and not _LC_OFF
+            and x2.dtype in (torch.float16, torch.bfloat16) and f8_input_ok(x2)
+            and identity_layout(pw))
 
 
 def f8_colmax_ok(pw: PackedWeight) -> bool:

@@ -186,3 +186,29 @@ def test_token_rows_inplace_matches_oracle(dt, M, K):
     got = x.clone()
     _fq_act(got, "per_token", 4)
     assert torch.equal(got.cpu().view(torch.int16), want.view(torch.int16))
+
+
+@pytest.mark.parametrize("M,K,N", [(2048, 4096, 4096), (301, 11008, 1024), (64, 4224, 520)])
+def test_f8_write_x_matches_two_passes(M, K, N):
+    """fp16 per_token without salient channels (quantize_llama_like's defaults) on the FP8
+    path: one pass writes the e4m3 codes, the row scales and x_hat over x (SQMP_QA_WRITE_X);
+    codes, scales, the mutated x and y equal the two-pass path (the table-driven F8 quantizer,
+    then the in-place quantizer), bit for bit."""
+    dev = _dev()
+    from smoothquant import ops
+    q = _linear(dev, K, N, torch.float16, seed=M + K)
+    pw = q.packed()
+    x0 = _x(dev, M, K, torch.float16, seed=K)
+    assert ops.f8_auto(pw, "per_token", 4) and ops.f8_write_x_ok(x0, pw, "per_token", 4)
+    xa, xb = x0.clone(), x0.clone()
+    a8n, san, _ = ops.quant_act_f8(xa, pw, "per_token", 4, write_x=True)
+    a8o, sao, xs = ops.quant_act_f8(xb, pw, "per_token", 4)
+    ops.fake_quant_inplace(xb, "per_token", 4, 128, pw.amap_fq, pw.nonsal, 0)
+    torch.cuda.synchronize()
+    assert torch.equal(a8n, a8o) and torch.equal(san, sao)
+    assert torch.equal(xa, xb)
+    xc, xd = x0.clone(), x0.clone()
+    y = q(xc)                                    # the forward takes the one-pass form
+    b = q.bias.reshape(-1)
+    y_old = ops.gemm_f8(a8o, sao, xs, pw, b)
+    assert torch.equal(xc, xb) and torch.equal(y, y_old)

@@ -8,7 +8,8 @@ last pass's kernels in order with their durations and the gaps between them.
 
 LT_FLOW=ppl_eval: the reference's smoothquant/ppl_eval.py configuration instead (bf16,
 per_channel weights, per_token activations, no salient channels, output quantization of
-q/k/v as quantize_model(quantize_bmm_input=True) binds it); LT_FP16=1 adds the unquantized
+q/k/v as quantize_model(quantize_bmm_input=True) binds it); LT_FLOW=token_fp16: the
+quantize_llama_like defaults in fp16 (per_channel W, per_token A, no salient, no output quant); LT_FP16=1 adds the unquantized
 F.linear pass of the same shapes after the W4A4 pass (a second separator in between).
 """
 import csv
@@ -75,8 +76,9 @@ def run(passes):
     import torch
     import bench
     from smoothquant.fake_quant import W4A4Linear
-    ppl_flow = os.environ.get("LT_FLOW") == "ppl_eval"
-    dt = torch.bfloat16 if ppl_flow else torch.float16
+    flow = os.environ.get("LT_FLOW", "")
+    ppl_flow = flow in ("ppl_eval", "token_fp16")
+    dt = torch.bfloat16 if flow == "ppl_eval" else torch.float16
     dev = torch.device("cuda")
     gen = torch.Generator(device=dev).manual_seed(7)
     xs = {}
@@ -92,7 +94,8 @@ def run(passes):
         dense.append((lin.weight.detach().clone(), xs[src]))
         if ppl_flow:
             q = W4A4Linear.from_float(lin, weight_quant="per_channel", act_quant="per_token",
-                                      quantize_output=name in ("q_proj", "k_proj", "v_proj"))
+                                      quantize_output=(flow == "ppl_eval"
+                                                       and name in ("q_proj", "k_proj", "v_proj")))
         else:
             imp = xs[src][:512].float().abs().mean(0).cpu()
             q = W4A4Linear.from_float(lin, weight_quant="per_group", act_quant="per_group",
