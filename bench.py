@@ -316,11 +316,13 @@ def llama_layer(dev, iters=40, flow="experiments"):
     (fp16, per_group sorted W and A, G 64, 5 % salient; run_experiments.py); "ppl_eval": the
     reference's SmoothQuant baseline evaluation (smoothquant/ppl_eval.py:69-83: bf16,
     quantize_model with per_channel W, per_token A, quantize_bmm_input=True, no salient
-    channels -- each linear quantizes its input in place, q/k/v their outputs)."""
+    channels -- each linear quantizes its input in place, q/k/v their outputs); "token":
+    quantize_llama_like's defaults (fp16, per_channel W, per_token A in place, no salient
+    channels, no output quantization)."""
     from smoothquant.fake_quant import W4A4Linear, link_siblings
     gen = torch.Generator(device=dev).manual_seed(7)
-    ppl = flow == "ppl_eval"
-    dt = torch.bfloat16 if ppl else torch.float16
+    ppl = flow in ("ppl_eval", "token")
+    dt = torch.bfloat16 if flow == "ppl_eval" else torch.float16
     xs = {}
     for name, K in (("attn", 4096), ("o", 4096), ("mlp", 4096), ("down", 11008)):
         x = torch.randn(LLAMA_T, K, generator=gen, device=dev)
@@ -333,7 +335,8 @@ def llama_layer(dev, iters=40, flow="experiments"):
             lin.weight.copy_((torch.randn(N, K, generator=gen, device=dev) * 0.02).to(dt))
         if ppl:
             q = W4A4Linear.from_float(lin, weight_quant="per_channel", act_quant="per_token",
-                                      quantize_output=name in ("q_proj", "k_proj", "v_proj"))
+                                      quantize_output=(flow == "ppl_eval" and
+                                                       name in ("q_proj", "k_proj", "v_proj")))
         else:
             imp = xs[src][:512].float().abs().mean(0).cpu()
             q = W4A4Linear.from_float(lin, weight_quant="per_group", act_quant="per_group",
@@ -372,15 +375,20 @@ def llama_layer(dev, iters=40, flow="experiments"):
     flops = sum(2.0 * LLAMA_T * K * N for _, K, N, _ in LLAMA_LINEARS)
     (pw4, tw4), (pf16, tf16) = out["w4a4"], out["fp16"]
     if ppl:
+        u = "bf16" if flow == "ppl_eval" else "fp16"
         return {
             "workload": (f"Llama-2-7B decoder layer linears, {LLAMA_T} tokens, the reference's "
                          "ppl_eval flow: bf16, W4 per_channel, A4 per_token (in place), q/k/v "
-                         "outputs quantized per_token, no salient channels"),
-            "w4a4_ms": round(tw4, 4), "bf16_linear_ms": round(tf16, 4),
-            "w4a4_over_bf16_speed": round(tf16 / tw4, 4),
+                         "outputs quantized per_token, no salient channels"
+                         if flow == "ppl_eval" else
+                         f"Llama-2-7B decoder layer linears, {LLAMA_T} tokens, "
+                         "quantize_llama_like's defaults: fp16, W4 per_channel, A4 per_token (in "
+                         "place), no salient channels, no output quantization"),
+            "w4a4_ms": round(tw4, 4), f"{u}_linear_ms": round(tf16, 4),
+            f"w4a4_over_{u}_speed": round(tf16 / tw4, 4),
             "w4a4_TFLOP_per_s": round(flops / (tw4 * 1e-3) / 1e12, 1),
-            "per_linear": {name: {"w4a4_ms": round(a, 4), "bf16_ms": round(b, 4),
-                                  "bf16_over_w4a4": round(b / a, 3)}
+            "per_linear": {name: {"w4a4_ms": round(a, 4), f"{u}_ms": round(b, 4),
+                                  f"{u}_over_w4a4": round(b / a, 3)}
                            for (name, _, _, _), a, b in zip(LLAMA_LINEARS, pw4, pf16)},
             "note": "median of 40 layer passes, best of 2 interleaved rounds; every input is "
                     "quantized in place by its layer, as in the reference (the passes re-run "
@@ -782,6 +790,7 @@ def main(argv=None):
     if not fp32 and not args.no_layer:
         out["llama_layer"] = llama_layer(dev)
         out["llama_layer_pplflow"] = llama_layer(dev, flow="ppl_eval")
+        out["llama_layer_token"] = llama_layer(dev, flow="token")
         out["fp32"] = fp32_leg(dev)
     if not fp32 and not args.no_layer and not args.no_e2e and world == 1:
         out["e2e"] = e2e_leg(args.e2e_windows, cpu=rank == 0 and not args.no_cpu)
