@@ -297,7 +297,10 @@ __device__ inline i32x8b cat8(const u32x4& a, const u32x4& b) {
 // DIAG (timing diagnostics, wrong results by design, only in a SQMP_DIAG_BUILD): 1 the code
 // stages' DMA from two L2-hot stages, 2 no code-stage DMA after the first two stages, 3 no
 // per-group fold (the MFMA accumulates straight into the totals)
-template <class DT, int OPT = 0, int DIAG = 0>
+// TMR (round 6): 256-row tiles, or 128-row tiles (8 waves as 2 x 4 of 64 rows x 64 columns)
+// where the 256-row grid would leave CUs idle (2048-token Llama shapes: 128 tiles for
+// N = 4096); the K order of every output is the same, so both are bit-identical.
+template <class DT, int OPT = 0, int DIAG = 0, int TMR = 256>
 __global__ __launch_bounds__(512, 1) void gemm_f8v2_kernel(
     const unsigned char* __restrict__ A8, const float* __restrict__ ascale,
     const typename DT::T* __restrict__ XS, const unsigned char* __restrict__ W8,
@@ -310,7 +313,9 @@ __global__ __launch_bounds__(512, 1) void gemm_f8v2_kernel(
 
   int tm, tn;
   tile_coords(tiles_m, tiles_n, group_m, tm, tn);
-  const int m0 = tm * 256, n0 = tn * 256;
+  constexpr int I = TMR / 32;       // 16-row activation tiles per wave
+  constexpr int APW = TMR / 64;     // A pieces (8 rows x 128 B) per virtual wave per stage
+  const int m0 = tm * TMR, n0 = tn * 256;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 2, wn = wave & 3;
@@ -335,27 +340,30 @@ __global__ __launch_bounds__(512, 1) void gemm_f8v2_kernel(
 #pragma unroll
     for (int o = 0; o < (SPLIT ? 2 : 1); ++o) {
       const int w = wave + 4 * o;  // the (virtual) wave whose pieces these are
-      const int r0 = 32 * w + (lane >> 3);
+      const int r0 = 32 * w + (lane >> 3);          // weight rows (256 per tile)
+      const int a0 = 8 * APW * w + (lane >> 3);     // activation rows (TMR per tile)
       auto row = [&](int j) { return r0 + 8 * j; };
-      auto ch = [&](int j) { return (uint32_t)(((lane & 7) ^ v2_sw(row(j))) << 4); };
+      auto arow = [&](int j) { return a0 + 8 * j; };
+      auto ch = [&](int r) { return (uint32_t)(((lane & 7) ^ v2_sw(r)) << 4); };
       if (kt < nk8) {
         if (DIAG == 2 && kt >= 2) continue;
         const uint32_t so = (uint32_t)(DIAG == 1 && kt >= 2 ? (kt & 1) : kt) * 128;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const uint32_t v = (uint32_t)row(j) * Kp + ch(j);
-          dma16(rA, v, so, slot + V2_A + (4 * w + j) * 1024);
-          dma16(rW, v, so, slot + V2_B + (4 * w + j) * 1024);
-        }
+        for (int j = 0; j < APW; ++j)
+          dma16(rA, (uint32_t)arow(j) * Kp + ch(arow(j)), so, slot + V2_A + (APW * w + j) * 1024);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          dma16(rW, (uint32_t)row(j) * Kp + ch(row(j)), so, slot + V2_B + (4 * w + j) * 1024);
       } else {
         const uint32_t so = (uint32_t)(kt - nk8) * 64 * sizeof(T);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const uint32_t c = ch(j);
-          dma16(rX, (uint32_t)row(j) * S_pad * sizeof(T) + c, so, slot + V2_A + (4 * w + j) * 1024);
-          dma16(rL, (uint32_t)min(n0 + row(j), N - 1) * S_pad * sizeof(T) + c, so,
+        for (int j = 0; j < APW; ++j)
+          dma16(rX, (uint32_t)arow(j) * S_pad * sizeof(T) + ch(arow(j)), so,
+                slot + V2_A + (APW * w + j) * 1024);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          dma16(rL, (uint32_t)min(n0 + row(j), N - 1) * S_pad * sizeof(T) + ch(row(j)), so,
                 slot + V2_B + (4 * w + j) * 1024);
-        }
       }
     }
     if (wave == 0) {
@@ -368,14 +376,14 @@ __global__ __launch_bounds__(512, 1) void gemm_f8v2_kernel(
     }
   };
 
-  f32x4 tot[8][4];
+  f32x4 tot[I][4];
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+  for (int i = 0; i < I; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) tot[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int wcol0 = wn * 64 + r16;   // + 16 j: the lane's weight row in the B image
-  const int xrow0 = wm * 128 + r16;  // + 16 i: the lane's activation row in the A image
+  const int wcol0 = wn * 64 + r16;          // + 16 j: the lane's weight row in the B image
+  const int xrow0 = wm * (TMR / 2) + r16;   // + 16 i: the lane's activation row in the A image
   auto compute_f8 = [&](const unsigned char* __restrict__ slot) {
     i32x8b bw[4];
     f32x4 sv[4];
@@ -401,8 +409,8 @@ __global__ __launch_bounds__(512, 1) void gemm_f8v2_kernel(
     ax[0] = ald(0);
     if constexpr (DIAG == 3) {
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        if (i + 1 < 8) ax[(i + 1) & 1] = ald(i + 1);
+      for (int i = 0; i < I; ++i) {
+        if (i + 1 < I) ax[(i + 1) & 1] = ald(i + 1);
 #pragma unroll
         for (int j = 0; j < 4; ++j)
           tot[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(bw[j], ax[i & 1], tot[i][j], 0, 0, 0, 127, 0, 127);
@@ -412,10 +420,10 @@ __global__ __launch_bounds__(512, 1) void gemm_f8v2_kernel(
     }
     f32x4 t[3];
 #pragma unroll
-    for (int u = 0; u < 34; ++u) {
+    for (int u = 0; u < 4 * I + 2; ++u) {
       const int i = u >> 2, j = u & 3;
-      if (u < 32) {
-        if (j == 0 && i + 1 < 8) ax[(i + 1) & 1] = ald(i + 1);
+      if (u < 4 * I) {
+        if (j == 0 && i + 1 < I) ax[(i + 1) & 1] = ald(i + 1);
         t[u % 3] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(bw[j], ax[i & 1], zero, 0, 0, 0, 127, 0, 127);
         __builtin_amdgcn_sched_barrier(0);
       }
@@ -430,8 +438,8 @@ __global__ __launch_bounds__(512, 1) void gemm_f8v2_kernel(
   // first tail stage (or the end, without a tail): scale row 16 i + r16 by its act scale
   auto apply_row_scales = [&](const float* rs) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const float s = rs[wm * 128 + 16 * i + r16];
+    for (int i = 0; i < I; ++i) {
+      const float s = rs[xrow0 + 16 * i];
 #pragma unroll
       for (int j = 0; j < 4; ++j) tot[i][j] *= s;
     }
@@ -443,7 +451,7 @@ __global__ __launch_bounds__(512, 1) void gemm_f8v2_kernel(
 #pragma unroll
       for (int j = 0; j < 4; ++j) bf[j] = *(const u32x4*)(slot + V2_B + v2_off(wcol0 + 16 * j, 4 * u + q));
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
+      for (int i = 0; i < I; ++i) {
         const u32x4 af = *(const u32x4*)(slot + V2_A + v2_off(xrow0 + 16 * i, 4 * u + q));
 #pragma unroll
         for (int j = 0; j < 4; ++j) Mfma<DT>::run(tot[i][j], bf[j], af);
@@ -483,8 +491,8 @@ __global__ __launch_bounds__(512, 1) void gemm_f8v2_kernel(
   }
   if (nkt == nk8) {  // no salient tail: row scales straight from global memory
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int gm = m0 + wm * 128 + 16 * i + r16;
+    for (int i = 0; i < I; ++i) {
+      const int gm = m0 + xrow0 + 16 * i;
       const float s = gm < M ? ascale[gm] : 0.f;
 #pragma unroll
       for (int j = 0; j < 4; ++j) tot[i][j] *= s;
@@ -502,7 +510,7 @@ __global__ __launch_bounds__(512, 1) void gemm_f8v2_kernel(
       for (int r = 0; r < 4; ++r) {
         const float bv = (bias && n0 + nl + r < N) ? DT::to_f(bias[n0 + nl + r]) : 0.f;
 #pragma unroll
-        for (int i = 0; i < 8; ++i)
+        for (int i = 0; i < I; ++i)
           if (m0 + xrow0 + 16 * i < M)
             cm[r] = fmaxf(cm[r], fabsf(DT::to_f(DT::from_f(tot[i][j][r] + bv))));
       }
@@ -518,7 +526,7 @@ __global__ __launch_bounds__(512, 1) void gemm_f8v2_kernel(
     }
   }
 
-  // ---- epilogue, full-width tiles: the 256 x 256 output tile is staged in LDS (row m:
+  // ---- epilogue, full-width tiles: the TMR x 256 output tile is staged in LDS (row m:
   // 512 B, 16-B chunk c at physical chunk c ^ (m & 31)), then each row leaves as one
   // 512-B run (32 lanes x 16 B) instead of 16 rows x 32 B per store instruction
   if (n0 + 256 <= N && (N & 7) == 0) {
@@ -531,7 +539,7 @@ __global__ __launch_bounds__(512, 1) void gemm_f8v2_kernel(
 #pragma unroll
       for (int r = 0; r < 4; ++r) bv[r] = bias ? DT::to_f(bias[n0 + nl + r]) : 0.f;
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
+      for (int i = 0; i < I; ++i) {
         const int ml = xrow0 + 16 * i;
         T v[4];
 #pragma unroll
@@ -545,7 +553,7 @@ __global__ __launch_bounds__(512, 1) void gemm_f8v2_kernel(
     asm volatile("" ::: "memory");
     const int c = tid & 31;
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
+    for (int k = 0; k < TMR / 16; ++k) {
       const int ml = 16 * k + (tid >> 5);
       const u32x4 val = *(const u32x4*)(lds + ml * 512 + ((c ^ (ml & 31)) << 4));
       if (m0 + ml < M) {
@@ -568,7 +576,7 @@ __global__ __launch_bounds__(512, 1) void gemm_f8v2_kernel(
 #pragma unroll
     for (int r = 0; r < 4; ++r) bv[r] = (bias && nb + r < N) ? DT::to_f(bias[nb + r]) : 0.f;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
+    for (int i = 0; i < I; ++i) {
       const int gm = m0 + xrow0 + 16 * i;
       if (gm >= M) continue;
       T v[4];
@@ -650,12 +658,22 @@ static int gemm_f8_impl(const void* a8, const float* ascale, const void* xs, con
   if (dtype != SQMP_F16 && dtype != SQMP_BF16) return SQMP_EUNSUPPORTED;
   if (M == 0) return SQMP_OK;
   hipStream_t s = (hipStream_t)stream;
-  const int tiles_m = cdiv(M, 256), tiles_n = cdiv(N, 256);
-  const dim3 grid(tiles_m * tiles_n), block(512);
   // Gw % 128 == 0 runs the 16x16x128 kernel (SQMP_F8_V1=1 keeps the 32x32x64 one, A/B)
   const char* v1e = knob("SQMP_F8_V1");
   const bool v1_only = v1e && atoi(v1e) != 0;
   const bool v2 = Gw % 128 == 0 && !v1_only;
+  // v2 row tiles: 128 where the 256-row grid does not fill one round of the CUs (2048 x 4096
+  // -> 4096: 128 tiles of 256 rows leave half the chip idle; 256 of 128 rows fill it: q/k/v/o
+  // 54.0 -> 44.5 us, down_proj 146.5 -> 118 us).  Past one round the 256-row tiles stay (gate /
+  // up, 344 tiles: 112 us, 129.5 on 688 of 128 rows; profiles/r06_token_fp16_layer_trace.txt).
+  // SQMP_F8_TM = 128 / 256 overrides (A/B, read per launch)
+  int tmr = 256;
+  if (v2) {
+    if ((long)cdiv(M, 256) * cdiv(N, 256) < 256) tmr = 128;
+    if (const char* te = knob("SQMP_F8_TM")) tmr = atoi(te) == 128 ? 128 : 256;
+  }
+  const int tiles_m = cdiv(M, tmr), tiles_n = cdiv(N, 256);
+  const dim3 grid(tiles_m * tiles_n), block(512);
   if (colmax && !v2) return SQMP_EUNSUPPORTED;  // fused statistics: the 16x16x128 kernel only
   // M-tiles per raster group (SQMP_GROUP_M: A/B knob, read per launch)
   const char* ge = knob("SQMP_GROUP_M");
@@ -665,11 +683,13 @@ static int gemm_f8_impl(const void* a8, const float* ascale, const void* xs, con
   // waves 4-7 +-0 (profiles/r03_ab_f8_opt.txt).  SQMP_F8_OPT: A/B knob, read per launch
   const char* oe = knob("SQMP_F8_OPT");
   const int opt = oe ? atoi(oe) & 3 : 2;
-#define SQMP_F8V2(DTT, O)                                                                    \
-  gemm_f8v2_kernel<DTT, O><<<grid, block, 0, s>>>(                                           \
+#define SQMP_F8V2T(DTT, O, TR)                                                               \
+  gemm_f8v2_kernel<DTT, O, 0, TR><<<grid, block, 0, s>>>(                                    \
       (const unsigned char*)a8, ascale, (const DTT::T*)xs, (const unsigned char*)w8, ws32,   \
       (const DTT::T*)wsal, (const DTT::T*)bias, (DTT::T*)y, M, N, Kp, S_pad, Gw, ngw, tiles_m, \
       tiles_n, group_m, colmax, nt ? 1 : 0)
+#define SQMP_F8V2(DTT, O) \
+  if (tmr == 128) { SQMP_F8V2T(DTT, O, 128); } else { SQMP_F8V2T(DTT, O, 256); }
 #ifdef SQMP_DIAG_BUILD
   const char* de = knob("SQMP_F8_DIAG");  // (sqmp_knobs.hip)
   const int diag = de ? atoi(de) : 0;
@@ -678,7 +698,7 @@ static int gemm_f8_impl(const void* a8, const float* ascale, const void* xs, con
       (const unsigned char*)a8, ascale, (const DTT::T*)xs, (const unsigned char*)w8, ws32,   \
       (const DTT::T*)wsal, (const DTT::T*)bias, (DTT::T*)y, M, N, Kp, S_pad, Gw, ngw, tiles_m, \
       tiles_n, group_m, colmax, nt ? 1 : 0)
-  if (v2 && dtype == SQMP_F16 && diag > 0) {
+  if (v2 && dtype == SQMP_F16 && diag > 0 && tmr == 256) {
     if (diag == 1) SQMP_F8D(F16, 1); else if (diag == 2) SQMP_F8D(F16, 2); else SQMP_F8D(F16, 3);
     SQMP_LAUNCH_CHECK();
     return SQMP_OK;
@@ -705,6 +725,7 @@ static int gemm_f8_impl(const void* a8, const float* ascale, const void* xs, con
   }
 #undef SQMP_F8L
 #undef SQMP_F8V2
+#undef SQMP_F8V2T
   SQMP_LAUNCH_CHECK();
   return SQMP_OK;
 }

@@ -17,7 +17,7 @@ static const char* const kKnobs[] = {
     "SQMP_NT_STORES",   "SQMP_RANK_TABLE_OFF", "SQMP_RT_TPO",      "SQMP_RT_R",
     "SQMP_RT_SB",       "SQMP_RT_BUCKET",      "SQMP_RT_DENSE",      "SQMP_RT_K16", "SQMP_RT_HIST",      "SQMP_RT_BTPO",     "SQMP_DISABLE_LC",
     "SQMP_LC_PERCU",    "SQMP_PW_RB",          "SQMP_C4_QPERCU",   "SQMP_F32_WN2",
-    "SQMP_F8_V1",       "SQMP_GROUP_M",        "SQMP_F8_OPT",      "SQMP_F8_DIAG",
+    "SQMP_F8_V1",       "SQMP_GROUP_M",        "SQMP_F8_OPT",      "SQMP_F8_DIAG",     "SQMP_F8_TM",
     "SQMP_FQ7_GROUP_M", "SQMP_FQT7_GROUP_M",   "SQMP_FQ7_OPT",     "SQMP_FQT7_OPT",
     "SQMP_FQ7_DIAG",    "SQMP_FQ7G_TM", "SQMP_FQ7_KS",        "SQMP_H2D_GROUP_M", "SQMP_H2_WIDE",
     "SQMP_H2_BK64",     "SQMP_H2_GROUP_M",     "SQMP_COLMAX_RPB",  "SQMP_LC_PPW",

@@ -154,3 +154,42 @@ def test_per_token_k_not_multiple_of_8_falls_back():
         want = D.f32(O.w4a4_forward(x, w_hat, b, "per_token", 4, 128, sal, False, D))
         y = to_np(q(to_t(x, "fp16", dev)))
         assert rel(y, want) < 2e-3
+
+
+@pytest.mark.parametrize("M,K,N,p", [(2048, 4096, 4096, 0.0), (2048, 11008, 4096, 0.05),
+                                     (333, 4096, 1000, 0.10), (2048, 4096, 11008, 0.0)])
+def test_f8_row_tiles_bit_identical(M, K, N, p, monkeypatch):
+    """The FP8 GEMM's 128-row tiles (the default where 256-row tiles leave CUs idle: the
+    2048-token Llama shapes) and its 256-row tiles: the same K order per output, so y and the
+    fused column maxima are bit-identical, with and without the salient tail, ragged M / N."""
+    import torch
+    from smoothquant import _lib, ops
+    from smoothquant.fake_quant import W4A4Linear
+    if not torch.cuda.is_available():
+        pytest.skip("no ROCm device")
+    dev = torch.device("cuda")
+    gen = torch.Generator(device=dev).manual_seed(M + N)
+    lin = torch.nn.Linear(K, N, bias=True).to(dev, torch.float16)
+    with torch.no_grad():
+        lin.weight.copy_((torch.randn(N, K, generator=gen, device=dev) * 0.02).half())
+        lin.bias.copy_((torch.randn(N, generator=gen, device=dev) * 0.01).half())
+    x = torch.randn(M, K, generator=gen, device=dev).half()
+    q = W4A4Linear.from_float(lin, weight_quant="per_group", act_quant="per_token",
+                              importance=x[:256].float().abs().mean(0).cpu(), salient_prop=p,
+                              group_size=128)
+    pw = q.packed()
+    a8, sa, xs = ops.quant_act_f8(x, pw, "per_token", 4)
+    b = lin.bias.detach()
+    out = {}
+    for tm in ("128", "256"):
+        monkeypatch.setenv("SQMP_F8_TM", tm)
+        _lib.reload_knobs()
+        cm = torch.zeros(N, dtype=torch.int32, device=dev)
+        y = ops.gemm_f8(a8, sa, xs, pw, b, colmax=cm)
+        out[tm] = (y, cm)
+    monkeypatch.delenv("SQMP_F8_TM")
+    _lib.reload_knobs()
+    assert torch.equal(out["128"][0], out["256"][0])
+    assert torch.equal(out["128"][1], out["256"][1])
+    y_auto = ops.gemm_f8(a8, sa, xs, pw, b)
+    assert torch.equal(y_auto, out["256"][0])
